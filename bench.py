@@ -1,0 +1,324 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident f32 gradient all-reduce of a 256 MiB bucket.
+
+Metric (BASELINE.json): "GiB/s device-resident f32 gradient all-reduce,
+256 MiB bucket, 1/2/4/8 GPUs".
+
+One process per GPU (python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N ...; single process for N = 1).  A *step* is one
+WorkerRingManager::pull_grads round (worker/src/middlewares/worker_ring.rs:82-94)
+on every rank over a freshly produced 256 MiB residual bucket already
+resident in HBM: grad = (sum over ranks of residual) / N, residual = 0.
+  N = 1   the reference's n == 1 round: grad = residual, residual = 0 (no
+          division, worker_ring.rs:166-171) — one fused gfx950 kernel.
+  N > 1   RCCL all-reduce over xGMI + one fused kernel (grad /= N, residual = 0).
+Every timed step consumes its own pre-generated residual bucket (W + K buckets
+of 256 MiB in HBM), so no step reduces an already-zeroed bucket.
+
+value = N * bucket_bytes * K / max-over-ranks(elapsed) / 2^30: the gradient
+bytes every rank fed into the reduction per second (weak scaling: the bucket
+per GPU is fixed).  algbw_gib_s (bucket / time) and busbw_gib_s
+(algbw * 2(N-1)/N) are reported beside it.
+
+Extra objects on the JSON line:
+  roofline      the step's dominant kernel, achieved vs peak, from HIP events
+                recorded on the launch stream inside the timed region
+  local_reduce  BASELINE config 2: the 64 MiB sum-and-scale kernel, k = 2, 4, 8
+  cpu_baseline  the reference-style CPU ring (TCP loopback, f16 wire, one pinned
+                core per worker) on the same host, rank 0 at N = 1 only
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "oxidized-neural-orchestra_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "GiB/s device-resident f32 gradient all-reduce, 256 MiB bucket, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+XGMI_LINK_GBS = 153.6 / 2      # per direction; 153.6 GB/s bidirectional per link (spec)
+GIB = float(1 << 30)
+SEED = 0x0402026
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bucket-mib", type=int, default=256)
+    ap.add_argument("--wire", choices=["f32", "f16"], default="f32")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-local-reduce", action="store_true")
+    ap.add_argument("--cpu-ranks", type=int, default=2)
+    ap.add_argument("--cpu-rounds", type=int, default=3)
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------- control plane
+class Ctl:
+    """Barrier / max / broadcast across ranks over gloo (CPU tensors only, so
+    the control plane never touches the GPU streams being timed)."""
+
+    def __init__(self, world: int, rank: int):
+        self.world, self.rank = world, rank
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("gloo", rank=rank, world_size=world)
+            self.dist = dist
+
+    def barrier(self) -> None:
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def close(self) -> None:
+        if self.dist and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def timed_region(step, steps: int, warmup: int, sync, ctl: Ctl, on_start=None) -> tuple[float, float]:
+    """W untimed steps, then exactly K steps bracketed by sync + barrier;
+    returns (max-over-ranks elapsed, local elapsed) in seconds.  `on_start`
+    runs after the warmup drained, before the opening barrier."""
+    for i in range(warmup):
+        step(i)
+    sync()
+    if on_start is not None:
+        on_start()
+    ctl.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    sync()
+    t1 = time.perf_counter()
+    ctl.barrier()
+    local = t1 - t0
+    return ctl.max(local), local
+
+
+def build_line(*, value, n_gpus, steps, warmup, elapsed, bucket_bytes, wire, extra) -> dict:
+    algbw = bucket_bytes * steps / elapsed / GIB
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": n_gpus,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY §8(d) distribution, counter-based generator, fresh bucket per step)",
+        "config": {
+            "workload": "pull_grads round: device-resident f32 all-reduce + average of a 256 MiB gradient bucket per GPU",
+            "bucket_mib": bucket_bytes / (1 << 20),
+            "bucket_elems": bucket_bytes // 4,
+            "global_batch": n_gpus,
+            "parallelism": f"dp{n_gpus}",
+            "wire": wire,
+            "collective": "none (n == 1)" if n_gpus == 1 else ("RCCL all-reduce over xGMI" if wire == "f32"
+                                                                 else "reference f16 hop ring over RCCL p2p"),
+        },
+        "algbw_gib_s": round(algbw, 3),
+        "busbw_gib_s": round(algbw * 2 * (n_gpus - 1) / n_gpus, 3) if n_gpus > 1 else None,
+    }
+    line.update(extra)
+    return line
+
+
+# -------------------------------------------------------------- PMC traffic
+def pmc_traffic(kernel_substr: str, elems: int) -> dict | None:
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (profiles/*pmc*.json written by tools/pmc_summary.py), matched on
+    the kernel name and bucket size; None when no such summary exists."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        for k in d.get("kernels", []):
+            if kernel_substr in k.get("name", "") and k.get("elems") == elems:
+                best = dict(k, source=os.path.relpath(f, ROOT))
+    return best
+
+
+# ------------------------------------------------------------- CPU baseline
+def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
+    """The reference CPU ring restated in C (oracle/ono_cpu_ring.c): n worker
+    threads, one pinned core each, loopback TCP, f16 wire, reference framing.
+    Checker-side code: it is timed here as the baseline, never used by the
+    product path."""
+    from oracle import oracle as O  # noqa: WPS433 (cpu_baseline leg only)
+
+    r = O.cpu_ring(ranks, bucket_elems, rounds, check=False, pin=True, timeout=900)
+    return {
+        "value": round(r["gib_s"], 4),
+        "unit": "GiB/s",
+        "cores": ranks,
+        "kind": "port",
+        "sample": (f"one {bucket_elems * 4 / (1 << 20):.0f} MiB f32 bucket per worker, {ranks} workers "
+                   f"(threads pinned to 1 core each, loopback TCP, reference framing + f16 wire), "
+                   f"{rounds} pull_grads rounds, {r['s_per_round']:.3f} s/round; C -O3 default x86-64"),
+        "host_cpu": _cpu_model(),
+        "host_nproc": os.cpu_count(),
+    }
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ---------------------------------------------------------- local reduce
+def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
+    """BASELINE config 2: ono_sum_scale_f32 over k 64 MiB buckets (÷k),
+    device time from HIP events on the launch stream."""
+    n = 16 << 20
+    out = {}
+    stream = torch.cuda.current_stream()
+    for k in (2, 4, 8):
+        ins = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(k)]
+        for r, t in enumerate(ins):
+            ono_amd.kernels.synth(t, SEED, r)
+        dst = torch.empty(n, dtype=torch.float32, device="cuda")
+        for _ in range(warmup):
+            ono_amd.kernels.sum_scale(dst, ins, float(k))
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in evs:
+            a.record(stream)
+            ono_amd.kernels.sum_scale(dst, ins, float(k))
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        nbytes = (k + 1) * 4 * n
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[f"k{k}"] = {"bytes_per_launch": nbytes, "us_per_launch": round(ms * 1e3, 2),
+                        "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        del ins, dst
+    torch.cuda.empty_cache()
+    return {"workload": "sum_scale_f32, 64 MiB buckets, out = (sum of k inputs) / k", "hbm_peak_gbs": HBM_PEAK_GBS,
+            **out}
+
+
+# ------------------------------------------------------------------- main
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+
+    import torch
+    import ono_amd
+
+    torch.cuda.set_device(local_rank)
+    ctl = Ctl(world, rank)
+    elems = args.bucket_mib * (1 << 20) // 4
+    bucket_bytes = elems * 4
+
+    uid = ono_amd.unique_id() if (world > 1 and rank == 0) else None
+    uid = ctl.bcast_bytes(uid) if world > 1 else None
+    ring = ono_amd.WorkerRingManager(rank, world, elems, uid=uid, wire=args.wire, device=local_rank)
+
+    nb = args.warmup + args.steps
+    residuals = [torch.empty(elems, dtype=torch.float32, device="cuda") for _ in range(nb)]
+    for i, t in enumerate(residuals):   # a fresh, distinct bucket for every step
+        ono_amd.kernels.synth(t, SEED + i, rank)
+    grad = torch.empty(elems, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    def step(i: int) -> None:
+        ring.pull_grads_dev(residuals[i], grad, stream)
+
+    elapsed, _local = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl,
+                                   on_start=lambda: ring.timing(True))
+    tim = ring.timing_read()
+    ring.timing(False)
+
+    extra = {}
+    if world == 1:
+        avg_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
+        per_launch = 12 * elems  # read residual, write grad, write zeros (12 N)
+        ach = per_launch / (avg_ms * 1e-3) / 1e9
+        pmc = pmc_traffic("ScaleZeroOp", elems)
+        extra["roofline"] = {
+            "bound": "hbm", "kernel": "ew_kernel<ScaleZeroOp<SCALE_NONE>> (grad = residual; residual = 0)",
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+            "algorithmic_bytes_per_launch": per_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
+            "launches": tim["kernels"], "timing": "HIP events on the launch stream, inside the timed region",
+        }
+        if pmc:
+            extra["roofline"]["traffic_source"] = pmc["source"]
+    else:
+        coll_ms = tim["collective_ms"] / max(tim["collectives"], 1)
+        busbw = bucket_bytes * 2 * (world - 1) / world / (coll_ms * 1e-3) / 1e9
+        peak = XGMI_LINK_GBS * (world - 1)
+        kern_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
+        extra["roofline"] = {
+            "bound": "xgmi", "kernel": "RCCL all-reduce (ring over xGMI)" if args.wire == "f32" else "RCCL p2p hops",
+            "achieved": round(busbw, 1), "peak": round(peak, 1), "unit": "GB/s", "frac": round(busbw / peak, 4),
+            "traffic": None, "avg_collective_us": round(coll_ms * 1e3, 2),
+            "peak_note": "busBW vs (N-1) direct xGMI links x 76.8 GB/s per direction (153.6 GB/s bidirectional spec)",
+            "finalize_kernel": {"bound": "hbm", "avg_launch_us": round(kern_ms * 1e3, 2),
+                                "achieved": round(12 * elems / (kern_ms * 1e-3) / 1e9, 1) if kern_ms > 0 else None,
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+        }
+
+    if rank == 0 and world == 1 and not args.no_local_reduce:
+        del residuals
+        torch.cuda.empty_cache()
+        extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        extra["cpu_baseline"] = cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds)
+
+    value = world * bucket_bytes * args.steps / elapsed / GIB
+    line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
+                      bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
+    ring.close()
+    ctl.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

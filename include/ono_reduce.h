@@ -1,0 +1,227 @@
+/*
+ * ono_reduce.h — C ABI of the MI355X-native gradient-bucket reduction path.
+ *
+ * Drop-in boundary for lminervino18/oxidized-neural-orchestra's data-parallel
+ * hot path: the worker ring all-reduce and the parameter-server gradient
+ * synchronizer/store.  The reference has no FFI for this path (it is pure
+ * Rust); these entry points are what a Rust `extern "C"` block in worker/ and
+ * parameter_server/ binds instead of the Rust types they replace (INTEGRATION.md
+ * shows the binding).  Plain pointers and sizes only; `stream` is a
+ * hipStream_t passed as void* (NULL = the legacy default stream).
+ *
+ * Conventions
+ *   - every call returns an ono_status; on failure ono_last_error() returns a
+ *     thread-local message (valid until the next failing call on that thread);
+ *   - "_dev" pointers are device (HBM) pointers, "_host" pointers host memory;
+ *   - the library owns every device buffer, stream and communicator it
+ *     creates; caller host buffers are only used for the duration of a call;
+ *   - numerics are bit-exact with the reference's CPU arithmetic (IEEE f32,
+ *     no FMA contraction, correctly rounded division/sqrt, half-2.7.1 f16 RNE),
+ *     except where a comment states a tolerance (RCCL summation order, n >= 3).
+ */
+#ifndef ONO_REDUCE_H
+#define ONO_REDUCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ONO_ABI_VERSION 1
+#define ONO_UID_BYTES 128 /* sizeof(ncclUniqueId) */
+#define ONO_MAX_INPUTS 16 /* max k of ono_sum_scale_f32 */
+
+typedef enum {
+    ONO_OK = 0,
+    ONO_E_SIZE = 1,    /* ParamServerErr::SizeMismatch   parameter_server/src/storage/error.rs:13-17 */
+    ONO_E_PROTO = 2,   /* "Received an invalid worker event"  worker/src/middlewares/worker_ring.rs:136-138 */
+    ONO_E_HIP = 3,     /* HIP runtime failure */
+    ONO_E_RCCL = 4,    /* RCCL failure (the TCP io::Error of the reference ring) */
+    ONO_E_ABORTED = 5, /* ono_ring_abort() — the reference drops the ring future in select!
+                          (worker/src/workers/all_reduce.rs:73-75) */
+    ONO_E_ARG = 6,     /* invalid argument (NULL handle, bad enum, k out of range) */
+    ONO_E_OTHER = 7    /* ParamServerErr::Other */
+} ono_status;
+
+/* Wire type of the ring.  F16 reproduces the reference exactly: gradients
+ * travel as f16 (comms/src/protocol/msg.rs:26, handles/compressor.rs:106-118),
+ * hop order c, c+1, ..., c+n-1, the chunk owner keeps f32 (worker_ring.rs:166)
+ * while replicas hold f16 copies (:200).  F32 is RCCL's ring all-reduce over
+ * xGMI (bit-exact with the f32-wire restatement for n <= 2; for n >= 3 within
+ * |d| <= 2(n-1) 2^-24 sum|g| — summation order only).                        */
+typedef enum { ONO_WIRE_F32 = 0, ONO_WIRE_F16 = 1 } ono_wire;
+
+const char *ono_last_error(void);
+int ono_abi_version(void);
+/* number of visible HIP devices (0 when no GPU); never fails on a CPU host */
+int ono_device_count(int *count);
+
+/* ===================================================================== */
+/* Elementwise kernels (HBM-bound, gfx950).  All pointers are device      */
+/* pointers; any alignment is accepted.                                    */
+/* ===================================================================== */
+
+/* out[i] = (((ins[0][i] + ins[1][i]) + ...) + ins[k-1][i]) / divisor
+ * — the per-chunk f32 sum-and-scale of the ring (worker_ring.rs:141-143 then
+ * param_manager.rs:183-188).  divisor == 1 skips the division (the reference
+ * only divides for n > 1).  1 <= k <= ONO_MAX_INPUTS; `ins` is a HOST array of
+ * k device pointers; out may alias ins[0].                                   */
+int ono_sum_scale_f32(float *out, const float *const *ins, int k, size_t n, float divisor,
+                      void *stream);
+
+/* acc[i] += in[i]   — ParamManager::acc_residual (param_manager.rs:191-197),
+ * BlockingShard::accumulate (storage/blocking/shard.rs:61-66)              */
+int ono_acc_f32(float *acc, const float *in, size_t n, void *stream);
+
+/* dst[i] = src[i] / divisor (copy when divisor == 1); then zero[i] = 0 when
+ * zero != NULL.  The tail of pull_grads(): normalize_gradient
+ * (param_manager.rs:183-188) fused with the residual reset
+ * (worker_ring.rs:168-171,191-193).  dst may equal src; zero may equal src. */
+int ono_scale_zero_f32(float *dst, const float *src, size_t n, float divisor, float *zero,
+                       void *stream);
+
+/* f16 wire codec (crate half 2.7.1: RNE, overflow -> inf, subnormals kept,
+ * NaN keeps payload + quiet bit).  compressor.rs:116 / handles/worker.rs:94  */
+int ono_f16_encode(uint16_t *out, const float *in, size_t n, void *stream);
+int ono_f16_decode(float *out, const uint16_t *in, size_t n, void *stream);
+/* scatter send: out = f16(chunk); chunk = 0      (compressor.rs:116 + worker_ring.rs:133) */
+int ono_f16_encode_zero(uint16_t *out, float *chunk, size_t n, void *stream);
+/* scatter receive: acc += f32(in)                 (worker.rs:94 + worker_ring.rs:141-143) */
+int ono_f16_decode_add(float *acc, const uint16_t *in, size_t n, void *stream);
+/* fused receive-then-forward of one hop: x = acc + f32(in); out = f16(x); acc = 0
+ * (a hop's :141-143 followed by the next hop's :122,:133 on the same chunk)   */
+int ono_f16_add_encode_zero(uint16_t *out, float *acc, const uint16_t *in, size_t n,
+                            void *stream);
+/* gather receive: out = f32(in) / divisor         (worker_ring.rs:200 + :101-105) */
+int ono_f16_decode_scale(float *out, const uint16_t *in, size_t n, float divisor, void *stream);
+
+/* synthetic gradient bucket (SURVEY.md §8(d) distribution), bit-identical to
+ * the CPU oracle's generator: out[j] = synth(seed, rank, offset + j)          */
+int ono_synth_f32(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset, void *stream);
+
+/* ===================================================================== */
+/* Ring all-reduce — WorkerRingManager (worker/src/middlewares/worker_ring.rs) */
+/* ===================================================================== */
+typedef struct ono_ring ono_ring;
+
+/* rank 0 generates the id; it travels to the other ranks out of band (over the
+ * ring's existing TCP links, worker/src/builder.rs:272-311).               */
+int ono_ring_unique_id(uint8_t uid[ONO_UID_BYTES]);
+
+/* WorkerRingManager::new(pos, addrs, prev, next, size, layers) (:39-56).
+ * Allocates the owned grad and residual buckets (size f32 each, zeroed) on
+ * `device`.  nranks == 1 needs no uid (may be NULL).                        */
+int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device,
+                    const uint8_t *uid, int wire);
+int ono_ring_destroy(ono_ring *ring);
+/* the owned buckets (device pointers): grad = WorkerRingManager.grad,
+ * residual = WorkerRingManager.residual                                      */
+float *ono_ring_grad(ono_ring *ring);
+float *ono_ring_residual(ono_ring *ring);
+size_t ono_ring_size(const ono_ring *ring);
+/* producer side: residual += grad_dev (ParamManager::acc_residual) */
+int ono_ring_acc_residual(ono_ring *ring, const float *grad_dev, void *stream);
+/* pull_grads (:82-94) on the owned buckets, device resident: on return
+ * (stream-ordered) grad = averaged all-reduced bucket, residual = 0.        */
+int ono_ring_pull_grads(ono_ring *ring, void *stream);
+/* the same on caller device buffers of ono_ring_size() elements */
+int ono_ring_pull_grads_dev(ono_ring *ring, float *residual_dev, float *grad_dev, size_t n,
+                            void *stream);
+/* host-fed form (the reference's buffers live in host memory and arrive on
+ * TCP): H2D through pinned staging, pull_grads, D2H; blocking.               */
+int ono_ring_pull_grads_host(ono_ring *ring, float *residual_host, float *grad_host, size_t n);
+/* in-place averaged all-reduce of a device buffer (buf = sum_r buf_r / n) */
+int ono_ring_allreduce_avg_dev(ono_ring *ring, float *buf_dev, size_t n, void *stream);
+/* Cancellation: makes the in-flight and every later call fail with
+ * ONO_E_ABORTED (RCCL communicator aborted).  Thread-safe.                   */
+int ono_ring_abort(ono_ring *ring);
+/* Device time of the library's own kernels inside pull_grads (HIP events on
+ * the launch stream).  enable=1 starts recording; read returns the summed ms
+ * and the launch count of the dominant local kernel since enabling.         */
+int ono_ring_timing_enable(ono_ring *ring, int enable);
+int ono_ring_timing_read(ono_ring *ring, double *kernel_ms, int64_t *launches,
+                         double *collective_ms, int64_t *collectives);
+
+/* n virtual ranks co-resident on ONE device (the device analog of the
+ * reference's loopback workers): residuals[r], grads[r] are device buckets of
+ * n_elems; executes the exact hop schedule of worker_ring.rs with the wire
+ * modelled by on-device f16/f32 message buffers.                            */
+int ono_local_ring_pull_grads(float *const *residuals, float *const *grads, int nranks,
+                              size_t n_elems, int wire, void *stream);
+
+/* ===================================================================== */
+/* Parameter-server store & synchronizer — parameter_server/src/{storage,synchronization} */
+/* ===================================================================== */
+typedef enum { ONO_OPT_GD = 0, ONO_OPT_MOMENTUM = 1, ONO_OPT_ADAM = 2, ONO_OPT_ADD = 3 } ono_opt_kind;
+typedef struct {
+    int kind;       /* ono_opt_kind; ADD = the reference tests' AddOptimizer */
+    float lr;       /* learning_rate (FloatPositive) */
+    float momentum; /* GradientDescentWithMomentum::momentum */
+    float beta1, beta2, eps; /* Adam */
+} ono_opt_spec;
+
+typedef enum { ONO_STORE_BLOCKING = 0, ONO_STORE_WILD = 1 } ono_store_kind;
+typedef struct ono_store ono_store;
+
+/* BlockingStore::new / WildStore::new (blocking/store.rs:49-75, wild/store.rs:36-61):
+ * init_params_host holds nparams initial values (the ParamGen output);
+ * shard_size as ServerBuilder::resolve_store computes it (builder.rs:164-173)
+ * bounds the per-shard optimizer state; nworkers = the barrier size.        */
+int ono_store_create(ono_store **out, int kind, const float *init_params_host, size_t nparams,
+                     size_t shard_size, size_t nworkers, const ono_opt_spec *opt, int device);
+int ono_store_destroy(ono_store *store);
+size_t ono_store_len(const ono_store *store);
+/* Store::accumulate (store.rs:84-91): thread-safe; ONO_E_SIZE on length mismatch */
+int ono_store_accumulate(ono_store *store, const float *grad_host, size_t n);
+int ono_store_accumulate_dev(ono_store *store, const float *grad_dev, size_t n);
+/* Store::update_params (store.rs:93-108): CAS-guarded; a concurrent second
+ * caller returns immediately without updating.                              */
+int ono_store_update_params(ono_store *store);
+/* Store::pull_params (store.rs:110-124) */
+int ono_store_pull_params(ono_store *store, float *out_host, size_t n);
+int ono_store_pull_params_dev(ono_store *store, float *out_dev, size_t n);
+/* test hooks mirroring the reference unit tests' field access (store.rs:186-214) */
+int ono_store_active_idx(const ono_store *store);
+int ono_store_set_updating(ono_store *store, int updating);
+
+typedef enum { ONO_SYNC_BARRIER = 0, ONO_SYNC_NONBLOCKING = 1 } ono_sync_kind;
+typedef struct ono_sync ono_sync;
+/* BarrierSync::new(size) / NoBlockingSync::new() */
+int ono_sync_create(ono_sync **out, int kind, size_t barrier_size);
+/* Clone: one handle per worker task (the Rust Arc clone) */
+int ono_sync_clone(ono_sync *sync);
+/* Drop of one clone: BarrierSync::drop shrinks the barrier when other clones
+ * remain (barrier.rs:30-38); the last release frees the synchronizer.        */
+int ono_sync_release(ono_sync *sync);
+/* Synchronizer::step (synchronizer.rs:7-21; barrier.rs:41-50; non_blocking.rs:20-31):
+ * accumulate(grad); [barrier: last arriver runs update_params]; pull_params(params) */
+int ono_sync_step(ono_sync *sync, ono_store *store, const float *grad_host, float *params_host,
+                  size_t n);
+
+/* DynBarrier (synchronization/dyn_barrier.rs:47-106), exposed for the host tests */
+typedef struct ono_barrier ono_barrier;
+typedef void (*ono_leader_fn)(void *ctx);
+int ono_barrier_create(ono_barrier **out, size_t size);
+int ono_barrier_destroy(ono_barrier *b);
+int ono_barrier_wait_with(ono_barrier *b, ono_leader_fn leader, void *ctx);
+int ono_barrier_acquire(ono_barrier *b);
+
+/* ===================================================================== */
+/* Multi-GPU parameter-server mode (BASELINE config 5): the sharded        */
+/* synchronizer as reduce-scatter + fused (÷nworkers + optimizer) + all-gather */
+/* over the ring's communicator.  Rank r owns shard r of split_chunks(n, nranks). */
+/* ===================================================================== */
+typedef struct ono_ps ono_ps;
+int ono_ps_create(ono_ps **out, ono_ring *ring, const float *init_params_host, size_t nparams,
+                  const ono_opt_spec *opt);
+int ono_ps_destroy(ono_ps *ps);
+/* grad_dev: this worker's gradient (nparams); params_dev: receives the
+ * updated full parameter vector.  Stream-ordered.                           */
+int ono_ps_step(ono_ps *ps, const float *grad_dev, float *params_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ONO_REDUCE_H */

@@ -1,0 +1,254 @@
+/*
+ * ono_cpu_ring.c — CPU BASELINE / ORACLE HARNESS (TEST INFRASTRUCTURE ONLY).
+ *
+ * The reference CPU ring all-reduce, restated in C and run the way the
+ * reference deploys it: n worker threads, each pinned to ONE core (reference
+ * docker/gen_compose.py:9, CPUS=1 per node), connected prev->self->next over
+ * loopback TCP, speaking the reference wire format
+ *   [u64 BE len][u32 BE kind=1][len-4 bytes of f16 LE]   (msg.rs:120-151, sink.rs:37-58)
+ * Per round each worker runs pull_grads() (worker_ring.rs:82-204):
+ *   scatter: encode chunk i to f16 (compressor.rs:106-118) and send it while
+ *            receiving prev's frame (try_join!, :122-123); zero chunk i (:133);
+ *            decode into a handle-owned f32 buffer (worker.rs:84-101); add it
+ *            into chunk i-1 (:141-143)
+ *   gather:  grad[own] = residual[own]; forward / copy f16 chunks; then /= n.
+ * Timed region = the pull_grads() rounds only (residual refill is outside).
+ *
+ * usage: ono_cpu_ring --ranks N --len L --rounds R [--seed S] [--check] [--no-pin]
+ * prints one JSON line: {"ranks":..,"len":..,"rounds":..,"s_per_round":..,"gib_s":..,"check":..}
+ */
+#include "ono_oracle.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+typedef struct {
+    int rank, n, rounds, pin;
+    size_t len;
+    uint64_t seed;
+    int listen_fd, port_next;
+    float *residual, *pristine, *grad;
+    double elapsed;
+} worker_t;
+
+static pthread_barrier_t g_bar;
+static double g_t0, g_total;
+
+static double now(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* send `out` and receive one frame into `in` concurrently (try_join!) */
+static int xchg(int fd_next, int fd_prev, const uint8_t *out, size_t out_n, uint8_t *in,
+                size_t in_cap, size_t *in_n) {
+    size_t sent = 0, got = 0, need = 8;
+    int have_len = 0;
+    while (sent < out_n || got < need) {
+        struct pollfd p[2];
+        int np = 0, is = -1, ir = -1;
+        if (sent < out_n) { p[np].fd = fd_next; p[np].events = POLLOUT; is = np++; }
+        if (got < need) { p[np].fd = fd_prev; p[np].events = POLLIN; ir = np++; }
+        if (poll(p, (nfds_t)np, 60000) <= 0) return -1;
+        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP))) {
+            ssize_t k = send(fd_next, out + sent, out_n - sent, MSG_NOSIGNAL);
+            if (k < 0 && errno != EAGAIN) return -2;
+            if (k > 0) sent += (size_t)k;
+        }
+        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP))) {
+            ssize_t k = recv(fd_prev, in + got, need - got, 0);
+            if (k == 0) return -3;
+            if (k < 0 && errno != EAGAIN) return -4;
+            if (k > 0) got += (size_t)k;
+            if (!have_len && got >= 8) {
+                uint64_t l = 0;
+                for (int i = 0; i < 8; i++) l = (l << 8) | in[i];
+                if (8 + l > in_cap) return -5;
+                need = 8 + (size_t)l;
+                have_len = 1;
+            }
+        }
+    }
+    *in_n = got;
+    return 0;
+}
+
+static int connect_to(int port) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    struct sockaddr_in a = {0};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    for (int tries = 0; tries < 2000; tries++) {
+        if (connect(fd, (struct sockaddr *)&a, sizeof a) == 0) return fd;
+        usleep(1000);
+    }
+    return -1;
+}
+
+static void set_nb(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
+}
+
+static void *worker_main(void *arg) {
+    worker_t *w = (worker_t *)arg;
+    if (w->pin) {
+        long nc = sysconf(_SC_NPROCESSORS_ONLN);
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        CPU_SET(w->rank % (nc > 0 ? nc : 1), &cs);
+        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+    }
+    int n = w->n;
+    int fd_next = -1, fd_prev = -1;
+    if (n > 1) {
+        fd_next = connect_to(w->port_next);
+        fd_prev = accept(w->listen_fd, NULL, NULL);
+        if (fd_next < 0 || fd_prev < 0) { fprintf(stderr, "connect failed\n"); exit(2); }
+        set_nb(fd_next);
+        set_nb(fd_prev);
+    }
+    size_t *off = (size_t *)malloc(sizeof(size_t) * (size_t)(n + 1));
+    ono_ref_split_chunks(w->len, (size_t)n, off);
+    size_t maxc = off[1] - off[0];
+    uint16_t *comp = (uint16_t *)malloc(2 * maxc + 16);           /* compression_buf */
+    uint8_t *frame = (uint8_t *)malloc(12 + 2 * maxc + 16);
+    uint32_t *inbuf = (uint32_t *)malloc(12 + 2 * maxc + 16);      /* 4-B aligned, source.rs */
+    float *dec = (float *)malloc(sizeof(float) * (maxc + 4));      /* handle-owned Vec<f32> */
+
+    for (int round = 0; round < w->rounds; round++) {
+        memcpy(w->residual, w->pristine, w->len * sizeof(float));
+        pthread_barrier_wait(&g_bar);
+        if (w->rank == 0) g_t0 = now();
+        /* ---- scatter ---- */
+        int i = w->rank;
+        for (int s = 0; s < n - 1; s++) {
+            size_t cl = off[i + 1] - off[i];
+            ono_ref_f16_encode(comp, w->residual + off[i], cl);
+            size_t fl = ono_ref_frame_dense(frame, comp, cl, 0);
+            size_t got = 0;
+            if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, 12 + 2 * maxc + 16, &got)) {
+                fprintf(stderr, "xchg failed\n"); exit(3);
+            }
+            memset(w->residual + off[i], 0, cl * sizeof(float));
+            const uint8_t *b = (const uint8_t *)inbuf;
+            size_t m = (got - 12) / 2;
+            ono_ref_f16_decode(dec, (const uint16_t *)(b + 12), m);
+            i = (i + n - 1) % n;
+            float *ch = w->residual + off[i];
+            size_t k = off[i + 1] - off[i] < m ? off[i + 1] - off[i] : m;
+            for (size_t j = 0; j < k; j++) ch[j] += dec[j];
+        }
+        /* ---- gather ---- */
+        i = (w->rank + 1) % n;
+        memcpy(w->grad + off[i], w->residual + off[i], (off[i + 1] - off[i]) * sizeof(float));
+        if (n == 1) {
+            memset(w->residual + off[i], 0, (off[i + 1] - off[i]) * sizeof(float));
+        } else {
+            for (int j = 0; j < n - 1; j++) {
+                size_t cl = off[i + 1] - off[i];
+                ono_ref_f16_encode(comp, w->grad + off[i], cl);
+                size_t fl = ono_ref_frame_dense(frame, comp, cl, 0);
+                size_t got = 0;
+                if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, 12 + 2 * maxc + 16, &got)) {
+                    fprintf(stderr, "xchg failed\n"); exit(3);
+                }
+                if (j == 0) memset(w->residual + off[i], 0, cl * sizeof(float));
+                const uint8_t *b = (const uint8_t *)inbuf;
+                size_t m = (got - 12) / 2;
+                ono_ref_f16_decode(dec, (const uint16_t *)(b + 12), m);
+                i = (i + n - 1) % n;
+                memcpy(w->grad + off[i], dec, (off[i + 1] - off[i]) * sizeof(float));
+            }
+            ono_ref_normalize(w->grad, w->len, (size_t)n);
+        }
+        pthread_barrier_wait(&g_bar);
+        if (w->rank == 0) g_total += now() - g_t0;
+    }
+    if (fd_next >= 0) close(fd_next);
+    if (fd_prev >= 0) close(fd_prev);
+    free(off); free(comp); free(frame); free(inbuf); free(dec);
+    return NULL;
+}
+
+int main(int argc, char **argv) {
+    int n = 2, rounds = 3, check = 0, pin = 1;
+    size_t len = 109386;
+    uint64_t seed = 0x0402026;
+    for (int a = 1; a < argc; a++) {
+        if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = (size_t)strtoull(argv[++a], 0, 10);
+        else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--seed") && a + 1 < argc) seed = strtoull(argv[++a], 0, 0);
+        else if (!strcmp(argv[a], "--check")) check = 1;
+        else if (!strcmp(argv[a], "--no-pin")) pin = 0;
+        else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
+    }
+    if (n < 1 || len < (size_t)n || rounds < 1) { fprintf(stderr, "need len >= ranks >= 1\n"); return 1; }
+    worker_t *w = (worker_t *)calloc((size_t)n, sizeof(worker_t));
+    int *ports = (int *)calloc((size_t)n, sizeof(int));
+    for (int r = 0; r < n; r++) {
+        int fd = socket(AF_INET, SOCK_STREAM, 0);
+        int one = 1;
+        setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+        struct sockaddr_in a = {0};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        if (bind(fd, (struct sockaddr *)&a, sizeof a) || listen(fd, 4)) { perror("bind"); return 2; }
+        socklen_t sl = sizeof a;
+        getsockname(fd, (struct sockaddr *)&a, &sl);
+        ports[r] = ntohs(a.sin_port);
+        w[r].listen_fd = fd;
+    }
+    for (int r = 0; r < n; r++) {
+        w[r].rank = r; w[r].n = n; w[r].rounds = rounds; w[r].pin = pin;
+        w[r].len = len; w[r].seed = seed; w[r].port_next = ports[(r + 1) % n];
+        w[r].residual = (float *)malloc(len * sizeof(float));
+        w[r].pristine = (float *)malloc(len * sizeof(float));
+        w[r].grad = (float *)calloc(len, sizeof(float));
+        ono_ref_synth(w[r].pristine, len, seed, (uint64_t)r, 0);
+    }
+    pthread_barrier_init(&g_bar, NULL, (unsigned)n);
+    pthread_t *th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
+    for (int r = 0; r < n; r++) pthread_create(&th[r], NULL, worker_main, &w[r]);
+    for (int r = 0; r < n; r++) pthread_join(th[r], NULL);
+
+    int ok = -1;
+    if (check) { /* compare against the in-memory lockstep oracle, bit for bit */
+        float **res = (float **)calloc((size_t)n, sizeof(float *));
+        float **gr = (float **)calloc((size_t)n, sizeof(float *));
+        for (int r = 0; r < n; r++) {
+            res[r] = (float *)malloc(len * sizeof(float));
+            gr[r] = (float *)calloc(len, sizeof(float));
+            memcpy(res[r], w[r].pristine, len * sizeof(float));
+        }
+        ono_ref_ring_pull_grads(res, gr, n, len, 0);
+        ok = 1;
+        for (int r = 0; r < n; r++) {
+            if (memcmp(gr[r], w[r].grad, len * sizeof(float))) ok = 0;
+            if (memcmp(res[r], w[r].residual, len * sizeof(float))) ok = 0;
+            free(res[r]); free(gr[r]);
+        }
+        free(res); free(gr);
+    }
+    double spr = g_total / rounds;
+    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"pinned\": %d, \"s_per_round\": %.9f, "
+           "\"gib_s\": %.6f, \"check\": %d}\n",
+           n, len, rounds, pin, spr, (double)len * 4.0 / spr / (double)(1ull << 30), ok);
+    return ok == 0 ? 4 : 0;
+}

@@ -1,0 +1,256 @@
+"""ctypes front-end for the C oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; it is the checker, never the thing measured or shipped.  The
+library it loads (oracle/_build/libono_oracle.so) is built from
+oracle/ono_oracle.c by ``make -C oracle`` (driven by __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+LIB_PATH = os.path.join(BUILD, "libono_oracle.so")
+CPU_RING = os.path.join(BUILD, "ono_cpu_ring")
+
+OPT = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
+
+_lib = None
+_fp = C.POINTER(C.c_float)
+_u16p = C.POINTER(C.c_uint16)
+_u8p = C.POINTER(C.c_uint8)
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or not os.path.exists(CPU_RING):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.ono_ref_f32_to_f16.restype = C.c_uint16
+        L.ono_ref_f32_to_f16.argtypes = [C.c_float]
+        L.ono_ref_f16_to_f32.restype = C.c_float
+        L.ono_ref_f16_to_f32.argtypes = [C.c_uint16]
+        L.ono_ref_f16_encode.argtypes = [_u16p, _fp, C.c_size_t]
+        L.ono_ref_f16_decode.argtypes = [_fp, _u16p, C.c_size_t]
+        L.ono_ref_split_chunks.restype = C.c_size_t
+        L.ono_ref_split_chunks.argtypes = [C.c_size_t, C.c_size_t, C.POINTER(C.c_size_t)]
+        L.ono_ref_ring_pull_grads.restype = C.c_int
+        L.ono_ref_ring_pull_grads.argtypes = [C.POINTER(_fp), C.POINTER(_fp), C.c_int, C.c_size_t, C.c_int]
+        L.ono_ref_sum_scale.argtypes = [_fp, C.POINTER(_fp), C.c_int, C.c_size_t, C.c_float]
+        L.ono_ref_normalize.argtypes = [_fp, C.c_size_t, C.c_size_t]
+        L.ono_ref_acc_residual.argtypes = [_fp, _fp, C.c_size_t]
+        L.ono_ref_store_new.restype = C.c_void_p
+        L.ono_ref_store_new.argtypes = [_fp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int,
+                                        C.c_float, C.c_float, C.c_float, C.c_float, C.c_float]
+        L.ono_ref_store_free.argtypes = [C.c_void_p]
+        L.ono_ref_store_accumulate.restype = C.c_int
+        L.ono_ref_store_accumulate.argtypes = [C.c_void_p, _fp, C.c_size_t]
+        L.ono_ref_store_update_params.argtypes = [C.c_void_p]
+        L.ono_ref_store_pull_params.restype = C.c_int
+        L.ono_ref_store_pull_params.argtypes = [C.c_void_p, _fp, C.c_size_t]
+        L.ono_ref_store_active_idx.restype = C.c_int
+        L.ono_ref_store_active_idx.argtypes = [C.c_void_p]
+        L.ono_ref_store_set_updating.argtypes = [C.c_void_p, C.c_int]
+        L.ono_ref_store_nshards.restype = C.c_size_t
+        L.ono_ref_store_nshards.argtypes = [C.c_void_p]
+        L.ono_ref_wild_new.restype = C.c_void_p
+        L.ono_ref_wild_new.argtypes = [_fp, C.c_size_t, C.c_size_t, C.c_int,
+                                       C.c_float, C.c_float, C.c_float, C.c_float, C.c_float]
+        L.ono_ref_wild_free.argtypes = [C.c_void_p]
+        L.ono_ref_wild_accumulate.restype = C.c_int
+        L.ono_ref_wild_accumulate.argtypes = [C.c_void_p, _fp, C.c_size_t]
+        L.ono_ref_wild_pull_params.restype = C.c_int
+        L.ono_ref_wild_pull_params.argtypes = [C.c_void_p, _fp, C.c_size_t]
+        L.ono_ref_sparse_threshold_full.restype = C.c_float
+        L.ono_ref_sparse_threshold_full.argtypes = [_fp, C.c_size_t, C.c_float]
+        L.ono_ref_grad_drop.restype = C.c_size_t
+        L.ono_ref_grad_drop.argtypes = [_u8p, _fp, C.c_size_t, C.c_float]
+        L.ono_ref_grad_lift.restype = C.c_int
+        L.ono_ref_grad_lift.argtypes = [_fp, C.c_size_t, C.POINTER(C.c_size_t), _u8p, C.c_size_t]
+        L.ono_ref_frame_dense.restype = C.c_size_t
+        L.ono_ref_frame_dense.argtypes = [_u8p, _u16p, C.c_size_t, C.c_int]
+        L.ono_ref_synth.argtypes = [_fp, C.c_size_t, C.c_uint64, C.c_uint64, C.c_size_t]
+        _lib = L
+    return _lib
+
+
+def _f(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_fp)
+
+
+def _u16(a: np.ndarray):
+    assert a.dtype == np.uint16 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u16p)
+
+
+# ----------------------------------------------------------------- functions
+def f16_encode(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.size, np.uint16)
+    lib().ono_ref_f16_encode(_u16(out), _f(x), x.size)
+    return out
+
+
+def f16_decode(h: np.ndarray) -> np.ndarray:
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    out = np.empty(h.size, np.float32)
+    lib().ono_ref_f16_decode(_f(out), _u16(h), h.size)
+    return out
+
+
+def split_chunks(length: int, n: int) -> list[tuple[int, int]]:
+    off = (C.c_size_t * (n + 1))()
+    k = lib().ono_ref_split_chunks(length, n, off)
+    return [(off[i], off[i + 1]) for i in range(k)]
+
+
+def ring_pull_grads(residuals: list[np.ndarray], wire: str = "f16"):
+    """All ranks' pull_grads() round; returns (grads, residuals_after)."""
+    n = len(residuals)
+    res = [np.array(r, dtype=np.float32, copy=True) for r in residuals]
+    length = res[0].size
+    grads = [np.zeros(length, np.float32) for _ in range(n)]
+    rp = (_fp * n)(*[_f(r) for r in res])
+    gp = (_fp * n)(*[_f(g) for g in grads])
+    rc = lib().ono_ref_ring_pull_grads(rp, gp, n, length, 0 if wire == "f16" else 1)
+    if rc != 0:
+        raise ValueError("reference panics: fewer chunks than ranks")
+    return grads, res
+
+
+def sum_scale(ins: list[np.ndarray], divisor: float) -> np.ndarray:
+    ins = [np.ascontiguousarray(x, dtype=np.float32) for x in ins]
+    out = np.empty(ins[0].size, np.float32)
+    ip = (_fp * len(ins))(*[_f(x) for x in ins])
+    lib().ono_ref_sum_scale(_f(out), ip, len(ins), out.size, divisor)
+    return out
+
+
+def synth(n: int, seed: int, rank: int, offset: int = 0) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    lib().ono_ref_synth(_f(out), n, seed, rank, offset)
+    return out
+
+
+def frame_dense(h: np.ndarray, is_last: bool = False) -> bytes:
+    h = np.ascontiguousarray(h, dtype=np.uint16)
+    buf = np.empty(12 + 2 * h.size, np.uint8)
+    k = lib().ono_ref_frame_dense(buf.ctypes.data_as(_u8p), _u16(h), h.size, int(is_last))
+    return bytes(buf[:k])
+
+
+def sparse_threshold(g: np.ndarray, r: float) -> float:
+    g = np.ascontiguousarray(g, dtype=np.float32)
+    return float(lib().ono_ref_sparse_threshold_full(_f(g), g.size, r))
+
+
+def grad_drop(g: np.ndarray, threshold: float) -> bytes:
+    g = np.ascontiguousarray(g, dtype=np.float32)
+    buf = np.empty(8 + 10 * max(g.size, 1), np.uint8)
+    k = lib().ono_ref_grad_drop(buf.ctypes.data_as(_u8p), _f(g), g.size, threshold)
+    return bytes(buf[:k])
+
+
+def grad_lift(buf: bytes, cap: int = 1 << 20) -> np.ndarray:
+    b = np.frombuffer(buf, dtype=np.uint8).copy()
+    out = np.zeros(cap, np.float32)
+    ln = C.c_size_t(0)
+    rc = lib().ono_ref_grad_lift(_f(out), cap, C.byref(ln), b.ctypes.data_as(_u8p), b.size)
+    if rc != 0:
+        raise ValueError(f"grad_lift error {rc}")
+    return out[: ln.value].copy()
+
+
+class Store:
+    """BlockingStore oracle."""
+
+    def __init__(self, params, shard_size: int, nworkers: int, kind: str = "gd",
+                 lr=0.1, momentum=0.9, beta1=0.9, beta2=0.999, eps=1e-8):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        self.n = p.size
+        self._h = lib().ono_ref_store_new(_f(p), p.size, shard_size, nworkers, OPT[kind],
+                                          lr, momentum, beta1, beta2, eps)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ono_ref_store_free(self._h)
+            self._h = None
+
+    def accumulate(self, g) -> None:
+        g = np.ascontiguousarray(g, dtype=np.float32)
+        if lib().ono_ref_store_accumulate(self._h, _f(g), g.size):
+            raise ValueError("SizeMismatch")
+
+    def update_params(self) -> None:
+        lib().ono_ref_store_update_params(self._h)
+
+    def pull_params(self) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        lib().ono_ref_store_pull_params(self._h, _f(out), self.n)
+        return out
+
+    @property
+    def active_idx(self) -> int:
+        return lib().ono_ref_store_active_idx(self._h)
+
+    def set_updating(self, v: bool) -> None:
+        lib().ono_ref_store_set_updating(self._h, int(v))
+
+    @property
+    def nshards(self) -> int:
+        return lib().ono_ref_store_nshards(self._h)
+
+
+class WildStore:
+    def __init__(self, params, shard_size: int, kind: str = "gd",
+                 lr=0.1, momentum=0.9, beta1=0.9, beta2=0.999, eps=1e-8):
+        p = np.ascontiguousarray(params, dtype=np.float32)
+        self.n = p.size
+        self._h = lib().ono_ref_wild_new(_f(p), p.size, shard_size, OPT[kind], lr, momentum,
+                                         beta1, beta2, eps)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ono_ref_wild_free(self._h)
+            self._h = None
+
+    def accumulate(self, g) -> None:
+        g = np.ascontiguousarray(g, dtype=np.float32)
+        if lib().ono_ref_wild_accumulate(self._h, _f(g), g.size):
+            raise ValueError("SizeMismatch")
+
+    def update_params(self) -> None:
+        pass
+
+    def pull_params(self) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        lib().ono_ref_wild_pull_params(self._h, _f(out), self.n)
+        return out
+
+
+def cpu_ring(ranks: int, length: int, rounds: int, seed: int = 0x0402026, check: bool = False,
+             pin: bool = True, timeout: float = 600) -> dict:
+    """Run the TCP-loopback reference-style CPU ring (oracle/ono_cpu_ring.c)."""
+    import json
+
+    if not os.path.exists(CPU_RING):
+        build()
+    cmd = [CPU_RING, "--ranks", str(ranks), "--len", str(length), "--rounds", str(rounds),
+           "--seed", str(seed)]
+    if check:
+        cmd.append("--check")
+    if not pin:
+        cmd.append("--no-pin")
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
+    return json.loads(out.stdout.strip().splitlines()[-1])

@@ -1,0 +1,70 @@
+// ono_internal.h — shared internals of libono_reduce.so (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "ono_reduce.h"
+
+namespace ono {
+
+// Records a thread-local error message and returns `code`.
+int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_error(hipError_t e, const char *what, const char *file, int line);
+
+#define ONO_HIP(expr)                                                                  \
+    do {                                                                               \
+        hipError_t ono_e_ = (expr);                                                    \
+        if (ono_e_ != hipSuccess) return ::ono::hip_error(ono_e_, #expr, __FILE__, __LINE__); \
+    } while (0)
+
+// Division by a run-time divisor d, bit-exact with IEEE `x / d`:
+//  NONE  d == 1 (the reference skips the division, param_manager.rs:183-188)
+//  RECIP d = 2^k: x * 2^-k is the same single rounding of the same real value
+//  DIV   everything else: correctly rounded v_div sequence
+enum ScaleMode { SCALE_NONE = 0, SCALE_RECIP = 1, SCALE_DIV = 2 };
+struct Scale {
+    ScaleMode mode;
+    float v;
+};
+Scale make_scale(float divisor);
+
+// split_chunks (worker/src/middlewares/mod.rs:15-59): offsets of min(len, n) chunks
+std::vector<size_t> split_chunks(size_t len, size_t n);
+
+// ---- kernel launchers (ono_kernels.hip); return hipSuccess or the launch error
+hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n, float divisor,
+                            hipStream_t s);
+hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s);
+hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divisor, float *zero,
+                             hipStream_t s);
+hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
+                        hipStream_t s);
+
+// wire-templated hop kernels: W = uint16_t (f16 wire) or float (f32 wire)
+template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, hipStream_t s);
+template <class W> hipError_t launch_decode_scale(float *out, const W *in, size_t n, float divisor,
+                                                  hipStream_t s);
+template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s);
+template <class W> hipError_t launch_decode_add(float *acc, const W *in, size_t n, hipStream_t s);
+template <class W> hipError_t launch_add_encode_zero(W *out, float *acc, const W *in, size_t n,
+                                                     hipStream_t s);
+// last scatter hop of the chunk owner: x = acc + in; grad = x / d; out = x; acc = 0
+template <class W> hipError_t launch_add_finish(float *grad, W *out, float *acc, const W *in,
+                                                size_t n, float divisor, hipStream_t s);
+
+// PS shard update (storage/blocking/shard.rs:74-92 + optimization/*.rs), fused:
+//   g /= nworkers (if > 1); optimizer step on w (state v, s); g = 0 when zero_grad
+struct OptLaunch {
+    int kind;        // ono_opt_kind
+    float lr, momentum, beta1, beta2, eps;
+    float step_size; // Adam: lr * (sqrt(1 - beta2^t) / (1 - beta1^t)), computed on the host in f32
+    float nworkers;  // divisor (1 = none)
+};
+hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_,
+                             size_t n, bool zero_grad, hipStream_t st);
+
+}  // namespace ono

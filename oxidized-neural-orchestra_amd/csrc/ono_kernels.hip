@@ -1,0 +1,590 @@
+// ono_kernels.hip — gfx950 elementwise kernels of the gradient-bucket reduction.
+//
+// Every kernel here is a pure HBM stream (10-16 B of traffic
+// per element against <= 10 VALU ops), so the design goal is bytes in flight,
+// not arithmetic:
+//   * 16-B per lane f32 accesses (global_load_dwordx4 / global_store_dwordx4),
+//     8-B per lane for f16 wire buffers, one 64-lane wave = 1 KiB per f32
+//     instruction, consecutive lanes on consecutive addresses;
+//   * U independent vectors per thread issued before any is consumed (the
+//     loads of all U iterations are in flight together), grid-stride over a
+//     grid capped at a few workgroups per CU (256 CUs, 8 XCDs);
+//   * misaligned chunk starts (split_chunks offsets are arbitrary) are handled
+//     by a <= 3-element scalar head and tail, so the body stays vectorised
+//     whenever all operands share the same 4-element phase;
+//   * no LDS: no element is read twice, so staging through LDS would only add
+//     instructions ("Why no LDS / MFMA").
+// Numerics: -ffp-contract=off, IEEE division and sqrt (hipcc default
+// -fhip-fp32-correctly-rounded-divide-sqrt), denormals preserved; f16 by
+// v_cvt_f16_f32 (round-to-nearest-even) with the `half` crate's NaN rule.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+#include "ono_internal.h"
+
+namespace ono {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint16_t h4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;  // 4 waves
+constexpr int kUnroll = 4;   // independent 16-B vectors in flight per thread per input
+
+// ------------------------------------------------------------------ f16 ----
+// half 2.7.1 f32_to_f16: RNE; NaN -> sign | 0x7C00 | 0x0200 | (mantissa >> 13)
+__device__ __forceinline__ uint16_t to_f16(float x) {
+    uint16_t b = __builtin_bit_cast(uint16_t, (_Float16)x);
+    uint32_t u = __builtin_bit_cast(uint32_t, x);
+    uint16_t nb = (uint16_t)(((u >> 16) & 0x8000u) | 0x7E00u | ((u & 0x7FFFFFu) >> 13));
+    return __builtin_isnan(x) ? nb : b;
+}
+// half 2.7.1 f16_to_f32: exact; NaN -> sign | 0x7FC00000 | (mantissa << 13)
+__device__ __forceinline__ float from_f16(uint16_t b) {
+    float f = (float)__builtin_bit_cast(_Float16, b);
+    uint32_t nb = ((uint32_t)(b & 0x8000u) << 16) | 0x7FC00000u | ((uint32_t)(b & 0x3FFu) << 13);
+    bool nan = ((b & 0x7C00u) == 0x7C00u) && (b & 0x3FFu);
+    return nan ? __builtin_bit_cast(float, nb) : f;
+}
+
+// wire traits: f16 (uint16_t) or f32 (float) messages
+template <class W> struct Wire;
+template <> struct Wire<uint16_t> {
+    typedef h4 V;
+    static __device__ __forceinline__ uint16_t enc(float x) { return to_f16(x); }
+    static __device__ __forceinline__ float dec(uint16_t h) { return from_f16(h); }
+    static __device__ __forceinline__ V enc4(f4 x) {
+        V r;
+        r.x = to_f16(x.x); r.y = to_f16(x.y); r.z = to_f16(x.z); r.w = to_f16(x.w);
+        return r;
+    }
+    static __device__ __forceinline__ f4 dec4(V h) {
+        f4 r;
+        r.x = from_f16(h.x); r.y = from_f16(h.y); r.z = from_f16(h.z); r.w = from_f16(h.w);
+        return r;
+    }
+};
+template <> struct Wire<float> {
+    typedef f4 V;
+    static __device__ __forceinline__ float enc(float x) { return x; }
+    static __device__ __forceinline__ float dec(float x) { return x; }
+    static __device__ __forceinline__ V enc4(f4 x) { return x; }
+    static __device__ __forceinline__ f4 dec4(V x) { return x; }
+};
+
+template <int M> __device__ __forceinline__ float scl(float x, float v) {
+    if constexpr (M == SCALE_NONE) return x;
+    else if constexpr (M == SCALE_RECIP) return x * v;
+    else return x / v;
+}
+template <int M> __device__ __forceinline__ f4 scl4(f4 x, float v) {
+    if constexpr (M == SCALE_NONE) return x;
+    else if constexpr (M == SCALE_RECIP) return x * v;
+    else return x / v;
+}
+
+template <class T> __device__ __forceinline__ T ld(const T *p) { return *p; }
+template <class T> __device__ __forceinline__ void st(T *p, T v) { *p = v; }
+// write-once outputs that nobody re-reads in this launch: non-temporal
+template <class T> __device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
+
+// --------------------------------------------------------- stream skeleton
+// Element range [0, n) split as [0, head) scalar | [head, head+4*nvec) 4-wide | tail scalar.
+// Op::load(i) issues every global load of the 4 elements at i and returns them;
+// Op::store(i, r) computes and writes.  All U loads are issued before any store.
+template <class Op>
+__global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t nvec, size_t n) {
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    const size_t tail0 = head + 4 * nvec;
+    if (tid < head) op.scalar(tid);
+    if (tid < n - tail0) op.scalar(tail0 + tid);
+    size_t v = tid;
+    for (; v + (kUnroll - 1) * stride < nvec; v += kUnroll * stride) {
+        typename Op::R r[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) r[u] = op.load(head + 4 * (v + u * stride));
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) op.store(head + 4 * (v + u * stride), r[u]);
+    }
+    for (; v < nvec; v += stride) op.store(head + 4 * v, op.load(head + 4 * v));
+}
+
+// scalar-only fallback for operands whose 4-element phases differ
+template <class Op>
+__global__ __launch_bounds__(kBlock) void ew_scalar_kernel(Op op, size_t n) {
+    const size_t stride = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) op.scalar(i);
+}
+
+// ---------------------------------------------------------------- grid ----
+struct DevInfo {
+    int cus = 0;
+};
+DevInfo g_dev[64];
+
+int blocks_per_cu() {
+    static int v = [] {
+        const char *e = getenv("ONO_EW_BLOCKS_PER_CU");
+        int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 8;
+    }();
+    return v;
+}
+
+int device_cus() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (g_dev[dev].cus == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        g_dev[dev].cus = c;
+    }
+    return g_dev[dev].cus;
+}
+
+inline unsigned phase_of(const void *p, size_t esz) {
+    return (unsigned)(((uintptr_t)p / esz) & 3u);
+}
+
+// Launch `op` over n elements.  phases: the 4-element phase of every operand.
+template <class Op>
+hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> phases, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    unsigned ph = *phases.begin();
+    bool same = true;
+    for (unsigned p : phases) same &= (p == ph);
+    const size_t cap = (size_t)device_cus() * (size_t)blocks_per_cu();
+    if (!same) {
+        size_t blocks = (n + kBlock - 1) / kBlock;
+        if (blocks > cap) blocks = cap;
+        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), 0, s, op, n);
+        return hipGetLastError();
+    }
+    size_t head = (4 - ph) & 3u;
+    if (head > n) head = n;
+    size_t nvec = (n - head) / 4;
+    size_t work = nvec > 4 ? nvec : 4; // threads needed (>= head/tail lanes)
+    size_t blocks = (work + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+    if (blocks < 1) blocks = 1;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(ew_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), 0, s, op, head, nvec, n);
+    return hipGetLastError();
+}
+
+// ============================================================== ops =======
+// sum-and-scale over K inputs (K compile-time), left fold in input order
+struct Ptrs {
+    const float *p[ONO_MAX_INPUTS];
+};
+template <int K, int M> struct SumScaleOp {
+    Ptrs in;
+    float *out;
+    float v;
+    typedef f4 R;
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float a = in.p[0][i];
+#pragma unroll
+        for (int j = 1; j < K; j++) a += in.p[j][i];
+        out[i] = scl<M>(a, v);
+    }
+    __device__ __forceinline__ R load(size_t i) const {
+        f4 a = ld((const f4 *)(in.p[0] + i));
+#pragma unroll
+        for (int j = 1; j < K; j++) a += ld((const f4 *)(in.p[j] + i));
+        return a;
+    }
+    __device__ __forceinline__ void store(size_t i, R a) const { st_nt((f4 *)(out + i), scl4<M>(a, v)); }
+};
+
+struct AccOp { // acc += in
+    float *acc;
+    const float *in;
+    struct R { f4 a, b; };
+    __device__ __forceinline__ void scalar(size_t i) const { acc[i] += in[i]; }
+    __device__ __forceinline__ R load(size_t i) const {
+        return R{ld((const f4 *)(acc + i)), ld((const f4 *)(in + i))};
+    }
+    __device__ __forceinline__ void store(size_t i, R r) const { st((f4 *)(acc + i), r.a + r.b); }
+};
+
+template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
+    float *dst;
+    const float *src;
+    float *zero;
+    float v;
+    typedef f4 R;
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float x = src[i];
+        dst[i] = scl<M>(x, v);
+        if (zero) zero[i] = 0.0f;
+    }
+    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(src + i)); }
+    __device__ __forceinline__ void store(size_t i, R x) const {
+        st_nt((f4 *)(dst + i), scl4<M>(x, v));
+        if (zero) st_nt((f4 *)(zero + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+    }
+};
+
+template <class W> struct EncodeOp {
+    typedef typename Wire<W>::V WV;
+    W *out;
+    const float *in;
+    typedef f4 R;
+    __device__ __forceinline__ void scalar(size_t i) const { out[i] = Wire<W>::enc(in[i]); }
+    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(in + i)); }
+    __device__ __forceinline__ void store(size_t i, R x) const { st_nt((WV *)(out + i), Wire<W>::enc4(x)); }
+};
+
+template <class W, int M> struct DecodeScaleOp {
+    typedef typename Wire<W>::V WV;
+    float *out;
+    const W *in;
+    float v;
+    typedef WV R;
+    __device__ __forceinline__ void scalar(size_t i) const { out[i] = scl<M>(Wire<W>::dec(in[i]), v); }
+    __device__ __forceinline__ R load(size_t i) const { return ld((const WV *)(in + i)); }
+    __device__ __forceinline__ void store(size_t i, R h) const {
+        st_nt((f4 *)(out + i), scl4<M>(Wire<W>::dec4(h), v));
+    }
+};
+
+template <class W> struct EncodeZeroOp {
+    typedef typename Wire<W>::V WV;
+    W *out;
+    float *chunk;
+    typedef f4 R;
+    __device__ __forceinline__ void scalar(size_t i) const {
+        out[i] = Wire<W>::enc(chunk[i]);
+        chunk[i] = 0.0f;
+    }
+    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(chunk + i)); }
+    __device__ __forceinline__ void store(size_t i, R x) const {
+        st_nt((WV *)(out + i), Wire<W>::enc4(x));
+        st_nt((f4 *)(chunk + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+    }
+};
+
+template <class W> struct DecodeAddOp {
+    typedef typename Wire<W>::V WV;
+    float *acc;
+    const W *in;
+    struct R { f4 a; WV h; };
+    __device__ __forceinline__ void scalar(size_t i) const { acc[i] += Wire<W>::dec(in[i]); }
+    __device__ __forceinline__ R load(size_t i) const {
+        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+    }
+    __device__ __forceinline__ void store(size_t i, R r) const { st((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
+};
+
+template <class W> struct AddEncodeZeroOp {
+    typedef typename Wire<W>::V WV;
+    W *out;
+    float *acc;
+    const W *in;
+    struct R { f4 a; WV h; };
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float x = acc[i] + Wire<W>::dec(in[i]);
+        out[i] = Wire<W>::enc(x);
+        acc[i] = 0.0f;
+    }
+    __device__ __forceinline__ R load(size_t i) const {
+        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+    }
+    __device__ __forceinline__ void store(size_t i, R r) const {
+        f4 x = r.a + Wire<W>::dec4(r.h);
+        st_nt((WV *)(out + i), Wire<W>::enc4(x));
+        st_nt((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+    }
+};
+
+template <class W, int M> struct AddFinishOp {
+    typedef typename Wire<W>::V WV;
+    float *grad;
+    W *out;
+    float *acc;
+    const W *in;
+    float v;
+    struct R { f4 a; WV h; };
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float x = acc[i] + Wire<W>::dec(in[i]);
+        grad[i] = scl<M>(x, v);
+        out[i] = Wire<W>::enc(x);
+        acc[i] = 0.0f;
+    }
+    __device__ __forceinline__ R load(size_t i) const {
+        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+    }
+    __device__ __forceinline__ void store(size_t i, R r) const {
+        f4 x = r.a + Wire<W>::dec4(r.h);
+        st_nt((f4 *)(grad + i), scl4<M>(x, v));
+        st_nt((WV *)(out + i), Wire<W>::enc4(x));
+        st_nt((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+    }
+};
+
+// ---------------------------------------------------------- synthetic ----
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+struct SynthOp {
+    float *out;
+    uint64_t key;
+    size_t offset;
+    typedef int R;
+    __device__ __forceinline__ float gen(size_t j) const {
+        const uint64_t G = 0x9E3779B97F4A7C15ULL;
+        uint64_t i = (uint64_t)(offset + j);
+        uint64_t h1 = mix64(key + G * (i + 1));
+        uint64_t h2 = mix64(h1 ^ 0xD1B54A32D192ED03ULL);
+        uint32_t cls = (uint32_t)((h1 >> 32) % 100u);
+        uint32_t sign = (uint32_t)(h2 >> 63);
+        if (cls == 0) return __builtin_bit_cast(float, sign << 31);
+        if (cls == 1) {
+            float x = (float)(uint32_t)((h2 >> 8) & 0x3FFFFu) * 0x1p-32f;
+            return sign ? -x : x;
+        }
+        if (cls == 2) {
+            uint32_t e = (uint32_t)((h2 >> 8) % 13u);
+            uint32_t m10 = (uint32_t)((h2 >> 16) & 0x3FFu);
+            return __builtin_bit_cast(float, (sign << 31) | ((e + 117u) << 23) | (m10 << 13) | 0x1000u);
+        }
+        int32_t s4 = (int32_t)(h2 & 0xFFFF) + (int32_t)((h2 >> 16) & 0xFFFF) +
+                     (int32_t)((h2 >> 32) & 0xFFFF) + (int32_t)((h2 >> 48) & 0xFFFF);
+        return (float)(s4 - 131070) * 0x1.3c1a2ep-22f;
+    }
+    __device__ __forceinline__ void scalar(size_t i) const { out[i] = gen(i); }
+    __device__ __forceinline__ R load(size_t) const { return 0; }
+    __device__ __forceinline__ void store(size_t i, R) const {
+        st((f4 *)(out + i), f4{gen(i), gen(i + 1), gen(i + 2), gen(i + 3)});
+    }
+};
+
+// --------------------------------------------------------- optimizers ----
+// BlockingShard::update_params (shard.rs:74-92) fused with the optimizer
+// (gradient_descent.rs:44-47, gradient_descent_with_momentum.rs:56-62, adam.rs:76-91).
+template <int KIND, int M, bool ZERO> struct OptOp {
+    float *g, *w, *v, *s;
+    float lr, mu, b1, omb1, b2, omb2, eps, step, nw;
+    struct R { f4 g, w, v, s; };
+    __device__ __forceinline__ void one(float &gi, float &wi, float &vi, float &si) const {
+        float gg = scl<M>(gi, nw);
+        if constexpr (KIND == ONO_OPT_GD) {
+            wi -= lr * gg;
+        } else if constexpr (KIND == ONO_OPT_MOMENTUM) {
+            vi = (mu * vi) + gg;
+            wi -= lr * vi;
+        } else if constexpr (KIND == ONO_OPT_ADAM) {
+            vi = b1 * vi + omb1 * gg;
+            si = b2 * si + omb2 * (gg * gg);
+            wi -= step * vi / (__builtin_sqrtf(si) + eps);
+        } else {
+            wi += gg;
+        }
+        gi = ZERO ? 0.0f : gg;
+    }
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float gi = g[i], wi = w[i], vi = 0.0f, si = 0.0f;
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) vi = v[i];
+        if constexpr (KIND == ONO_OPT_ADAM) si = s[i];
+        one(gi, wi, vi, si);
+        g[i] = gi;
+        w[i] = wi;
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) v[i] = vi;
+        if constexpr (KIND == ONO_OPT_ADAM) s[i] = si;
+    }
+    __device__ __forceinline__ R load(size_t i) const {
+        R r{};
+        r.g = ld((const f4 *)(g + i));
+        r.w = ld((const f4 *)(w + i));
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) r.v = ld((const f4 *)(v + i));
+        if constexpr (KIND == ONO_OPT_ADAM) r.s = ld((const f4 *)(s + i));
+        return r;
+    }
+    __device__ __forceinline__ void store(size_t i, R r) const {
+        float gg[4] = {r.g.x, r.g.y, r.g.z, r.g.w}, ww[4] = {r.w.x, r.w.y, r.w.z, r.w.w};
+        float vv[4] = {r.v.x, r.v.y, r.v.z, r.v.w}, ss[4] = {r.s.x, r.s.y, r.s.z, r.s.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) one(gg[j], ww[j], vv[j], ss[j]);
+        st((f4 *)(g + i), f4{gg[0], gg[1], gg[2], gg[3]});
+        st((f4 *)(w + i), f4{ww[0], ww[1], ww[2], ww[3]});
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) st((f4 *)(v + i), f4{vv[0], vv[1], vv[2], vv[3]});
+        if constexpr (KIND == ONO_OPT_ADAM) st((f4 *)(s + i), f4{ss[0], ss[1], ss[2], ss[3]});
+    }
+};
+
+template <int K>
+hipError_t sum_scale_k(float *out, const Ptrs &p, size_t n, const Scale &sc, hipStream_t s) {
+    auto ph = {phase_of(out, 4), phase_of(p.p[0], 4), phase_of(p.p[K > 1 ? 1 : 0], 4),
+               phase_of(p.p[K > 2 ? 2 : 0], 4), phase_of(p.p[K > 3 ? 3 : 0], 4),
+               phase_of(p.p[K > 4 ? 4 : 0], 4), phase_of(p.p[K > 5 ? 5 : 0], 4),
+               phase_of(p.p[K > 6 ? 6 : 0], 4), phase_of(p.p[K > 7 ? 7 : 0], 4),
+               phase_of(p.p[K > 8 ? 8 : 0], 4), phase_of(p.p[K > 9 ? 9 : 0], 4),
+               phase_of(p.p[K > 10 ? 10 : 0], 4), phase_of(p.p[K > 11 ? 11 : 0], 4),
+               phase_of(p.p[K > 12 ? 12 : 0], 4), phase_of(p.p[K > 13 ? 13 : 0], 4),
+               phase_of(p.p[K > 14 ? 14 : 0], 4), phase_of(p.p[K > 15 ? 15 : 0], 4)};
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE>{p, out, sc.v}, n, ph, s);
+    case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP>{p, out, sc.v}, n, ph, s);
+    default: return launch_ew(SumScaleOp<K, SCALE_DIV>{p, out, sc.v}, n, ph, s);
+    }
+}
+
+template <int K>
+hipError_t sum_scale_dispatch(int k, float *out, const Ptrs &p, size_t n, const Scale &sc,
+                              hipStream_t s) {
+    if constexpr (K > ONO_MAX_INPUTS) {
+        return hipErrorInvalidValue;
+    } else {
+        if (k == K) return sum_scale_k<K>(out, p, n, sc, s);
+        return sum_scale_dispatch<K + 1>(k, out, p, n, sc, s);
+    }
+}
+
+template <int KIND, bool ZERO>
+hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_, size_t n,
+                    hipStream_t st) {
+    Scale sc = make_scale(o.nworkers);
+    float omb1 = 1.0f - o.beta1, omb2 = 1.0f - o.beta2;
+    auto ph = {phase_of(g, 4), phase_of(w, 4), v ? phase_of(v, 4) : phase_of(g, 4),
+               s_ ? phase_of(s_, 4) : phase_of(g, 4)};
+#define ONO_OPT_OP(MODE) \
+    OptOp<KIND, MODE, ZERO>{g, w, v, s_, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE), n, ph, st);
+    case SCALE_RECIP: return launch_ew(ONO_OPT_OP(SCALE_RECIP), n, ph, st);
+    default: return launch_ew(ONO_OPT_OP(SCALE_DIV), n, ph, st);
+    }
+#undef ONO_OPT_OP
+}
+
+template <class W> unsigned wph(const W *p) { return phase_of(p, sizeof(W)); }
+
+}  // namespace
+
+// ================================================================ API ======
+Scale make_scale(float d) {
+    if (d == 1.0f) return Scale{SCALE_NONE, 1.0f};
+    uint32_t u;
+    memcpy(&u, &d, 4);
+    uint32_t e = (u >> 23) & 0xFF, m = u & 0x7FFFFF;
+    // power of two with an exactly representable normal reciprocal
+    if (m == 0 && e >= 2 && e <= 252) return Scale{SCALE_RECIP, 1.0f / d};
+    return Scale{SCALE_DIV, d};
+}
+
+std::vector<size_t> split_chunks(size_t len, size_t n) {
+    std::vector<size_t> off{0};
+    if (n == 0) return off;
+    size_t base = len / n, rem = len % n, pos = 0;
+    while (pos < len && off.size() < n + 1) {
+        size_t l = base + (rem > 0 ? 1 : 0);
+        if (rem > 0) rem--;
+        pos += l;
+        off.push_back(pos);
+    }
+    return off;
+}
+
+hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n, float divisor,
+                            hipStream_t s) {
+    if (k < 1 || k > ONO_MAX_INPUTS) return hipErrorInvalidValue;
+    Ptrs p{};
+    for (int j = 0; j < k; j++) p.p[j] = ins[j];
+    return sum_scale_dispatch<1>(k, out, p, n, make_scale(divisor), s);
+}
+
+hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s) {
+    return launch_ew(AccOp{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);
+}
+
+hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divisor, float *zero,
+                             hipStream_t s) {
+    Scale sc = make_scale(divisor);
+    auto ph = {phase_of(dst, 4), phase_of(src, 4), zero ? phase_of(zero, 4) : phase_of(dst, 4)};
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_ew(ScaleZeroOp<SCALE_NONE>{dst, src, zero, sc.v}, n, ph, s);
+    case SCALE_RECIP: return launch_ew(ScaleZeroOp<SCALE_RECIP>{dst, src, zero, sc.v}, n, ph, s);
+    default: return launch_ew(ScaleZeroOp<SCALE_DIV>{dst, src, zero, sc.v}, n, ph, s);
+    }
+}
+
+hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
+                        hipStream_t s) {
+    auto mix = [](uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    uint64_t key = mix(seed + 0x9E3779B97F4A7C15ULL * (rank + 1));
+    return launch_ew(SynthOp{out, key, offset}, n, {phase_of(out, 4)}, s);
+}
+
+template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, hipStream_t s) {
+    return launch_ew(EncodeOp<W>{out, in}, n, {wph(out), phase_of(in, 4)}, s);
+}
+template <class W>
+hipError_t launch_decode_scale(float *out, const W *in, size_t n, float divisor, hipStream_t s) {
+    Scale sc = make_scale(divisor);
+    auto ph = {phase_of(out, 4), wph(in)};
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_ew(DecodeScaleOp<W, SCALE_NONE>{out, in, sc.v}, n, ph, s);
+    case SCALE_RECIP: return launch_ew(DecodeScaleOp<W, SCALE_RECIP>{out, in, sc.v}, n, ph, s);
+    default: return launch_ew(DecodeScaleOp<W, SCALE_DIV>{out, in, sc.v}, n, ph, s);
+    }
+}
+template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s) {
+    return launch_ew(EncodeZeroOp<W>{out, chunk}, n, {wph(out), phase_of(chunk, 4)}, s);
+}
+template <class W> hipError_t launch_decode_add(float *acc, const W *in, size_t n, hipStream_t s) {
+    return launch_ew(DecodeAddOp<W>{acc, in}, n, {phase_of(acc, 4), wph(in)}, s);
+}
+template <class W>
+hipError_t launch_add_encode_zero(W *out, float *acc, const W *in, size_t n, hipStream_t s) {
+    return launch_ew(AddEncodeZeroOp<W>{out, acc, in}, n, {wph(out), phase_of(acc, 4), wph(in)}, s);
+}
+template <class W>
+hipError_t launch_add_finish(float *grad, W *out, float *acc, const W *in, size_t n, float divisor,
+                             hipStream_t s) {
+    Scale sc = make_scale(divisor);
+    auto ph = {phase_of(grad, 4), wph(out), phase_of(acc, 4), wph(in)};
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_ew(AddFinishOp<W, SCALE_NONE>{grad, out, acc, in, sc.v}, n, ph, s);
+    case SCALE_RECIP: return launch_ew(AddFinishOp<W, SCALE_RECIP>{grad, out, acc, in, sc.v}, n, ph, s);
+    default: return launch_ew(AddFinishOp<W, SCALE_DIV>{grad, out, acc, in, sc.v}, n, ph, s);
+    }
+}
+
+#define ONO_INST(W)                                                                            \
+    template hipError_t launch_encode<W>(W *, const float *, size_t, hipStream_t);            \
+    template hipError_t launch_decode_scale<W>(float *, const W *, size_t, float, hipStream_t); \
+    template hipError_t launch_encode_zero<W>(W *, float *, size_t, hipStream_t);             \
+    template hipError_t launch_decode_add<W>(float *, const W *, size_t, hipStream_t);        \
+    template hipError_t launch_add_encode_zero<W>(W *, float *, const W *, size_t, hipStream_t); \
+    template hipError_t launch_add_finish<W>(float *, W *, float *, const W *, size_t, float, hipStream_t);
+ONO_INST(uint16_t)
+ONO_INST(float)
+#undef ONO_INST
+
+hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_, size_t n,
+                             bool zero_grad, hipStream_t st) {
+    switch (o.kind) {
+    case ONO_OPT_GD: return zero_grad ? opt_kind<ONO_OPT_GD, true>(o, g, w, v, s_, n, st)
+                                      : opt_kind<ONO_OPT_GD, false>(o, g, w, v, s_, n, st);
+    case ONO_OPT_MOMENTUM: return zero_grad ? opt_kind<ONO_OPT_MOMENTUM, true>(o, g, w, v, s_, n, st)
+                                            : opt_kind<ONO_OPT_MOMENTUM, false>(o, g, w, v, s_, n, st);
+    case ONO_OPT_ADAM: return zero_grad ? opt_kind<ONO_OPT_ADAM, true>(o, g, w, v, s_, n, st)
+                                        : opt_kind<ONO_OPT_ADAM, false>(o, g, w, v, s_, n, st);
+    case ONO_OPT_ADD: return zero_grad ? opt_kind<ONO_OPT_ADD, true>(o, g, w, v, s_, n, st)
+                                       : opt_kind<ONO_OPT_ADD, false>(o, g, w, v, s_, n, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace ono

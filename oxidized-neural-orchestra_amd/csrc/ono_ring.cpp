@@ -1,0 +1,540 @@
+// ono_ring.cpp — the ring all-reduce (WorkerRingManager) over RCCL/xGMI, the
+// co-resident "local ring", and the multi-GPU parameter-server step.
+//
+// Reference: worker/src/middlewares/worker_ring.rs:82-204.  Two wires:
+//   ONO_WIRE_F32 — ncclAllReduce(sum) + one fused kernel (grad /= n,
+//                  residual = 0).  RCCL picks its own ring/channel order.
+//   ONO_WIRE_F16 — the reference's exact hop schedule, point-to-point over
+//                  RCCL (ncclSend/ncclRecv), with fused codec kernels:
+//                    scatter hop 0      encode_zero        (:122, :133)
+//                    scatter hops 1..   add_encode_zero    (:141-143 then :122, :133)
+//                    last scatter hop   add_finish         (:141-143, :166, :191-193, ÷n)
+//                    gather hops        decode_scale       (:200, ÷n) + forward the
+//                                       received bytes (f16(f32(h)) == h)
+// The division by n is applied to the same value the reference divides at
+// the end (param_manager.rs:183-188), so fusing it is bit-identical.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ono_internal.h"
+
+using namespace ono;
+
+#define ONO_NCCL(expr)                                                                        \
+    do {                                                                                      \
+        ncclResult_t ono_r_ = (expr);                                                         \
+        if (ono_r_ != ncclSuccess)                                                            \
+            return set_error(ONO_E_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(ono_r_), \
+                             __FILE__, __LINE__);                                             \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == ONO_UID_BYTES, "ncclUniqueId size");
+
+namespace {
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int kind = 0;  // 0 = library kernel, 1 = collective
+};
+
+// HIP-event timer for the library's own launches (on the launch stream).
+struct Timer {
+    bool on = false;
+    std::vector<EventPair> pending, pool;
+    double kernel_ms = 0, coll_ms = 0;
+    int64_t kernels = 0, colls = 0;
+
+    hipError_t begin(hipStream_t s, EventPair &p, int kind) {
+        if (!pool.empty()) {
+            p = pool.back();
+            pool.pop_back();
+        } else {
+            hipError_t e = hipEventCreate(&p.a);
+            if (e != hipSuccess) return e;
+            e = hipEventCreate(&p.b);
+            if (e != hipSuccess) return e;
+        }
+        p.kind = kind;
+        return hipEventRecord(p.a, s);
+    }
+    hipError_t end(hipStream_t s, EventPair &p) {
+        hipError_t e = hipEventRecord(p.b, s);
+        pending.push_back(p);
+        return e;
+    }
+    hipError_t drain() {
+        for (auto &p : pending) {
+            hipError_t e = hipEventSynchronize(p.b);
+            if (e != hipSuccess) return e;
+            float ms = 0;
+            e = hipEventElapsedTime(&ms, p.a, p.b);
+            if (e != hipSuccess) return e;
+            if (p.kind == 0) { kernel_ms += ms; kernels++; }
+            else { coll_ms += ms; colls++; }
+            pool.push_back(p);
+        }
+        pending.clear();
+        return hipSuccess;
+    }
+    void destroy() {
+        for (auto &p : pending) pool.push_back(p);
+        pending.clear();
+        for (auto &p : pool) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+        pool.clear();
+    }
+};
+
+// RAII device guard: run on the ring's device, restore the caller's afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to chunk starts
+
+}  // namespace
+
+struct ono_ring {
+    int pos = 0, n = 1, device = 0, wire = ONO_WIRE_F32;
+    size_t size = 0;
+    float *grad = nullptr, *residual = nullptr;
+    std::vector<size_t> off;
+    size_t maxc = 0;
+    void *wbuf[2] = {nullptr, nullptr};
+    ncclComm_t comm = nullptr;
+    std::atomic<bool> aborted{false};
+    std::mutex mu;  // serialises host-form calls and the timer
+    float *pin = nullptr;
+    hipStream_t hstream = nullptr;
+    Timer timer;
+};
+
+namespace {
+
+template <class F>
+int timed(ono_ring *r, hipStream_t s, int kind, F &&f) {
+    EventPair p;
+    if (r->timer.on) ONO_HIP(r->timer.begin(s, p, kind));
+    int rc = f();
+    if (rc != ONO_OK) return rc;
+    if (r->timer.on) ONO_HIP(r->timer.end(s, p));
+    return ONO_OK;
+}
+
+#define ONO_K(ring, s, expr) \
+    do { int rc_ = timed(ring, s, 0, [&]() -> int { ONO_HIP(expr); return ONO_OK; }); if (rc_) return rc_; } while (0)
+
+template <class W> ncclDataType_t nccl_type();
+template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
+template <> [[maybe_unused]] ncclDataType_t nccl_type<float>() { return ncclFloat32; }
+
+// One pull_grads round of rank `pos`, exact reference hop order, wire W.
+template <class W>
+int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    const int n = r->n, pos = r->pos;
+    const auto &off = r->off;
+    auto len = [&](int c) { return off[c + 1] - off[c]; };
+    auto slot = [&](int b, int c) { return static_cast<W *>(r->wbuf[b]) + ph(off[c]); };
+    const int next = (pos + 1) % n, prev = (pos + n - 1) % n;
+    const float fn = (float)n;
+    auto xchg = [&](int bs, int cs, int br, int cr) -> int {
+        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        return timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclGroupStart());
+            ONO_NCCL(ncclSend(slot(bs, cs), len(cs), nccl_type<W>(), next, r->comm, s));
+            ONO_NCCL(ncclRecv(slot(br, cr), len(cr), nccl_type<W>(), prev, r->comm, s));
+            ONO_NCCL(ncclGroupEnd());
+            return ONO_OK;
+        });
+    };
+    // ---- scatter: out buffer 0, in buffer 1 ----
+    ONO_K(r, s, launch_encode_zero<W>(slot(0, pos), res + off[pos], len(pos), s));
+    for (int st = 0; st < n - 1; st++) {
+        int cs = ((pos - st) % n + n) % n, cr = ((pos - st - 1) % n + n) % n;
+        int rc = xchg(0, cs, 1, cr);
+        if (rc) return rc;
+        if (st < n - 2)
+            ONO_K(r, s, launch_add_encode_zero<W>(slot(0, cr), res + off[cr], slot(1, cr), len(cr), s));
+        else
+            ONO_K(r, s, launch_add_finish<W>(grad + off[cr], slot(0, cr), res + off[cr], slot(1, cr),
+                                             len(cr), fn, s));
+    }
+    // ---- gather: forward what arrived, alternate the two buffers ----
+    int bo = 0, bi = 1;
+    for (int j = 0; j < n - 1; j++) {
+        int cs = ((pos + 1 - j) % n + n) % n, cr = ((pos - j) % n + n) % n;
+        int rc = xchg(bo, cs, bi, cr);
+        if (rc) return rc;
+        ONO_K(r, s, launch_decode_scale<W>(grad + off[cr], slot(bi, cr), len(cr), fn, s));
+        std::swap(bo, bi);
+    }
+    return ONO_OK;
+}
+
+int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    if (r->n == 1) {  // worker_ring.rs:166-171: grad = residual; residual = 0; no ÷
+        ONO_K(r, s, launch_scale_zero(grad, res, r->size, 1.0f, res, s));
+        return ONO_OK;
+    }
+    if (r->wire == ONO_WIRE_F32) {
+        int rc = timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclAllReduce(res, grad, r->size, ncclFloat32, ncclSum, r->comm, s));
+            return ONO_OK;
+        });
+        if (rc) return rc;
+        ONO_K(r, s, launch_scale_zero(grad, grad, r->size, (float)r->n, res, s));
+        return ONO_OK;
+    }
+    return ring_hops<uint16_t>(r, res, grad, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ono_ring_unique_id(uint8_t uid[ONO_UID_BYTES]) {
+    if (!uid) return set_error(ONO_E_ARG, "uid is NULL");
+    ncclUniqueId id;
+    ONO_NCCL(ncclGetUniqueId(&id));
+    memcpy(uid, &id, sizeof id);
+    return ONO_OK;
+}
+
+int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device,
+                    const uint8_t *uid, int wire) {
+    if (!out) return set_error(ONO_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (nranks < 1 || pos < 0 || pos >= nranks) return set_error(ONO_E_ARG, "pos=%d nranks=%d", pos, nranks);
+    if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
+    if (size < (size_t)nranks)  // reference: chunks[pos] out of bounds (worker_ring.rs:120-122)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, nranks);
+    if (nranks > 1 && !uid) return set_error(ONO_E_ARG, "uid required for nranks > 1");
+    ono_ring *r = new ono_ring();
+    r->pos = pos; r->n = nranks; r->size = size; r->device = device; r->wire = wire;
+    r->off = split_chunks(size, (size_t)nranks);
+    r->maxc = r->off[1] - r->off[0];
+    DeviceGuard g(device);
+    auto fail = [&](int rc) { ono_ring_destroy(r); return rc; };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return fail(hip_error(e, "hipSetDevice", __FILE__, __LINE__));
+    if ((e = hipMalloc((void **)&r->grad, size * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc((void **)&r->residual, size * sizeof(float))) != hipSuccess ||
+        (e = hipMemset(r->grad, 0, size * sizeof(float))) != hipSuccess ||
+        (e = hipMemset(r->residual, 0, size * sizeof(float))) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&r->hstream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(hip_error(e, "bucket allocation", __FILE__, __LINE__));
+    if (wire == ONO_WIRE_F16 && nranks > 1) {
+        for (int b = 0; b < 2; b++)
+            if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(uint16_t))) != hipSuccess)
+                return fail(hip_error(e, "wire buffer allocation", __FILE__, __LINE__));
+    }
+    if (nranks > 1) {
+        ncclUniqueId id;
+        memcpy(&id, uid, sizeof id);
+        ncclResult_t nr = ncclCommInitRank(&r->comm, nranks, id, pos);
+        if (nr != ncclSuccess)
+            return fail(set_error(ONO_E_RCCL, "ncclCommInitRank(rank %d of %d): %s", pos, nranks,
+                                  ncclGetErrorString(nr)));
+    }
+    *out = r;
+    return ONO_OK;
+}
+
+int ono_ring_destroy(ono_ring *r) {
+    if (!r) return ONO_OK;
+    {
+        DeviceGuard g(r->device);
+        if (r->hstream) (void)hipStreamSynchronize(r->hstream);
+        if (r->comm) {
+            if (r->aborted.load()) ncclCommAbort(r->comm);
+            else ncclCommDestroy(r->comm);
+        }
+        r->timer.destroy();
+        (void)hipFree(r->grad);
+        (void)hipFree(r->residual);
+        (void)hipFree(r->wbuf[0]);
+        (void)hipFree(r->wbuf[1]);
+        if (r->pin) (void)hipHostFree(r->pin);
+        if (r->hstream) (void)hipStreamDestroy(r->hstream);
+    }
+    delete r;
+    return ONO_OK;
+}
+
+float *ono_ring_grad(ono_ring *r) { return r ? r->grad : nullptr; }
+float *ono_ring_residual(ono_ring *r) { return r ? r->residual : nullptr; }
+size_t ono_ring_size(const ono_ring *r) { return r ? r->size : 0; }
+
+int ono_ring_acc_residual(ono_ring *r, const float *grad_dev, void *stream) {
+    if (!r || !grad_dev) return set_error(ONO_E_ARG, "NULL argument");
+    DeviceGuard g(r->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ONO_K(r, s, launch_acc(r->residual, grad_dev, r->size, s));
+    return ONO_OK;
+}
+
+int ono_ring_pull_grads(ono_ring *r, void *stream) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    DeviceGuard g(r->device);
+    return pull_grads_impl(r, r->residual, r->grad, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ono_ring_pull_grads_dev(ono_ring *r, float *res, float *grad, size_t n, void *stream) {
+    if (!r || !res || !grad) return set_error(ONO_E_ARG, "NULL argument");
+    if (n != r->size) return set_error(ONO_E_SIZE, "buffer of %zu elements, ring of %zu", n, r->size);
+    if (res == grad) return set_error(ONO_E_ARG, "residual and grad must not alias");
+    DeviceGuard g(r->device);
+    return pull_grads_impl(r, res, grad, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t n) {
+    if (!r || !res_host || !grad_host) return set_error(ONO_E_ARG, "NULL argument");
+    if (n != r->size) return set_error(ONO_E_SIZE, "buffer of %zu elements, ring of %zu", n, r->size);
+    std::lock_guard<std::mutex> lk(r->mu);
+    DeviceGuard g(r->device);
+    hipStream_t s = r->hstream;
+    const size_t bytes = n * sizeof(float);
+    if (!r->pin) ONO_HIP(hipHostMalloc((void **)&r->pin, bytes, hipHostMallocDefault));
+    memcpy(r->pin, res_host, bytes);
+    ONO_HIP(hipMemcpyAsync(r->residual, r->pin, bytes, hipMemcpyHostToDevice, s));
+    int rc = pull_grads_impl(r, r->residual, r->grad, s);
+    if (rc) return rc;
+    ONO_HIP(hipMemcpyAsync(r->pin, r->grad, bytes, hipMemcpyDeviceToHost, s));
+    ONO_HIP(hipStreamSynchronize(s));
+    memcpy(grad_host, r->pin, bytes);
+    memset(res_host, 0, bytes);  // the device residual is exactly zero after pull_grads
+    return ONO_OK;
+}
+
+int ono_ring_allreduce_avg_dev(ono_ring *r, float *buf, size_t n, void *stream) {
+    if (!r || !buf) return set_error(ONO_E_ARG, "NULL argument");
+    if (n != r->size) return set_error(ONO_E_SIZE, "buffer of %zu elements, ring of %zu", n, r->size);
+    DeviceGuard g(r->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    if (r->n == 1) return ONO_OK;
+    if (r->wire == ONO_WIRE_F32) {
+        int rc = timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, r->comm, s));
+            return ONO_OK;
+        });
+        if (rc) return rc;
+        ONO_K(r, s, launch_scale_zero(buf, buf, n, (float)r->n, nullptr, s));
+        return ONO_OK;
+    }
+    int rc = ring_hops<uint16_t>(r, buf, r->grad, s);
+    if (rc) return rc;
+    ONO_HIP(hipMemcpyAsync(buf, r->grad, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return ONO_OK;
+}
+
+int ono_ring_abort(ono_ring *r) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    r->aborted.store(true);
+    return ONO_OK;
+}
+
+int ono_ring_timing_enable(ono_ring *r, int enable) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    DeviceGuard g(r->device);
+    ONO_HIP(r->timer.drain());
+    r->timer.on = enable != 0;
+    r->timer.kernel_ms = r->timer.coll_ms = 0;
+    r->timer.kernels = r->timer.colls = 0;
+    return ONO_OK;
+}
+
+int ono_ring_timing_read(ono_ring *r, double *kernel_ms, int64_t *launches, double *coll_ms,
+                         int64_t *colls) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    DeviceGuard g(r->device);
+    ONO_HIP(r->timer.drain());
+    if (kernel_ms) *kernel_ms = r->timer.kernel_ms;
+    if (launches) *launches = r->timer.kernels;
+    if (coll_ms) *coll_ms = r->timer.coll_ms;
+    if (colls) *colls = r->timer.colls;
+    return ONO_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ local ring ----
+// All ranks of one round on one device, lockstep.  Rank r at scatter step s
+// reads the message rank r-1 produced at step s (parity s%2) and writes its
+// own step-s+1 message (parity (s+1)%2).  The gather is each replica decoding
+// the owner's final message — the exact bytes the reference forwards hop by
+// hop (f16(f32(h)) == h).
+template <class W>
+static int local_ring(float *const *res, float *const *grad, int R, size_t n, hipStream_t s) {
+    auto off = split_chunks(n, (size_t)R);
+    if (off.size() - 1 < (size_t)R)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", n, R);
+    const size_t maxc = off[1] - off[0], slot_elems = maxc + 4;
+    auto len = [&](int c) { return off[c + 1] - off[c]; };
+    W *msg = nullptr;
+    ONO_HIP(hipMallocAsync((void **)&msg, 2 * (size_t)R * slot_elems * sizeof(W), s));
+    auto M = [&](int par, int rank, int c) { return msg + ((size_t)par * R + rank) * slot_elems + ph(off[c]); };
+    const float fn = (float)R;
+    std::vector<int> idx(R);
+    int rc = ONO_OK;
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "local ring kernel", __FILE__, __LINE__); };
+    for (int r = 0; r < R; r++) {
+        idx[r] = r;
+        chk(launch_encode_zero<W>(M(0, r, r), res[r] + off[r], len(r), s));
+    }
+    for (int st = 0; st < R - 1; st++) {
+        for (int r = 0; r < R; r++) {
+            int p = (r + R - 1) % R;
+            int c = (idx[r] + R - 1) % R;
+            const W *in = M(st & 1, p, c);
+            if (st < R - 2) chk(launch_add_encode_zero<W>(M((st + 1) & 1, r, c), res[r] + off[c], in, len(c), s));
+            else chk(launch_add_finish<W>(grad[r] + off[c], M((st + 1) & 1, r, c), res[r] + off[c], in, len(c), fn, s));
+            idx[r] = c;
+        }
+    }
+    const int fin = (R - 1) & 1;
+    for (int r = 0; r < R; r++) {
+        int own = (r + 1) % R;
+        for (int c = 0; c < R; c++) {
+            if (c == own) continue;
+            int owner = (c + R - 1) % R;
+            chk(launch_decode_scale<W>(grad[r] + off[c], M(fin, owner, c), len(c), fn, s));
+        }
+    }
+    hipError_t e = hipFreeAsync(msg, s);
+    if (rc) return rc;
+    ONO_HIP(e);
+    return ONO_OK;
+}
+
+extern "C" {
+
+int ono_local_ring_pull_grads(float *const *residuals, float *const *grads, int nranks,
+                              size_t n, int wire, void *stream) {
+    if (!residuals || !grads || nranks < 1 || nranks > 4096) return set_error(ONO_E_ARG, "bad arguments");
+    for (int r = 0; r < nranks; r++)
+        if (!residuals[r] || !grads[r]) return set_error(ONO_E_ARG, "NULL bucket for rank %d", r);
+    if (n < (size_t)nranks)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", n, nranks);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (nranks == 1) {
+        ONO_HIP(launch_scale_zero(grads[0], residuals[0], n, 1.0f, residuals[0], s));
+        return ONO_OK;
+    }
+    if (wire == ONO_WIRE_F16) return local_ring<uint16_t>(residuals, grads, nranks, n, s);
+    if (wire == ONO_WIRE_F32) return local_ring<float>(residuals, grads, nranks, n, s);
+    return set_error(ONO_E_ARG, "wire=%d", wire);
+}
+
+// --------------------------------------------------- multi-GPU PS mode -----
+// Sharded synchronizer (BlockingStore + BarrierSync across n workers):
+// reduce-scatter of the gradients (store.rs:84-91 accumulate) -> fused
+// ÷nworkers + optimizer on the owned shard (shard.rs:74-92) -> all-gather of
+// the parameters (store.rs:110-124 pull).  Shards are padded to ceil(N/n).
+struct ono_ps {
+    ono_ring *ring = nullptr;
+    size_t nparams = 0, shard = 0, padded = 0;
+    float *gpad = nullptr, *ppad = nullptr, *gshard = nullptr, *v = nullptr, *s = nullptr;
+    OptLaunch opt{};
+    float beta1_t = 1.0f, beta2_t = 1.0f;
+};
+
+int ono_ps_create(ono_ps **out, ono_ring *ring, const float *init, size_t nparams,
+                  const ono_opt_spec *opt) {
+    if (!out || !ring || !init || !opt) return set_error(ONO_E_ARG, "NULL argument");
+    if (opt->kind < ONO_OPT_GD || opt->kind > ONO_OPT_ADD) return set_error(ONO_E_ARG, "optimizer kind %d", opt->kind);
+    *out = nullptr;
+    DeviceGuard g(ring->device);
+    ono_ps *p = new ono_ps();
+    p->ring = ring;
+    p->nparams = nparams;
+    const size_t n = (size_t)ring->n;
+    p->shard = (nparams + n - 1) / n;
+    p->padded = p->shard * n;
+    p->opt = OptLaunch{opt->kind, opt->lr, opt->momentum, opt->beta1, opt->beta2, opt->eps, 0.0f, (float)ring->n};
+    auto fail = [&](hipError_t e) { ono_ps_destroy(p); return hip_error(e, "ps allocation", __FILE__, __LINE__); };
+    hipError_t e;
+    const size_t pb = p->padded * sizeof(float), sb = p->shard * sizeof(float);
+    if ((e = hipMalloc((void **)&p->gpad, pb)) != hipSuccess || (e = hipMemset(p->gpad, 0, pb)) != hipSuccess ||
+        (e = hipMalloc((void **)&p->ppad, pb)) != hipSuccess || (e = hipMemset(p->ppad, 0, pb)) != hipSuccess ||
+        (e = hipMalloc((void **)&p->gshard, sb)) != hipSuccess ||
+        (e = hipMalloc((void **)&p->v, sb)) != hipSuccess || (e = hipMemset(p->v, 0, sb)) != hipSuccess ||
+        (e = hipMalloc((void **)&p->s, sb)) != hipSuccess || (e = hipMemset(p->s, 0, sb)) != hipSuccess)
+        return fail(e);
+    if ((e = hipMemcpy(p->ppad, init, nparams * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    *out = p;
+    return ONO_OK;
+}
+
+int ono_ps_destroy(ono_ps *p) {
+    if (!p) return ONO_OK;
+    {
+        DeviceGuard g(p->ring->device);
+        (void)hipFree(p->gpad); (void)hipFree(p->ppad); (void)hipFree(p->gshard); (void)hipFree(p->v); (void)hipFree(p->s);
+    }
+    delete p;
+    return ONO_OK;
+}
+
+int ono_ps_step(ono_ps *p, const float *grad, float *params, void *stream) {
+    if (!p || !grad || !params) return set_error(ONO_E_ARG, "NULL argument");
+    ono_ring *r = p->ring;
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    DeviceGuard g(r->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t N = p->nparams, C = p->shard;
+    const size_t lo = std::min(N, (size_t)r->pos * C), hi = std::min(N, lo + C);
+    if (p->opt.kind == ONO_OPT_ADAM) {  // adam.rs:76-80 in f32 on the host
+        p->beta1_t *= p->opt.beta1;
+        p->beta2_t *= p->opt.beta2;
+        float bc1 = 1.0f - p->beta1_t, bc2 = 1.0f - p->beta2_t;
+        p->opt.step_size = p->opt.lr * (std::sqrt(bc2) / bc1);
+    }
+    const float *gsrc = grad;
+    if (p->padded != N) {
+        ONO_HIP(hipMemcpyAsync(p->gpad, grad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
+        gsrc = p->gpad;
+    }
+    if (r->n > 1) {
+        int rc = timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclReduceScatter(gsrc, p->gshard, C, ncclFloat32, ncclSum, r->comm, s));
+            return ONO_OK;
+        });
+        if (rc) return rc;
+    } else {
+        ONO_HIP(hipMemcpyAsync(p->gshard, gsrc, C * sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
+    float *wshard = p->ppad + (size_t)r->pos * C;
+    if (hi > lo) ONO_K(r, s, launch_opt_update(p->opt, p->gshard, wshard, p->v, p->s, hi - lo, true, s));
+    if (r->n > 1) {
+        float *dst = p->padded != N ? p->ppad : params;
+        int rc = timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclAllGather(wshard, dst, C, ncclFloat32, r->comm, s));
+            return ONO_OK;
+        });
+        if (rc) return rc;
+        if (dst != params) ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
+    } else {
+        ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
+    return ONO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+"""ctypes binding of libono_reduce.so (include/ono_reduce.h).
+
+The library is the product: every call here goes straight to the HIP/RCCL
+code.  There is no fallback — if the shared object is missing or fails to
+load, importing ono_amd raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libono_reduce.so")
+HEADER = os.path.normpath(os.path.join(HERE, "..", "..", "include", "ono_reduce.h"))
+
+ONO_OK, ONO_E_SIZE, ONO_E_PROTO, ONO_E_HIP, ONO_E_RCCL, ONO_E_ABORTED, ONO_E_ARG, ONO_E_OTHER = range(8)
+WIRE = {"f32": 0, "f16": 1}
+OPT_KIND = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
+STORE_KIND = {"blocking": 0, "wild": 1}
+SYNC_KIND = {"barrier": 0, "nonblocking": 1}
+UID_BYTES = 128
+MAX_INPUTS = 16
+
+
+class OnoError(RuntimeError):
+    """Base error; `.code` is the ono_status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[ono {code}] {msg}")
+        self.code = code
+
+
+class SizeMismatch(OnoError):
+    """ParamServerErr::SizeMismatch (parameter_server/src/storage/error.rs:13-17)."""
+
+
+class InvalidWorkerEvent(OnoError):
+    """io::Error "Received an invalid worker event" (worker_ring.rs:136-138)."""
+
+
+class HipError(OnoError):
+    pass
+
+
+class RcclError(OnoError):
+    pass
+
+
+class Aborted(OnoError):
+    pass
+
+
+class InvalidArgument(OnoError, ValueError):
+    pass
+
+
+_ERR = {ONO_E_SIZE: SizeMismatch, ONO_E_PROTO: InvalidWorkerEvent, ONO_E_HIP: HipError,
+        ONO_E_RCCL: RcclError, ONO_E_ABORTED: Aborted, ONO_E_ARG: InvalidArgument}
+
+
+class OptSpec(C.Structure):
+    _fields_ = [("kind", C.c_int), ("lr", C.c_float), ("momentum", C.c_float),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float)]
+
+
+LEADER_FN = C.CFUNCTYPE(None, C.c_void_p)
+
+_vp, _fp, _sz, _i, _u64 = C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_uint64
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ono_last_error": (C.c_char_p, []),
+    "ono_abi_version": (_i, []),
+    "ono_device_count": (_i, [C.POINTER(C.c_int)]),
+    "ono_sum_scale_f32": (_i, [_fp, C.POINTER(C.c_void_p), _i, _sz, C.c_float, _vp]),
+    "ono_acc_f32": (_i, [_fp, _fp, _sz, _vp]),
+    "ono_scale_zero_f32": (_i, [_fp, _fp, _sz, C.c_float, _fp, _vp]),
+    "ono_f16_encode": (_i, [_vp, _fp, _sz, _vp]),
+    "ono_f16_decode": (_i, [_fp, _vp, _sz, _vp]),
+    "ono_f16_encode_zero": (_i, [_vp, _fp, _sz, _vp]),
+    "ono_f16_decode_add": (_i, [_fp, _vp, _sz, _vp]),
+    "ono_f16_add_encode_zero": (_i, [_vp, _fp, _vp, _sz, _vp]),
+    "ono_f16_decode_scale": (_i, [_fp, _vp, _sz, C.c_float, _vp]),
+    "ono_synth_f32": (_i, [_fp, _sz, _u64, _u64, _sz, _vp]),
+    "ono_ring_unique_id": (_i, [C.c_char_p]),
+    "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
+    "ono_ring_destroy": (_i, [_vp]),
+    "ono_ring_grad": (C.c_void_p, [_vp]),
+    "ono_ring_residual": (C.c_void_p, [_vp]),
+    "ono_ring_size": (_sz, [_vp]),
+    "ono_ring_acc_residual": (_i, [_vp, _fp, _vp]),
+    "ono_ring_pull_grads": (_i, [_vp, _vp]),
+    "ono_ring_pull_grads_dev": (_i, [_vp, _fp, _fp, _sz, _vp]),
+    "ono_ring_pull_grads_host": (_i, [_vp, _fp, _fp, _sz]),
+    "ono_ring_allreduce_avg_dev": (_i, [_vp, _fp, _sz, _vp]),
+    "ono_ring_abort": (_i, [_vp]),
+    "ono_ring_timing_enable": (_i, [_vp, _i]),
+    "ono_ring_timing_read": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                  C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "ono_local_ring_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
+    "ono_store_create": (_i, [C.POINTER(C.c_void_p), _i, _fp, _sz, _sz, _sz, C.POINTER(OptSpec), _i]),
+    "ono_store_destroy": (_i, [_vp]),
+    "ono_store_len": (_sz, [_vp]),
+    "ono_store_accumulate": (_i, [_vp, _fp, _sz]),
+    "ono_store_accumulate_dev": (_i, [_vp, _fp, _sz]),
+    "ono_store_update_params": (_i, [_vp]),
+    "ono_store_pull_params": (_i, [_vp, _fp, _sz]),
+    "ono_store_pull_params_dev": (_i, [_vp, _fp, _sz]),
+    "ono_store_active_idx": (_i, [_vp]),
+    "ono_store_set_updating": (_i, [_vp, _i]),
+    "ono_sync_create": (_i, [C.POINTER(C.c_void_p), _i, _sz]),
+    "ono_sync_clone": (_i, [_vp]),
+    "ono_sync_release": (_i, [_vp]),
+    "ono_sync_step": (_i, [_vp, _vp, _fp, _fp, _sz]),
+    "ono_barrier_create": (_i, [C.POINTER(C.c_void_p), _sz]),
+    "ono_barrier_destroy": (_i, [_vp]),
+    "ono_barrier_wait_with": (_i, [_vp, LEADER_FN, _vp]),
+    "ono_barrier_acquire": (_i, [_vp]),
+    "ono_ps_create": (_i, [C.POINTER(C.c_void_p), _vp, _fp, _sz, C.POINTER(OptSpec)]),
+    "ono_ps_destroy": (_i, [_vp]),
+    "ono_ps_step": (_i, [_vp, _fp, _fp, _vp]),
+}
+
+_lib = None
+
+
+def header_functions() -> list[str]:
+    """Every function declared in include/ono_reduce.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ono_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C oxidized-neural-orchestra_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.ono_abi_version() != 1:
+            raise ImportError("libono_reduce.so ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != ONO_OK:
+        msg = lib().ono_last_error().decode(errors="replace")
+        raise _ERR.get(rc, OnoError)(rc, msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args))

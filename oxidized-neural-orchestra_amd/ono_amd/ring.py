@@ -1,0 +1,136 @@
+"""WorkerRingManager — the ring all-reduce middleware, MI355X-native.
+
+Mirrors worker/src/middlewares/worker_ring.rs (WorkerRingManager::{new,
+build_param_manager, pull_grads}) and the ParamManager view it hands back
+(machine_learning/src/param_manager.rs:97-108, 183-197).  The manager owns the
+`grad` and `residual` buckets (in HBM here); the caller owns `params`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import kernels
+from ._lib import UID_BYTES, WIRE, call, lib
+
+
+class _DevArray:
+    """__cuda_array_interface__ view of library-owned device memory."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def unique_id() -> bytes:
+    """Rank 0 generates the RCCL id; it reaches the other ranks out of band
+    (the reference's ring TCP links, worker/src/builder.rs:272-311)."""
+    buf = C.create_string_buffer(UID_BYTES)
+    call("ono_ring_unique_id", buf)
+    return buf.raw
+
+
+class ParamManager:
+    """The all-reduce ParamManager: one entity over (params, grad, residual)."""
+
+    def __init__(self, params, grad: torch.Tensor, residual: torch.Tensor):
+        self.params, self.grad, self.residual = params, grad, residual
+
+    def acc_residual(self, stream=None) -> None:
+        """residual += grad (param_manager.rs:191-197)."""
+        kernels.acc(self.residual, self.grad, stream)
+
+    def normalize_gradient(self, n: int, stream=None) -> None:
+        """grad /= n (param_manager.rs:183-188)."""
+        kernels.scale_zero(self.grad, self.grad, float(n), None, stream)
+
+    def zero_grad(self) -> None:
+        """param_manager.rs:168-172."""
+        self.grad.zero_()
+
+
+class WorkerRingManager:
+    """worker_ring.rs:10-56.  `addrs` is the worker list (only its length is
+    used: the ring order is the list order); `wire` selects "f32" (RCCL
+    all-reduce) or "f16" (the reference's exact f16 hop schedule)."""
+
+    def __init__(self, pos: int, addrs, size: int, amount_of_layers: int = 1, *,
+                 uid: bytes | None = None, wire: str = "f32", device: int | None = None):
+        nranks = addrs if isinstance(addrs, int) else len(addrs)
+        self.pos, self.nranks, self.size = pos, nranks, size
+        self.amount_of_layers = amount_of_layers
+        self.device = torch.cuda.current_device() if device is None else device
+        self.wire = wire
+        h = C.c_void_p()
+        call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
+        self._h = h
+        dev = f"cuda:{self.device}"
+        self.grad = torch.as_tensor(_DevArray(lib().ono_ring_grad(h), size), device=dev)
+        self.residual = torch.as_tensor(_DevArray(lib().ono_ring_residual(h), size), device=dev)
+
+    # -- worker_ring.rs:65-72
+    def build_param_manager(self, params) -> ParamManager:
+        return ParamManager(params, self.grad, self.residual)
+
+    # -- worker_ring.rs:82-94 (device resident; stream-ordered)
+    def pull_grads(self, params=None, stream=None) -> ParamManager:
+        call("ono_ring_pull_grads", self._h, kernels.stream_handle(stream))
+        return self.build_param_manager(params)
+
+    def pull_grads_dev(self, residual: torch.Tensor, grad: torch.Tensor, stream=None) -> None:
+        call("ono_ring_pull_grads_dev", self._h, kernels.f32_ptr(residual), kernels.f32_ptr(grad),
+             residual.numel(), kernels.stream_handle(stream))
+
+    def pull_grads_host(self, residual: np.ndarray, grad: np.ndarray) -> None:
+        """Host-fed round (the reference's buffers arrive from comms/): H2D,
+        reduce, D2H; residual is zeroed in place, grad receives the average."""
+        for a in (residual, grad):
+            if a.dtype != np.float32 or not a.flags.c_contiguous or a.size != self.size:
+                raise ValueError("expected contiguous float32 host buffers of ring size")
+        call("ono_ring_pull_grads_host", self._h, residual.ctypes.data, grad.ctypes.data, self.size)
+
+    def allreduce_avg_(self, buf: torch.Tensor, stream=None) -> torch.Tensor:
+        call("ono_ring_allreduce_avg_dev", self._h, kernels.f32_ptr(buf), buf.numel(),
+             kernels.stream_handle(stream))
+        return buf
+
+    def acc_residual(self, grad: torch.Tensor, stream=None) -> None:
+        call("ono_ring_acc_residual", self._h, kernels.f32_ptr(grad), kernels.stream_handle(stream))
+
+    def abort(self) -> None:
+        call("ono_ring_abort", self._h)
+
+    def timing(self, enable: bool) -> None:
+        call("ono_ring_timing_enable", self._h, int(enable))
+
+    def timing_read(self) -> dict:
+        km, kn, cm, cn = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
+        call("ono_ring_timing_read", self._h, C.byref(km), C.byref(kn), C.byref(cm), C.byref(cn))
+        return {"kernel_ms": km.value, "kernels": kn.value, "collective_ms": cm.value, "collectives": cn.value}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.grad = self.residual = None
+            call("ono_ring_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def local_ring_pull_grads(residuals: list[torch.Tensor], grads: list[torch.Tensor], wire: str = "f16",
+                          stream=None) -> None:
+    """Every rank of one pull_grads round, co-resident on one device (the
+    device analog of the reference's loopback workers)."""
+    n = len(residuals)
+    size = residuals[0].numel()
+    if len(grads) != n or any(t.numel() != size for t in residuals + grads):
+        raise ValueError("one residual and one grad bucket of equal size per rank")
+    rp = (C.c_void_p * n)(*[kernels.f32_ptr(t) for t in residuals])
+    gp = (C.c_void_p * n)(*[kernels.f32_ptr(t) for t in grads])
+    call("ono_local_ring_pull_grads", rp, gp, n, size, WIRE[wire], kernels.stream_handle(stream))
