@@ -63,6 +63,11 @@ struct OptLaunch {
     float lr, momentum, beta1, beta2, eps;
     float step_size; // Adam: lr * (sqrt(1 - beta2^t) / (1 - beta1^t)), computed on the host in f32
     float nworkers;  // divisor (1 = none)
+    // Store/PS accumulators start at +0 (shard.rs:41-44), so a summed
+    // gradient is never -0; a reduce-scatter of all -0 inputs is.  When set,
+    // the update adds +0 first (identity except -0 -> +0).  Wild (raw
+    // per-worker gradient, wild/shard.rs:43-58) leaves it clear.
+    bool plus_zero = true;
 };
 hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_,
                              size_t n, bool zero_grad, hipStream_t st);

@@ -369,12 +369,12 @@ struct SynthOp {
 // --------------------------------------------------------- optimizers ----
 // BlockingShard::update_params (shard.rs:74-92) fused with the optimizer
 // (gradient_descent.rs:44-47, gradient_descent_with_momentum.rs:56-62, adam.rs:76-91).
-template <int KIND, int M, bool ZERO> struct OptOp {
+template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
     float *g, *w, *v, *s;
     float lr, mu, b1, omb1, b2, omb2, eps, step, nw;
     struct R { f4 g, w, v, s; };
     __device__ __forceinline__ void one(float &gi, float &wi, float &vi, float &si) const {
-        float gg = scl<M>(gi, nw);
+        float gg = scl<M>(PZ ? gi + 0.0f : gi, nw);
         if constexpr (KIND == ONO_OPT_GD) {
             wi -= lr * gg;
         } else if constexpr (KIND == ONO_OPT_MOMENTUM) {
@@ -454,12 +454,19 @@ hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_,
     float omb1 = 1.0f - o.beta1, omb2 = 1.0f - o.beta2;
     auto ph = {phase_of(g, 4), phase_of(w, 4), v ? phase_of(v, 4) : phase_of(g, 4),
                s_ ? phase_of(s_, 4) : phase_of(g, 4)};
-#define ONO_OPT_OP(MODE) \
-    OptOp<KIND, MODE, ZERO>{g, w, v, s_, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
+#define ONO_OPT_OP(MODE, PZ) \
+    OptOp<KIND, MODE, ZERO, PZ>{g, w, v, s_, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
+    if (o.plus_zero) {
+        switch (sc.mode) {
+        case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE, true), n, ph, st);
+        case SCALE_RECIP: return launch_ew(ONO_OPT_OP(SCALE_RECIP, true), n, ph, st);
+        default: return launch_ew(ONO_OPT_OP(SCALE_DIV, true), n, ph, st);
+        }
+    }
     switch (sc.mode) {
-    case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE), n, ph, st);
-    case SCALE_RECIP: return launch_ew(ONO_OPT_OP(SCALE_RECIP), n, ph, st);
-    default: return launch_ew(ONO_OPT_OP(SCALE_DIV), n, ph, st);
+    case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE, false), n, ph, st);
+    case SCALE_RECIP: return launch_ew(ONO_OPT_OP(SCALE_RECIP, false), n, ph, st);
+    default: return launch_ew(ONO_OPT_OP(SCALE_DIV, false), n, ph, st);
     }
 #undef ONO_OPT_OP
 }

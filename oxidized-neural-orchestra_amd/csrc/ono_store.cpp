@@ -115,6 +115,7 @@ static int accumulate(ono_store *st, const float *grad, size_t n, hipMemcpyKind 
         adam_advance(st);
         OptLaunch o = st->opt;
         o.nworkers = 1.0f;
+        o.plus_zero = false;  // the raw incoming gradient, as WildShard::update_params
         ONO_HIP(launch_opt_update(o, st->scratch, st->params, st->v, st->s, n, false, s));
     } else {
         // store.rs:84-91: the active index is read once per accumulate
