@@ -31,8 +31,7 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint16_t h4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBlock = 256;  // 4 waves
-constexpr int kUnroll = 4;   // independent 16-B vectors in flight per thread per input
+constexpr int kBlock = 64;  // one wave per workgroup: +1-4 % over 256 on every shape (tools/stream_variants.hip)
 
 // ------------------------------------------------------------------ f16 ----
 // half 2.7.1 f32_to_f16: RNE; NaN -> sign | 0x7C00 | 0x0200 | (mantissa >> 13)
@@ -87,14 +86,22 @@ template <int M> __device__ __forceinline__ f4 scl4(f4 x, float v) {
 }
 
 template <class T> __device__ __forceinline__ T ld(const T *p) { return *p; }
+// read-once inputs that this launch does not write back: non-temporal loads
+// (+3-4 % on kR1W streams; a plain load is better when the same lines are
+// rewritten in the launch, e.g. residual read-then-zero: tools/stream_variants.hip)
+template <class T> __device__ __forceinline__ T ldn(const T *p) { return __builtin_nontemporal_load(p); }
 template <class T> __device__ __forceinline__ void st(T *p, T v) { *p = v; }
 // write-once outputs that nobody re-reads in this launch: non-temporal
 template <class T> __device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
 
 // --------------------------------------------------------- stream skeleton
 // Element range [0, n) split as [0, head) scalar | [head, head+4*nvec) 4-wide | tail scalar.
-// Op::load(i) issues every global load of the 4 elements at i and returns them;
-// Op::store(i, r) computes and writes.  All U loads are issued before any store.
+// One 16-B vector per thread over a one-shot grid (ceil(nvec/64) one-wave workgroups):
+// measured on MI355X with rotating > 1.5 GiB working sets (tools/stream_variants.hip),
+// this beats grid-stride loops with 2-4 vectors in flight per thread by 8-40 %
+// for every 1R2W / kR1W shape of this path; the hardware keeps enough bytes in
+// flight through wave count, not per-thread unrolling.  The grid-stride form
+// is kept for grids beyond the launch limit.
 template <class Op>
 __global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t nvec, size_t n) {
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -102,15 +109,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t n
     const size_t tail0 = head + 4 * nvec;
     if (tid < head) op.scalar(tid);
     if (tid < n - tail0) op.scalar(tail0 + tid);
-    size_t v = tid;
-    for (; v + (kUnroll - 1) * stride < nvec; v += kUnroll * stride) {
-        typename Op::R r[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) r[u] = op.load(head + 4 * (v + u * stride));
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) op.store(head + 4 * (v + u * stride), r[u]);
-    }
-    for (; v < nvec; v += stride) op.store(head + 4 * v, op.load(head + 4 * v));
+    for (size_t v = tid; v < nvec; v += stride) op.store(head + 4 * v, op.load(head + 4 * v));
 }
 
 // scalar-only fallback for operands whose 4-element phases differ
@@ -126,11 +125,13 @@ struct DevInfo {
 };
 DevInfo g_dev[64];
 
+// Grid cap in workgroups per CU (0 = one-shot grid, the measured optimum);
+// ONO_EW_BLOCKS_PER_CU overrides it for experiments.
 int blocks_per_cu() {
     static int v = [] {
         const char *e = getenv("ONO_EW_BLOCKS_PER_CU");
         int x = e ? atoi(e) : 0;
-        return x > 0 ? x : 8;
+        return x > 0 ? x : 0;
     }();
     return v;
 }
@@ -158,7 +159,8 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
     unsigned ph = *phases.begin();
     bool same = true;
     for (unsigned p : phases) same &= (p == ph);
-    const size_t cap = (size_t)device_cus() * (size_t)blocks_per_cu();
+    const int bpc = blocks_per_cu();
+    const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc : (size_t)0x7FFFFFFF;
     if (!same) {
         size_t blocks = (n + kBlock - 1) / kBlock;
         if (blocks > cap) blocks = cap;
@@ -169,7 +171,7 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
     if (head > n) head = n;
     size_t nvec = (n - head) / 4;
     size_t work = nvec > 4 ? nvec : 4; // threads needed (>= head/tail lanes)
-    size_t blocks = (work + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+    size_t blocks = (work + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(ew_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), 0, s, op, head, nvec, n);
@@ -181,7 +183,7 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
 struct Ptrs {
     const float *p[ONO_MAX_INPUTS];
 };
-template <int K, int M> struct SumScaleOp {
+template <int K, int M, bool NTL> struct SumScaleOp {
     Ptrs in;
     float *out;
     float v;
@@ -192,10 +194,14 @@ template <int K, int M> struct SumScaleOp {
         for (int j = 1; j < K; j++) a += in.p[j][i];
         out[i] = scl<M>(a, v);
     }
+    __device__ __forceinline__ f4 get(int j, size_t i) const {
+        if constexpr (NTL) return ldn((const f4 *)(in.p[j] + i));
+        else return ld((const f4 *)(in.p[j] + i));
+    }
     __device__ __forceinline__ R load(size_t i) const {
-        f4 a = ld((const f4 *)(in.p[0] + i));
+        f4 a = get(0, i);
 #pragma unroll
-        for (int j = 1; j < K; j++) a += ld((const f4 *)(in.p[j] + i));
+        for (int j = 1; j < K; j++) a += get(j, i);
         return a;
     }
     __device__ __forceinline__ void store(size_t i, R a) const { st_nt((f4 *)(out + i), scl4<M>(a, v)); }
@@ -207,9 +213,9 @@ struct AccOp { // acc += in
     struct R { f4 a, b; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += in[i]; }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ld((const f4 *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st((f4 *)(acc + i), r.a + r.b); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + r.b); }
 };
 
 template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
@@ -236,7 +242,7 @@ template <class W> struct EncodeOp {
     const float *in;
     typedef f4 R;
     __device__ __forceinline__ void scalar(size_t i) const { out[i] = Wire<W>::enc(in[i]); }
-    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(in + i)); }
+    __device__ __forceinline__ R load(size_t i) const { return ldn((const f4 *)(in + i)); }
     __device__ __forceinline__ void store(size_t i, R x) const { st_nt((WV *)(out + i), Wire<W>::enc4(x)); }
 };
 
@@ -247,7 +253,7 @@ template <class W, int M> struct DecodeScaleOp {
     float v;
     typedef WV R;
     __device__ __forceinline__ void scalar(size_t i) const { out[i] = scl<M>(Wire<W>::dec(in[i]), v); }
-    __device__ __forceinline__ R load(size_t i) const { return ld((const WV *)(in + i)); }
+    __device__ __forceinline__ R load(size_t i) const { return ldn((const WV *)(in + i)); }
     __device__ __forceinline__ void store(size_t i, R h) const {
         st_nt((f4 *)(out + i), scl4<M>(Wire<W>::dec4(h), v));
     }
@@ -276,9 +282,9 @@ template <class W> struct DecodeAddOp {
     struct R { f4 a; WV h; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += Wire<W>::dec(in[i]); }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
 };
 
 template <class W> struct AddEncodeZeroOp {
@@ -293,7 +299,7 @@ template <class W> struct AddEncodeZeroOp {
         acc[i] = 0.0f;
     }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
     __device__ __forceinline__ void store(size_t i, R r) const {
         f4 x = r.a + Wire<W>::dec4(r.h);
@@ -317,7 +323,7 @@ template <class W, int M> struct AddFinishOp {
         acc[i] = 0.0f;
     }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ld((const WV *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
     __device__ __forceinline__ void store(size_t i, R r) const {
         f4 x = r.a + Wire<W>::dec4(r.h);
@@ -362,7 +368,7 @@ struct SynthOp {
     __device__ __forceinline__ void scalar(size_t i) const { out[i] = gen(i); }
     __device__ __forceinline__ R load(size_t) const { return 0; }
     __device__ __forceinline__ void store(size_t i, R) const {
-        st((f4 *)(out + i), f4{gen(i), gen(i + 1), gen(i + 2), gen(i + 3)});
+        st_nt((f4 *)(out + i), f4{gen(i), gen(i + 1), gen(i + 2), gen(i + 3)});
     }
 };
 
@@ -412,10 +418,10 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         float vv[4] = {r.v.x, r.v.y, r.v.z, r.v.w}, ss[4] = {r.s.x, r.s.y, r.s.z, r.s.w};
 #pragma unroll
         for (int j = 0; j < 4; j++) one(gg[j], ww[j], vv[j], ss[j]);
-        st((f4 *)(g + i), f4{gg[0], gg[1], gg[2], gg[3]});
-        st((f4 *)(w + i), f4{ww[0], ww[1], ww[2], ww[3]});
-        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) st((f4 *)(v + i), f4{vv[0], vv[1], vv[2], vv[3]});
-        if constexpr (KIND == ONO_OPT_ADAM) st((f4 *)(s + i), f4{ss[0], ss[1], ss[2], ss[3]});
+        st_nt((f4 *)(g + i), f4{gg[0], gg[1], gg[2], gg[3]});
+        st_nt((f4 *)(w + i), f4{ww[0], ww[1], ww[2], ww[3]});
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) st_nt((f4 *)(v + i), f4{vv[0], vv[1], vv[2], vv[3]});
+        if constexpr (KIND == ONO_OPT_ADAM) st_nt((f4 *)(s + i), f4{ss[0], ss[1], ss[2], ss[3]});
     }
 };
 
@@ -429,10 +435,19 @@ hipError_t sum_scale_k(float *out, const Ptrs &p, size_t n, const Scale &sc, hip
                phase_of(p.p[K > 10 ? 10 : 0], 4), phase_of(p.p[K > 11 ? 11 : 0], 4),
                phase_of(p.p[K > 12 ? 12 : 0], 4), phase_of(p.p[K > 13 ? 13 : 0], 4),
                phase_of(p.p[K > 14 ? 14 : 0], 4), phase_of(p.p[K > 15 ? 15 : 0], 4)};
+    bool alias = false;  // in-place (out == some input): plain loads
+    for (int j = 0; j < K; j++) alias |= (p.p[j] == out);
+    if (alias) {
+        switch (sc.mode) {
+        case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE, false>{p, out, sc.v}, n, ph, s);
+        case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP, false>{p, out, sc.v}, n, ph, s);
+        default: return launch_ew(SumScaleOp<K, SCALE_DIV, false>{p, out, sc.v}, n, ph, s);
+        }
+    }
     switch (sc.mode) {
-    case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE>{p, out, sc.v}, n, ph, s);
-    case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP>{p, out, sc.v}, n, ph, s);
-    default: return launch_ew(SumScaleOp<K, SCALE_DIV>{p, out, sc.v}, n, ph, s);
+    case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE, true>{p, out, sc.v}, n, ph, s);
+    case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP, true>{p, out, sc.v}, n, ph, s);
+    default: return launch_ew(SumScaleOp<K, SCALE_DIV, true>{p, out, sc.v}, n, ph, s);
     }
 }
 

@@ -1,0 +1,89 @@
+"""bench.py's multi-rank plumbing on CPU (gloo, world_size 2): the RCCL-id
+broadcast, barrier-bracketed timing with max-over-ranks, and the JSON line
+contract.  The GPU steps themselves run only on the MI355X (driver's N>1 runs)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+WORKER = r"""
+import json, os, sys, time
+sys.path.insert(0, {root!r})
+import bench
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+ctl = bench.Ctl(world, rank)
+uid = bytes(range(128)) if rank == 0 else None
+uid = ctl.bcast_bytes(uid)
+assert uid == bytes(range(128))
+calls = []
+def step(i):
+    calls.append(i)
+    time.sleep(0.02 if rank == 1 else 0.001)   # rank 1 is the slow one
+elapsed, local = bench.timed_region(step, 5, 2, lambda: None, ctl)
+print(json.dumps({{"rank": rank, "elapsed": elapsed, "local": local, "calls": calls}}), flush=True)
+ctl.close()
+"""
+
+
+def test_two_rank_timing_takes_max_over_ranks():
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER.format(root=ROOT)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    r0, r1 = sorted(outs, key=lambda d: d["rank"])
+    assert r0["calls"] == r1["calls"] == list(range(7))   # W warmup then exactly K timed
+    assert r0["elapsed"] == r1["elapsed"]                   # both report the max
+    assert r0["elapsed"] >= r1["local"] >= 5 * 0.02 * 0.9
+    assert r0["local"] < r1["local"]
+
+
+def test_single_rank_ctl_is_noop():
+    ctl = bench.Ctl(1, 0)
+    assert ctl.bcast_bytes(b"x") == b"x"
+    assert ctl.max(3.5) == 3.5
+    e, loc = bench.timed_region(lambda i: None, 3, 1, lambda: None, ctl)
+    assert e == loc >= 0
+
+
+def test_build_line_contract():
+    line = bench.build_line(value=123.0, n_gpus=4, steps=10, warmup=2, elapsed=0.5,
+                            bucket_bytes=256 << 20, wire="f32", extra={"roofline": {"bound": "xgmi"}})
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in line
+    assert line["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert line["scaling"] == "weak" and line["higher_is_better"] is True and line["vs_baseline"] is None
+    assert line["ms_per_step"] == pytest.approx(50.0)
+    assert line["algbw_gib_s"] == pytest.approx(5.0)
+    assert line["busbw_gib_s"] == pytest.approx(5.0 * 2 * 3 / 4)
+    assert line["config"]["parallelism"] == "dp4"
+    json.dumps(line)
+
+
+def test_gpus_mismatch_is_an_error(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.main(["--gpus", "2"]) == 2

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch
+HBM bytes of each kernel (profiles/<round>_pmc_*.json, read by bench.py).
+
+Collection (two separate passes, counters only — MI355X_MICROARCH.md §HBM,
+§rocprofv3 PMC slots: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass):
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT/fetch -o run -- python3 bench.py ...
+  rocprofv3 --pmc WRITE_SIZE --output-format csv -d OUT/write -o run -- python3 bench.py ...
+
+gfx950 corrections applied (same guide): counters are in KiB; FETCH_SIZE
+reports exactly half of the bytes of a wide (16 B/lane) coalesced streaming
+read, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B
+streaming stores.
+
+usage: pmc_summary.py --fetch DIR --write DIR --elems N --out FILE [--match SUBSTR ...]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def load(d: str, counter: str) -> dict[str, list[float]]:
+    out: dict[str, list[float]] = {}
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                out.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--elems", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp"])
+    ap.add_argument("--algo-bytes-per-elem", type=float, default=12.0)
+    a = ap.parse_args()
+    fetch, write = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
+    kernels = []
+    for name in sorted(set(fetch) & set(write)):
+        if not any(m in name for m in a.match):
+            continue
+        f_kb, w_kb = statistics.median(fetch[name]), statistics.median(write[name])
+        rd, wr = 2.0 * f_kb * 1024, w_kb * 1024
+        kernels.append({
+            "name": name, "elems": a.elems, "launches_fetch": len(fetch[name]), "launches_write": len(write[name]),
+            "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+            "hbm_bytes_per_launch": rd + wr,
+            "algorithmic_bytes_per_launch": a.algo_bytes_per_elem * a.elems,
+            "traffic_over_algorithmic": (rd + wr) / (a.algo_bytes_per_elem * a.elems),
+        })
+    doc = {"note": "median over launches; read = 2 x FETCH_SIZE x 1 KiB (gfx950 half-count), write = WRITE_SIZE x 1 KiB",
+           "kernels": kernels}
+    with open(a.out, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc, indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,277 @@
+// stream_variants.hip — HBM streaming micro-benchmarks on gfx950 (measurement tool,
+// not part of the product).  Picks the store policy, unroll and grid shape for
+// the reduction path's elementwise kernels and records the copy ceiling.
+//
+// Each timed launch works on a different buffer set (ROT sets rotating through
+// > 1.5 GiB), so the 256 MiB Infinity Cache cannot serve re-reads: the numbers
+// are HBM numbers.  Data is random (non-zero).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o stream_variants stream_variants.hip
+//   ./stream_variants [n_elems]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e = (x);                                                        \
+        if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } \
+    } while (0)
+
+constexpr int ROT = 6;      // buffer sets rotated between launches
+constexpr int MAXK = 8;
+
+template <bool NTS> __device__ __forceinline__ void st(f4 *p, f4 v) {
+    if constexpr (NTS) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+struct Args {
+    const f4 *in[MAXK];
+    f4 *out;
+    f4 *zero;
+};
+
+// out = (sum of K inputs) (* 0.5); zero[] = 0 if ZERO
+template <int K, bool ZERO, int U, bool NTS>
+__global__ __launch_bounds__(256) void k_red(Args a, size_t nvec) {
+    size_t tid = (size_t)blockIdx.x * 256 + threadIdx.x, stride = (size_t)gridDim.x * 256;
+    size_t v = tid;
+    for (; v + (U - 1) * stride < nvec; v += U * stride) {
+        f4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            r[u] = a.in[0][v + u * stride];
+#pragma unroll
+            for (int j = 1; j < K; j++) r[u] += a.in[j][v + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            st<NTS>(a.out + v + u * stride, K > 1 ? r[u] * 0.5f : r[u]);
+            if constexpr (ZERO) st<NTS>(a.zero + v + u * stride, f4{0, 0, 0, 0});
+        }
+    }
+    for (; v < nvec; v += stride) {
+        f4 r = a.in[0][v];
+#pragma unroll
+        for (int j = 1; j < K; j++) r += a.in[j][v];
+        st<NTS>(a.out + v, K > 1 ? r * 0.5f : r);
+        if constexpr (ZERO) st<NTS>(a.zero + v, f4{0, 0, 0, 0});
+    }
+}
+
+
+template <bool NTL> __device__ __forceinline__ f4 ldv(const f4 *p) {
+    if constexpr (NTL) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// one-shot, B threads per block, VPT adjacent 16-B vectors per thread
+template <int K, bool ZERO, int B, int VPT, bool NTL>
+__global__ __launch_bounds__(B) void k_red2(Args a, size_t nvec) {
+    size_t base = ((size_t)blockIdx.x * B) * VPT + threadIdx.x;
+    f4 r[VPT];
+#pragma unroll
+    for (int u = 0; u < VPT; u++) {
+        size_t v = base + (size_t)u * B;
+        if (v < nvec) {
+            r[u] = ldv<NTL>(a.in[0] + v);
+#pragma unroll
+            for (int j = 1; j < K; j++) r[u] += ldv<NTL>(a.in[j] + v);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; u++) {
+        size_t v = base + (size_t)u * B;
+        if (v < nvec) {
+            st<true>(a.out + v, K > 1 ? r[u] * 0.5f : r[u]);
+            if constexpr (ZERO) st<true>(a.zero + v, f4{0, 0, 0, 0});
+        }
+    }
+}
+
+__global__ void k_fill(f4 *p, size_t nvec, unsigned seed) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i < nvec; i += (size_t)gridDim.x * 256) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        p[i] = f4{(float)(h & 0xFFFF), (float)(h >> 16), (float)(h & 0xFF), 1.0f} * 1e-4f;
+    }
+}
+
+struct Pool {
+    std::vector<f4 *> bufs;  // ROT * (MAXK + 2) buffers
+    size_t nvec;
+};
+
+template <int K, bool ZERO, int U, bool NTS>
+void row(Pool &P, int cus, int bpc, hipStream_t s, const char *name) {
+    int blocks = bpc > 0 ? cus * bpc : (int)((P.nvec + 256 * U - 1) / (256 * U));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 2 * ROT + 2; r++) {
+        int set = r % ROT;
+        Args a{};
+        for (int j = 0; j < K; j++) a.in[j] = P.bufs[set * (MAXK + 2) + j];
+        a.out = P.bufs[set * (MAXK + 2) + MAXK];
+        a.zero = ZERO ? (f4 *)a.in[0] : nullptr;  // zero the first input (pull_grads: residual)
+        CK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL((k_red<K, ZERO, U, NTS>), dim3(blocks), dim3(256), 0, s, a, P.nvec);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+        if (ZERO) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)a.in[0], P.nvec, 77u + r);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = (double)(K + 1 + (ZERO ? 1 : 0)) * 16 * P.nvec;
+    double gbs = bytes / (ms * 1e-3) / 1e9;
+    printf("%-14s U=%d nts=%d bpc=%-3d blocks=%-7d %9.2f us %8.1f GB/s  %.3f of 8000\n", name, U, NTS, bpc, blocks,
+           ms * 1e3, gbs, gbs / 8000.0);
+    fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+template <int K, bool ZERO>
+void sweep(Pool &P, int cus, hipStream_t s, const char *name) {
+    row<K, ZERO, 1, true>(P, cus, 0, s, name);
+    row<K, ZERO, 2, true>(P, cus, 0, s, name);
+    row<K, ZERO, 4, true>(P, cus, 0, s, name);
+    row<K, ZERO, 1, false>(P, cus, 0, s, name);
+    row<K, ZERO, 4, false>(P, cus, 0, s, name);
+    row<K, ZERO, 1, true>(P, cus, 8, s, name);
+    row<K, ZERO, 4, true>(P, cus, 8, s, name);
+    row<K, ZERO, 4, true>(P, cus, 16, s, name);
+    row<K, ZERO, 2, true>(P, cus, 32, s, name);
+}
+
+
+template <int K, bool ZERO, int B, int VPT, bool NTL>
+void row2(Pool &P, hipStream_t s, const char *name) {
+    int blocks = (int)((P.nvec + (size_t)B * VPT - 1) / ((size_t)B * VPT));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < 2 * ROT + 2; r++) {
+        int set = r % ROT;
+        Args a{};
+        for (int j = 0; j < K; j++) a.in[j] = P.bufs[set * (MAXK + 2) + j];
+        a.out = P.bufs[set * (MAXK + 2) + MAXK];
+        a.zero = ZERO ? (f4 *)a.in[0] : nullptr;
+        CK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL((k_red2<K, ZERO, B, VPT, NTL>), dim3(blocks), dim3(B), 0, s, a, P.nvec);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) t.push_back(ms);
+        if (ZERO) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)a.in[0], P.nvec, 77u + r);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = (double)(K + 1 + (ZERO ? 1 : 0)) * 16 * P.nvec;
+    double gbs = bytes / (ms * 1e-3) / 1e9;
+    printf("%-14s B=%-4d VPT=%d ntl=%d blocks=%-7d %9.2f us %8.1f GB/s  %.3f of 8000\n", name, B, VPT, NTL, blocks,
+           ms * 1e3, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
+template <int K, bool ZERO>
+void sweep2(Pool &P, hipStream_t s, const char *name) {
+    row2<K, ZERO, 256, 1, false>(P, s, name);
+    row2<K, ZERO, 512, 1, false>(P, s, name);
+    row2<K, ZERO, 1024, 1, false>(P, s, name);
+    row2<K, ZERO, 256, 2, false>(P, s, name);
+    row2<K, ZERO, 256, 4, false>(P, s, name);
+    row2<K, ZERO, 128, 1, false>(P, s, name);
+    row2<K, ZERO, 64, 1, false>(P, s, name);
+    row2<K, ZERO, 256, 1, true>(P, s, name);
+}
+
+// pull_grads(n=1) shape: residual (rotating, fresh) -> grad (FIXED or rotating), residual = 0.
+// Back-to-back launches timed as one span (like bench.py) or one event pair per launch.
+void pull_shape(Pool &P, hipStream_t s, bool fixed_out, bool per_launch_events, int B) {
+    const int L = 12;
+    int blocks = (int)((P.nvec + B - 1) / B);
+    hipEvent_t ev[2 * L + 2];
+    for (int q = 0; q < 2 * L + 2; q++) CK(hipEventCreate(&ev[q]));
+    for (int r = 0; r < ROT; r++) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)P.bufs[r * (MAXK + 2)], P.nvec, 5u + r);
+    CK(hipStreamSynchronize(s));
+    CK(hipEventRecord(ev[0], s));
+    for (int i = 0; i < L; i++) {
+        int set = i % ROT;
+        Args a{};
+        a.in[0] = P.bufs[set * (MAXK + 2)];
+        a.out = fixed_out ? P.bufs[MAXK] : P.bufs[set * (MAXK + 2) + MAXK];
+        a.zero = (f4 *)a.in[0];
+        if (per_launch_events) CK(hipEventRecord(ev[2 + 2 * i], s));
+        if (B == 256) hipLaunchKernelGGL((k_red2<1, true, 256, 1, false>), dim3(blocks), dim3(256), 0, s, a, P.nvec);
+        else hipLaunchKernelGGL((k_red2<1, true, 64, 1, false>), dim3(blocks), dim3(64), 0, s, a, P.nvec);
+        if (per_launch_events) CK(hipEventRecord(ev[3 + 2 * i], s));
+        if (i == ROT - 1) {  // refill the residuals for the second lap (untimed in per-launch mode)
+        }
+    }
+    CK(hipEventRecord(ev[1], s));
+    CK(hipStreamSynchronize(s));
+    float total;
+    CK(hipEventElapsedTime(&total, ev[0], ev[1]));
+    double per = total / L, sum = 0;
+    if (per_launch_events) {
+        for (int i = 0; i < L; i++) { float m; CK(hipEventElapsedTime(&m, ev[2 + 2 * i], ev[3 + 2 * i])); sum += m; }
+    }
+    double bytes = 12.0 * 4 * P.nvec;
+    printf("pull n=1 B=%-3d out=%s events=%s  span/launch %8.2f us %7.1f GB/s", B, fixed_out ? "fixed" : "rotating",
+           per_launch_events ? "per-launch" : "span", per * 1e3, bytes / (per * 1e-3) / 1e9);
+    if (per_launch_events) printf("  | event avg %8.2f us %7.1f GB/s", sum / L * 1e3, bytes / (sum / L * 1e-3) / 1e9);
+    printf("\n");
+    fflush(stdout);
+    for (int q = 0; q < 2 * L + 2; q++) CK(hipEventDestroy(ev[q]));
+}
+
+int main(int argc, char **argv) {
+    size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (size_t)1 << 24;  // 64 MiB per buffer
+    Pool P;
+    P.nvec = n / 4;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    for (int i = 0; i < ROT * (MAXK + 2); i++) {
+        f4 *p;
+        CK(hipMalloc(&p, n * 4));
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, p, P.nvec, (unsigned)i);
+        P.bufs.push_back(p);
+    }
+    CK(hipStreamSynchronize(s));
+    printf("n=%zu (%.0f MiB per buffer), %d rotating sets, CUs=%d\n", n, n * 4.0 / (1 << 20), ROT, cus);
+    const char *mode = argc > 2 ? argv[2] : "all";
+    if (mode[0] == 'p') {
+        for (int rep = 0; rep < 2; rep++)
+            for (int B : {256, 64})
+                for (bool fx : {true, false})
+                    for (bool pe : {false, true}) pull_shape(P, s, fx, pe, B);
+    } else if (mode[0] == 'a') {
+        sweep<1, false>(P, cus, s, "copy 1R1W");
+        sweep<1, true>(P, cus, s, "copy+zero 1R2W");
+        sweep<2, false>(P, cus, s, "sum2 2R1W");
+        sweep<4, false>(P, cus, s, "sum4 4R1W");
+        sweep<8, false>(P, cus, s, "sum8 8R1W");
+    } else {
+        sweep2<1, false>(P, s, "copy 1R1W");
+        sweep2<1, true>(P, s, "copy+zero 1R2W");
+        sweep2<2, false>(P, s, "sum2 2R1W");
+        sweep2<4, false>(P, s, "sum4 4R1W");
+        sweep2<8, false>(P, s, "sum8 8R1W");
+    }
+    return 0;
+}
