@@ -58,6 +58,7 @@ def parse_args(argv=None):
     ap.add_argument("--wire", choices=["f32", "f16"], default="f32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-local-reduce", action="store_true")
+    ap.add_argument("--no-host-fed", action="store_true")
     ap.add_argument("--cpu-ranks", type=int, default=2)
     ap.add_argument("--cpu-rounds", type=int, default=3)
     return ap.parse_args(argv)
@@ -243,6 +244,36 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
             **out}
 
 
+def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
+    """PCIe-inclusive pull_grads from host buffers (never
+    `value`): the reference's buckets live in host memory and arrive from
+    comms/.  Registered (page-locked once, DMA in place) and pageable (pinned
+    bounce slots) forms; each round refills the host residual first (untimed)."""
+    import numpy as np
+
+    res = np.empty(elems, np.float32)
+    grad = np.empty(elems, np.float32)
+    src = np.random.default_rng(1).standard_normal(elems, dtype=np.float32) * np.float32(0.01)
+    out = {}
+    for form in ("pageable", "registered"):
+        if form == "registered":
+            ring.register_host(res)
+            ring.register_host(grad)
+        ts = []
+        for r in range(rounds + 1):
+            res[:] = src
+            t0 = time.perf_counter()
+            ring.pull_grads_host(res, grad)
+            if r:
+                ts.append(time.perf_counter() - t0)
+        t = sorted(ts)[len(ts) // 2]
+        out[form] = {"ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 2)}
+    ring.unregister_host(res)
+    ring.unregister_host(grad)
+    return {"workload": "pull_grads_host, 256 MiB host bucket in, 256 MiB host grad out, n = 1 device round trip",
+            "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
+
+
 # ------------------------------------------------------------------- main
 def main(argv=None) -> int:
     args = parse_args(argv)
@@ -330,6 +361,8 @@ def main(argv=None) -> int:
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s"},
         }
 
+    if rank == 0 and world == 1 and not args.no_host_fed:
+        extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
     if rank == 0 and world == 1 and not args.no_local_reduce:
         del residuals
         torch.cuda.empty_cache()

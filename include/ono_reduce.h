@@ -130,8 +130,13 @@ int ono_ring_pull_grads(ono_ring *ring, void *stream);
 int ono_ring_pull_grads_dev(ono_ring *ring, float *residual_dev, float *grad_dev, size_t n,
                             void *stream);
 /* host-fed form (the reference's buffers live in host memory and arrive on
- * TCP): H2D through pinned staging, pull_grads, D2H; blocking.               */
+ * TCP): chunked H2D -> reduce -> D2H pipeline on three streams; blocking.    */
 int ono_ring_pull_grads_host(ono_ring *ring, float *residual_host, float *grad_host, size_t n);
+/* Page-lock long-lived caller buckets (the reference's WorkerRingManager
+ * Vec<f32>s live as long as the manager) so pull_grads_host DMAs them in
+ * place; unregistered buffers are staged through pinned bounce slots.       */
+int ono_ring_register_host(ono_ring *ring, void *ptr, size_t bytes);
+int ono_ring_unregister_host(ono_ring *ring, void *ptr);
 /* in-place averaged all-reduce of a device buffer (buf = sum_r buf_r / n) */
 int ono_ring_allreduce_avg_dev(ono_ring *ring, float *buf_dev, size_t n, void *stream);
 /* Cancellation: makes the in-flight and every later call fail with

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -118,8 +119,12 @@ struct ono_ring {
     ncclComm_t comm = nullptr;
     std::atomic<bool> aborted{false};
     std::mutex mu;  // serialises host-form calls and the timer
-    float *pin = nullptr;
-    hipStream_t hstream = nullptr;
+    // host-fed pipeline (ono_ring_pull_grads_host): H2D on hstream, reduce on
+    // cstream, D2H on dstream; pinned bounce slots for unregistered buffers
+    hipStream_t hstream = nullptr, cstream = nullptr, dstream = nullptr;
+    float *pin_in = nullptr, *pin_out = nullptr;  // kSlots x chunk elements each
+    std::vector<hipEvent_t> ev_h, ev_c, ev_d;
+    std::vector<std::pair<void *, size_t>> registered;  // ono_ring_register_host
     Timer timer;
 };
 
@@ -236,7 +241,9 @@ int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device
         (e = hipMalloc((void **)&r->residual, size * sizeof(float))) != hipSuccess ||
         (e = hipMemset(r->grad, 0, size * sizeof(float))) != hipSuccess ||
         (e = hipMemset(r->residual, 0, size * sizeof(float))) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&r->hstream, hipStreamNonBlocking)) != hipSuccess)
+        (e = hipStreamCreateWithFlags(&r->hstream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&r->cstream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&r->dstream, hipStreamNonBlocking)) != hipSuccess)
         return fail(hip_error(e, "bucket allocation", __FILE__, __LINE__));
     if (wire == ONO_WIRE_F16 && nranks > 1) {
         for (int b = 0; b < 2; b++)
@@ -269,8 +276,15 @@ int ono_ring_destroy(ono_ring *r) {
         (void)hipFree(r->residual);
         (void)hipFree(r->wbuf[0]);
         (void)hipFree(r->wbuf[1]);
-        if (r->pin) (void)hipHostFree(r->pin);
-        if (r->hstream) (void)hipStreamDestroy(r->hstream);
+        for (hipStream_t st : {r->cstream, r->dstream})
+            if (st) (void)hipStreamSynchronize(st);
+        if (r->pin_in) (void)hipHostFree(r->pin_in);
+        if (r->pin_out) (void)hipHostFree(r->pin_out);
+        for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
+        for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
+            for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {r->hstream, r->cstream, r->dstream})
+            if (st) (void)hipStreamDestroy(st);
     }
     delete r;
     return ONO_OK;
@@ -302,22 +316,146 @@ int ono_ring_pull_grads_dev(ono_ring *r, float *res, float *grad, size_t n, void
     return pull_grads_impl(r, res, grad, reinterpret_cast<hipStream_t>(stream));
 }
 
+// ---- host-fed form (buckets arrive from comms/ in host memory)
+// Chunked three-stage pipeline: H2D (hstream) -> reduce (cstream: per-chunk RCCL
+// all-reduce + finalise, or copy+zero at n = 1) -> D2H (dstream), chunks of
+// ONO_HOST_CHUNK_MIB (16 MiB).  Registered caller buffers (ono_ring_register_host)
+// are DMA'd in place; others go through kSlots pinned bounce slots whose CPU
+// copies overlap the DMA of other chunks.  The host residual is zeroed by the
+// CPU as soon as its chunk has left for the device.  The f16 wire runs the
+// exact hop schedule on the whole bucket (chunking would move chunk owners).
+static constexpr int kSlots = 3;
+
+static size_t host_chunk_elems() {
+    static size_t v = [] {
+        const char *e = getenv("ONO_HOST_CHUNK_MIB");
+        long m = e ? atol(e) : 16;
+        return (size_t)(m > 0 ? m : 16) << 18;  // MiB -> f32 elements
+    }();
+    return v;
+}
+
+static bool is_registered(ono_ring *r, const void *p, size_t bytes) {
+    for (auto &reg : r->registered)
+        if ((const char *)p >= (const char *)reg.first &&
+            (const char *)p + bytes <= (const char *)reg.first + reg.second)
+            return true;
+    return false;
+}
+
+static int ensure_events(ono_ring *r, size_t nchunks) {
+    for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
+        while (v->size() < nchunks) {
+            hipEvent_t ev;
+            ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            v->push_back(ev);
+        }
+    return ONO_OK;
+}
+
+// reduce one chunk [lo, lo+len) of the device buckets on cstream
+static int reduce_chunk(ono_ring *r, size_t lo, size_t len) {
+    hipStream_t s = r->cstream;
+    if (r->n == 1) {
+        ONO_HIP(launch_scale_zero(r->grad + lo, r->residual + lo, len, 1.0f, r->residual + lo, s));
+        return ONO_OK;
+    }
+    ONO_NCCL(ncclAllReduce(r->residual + lo, r->grad + lo, len, ncclFloat32, ncclSum, r->comm, s));
+    ONO_HIP(launch_scale_zero(r->grad + lo, r->grad + lo, len, (float)r->n, r->residual + lo, s));
+    return ONO_OK;
+}
+
+extern "C" int ono_ring_register_host(ono_ring *r, void *p, size_t bytes) {
+    if (!r || !p || !bytes) return set_error(ONO_E_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    if (is_registered(r, p, bytes)) return ONO_OK;
+    DeviceGuard g(r->device);
+    ONO_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    r->registered.emplace_back(p, bytes);
+    return ONO_OK;
+}
+
+extern "C" int ono_ring_unregister_host(ono_ring *r, void *p) {
+    if (!r || !p) return set_error(ONO_E_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    DeviceGuard g(r->device);
+    for (size_t i = 0; i < r->registered.size(); i++)
+        if (r->registered[i].first == p) {
+            ONO_HIP(hipHostUnregister(p));
+            r->registered.erase(r->registered.begin() + (long)i);
+            return ONO_OK;
+        }
+    return set_error(ONO_E_ARG, "pointer was not registered");
+}
+
 int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t n) {
     if (!r || !res_host || !grad_host) return set_error(ONO_E_ARG, "NULL argument");
     if (n != r->size) return set_error(ONO_E_SIZE, "buffer of %zu elements, ring of %zu", n, r->size);
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
     std::lock_guard<std::mutex> lk(r->mu);
     DeviceGuard g(r->device);
-    hipStream_t s = r->hstream;
     const size_t bytes = n * sizeof(float);
-    if (!r->pin) ONO_HIP(hipHostMalloc((void **)&r->pin, bytes, hipHostMallocDefault));
-    memcpy(r->pin, res_host, bytes);
-    ONO_HIP(hipMemcpyAsync(r->residual, r->pin, bytes, hipMemcpyHostToDevice, s));
-    int rc = pull_grads_impl(r, r->residual, r->grad, s);
+    const bool reg = is_registered(r, res_host, bytes) && is_registered(r, grad_host, bytes);
+    const size_t CH = host_chunk_elems();
+
+    if (r->wire == ONO_WIRE_F16 && r->n > 1) {  // whole-bucket exact hop schedule
+        ONO_HIP(hipMemcpyAsync(r->residual, res_host, bytes, hipMemcpyHostToDevice, r->cstream));
+        int rc = ring_hops<uint16_t>(r, r->residual, r->grad, r->cstream);
+        if (rc) return rc;
+        ONO_HIP(hipMemcpyAsync(grad_host, r->grad, bytes, hipMemcpyDeviceToHost, r->cstream));
+        ONO_HIP(hipStreamSynchronize(r->cstream));
+        memset(res_host, 0, bytes);
+        return ONO_OK;
+    }
+
+    const size_t nch = (n + CH - 1) / CH;
+    int rc = ensure_events(r, nch);
     if (rc) return rc;
-    ONO_HIP(hipMemcpyAsync(r->pin, r->grad, bytes, hipMemcpyDeviceToHost, s));
-    ONO_HIP(hipStreamSynchronize(s));
-    memcpy(grad_host, r->pin, bytes);
-    memset(res_host, 0, bytes);  // the device residual is exactly zero after pull_grads
+    if (!reg && !r->pin_in) {
+        ONO_HIP(hipHostMalloc((void **)&r->pin_in, kSlots * CH * sizeof(float), hipHostMallocDefault));
+        ONO_HIP(hipHostMalloc((void **)&r->pin_out, kSlots * CH * sizeof(float), hipHostMallocDefault));
+    }
+    auto lo_of = [&](size_t c) { return c * CH; };
+    auto len_of = [&](size_t c) { return std::min(CH, n - c * CH); };
+    auto drain_out = [&](size_t c) -> int {  // bounce path: wait D2H of chunk c, copy to caller
+        ONO_HIP(hipEventSynchronize(r->ev_d[c]));
+        memcpy(grad_host + lo_of(c), r->pin_out + (c % kSlots) * CH, len_of(c) * sizeof(float));
+        return ONO_OK;
+    };
+    for (size_t c = 0; c < nch; c++) {
+        const size_t lo = lo_of(c), len = len_of(c), cb = len * sizeof(float);
+        const float *src = res_host + lo;
+        float *dst = grad_host + lo;
+        if (!reg) {
+            if (c >= (size_t)kSlots && (rc = drain_out(c - kSlots))) return rc;  // slot free again
+            float *slot_in = r->pin_in + (c % kSlots) * CH;
+            memcpy(slot_in, src, cb);
+            src = slot_in;
+            dst = r->pin_out + (c % kSlots) * CH;
+        }
+        ONO_HIP(hipMemcpyAsync(r->residual + lo, src, cb, hipMemcpyHostToDevice, r->hstream));
+        ONO_HIP(hipEventRecord(r->ev_h[c], r->hstream));
+        ONO_HIP(hipStreamWaitEvent(r->cstream, r->ev_h[c], 0));
+        if ((rc = reduce_chunk(r, lo, len))) return rc;
+        ONO_HIP(hipEventRecord(r->ev_c[c], r->cstream));
+        ONO_HIP(hipStreamWaitEvent(r->dstream, r->ev_c[c], 0));
+        ONO_HIP(hipMemcpyAsync(dst, r->grad + lo, cb, hipMemcpyDeviceToHost, r->dstream));
+        ONO_HIP(hipEventRecord(r->ev_d[c], r->dstream));
+        if (!reg) {
+            memset(res_host + lo, 0, cb);  // already copied to the bounce slot
+        } else if (c > 0) {
+            ONO_HIP(hipEventSynchronize(r->ev_h[c - 1]));  // chunk c-1 has reached HBM
+            memset(res_host + lo_of(c - 1), 0, len_of(c - 1) * sizeof(float));
+        }
+    }
+    if (reg) {
+        ONO_HIP(hipEventSynchronize(r->ev_h[nch - 1]));
+        memset(res_host + lo_of(nch - 1), 0, len_of(nch - 1) * sizeof(float));
+        ONO_HIP(hipStreamSynchronize(r->dstream));
+    } else {
+        for (size_t c = nch > (size_t)kSlots ? nch - kSlots : 0; c < nch; c++)
+            if ((rc = drain_out(c))) return rc;
+    }
     return ONO_OK;
 }
 

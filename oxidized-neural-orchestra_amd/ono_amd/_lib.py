@@ -93,6 +93,8 @@ _SIGS = {
     "ono_ring_pull_grads": (_i, [_vp, _vp]),
     "ono_ring_pull_grads_dev": (_i, [_vp, _fp, _fp, _sz, _vp]),
     "ono_ring_pull_grads_host": (_i, [_vp, _fp, _fp, _sz]),
+    "ono_ring_register_host": (_i, [_vp, _vp, _sz]),
+    "ono_ring_unregister_host": (_i, [_vp, _vp]),
     "ono_ring_allreduce_avg_dev": (_i, [_vp, _fp, _sz, _vp]),
     "ono_ring_abort": (_i, [_vp]),
     "ono_ring_timing_enable": (_i, [_vp, _i]),

@@ -91,6 +91,13 @@ class WorkerRingManager:
                 raise ValueError("expected contiguous float32 host buffers of ring size")
         call("ono_ring_pull_grads_host", self._h, residual.ctypes.data, grad.ctypes.data, self.size)
 
+    def register_host(self, a: np.ndarray) -> None:
+        """Page-lock a long-lived host bucket for in-place DMA by pull_grads_host."""
+        call("ono_ring_register_host", self._h, a.ctypes.data, a.nbytes)
+
+    def unregister_host(self, a: np.ndarray) -> None:
+        call("ono_ring_unregister_host", self._h, a.ctypes.data)
+
     def allreduce_avg_(self, buf: torch.Tensor, stream=None) -> torch.Tensor:
         call("ono_ring_allreduce_avg_dev", self._h, kernels.f32_ptr(buf), buf.numel(),
              kernels.stream_handle(stream))

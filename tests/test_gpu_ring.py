@@ -176,3 +176,27 @@ def test_full_size_256mib_local_ring_f16_n8_properties():
 def test_unique_id_roundtrip():
     uid = ono_amd.unique_id()
     assert isinstance(uid, bytes) and len(uid) == 128
+
+
+@pytest.mark.parametrize("register", [False, True])
+@pytest.mark.parametrize("size", [4099, (5 << 20) + 3, (12 << 20) + 7])
+def test_host_fed_pipeline(register, size):
+    """ono_ring_pull_grads_host: chunked H2D -> reduce -> D2H (16 MiB chunks,
+    ragged last chunk), registered in-place DMA and pinned bounce slots."""
+    ring = ono_amd.WorkerRingManager(0, 1, size)
+    x = O.synth(size, SEED, 7)
+    res, grad = x.copy(), np.full(size, 3.0, np.float32)
+    if register:
+        ring.register_host(res)
+        ring.register_host(grad)
+    for _ in range(2):
+        res[:] = x
+        ring.pull_grads_host(res, grad)
+        assert_bitexact(grad, x)
+        assert not res.view(np.uint32).any()
+    if register:
+        ring.unregister_host(res)
+        ring.unregister_host(grad)
+        with pytest.raises(ono_amd.InvalidArgument):
+            ring.unregister_host(res)
+    ring.close()
