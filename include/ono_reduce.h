@@ -137,6 +137,15 @@ int ono_ring_pull_grads_host(ono_ring *ring, float *residual_host, float *grad_h
  * place; unregistered buffers are staged through pinned bounce slots.       */
 int ono_ring_register_host(ono_ring *ring, void *ptr, size_t bytes);
 int ono_ring_unregister_host(ono_ring *ring, void *ptr);
+/* Schedule of the n > 1 exchange (default AUTO: F32 -> ALLREDUCE, F16 -> HOPS).
+ *   ALLREDUCE  ncclAllReduce + fused ÷n / residual reset (f32 wire only)
+ *   HOPS       the reference hop ring (n-1 scatter + n-1 gather hops) over
+ *              ncclSend/ncclRecv, bit-exact for both wires
+ *   DIRECT     all-to-all of chunk slices over every xGMI link at once, the
+ *              owner replays the reference chain in one fused kernel, then an
+ *              all-gather; bit-exact for both wires; n <= ONO_MAX_INPUTS     */
+typedef enum { ONO_ALGO_AUTO = 0, ONO_ALGO_ALLREDUCE = 1, ONO_ALGO_HOPS = 2, ONO_ALGO_DIRECT = 3 } ono_algo;
+int ono_ring_set_algo(ono_ring *ring, int algo);
 /* in-place averaged all-reduce of a device buffer (buf = sum_r buf_r / n) */
 int ono_ring_allreduce_avg_dev(ono_ring *ring, float *buf_dev, size_t n, void *stream);
 /* Cancellation: makes the in-flight and every later call fail with
@@ -155,6 +164,10 @@ int ono_ring_timing_read(ono_ring *ring, double *kernel_ms, int64_t *launches,
  * modelled by on-device f16/f32 message buffers.                            */
 int ono_local_ring_pull_grads(float *const *residuals, float *const *grads, int nranks,
                               size_t n_elems, int wire, void *stream);
+/* the same round with the DIRECT schedule's arithmetic (one fused owner kernel
+ * per chunk reading every rank's slice); nranks <= ONO_MAX_INPUTS          */
+int ono_local_direct_pull_grads(float *const *residuals, float *const *grads, int nranks,
+                                size_t n_elems, int wire, void *stream);
 
 /* ===================================================================== */
 /* Parameter-server store & synchronizer — parameter_server/src/{storage,synchronization} */

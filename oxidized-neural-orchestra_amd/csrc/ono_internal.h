@@ -56,6 +56,14 @@ template <class W> hipError_t launch_add_encode_zero(W *out, float *acc, const W
 template <class W> hipError_t launch_add_finish(float *grad, W *out, float *acc, const W *in,
                                                 size_t n, float divisor, hipStream_t s);
 
+// Chunk owner's reduction of the direct schedule (ono_kernels.hip DirectOp):
+// ins[k] = rank (c+k)'s slice of chunk c (owner's own residual last);
+// grad = chain(ins) / divisor; out = wire(chain) (f16 wire; NULL for f32);
+// zero the last input, or every input when zero_all.
+template <class W>
+hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, size_t n, float divisor,
+                         bool zero_all, hipStream_t s);
+
 // PS shard update (storage/blocking/shard.rs:74-92 + optimization/*.rs), fused:
 //   g /= nworkers (if > 1); optimizer step on w (state v, s); g = 0 when zero_grad
 struct OptLaunch {

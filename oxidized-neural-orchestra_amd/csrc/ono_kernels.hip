@@ -154,11 +154,11 @@ inline unsigned phase_of(const void *p, size_t esz) {
 
 // Launch `op` over n elements.  phases: the 4-element phase of every operand.
 template <class Op>
-hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> phases, hipStream_t s) {
+hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    unsigned ph = *phases.begin();
+    unsigned ph = phases[0];
     bool same = true;
-    for (unsigned p : phases) same &= (p == ph);
+    for (int i = 0; i < nph; i++) same &= (phases[i] == ph);
     const int bpc = blocks_per_cu();
     const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc : (size_t)0x7FFFFFFF;
     if (!same) {
@@ -176,6 +176,11 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
     if (blocks > cap) blocks = cap;
     hipLaunchKernelGGL(ew_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), 0, s, op, head, nvec, n);
     return hipGetLastError();
+}
+
+template <class Op>
+hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> phases, hipStream_t s) {
+    return launch_ew_arr(op, n, phases.begin(), (int)phases.size(), s);
 }
 
 // ============================================================== ops =======
@@ -205,6 +210,63 @@ template <int K, int M, bool NTL> struct SumScaleOp {
         return a;
     }
     __device__ __forceinline__ void store(size_t i, R a) const { st_nt((f4 *)(out + i), scl4<M>(a, v)); }
+};
+
+// The chunk owner's reduction in the direct (all-to-all) schedule.  in[k] is
+// rank (c+k)'s slice of chunk c, k = 0..K-1, the owner's own residual last.
+//   p = in[0];  p = in[k] + wire(p) for k = 1..K-1
+// reproduces the reference's hop chain (worker_ring.rs:122-143: each hop adds
+// the received wire value into the local f32 chunk), wire() being the f16
+// round trip (f16 wire) or the identity (f32 wire).  Then grad = p / d (:166 +
+// :101-105), out = enc(p) for the all-gather (f16 wire only), and the slices
+// that were "sent" are zeroed (:133, :191-193): the own one, or all of them
+// when every rank is co-resident (zall).  Scale mode and zall are uniform
+// run-time flags (uniform branches, no divergence).
+template <int K, class W> struct DirectOp {
+    typedef typename Wire<W>::V WV;
+    Ptrs in;
+    float *grad;
+    W *out;
+    float v;
+    int mode;  // SCALE_RECIP or SCALE_DIV
+    int zall;
+    typedef f4 R;
+    __device__ __forceinline__ float wq(float p) const { return Wire<W>::dec(Wire<W>::enc(p)); }
+    __device__ __forceinline__ f4 wq4(f4 p) const { return Wire<W>::dec4(Wire<W>::enc4(p)); }
+    __device__ __forceinline__ void scalar(size_t i) const {
+        float p = in.p[0][i];
+#pragma unroll
+        for (int k = 1; k < K; k++) p = in.p[k][i] + wq(p);
+        grad[i] = mode == SCALE_RECIP ? p * v : p / v;
+        if constexpr (sizeof(W) == 2) out[i] = Wire<W>::enc(p);
+        if (zall) {
+#pragma unroll
+            for (int k = 0; k < K; k++) const_cast<float *>(in.p[k])[i] = 0.0f;
+        } else {
+            const_cast<float *>(in.p[K - 1])[i] = 0.0f;
+        }
+    }
+    __device__ __forceinline__ f4 get(int k, size_t i) const {
+        if (!zall && k < K - 1) return ldn((const f4 *)(in.p[k] + i));  // received slices: read once
+        return ld((const f4 *)(in.p[k] + i));                          // rewritten (zeroed) below
+    }
+    __device__ __forceinline__ R load(size_t i) const {
+        f4 p = get(0, i);
+#pragma unroll
+        for (int k = 1; k < K; k++) p = get(k, i) + wq4(p);
+        return p;
+    }
+    __device__ __forceinline__ void store(size_t i, R p) const {
+        st_nt((f4 *)(grad + i), mode == SCALE_RECIP ? p * v : p / v);
+        if constexpr (sizeof(W) == 2) st_nt((WV *)(out + i), Wire<W>::enc4(p));
+        const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (zall) {
+#pragma unroll
+            for (int k = 0; k < K; k++) st_nt((f4 *)const_cast<float *>(in.p[k] + i), z);
+        } else {
+            st_nt((f4 *)const_cast<float *>(in.p[K - 1] + i), z);
+        }
+    }
 };
 
 struct AccOp { // acc += in
@@ -488,6 +550,31 @@ hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_,
 
 template <class W> unsigned wph(const W *p) { return phase_of(p, sizeof(W)); }
 
+template <int K, class W>
+hipError_t direct_k(float *grad, W *out, const Ptrs &p, size_t n, const Scale &sc, bool zall,
+                    hipStream_t s) {
+    unsigned ph[ONO_MAX_INPUTS + 2];
+    int c = 0;
+    ph[c++] = phase_of(grad, 4);
+    if (out) ph[c++] = wph(out);
+    for (int k = 0; k < K; k++) ph[c++] = phase_of(p.p[k], 4);
+    // SCALE_NONE (d == 1) runs as a multiply by 1: the identity, -0 and NaN payloads included
+    const int mode = sc.mode == SCALE_DIV ? SCALE_DIV : SCALE_RECIP;
+    DirectOp<K, W> op{p, grad, out, sc.mode == SCALE_NONE ? 1.0f : sc.v, mode, zall ? 1 : 0};
+    return launch_ew_arr(op, n, ph, c, s);
+}
+
+template <int K, class W>
+hipError_t direct_dispatch(int k, float *grad, W *out, const Ptrs &p, size_t n, const Scale &sc,
+                           bool zall, hipStream_t s) {
+    if constexpr (K > ONO_MAX_INPUTS) {
+        return hipErrorInvalidValue;
+    } else {
+        if (k == K) return direct_k<K, W>(grad, out, p, n, sc, zall, s);
+        return direct_dispatch<K + 1, W>(k, grad, out, p, n, sc, zall, s);
+    }
+}
+
 }  // namespace
 
 // ================================================================ API ======
@@ -521,6 +608,19 @@ hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n
     for (int j = 0; j < k; j++) p.p[j] = ins[j];
     return sum_scale_dispatch<1>(k, out, p, n, make_scale(divisor), s);
 }
+
+template <class W>
+hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, size_t n, float divisor,
+                         bool zero_all, hipStream_t s) {
+    if (k < 1 || k > ONO_MAX_INPUTS) return hipErrorInvalidValue;
+    Ptrs p{};
+    for (int j = 0; j < k; j++) p.p[j] = ins[j];
+    return direct_dispatch<1, W>(k, grad, out, p, n, make_scale(divisor), zero_all, s);
+}
+template hipError_t launch_direct<uint16_t>(float *, uint16_t *, const float *const *, int, size_t, float, bool,
+                                            hipStream_t);
+template hipError_t launch_direct<float>(float *, float *, const float *const *, int, size_t, float, bool,
+                                         hipStream_t);
 
 hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s) {
     return launch_ew(AccOp{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);

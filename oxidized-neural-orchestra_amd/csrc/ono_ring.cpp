@@ -115,7 +115,14 @@ struct ono_ring {
     float *grad = nullptr, *residual = nullptr;
     std::vector<size_t> off;
     size_t maxc = 0;
-    void *wbuf[2] = {nullptr, nullptr};
+    void *wbuf[2] = {nullptr, nullptr};  // hop-ring wire buffers, (maxc + 4) x 4 B each
+    int algo = ONO_ALGO_AUTO;
+    // direct schedule: all-to-all receive slots, all-gather staging (f16),
+    // the owner's f16 message; zstream zeroes the residual beside the all-gather
+    float *rbuf = nullptr;
+    uint16_t *gstage = nullptr, *msg = nullptr;
+    hipStream_t zstream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ncclComm_t comm = nullptr;
     std::atomic<bool> aborted{false};
     std::mutex mu;  // serialises host-form calls and the timer
@@ -145,7 +152,7 @@ int timed(ono_ring *r, hipStream_t s, int kind, F &&f) {
 
 template <class W> ncclDataType_t nccl_type();
 template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
-template <> [[maybe_unused]] ncclDataType_t nccl_type<float>() { return ncclFloat32; }
+template <> ncclDataType_t nccl_type<float>() { return ncclFloat32; }
 
 // One pull_grads round of rank `pos`, exact reference hop order, wire W.
 template <class W>
@@ -190,13 +197,106 @@ int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
     return ONO_OK;
 }
 
+// The direct schedule, built for the fully connected xGMI of one node (every
+// GPU pair has its own link): instead of n-1 dependent hops over one link,
+//   1. all-to-all (grouped ncclSend/ncclRecv to every peer): rank q receives
+//      every rank's slice of the chunk it owns, c = q+1 (worker_ring.rs:162-166);
+//   2. one fused kernel on the owner replays the reference chain for chunk c in
+//      the reference order c, c+1, ..., c+n-1 (DirectOp): bit-exact with the
+//      hop ring for both wires at every n; grad[c] = chain / n; own slice zeroed;
+//   3. the rest of the residual is zeroed on a side stream, beside
+//   4. the all-gather of the owned chunk (f32 values, or the f16 message that
+//      the reference forwards hop by hop), decoded and divided on arrival.
+// Bytes per rank on the wire: (n-1)/n (4 + 4) N for f32, (n-1)/n (4 + 2) N for
+// f16 — all links busy at once.
+int alloc_direct(ono_ring *r) {
+    if (r->rbuf) return ONO_OK;
+    const size_t slot = r->maxc + 4;
+    ONO_HIP(hipMalloc((void **)&r->rbuf, (size_t)r->n * slot * sizeof(float)));
+    ONO_HIP(hipMalloc((void **)&r->gstage, (size_t)r->n * slot * sizeof(uint16_t)));
+    ONO_HIP(hipMalloc((void **)&r->msg, slot * sizeof(uint16_t)));
+    ONO_HIP(hipStreamCreateWithFlags(&r->zstream, hipStreamNonBlocking));
+    ONO_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming));
+    ONO_HIP(hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming));
+    return ONO_OK;
+}
+
+template <class W>
+int direct_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    const int n = r->n, pos = r->pos, c = (pos + 1) % n;
+    if (n > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "direct schedule supports up to %d ranks", ONO_MAX_INPUTS);
+    int rc = alloc_direct(r);
+    if (rc) return rc;
+    const auto &off = r->off;
+    auto len = [&](int q) { return off[q + 1] - off[q]; };
+    const size_t slot = r->maxc + 4;
+    constexpr bool f16 = sizeof(W) == 2;
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    rc = timed(r, s, 1, [&]() -> int {  // 1. all-to-all of chunk slices
+        ONO_NCCL(ncclGroupStart());
+        for (int q = 0; q < n; q++) {
+            if (q == pos) continue;
+            const int cq = (q + 1) % n, k = (q - c + n) % n;
+            ONO_NCCL(ncclSend(res + off[cq], len(cq), ncclFloat32, q, r->comm, s));
+            ONO_NCCL(ncclRecv(r->rbuf + (size_t)k * slot + ph(off[c]), len(c), ncclFloat32, q, r->comm, s));
+        }
+        ONO_NCCL(ncclGroupEnd());
+        return ONO_OK;
+    });
+    if (rc) return rc;
+    const float *ins[ONO_MAX_INPUTS];  // 2. the chain, in the reference order
+    for (int k = 0; k < n - 1; k++) ins[k] = r->rbuf + (size_t)k * slot + ph(off[c]);
+    ins[n - 1] = res + off[c];
+    W *out = f16 ? reinterpret_cast<W *>(r->msg + ph(off[c])) : nullptr;
+    ONO_K(r, s, launch_direct<W>(grad + off[c], out, ins, n, len(c), (float)n, false, s));
+    ONO_HIP(hipEventRecord(r->ev_fork, s));  // 3. zero the sent slices beside the all-gather
+    ONO_HIP(hipStreamWaitEvent(r->zstream, r->ev_fork, 0));
+    if (off[c] > 0) ONO_HIP(hipMemsetAsync(res, 0, off[c] * sizeof(float), r->zstream));
+    if (off[c + 1] < r->size)
+        ONO_HIP(hipMemsetAsync(res + off[c + 1], 0, (r->size - off[c + 1]) * sizeof(float), r->zstream));
+    ONO_HIP(hipEventRecord(r->ev_join, r->zstream));
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    rc = timed(r, s, 1, [&]() -> int {  // 4. all-gather of the owned chunk
+        ONO_NCCL(ncclGroupStart());
+        for (int q = 0; q < n; q++) {
+            if (q == pos) continue;
+            const int cq = (q + 1) % n;
+            if (f16) {
+                ONO_NCCL(ncclSend(r->msg + ph(off[c]), len(c), ncclFloat16, q, r->comm, s));
+                ONO_NCCL(ncclRecv(r->gstage + (size_t)q * slot + ph(off[cq]), len(cq), ncclFloat16, q, r->comm, s));
+            } else {
+                ONO_NCCL(ncclSend(grad + off[c], len(c), ncclFloat32, q, r->comm, s));
+                ONO_NCCL(ncclRecv(grad + off[cq], len(cq), ncclFloat32, q, r->comm, s));
+            }
+        }
+        ONO_NCCL(ncclGroupEnd());
+        return ONO_OK;
+    });
+    if (rc) return rc;
+    if (f16)
+        for (int q = 0; q < n; q++) {
+            if (q == pos) continue;
+            const int cq = (q + 1) % n;
+            ONO_K(r, s, launch_decode_scale<uint16_t>(grad + off[cq], r->gstage + (size_t)q * slot + ph(off[cq]),
+                                                      len(cq), (float)n, s));
+        }
+    ONO_HIP(hipStreamWaitEvent(s, r->ev_join, 0));
+    return ONO_OK;
+}
+
+int resolved_algo(const ono_ring *r) {
+    if (r->algo != ONO_ALGO_AUTO) return r->algo;
+    return r->wire == ONO_WIRE_F32 ? ONO_ALGO_ALLREDUCE : ONO_ALGO_HOPS;
+}
+
 int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
     if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
     if (r->n == 1) {  // worker_ring.rs:166-171: grad = residual; residual = 0; no ÷
         ONO_K(r, s, launch_scale_zero(grad, res, r->size, 1.0f, res, s));
         return ONO_OK;
     }
-    if (r->wire == ONO_WIRE_F32) {
+    switch (resolved_algo(r)) {
+    case ONO_ALGO_ALLREDUCE: {
         int rc = timed(r, s, 1, [&]() -> int {
             ONO_NCCL(ncclAllReduce(res, grad, r->size, ncclFloat32, ncclSum, r->comm, s));
             return ONO_OK;
@@ -205,7 +305,13 @@ int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
         ONO_K(r, s, launch_scale_zero(grad, grad, r->size, (float)r->n, res, s));
         return ONO_OK;
     }
-    return ring_hops<uint16_t>(r, res, grad, s);
+    case ONO_ALGO_HOPS:
+        return r->wire == ONO_WIRE_F16 ? ring_hops<uint16_t>(r, res, grad, s) : ring_hops<float>(r, res, grad, s);
+    case ONO_ALGO_DIRECT:
+        return r->wire == ONO_WIRE_F16 ? direct_impl<uint16_t>(r, res, grad, s) : direct_impl<float>(r, res, grad, s);
+    default:
+        return set_error(ONO_E_ARG, "algo %d", r->algo);
+    }
 }
 
 }  // namespace
@@ -245,9 +351,9 @@ int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device
         (e = hipStreamCreateWithFlags(&r->cstream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&r->dstream, hipStreamNonBlocking)) != hipSuccess)
         return fail(hip_error(e, "bucket allocation", __FILE__, __LINE__));
-    if (wire == ONO_WIRE_F16 && nranks > 1) {
+    if (nranks > 1) {  // hop-ring wire buffers, sized for either wire
         for (int b = 0; b < 2; b++)
-            if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(uint16_t))) != hipSuccess)
+            if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(float))) != hipSuccess)
                 return fail(hip_error(e, "wire buffer allocation", __FILE__, __LINE__));
     }
     if (nranks > 1) {
@@ -283,7 +389,13 @@ int ono_ring_destroy(ono_ring *r) {
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);
-        for (hipStream_t st : {r->hstream, r->cstream, r->dstream})
+        if (r->zstream) (void)hipStreamSynchronize(r->zstream);
+        (void)hipFree(r->rbuf);
+        (void)hipFree(r->gstage);
+        (void)hipFree(r->msg);
+        for (hipEvent_t ev : {r->ev_fork, r->ev_join})
+            if (ev) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {r->hstream, r->cstream, r->dstream, r->zstream})
             if (st) (void)hipStreamDestroy(st);
     }
     delete r;
@@ -398,9 +510,9 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const bool reg = is_registered(r, res_host, bytes) && is_registered(r, grad_host, bytes);
     const size_t CH = host_chunk_elems();
 
-    if (r->wire == ONO_WIRE_F16 && r->n > 1) {  // whole-bucket exact hop schedule
+    if (r->n > 1 && resolved_algo(r) != ONO_ALGO_ALLREDUCE) {  // whole-bucket exact schedules
         ONO_HIP(hipMemcpyAsync(r->residual, res_host, bytes, hipMemcpyHostToDevice, r->cstream));
-        int rc = ring_hops<uint16_t>(r, r->residual, r->grad, r->cstream);
+        int rc = pull_grads_impl(r, r->residual, r->grad, r->cstream);
         if (rc) return rc;
         ONO_HIP(hipMemcpyAsync(grad_host, r->grad, bytes, hipMemcpyDeviceToHost, r->cstream));
         ONO_HIP(hipStreamSynchronize(r->cstream));
@@ -466,7 +578,7 @@ int ono_ring_allreduce_avg_dev(ono_ring *r, float *buf, size_t n, void *stream) 
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
     if (r->n == 1) return ONO_OK;
-    if (r->wire == ONO_WIRE_F32) {
+    if (resolved_algo(r) == ONO_ALGO_ALLREDUCE) {
         int rc = timed(r, s, 1, [&]() -> int {
             ONO_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, r->comm, s));
             return ONO_OK;
@@ -475,9 +587,21 @@ int ono_ring_allreduce_avg_dev(ono_ring *r, float *buf, size_t n, void *stream) 
         ONO_K(r, s, launch_scale_zero(buf, buf, n, (float)r->n, nullptr, s));
         return ONO_OK;
     }
-    int rc = ring_hops<uint16_t>(r, buf, r->grad, s);
+    int rc = pull_grads_impl(r, buf, r->grad, s);
     if (rc) return rc;
     ONO_HIP(hipMemcpyAsync(buf, r->grad, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return ONO_OK;
+}
+
+int ono_ring_set_algo(ono_ring *r, int algo) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    if (algo < ONO_ALGO_AUTO || algo > ONO_ALGO_DIRECT) return set_error(ONO_E_ARG, "algo %d", algo);
+    if (algo == ONO_ALGO_ALLREDUCE && r->wire == ONO_WIRE_F16)
+        return set_error(ONO_E_ARG, "an RCCL all-reduce cannot carry the f16 wire semantics");
+    if (algo == ONO_ALGO_DIRECT && r->n > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "direct schedule supports up to %d ranks", ONO_MAX_INPUTS);
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->algo = algo;
     return ONO_OK;
 }
 
@@ -562,7 +686,64 @@ static int local_ring(float *const *res, float *const *grad, int R, size_t n, hi
     return ONO_OK;
 }
 
+// Co-resident direct schedule: for each chunk c the owner's kernel reads all
+// ranks' slices in the reference order straight from HBM (no all-to-all on one
+// device) and zeroes them; replicas then take the owner's f32 value or decode
+// its f16 message.
+template <class W>
+static int local_direct(float *const *res, float *const *grad, int R, size_t n, hipStream_t s) {
+    auto off = split_chunks(n, (size_t)R);
+    if (off.size() - 1 < (size_t)R)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", n, R);
+    constexpr bool f16 = sizeof(W) == 2;
+    const size_t slot = off[1] - off[0] + 4;
+    auto len = [&](int c) { return off[c + 1] - off[c]; };
+    uint16_t *msg = nullptr;
+    if (f16) ONO_HIP(hipMallocAsync((void **)&msg, (size_t)R * slot * sizeof(uint16_t), s));
+    int rc = ONO_OK;
+    auto chk = [&](hipError_t e) { if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "local direct", __FILE__, __LINE__); };
+    for (int c = 0; c < R; c++) {
+        const int owner = (c + R - 1) % R;
+        const float *ins[ONO_MAX_INPUTS];
+        for (int k = 0; k < R; k++) ins[k] = res[(c + k) % R] + off[c];
+        W *out = f16 ? reinterpret_cast<W *>(msg + (size_t)c * slot + ph(off[c])) : nullptr;
+        chk(launch_direct<W>(grad[owner] + off[c], out, ins, R, len(c), (float)R, true, s));
+    }
+    for (int c = 0; c < R; c++) {
+        const int owner = (c + R - 1) % R;
+        for (int r = 0; r < R; r++) {
+            if (r == owner) continue;
+            if (f16)
+                chk(launch_decode_scale<uint16_t>(grad[r] + off[c], msg + (size_t)c * slot + ph(off[c]), len(c),
+                                                  (float)R, s));
+            else
+                chk(hipMemcpyAsync(grad[r] + off[c], grad[owner] + off[c], len(c) * sizeof(float),
+                                   hipMemcpyDeviceToDevice, s));
+        }
+    }
+    if (f16) chk(hipFreeAsync(msg, s));
+    return rc;
+}
+
 extern "C" {
+
+int ono_local_direct_pull_grads(float *const *residuals, float *const *grads, int nranks, size_t n,
+                                int wire, void *stream) {
+    if (!residuals || !grads || nranks < 1 || nranks > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "nranks must be in [1, %d]", ONO_MAX_INPUTS);
+    for (int r = 0; r < nranks; r++)
+        if (!residuals[r] || !grads[r]) return set_error(ONO_E_ARG, "NULL bucket for rank %d", r);
+    if (n < (size_t)nranks)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", n, nranks);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (nranks == 1) {
+        ONO_HIP(launch_scale_zero(grads[0], residuals[0], n, 1.0f, residuals[0], s));
+        return ONO_OK;
+    }
+    if (wire == ONO_WIRE_F16) return local_direct<uint16_t>(residuals, grads, nranks, n, s);
+    if (wire == ONO_WIRE_F32) return local_direct<float>(residuals, grads, nranks, n, s);
+    return set_error(ONO_E_ARG, "wire=%d", wire);
+}
 
 int ono_local_ring_pull_grads(float *const *residuals, float *const *grads, int nranks,
                               size_t n, int wire, void *stream) {

@@ -16,6 +16,7 @@ HEADER = os.path.normpath(os.path.join(HERE, "..", "..", "include", "ono_reduce.
 
 ONO_OK, ONO_E_SIZE, ONO_E_PROTO, ONO_E_HIP, ONO_E_RCCL, ONO_E_ABORTED, ONO_E_ARG, ONO_E_OTHER = range(8)
 WIRE = {"f32": 0, "f16": 1}
+ALGO = {"auto": 0, "allreduce": 1, "hops": 2, "direct": 3}
 OPT_KIND = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
 STORE_KIND = {"blocking": 0, "wild": 1}
 SYNC_KIND = {"barrier": 0, "nonblocking": 1}
@@ -96,11 +97,13 @@ _SIGS = {
     "ono_ring_register_host": (_i, [_vp, _vp, _sz]),
     "ono_ring_unregister_host": (_i, [_vp, _vp]),
     "ono_ring_allreduce_avg_dev": (_i, [_vp, _fp, _sz, _vp]),
+    "ono_ring_set_algo": (_i, [_vp, _i]),
     "ono_ring_abort": (_i, [_vp]),
     "ono_ring_timing_enable": (_i, [_vp, _i]),
     "ono_ring_timing_read": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                   C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ono_local_ring_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
+    "ono_local_direct_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
     "ono_store_create": (_i, [C.POINTER(C.c_void_p), _i, _fp, _sz, _sz, _sz, C.POINTER(OptSpec), _i]),
     "ono_store_destroy": (_i, [_vp]),
     "ono_store_len": (_sz, [_vp]),

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import kernels
-from ._lib import UID_BYTES, WIRE, call, lib
+from ._lib import ALGO, UID_BYTES, WIRE, call, lib
 
 
 class _DevArray:
@@ -57,7 +57,8 @@ class WorkerRingManager:
     all-reduce) or "f16" (the reference's exact f16 hop schedule)."""
 
     def __init__(self, pos: int, addrs, size: int, amount_of_layers: int = 1, *,
-                 uid: bytes | None = None, wire: str = "f32", device: int | None = None):
+                 uid: bytes | None = None, wire: str = "f32", device: int | None = None,
+                 algo: str = "auto"):
         nranks = addrs if isinstance(addrs, int) else len(addrs)
         self.pos, self.nranks, self.size = pos, nranks, size
         self.amount_of_layers = amount_of_layers
@@ -66,6 +67,8 @@ class WorkerRingManager:
         h = C.c_void_p()
         call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
         self._h = h
+        if algo != "auto":
+            self.set_algo(algo)
         dev = f"cuda:{self.device}"
         self.grad = torch.as_tensor(_DevArray(lib().ono_ring_grad(h), size), device=dev)
         self.residual = torch.as_tensor(_DevArray(lib().ono_ring_residual(h), size), device=dev)
@@ -106,6 +109,11 @@ class WorkerRingManager:
     def acc_residual(self, grad: torch.Tensor, stream=None) -> None:
         call("ono_ring_acc_residual", self._h, kernels.f32_ptr(grad), kernels.stream_handle(stream))
 
+    def set_algo(self, algo: str) -> None:
+        """n > 1 exchange schedule: "allreduce" | "hops" | "direct" | "auto"."""
+        call("ono_ring_set_algo", self._h, ALGO[algo])
+        self.algo = algo
+
     def abort(self) -> None:
         call("ono_ring_abort", self._h)
 
@@ -131,13 +139,15 @@ class WorkerRingManager:
 
 
 def local_ring_pull_grads(residuals: list[torch.Tensor], grads: list[torch.Tensor], wire: str = "f16",
-                          stream=None) -> None:
+                          stream=None, algo: str = "hops") -> None:
     """Every rank of one pull_grads round, co-resident on one device (the
-    device analog of the reference's loopback workers)."""
+    device analog of the reference's loopback workers).  algo "hops" runs the
+    reference hop schedule, "direct" the direct schedule's fused owner kernel."""
     n = len(residuals)
     size = residuals[0].numel()
     if len(grads) != n or any(t.numel() != size for t in residuals + grads):
         raise ValueError("one residual and one grad bucket of equal size per rank")
     rp = (C.c_void_p * n)(*[kernels.f32_ptr(t) for t in residuals])
     gp = (C.c_void_p * n)(*[kernels.f32_ptr(t) for t in grads])
-    call("ono_local_ring_pull_grads", rp, gp, n, size, WIRE[wire], kernels.stream_handle(stream))
+    fn = {"hops": "ono_local_ring_pull_grads", "direct": "ono_local_direct_pull_grads"}[algo]
+    call(fn, rp, gp, n, size, WIRE[wire], kernels.stream_handle(stream))

@@ -200,3 +200,71 @@ def test_host_fed_pipeline(register, size):
         with pytest.raises(ono_amd.InvalidArgument):
             ring.unregister_host(res)
     ring.close()
+
+
+def run_local_direct(ins, wire):
+    res = [to_dev(x) for x in ins]
+    grads = [torch.full_like(r, 7.0) for r in res]
+    ono_amd.local_ring_pull_grads(res, grads, wire, algo="direct")
+    return [host(g) for g in grads], [host(r) for r in res]
+
+
+def test_local_direct_golden(golden):
+    """The direct schedule's fused owner kernel (all-to-all order, one pass)
+    reproduces the reference hop ring bit for bit on every golden case."""
+    g = golden("ring")
+    keys = sorted({k.rsplit("_", 1)[0] for k in g.files if k.endswith("_in")})
+    for key in keys:
+        wire = key.rsplit("_", 1)[1]
+        ins = list(g[key + "_in"])
+        grads, res = run_local_direct(ins, wire)
+        for r in range(len(ins)):
+            assert_bitexact(grads[r], g[key + "_grad"][r], f"{key} rank {r}")
+            assert not res[r].view(np.uint32).any()
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 16])
+@pytest.mark.parametrize("length", [109386, 2 ** 18 + 5])
+@pytest.mark.parametrize("wire", ["f16", "f32"])
+def test_local_direct_vs_oracle(n, length, wire):
+    ins = [O.synth(length, SEED + 13, r) for r in range(n)]
+    grads, res = run_local_direct(ins, wire)
+    eg, _ = O.ring_pull_grads(ins, wire)
+    for r in range(n):
+        assert_bitexact(grads[r], eg[r], f"rank {r}")
+        assert not res[r].view(np.uint32).any()
+
+
+def test_local_direct_full_size_f16_n8_equals_hops():
+    """256 MiB per rank, n = 8, ragged: direct == hop schedule bit for bit."""
+    n, n_el = 8, (1 << 26) + 5
+    outs = {}
+    for algo in ("hops", "direct"):
+        res = [torch.empty(n_el, dtype=torch.float32, device=DEV) for _ in range(n)]
+        for r, t in enumerate(res):
+            ono_amd.kernels.synth(t, SEED, r)
+        grads = [torch.empty_like(res[0]) for _ in range(n)]
+        ono_amd.local_ring_pull_grads(res, grads, "f16", algo=algo)
+        torch.cuda.synchronize()
+        for t in res:
+            assert int(torch.count_nonzero(t.view(torch.int32))) == 0
+        outs[algo] = grads
+        del res
+    for r in range(n):
+        assert torch.equal(outs["hops"][r].view(torch.int32), outs["direct"][r].view(torch.int32)), r
+    del outs
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("algo", ["allreduce", "hops", "direct"])
+def test_ring_set_algo_n1(algo):
+    ring = ono_amd.WorkerRingManager(0, 1, 1000, algo=algo)
+    x = O.synth(1000, SEED, 3)
+    ring.residual.copy_(torch.from_numpy(x))
+    ring.pull_grads()
+    assert_bitexact(host(ring.grad), x)
+    ring.close()
+    f16ring = ono_amd.WorkerRingManager(0, 1, 1000, wire="f16")
+    with pytest.raises(ono_amd.InvalidArgument):
+        f16ring.set_algo("allreduce")
+    f16ring.close()
