@@ -34,6 +34,7 @@ import glob
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -56,6 +57,13 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket-mib", type=int, default=256)
     ap.add_argument("--wire", choices=["f32", "f16"], default="f32")
+    ap.add_argument("--algo", choices=["auto", "allreduce", "hops", "direct"], default="auto")
+    ap.add_argument("--alt-schedules", default="direct:f32,direct:f16,hops:f16",
+                    help="N > 1 only: extra schedules measured after the main line (algo:wire,...; '' = none)")
+    ap.add_argument("--alt-timeout", type=float, default=240.0)
+    ap.add_argument("--alt-at-n1", action="store_true", help="exercise the alternative-schedule plumbing at N = 1")
+    ap.add_argument("--no-ps-mode", dest="ps_mode", action="store_false",
+                    help="skip the N > 1 parameter-server (RS + update + AG) measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-local-reduce", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
@@ -292,43 +300,50 @@ def main(argv=None) -> int:
     elems = args.bucket_mib * (1 << 20) // 4
     bucket_bytes = elems * 4
 
-    uid = ono_amd.unique_id() if (world > 1 and rank == 0) else None
-    uid = ctl.bcast_bytes(uid) if world > 1 else None
-    ring = ono_amd.WorkerRingManager(rank, world, elems, uid=uid, wire=args.wire, device=local_rank)
+    def new_ring(wire: str, algo: str):
+        uid = ono_amd.unique_id() if (world > 1 and rank == 0) else None
+        uid = ctl.bcast_bytes(uid) if world > 1 else None
+        return ono_amd.WorkerRingManager(rank, world, elems, uid=uid, wire=wire, device=local_rank, algo=algo)
+
+    ring = new_ring(args.wire, args.algo)
 
     nb = args.warmup + args.steps
     residuals = [torch.empty(elems, dtype=torch.float32, device="cuda") for _ in range(nb)]
-    for i, t in enumerate(residuals):   # a fresh, distinct bucket for every step
-        ono_amd.kernels.synth(t, SEED + i, rank)
     grad = torch.empty(elems, dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()
 
-    def step(i: int) -> None:
-        ring.pull_grads_dev(residuals[i], grad, stream)
+    def refill() -> None:  # a fresh, distinct bucket for every step (untimed)
+        for i, t in enumerate(residuals):
+            ono_amd.kernels.synth(t, SEED + i, rank)
+        torch.cuda.synchronize()
 
-    # Kernel timing on the launch stream.  N = 1: a step is exactly one kernel,
-    # so one HIP event pair around the timed region gives its average launch
-    # duration without per-launch events (which add ~6 % to a 130 us stream,
-    # tools/stream_variants.hip "pull" mode).  N > 1: per-launch events
-    # separate the collective from the finalize kernel.
-    span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    def measure(r) -> tuple[float, dict]:
+        """W + K pull_grads rounds with ring r; (max-over-ranks seconds, timing).
+        N = 1: a step is exactly one kernel, so one HIP event pair around the
+        timed region gives its average launch duration without per-launch
+        events (which add ~6 % to a 130 us stream, tools/stream_variants.hip
+        "pull" mode).  N > 1: per-launch events split collectives and kernels."""
+        refill()
+        span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
 
-    def on_start():
-        if world > 1:
-            ring.timing(True)
-        span[0].record(stream)
+        def on_start():
+            if world > 1:
+                r.timing(True)
+            span[0].record(stream)
 
-    def step_last(i: int) -> None:
-        step(i)
-        if i == args.warmup + args.steps - 1:
-            span[1].record(stream)
+        def step(i: int) -> None:
+            r.pull_grads_dev(residuals[i], grad, stream)
+            if i == nb - 1:
+                span[1].record(stream)
 
-    elapsed, _local = timed_region(step_last, args.steps, args.warmup, torch.cuda.synchronize, ctl,
-                                   on_start=on_start)
-    span_ms = span[0].elapsed_time(span[1])
-    tim = ring.timing_read() if world > 1 else {"kernel_ms": span_ms, "kernels": args.steps}
-    ring.timing(False)
+        el, _ = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl, on_start=on_start)
+        span_ms = span[0].elapsed_time(span[1])
+        tim = (r.timing_read() if world > 1 else
+               {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0})
+        r.timing(False)
+        return el, tim
+
+    elapsed, tim = measure(ring)
 
     extra = {}
     if world == 1:
@@ -347,25 +362,11 @@ def main(argv=None) -> int:
         if pmc:
             extra["roofline"]["traffic_source"] = pmc["source"]
     else:
-        coll_ms = tim["collective_ms"] / max(tim["collectives"], 1)
-        busbw = bucket_bytes * 2 * (world - 1) / world / (coll_ms * 1e-3) / 1e9
-        peak = XGMI_LINK_GBS * (world - 1)
-        kern_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
-        extra["roofline"] = {
-            "bound": "xgmi", "kernel": "RCCL all-reduce (ring over xGMI)" if args.wire == "f32" else "RCCL p2p hops",
-            "achieved": round(busbw, 1), "peak": round(peak, 1), "unit": "GB/s", "frac": round(busbw / peak, 4),
-            "traffic": None, "avg_collective_us": round(coll_ms * 1e3, 2),
-            "peak_note": "busBW vs (N-1) direct xGMI links x 76.8 GB/s per direction (153.6 GB/s bidirectional spec)",
-            "finalize_kernel": {"bound": "hbm", "avg_launch_us": round(kern_ms * 1e3, 2),
-                                "achieved": round(12 * elems / (kern_ms * 1e-3) / 1e9, 1) if kern_ms > 0 else None,
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s"},
-        }
+        extra["roofline"] = xgmi_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo)
 
     if rank == 0 and world == 1 and not args.no_host_fed:
         extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
     if rank == 0 and world == 1 and not args.no_local_reduce:
-        del residuals
-        torch.cuda.empty_cache()
         extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds)
@@ -373,11 +374,96 @@ def main(argv=None) -> int:
     value = world * bucket_bytes * args.steps / elapsed / GIB
     line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
                       bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
+    line["config"]["schedule"] = ring.algo
+
+    # Informational: the other exchange schedules at N > 1 (never `value`).
+    # A watchdog keeps an untested-at-scale schedule from costing the main line.
+    alts = [a.split(":") for a in args.alt_schedules.split(",") if a] if (world > 1 or args.alt_at_n1) else []
+    if alts:
+        line["alt_schedules"] = {}
+
+        def fire():
+            line["alt_schedules"]["error"] = f"watchdog: alternative schedules exceeded {args.alt_timeout:.0f} s"
+            if rank == 0:
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        dog = threading.Timer(args.alt_timeout, fire)
+        dog.daemon = True
+        dog.start()
+        rings = {args.wire: ring}
+        for algo, wire in alts:
+            key = f"{algo}:{wire}"
+            try:
+                if wire not in rings:
+                    rings[wire] = new_ring(wire, "auto")
+                r = rings[wire]
+                r.set_algo(algo)
+                el, t = measure(r)
+                line["alt_schedules"][key] = {
+                    "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
+                    "ms_per_step": round(el / args.steps * 1e3, 4),
+                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo)}
+            except Exception as e:  # recorded, never fatal for the main line
+                line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if args.ps_mode:  # BASELINE config 5: sharded synchronizer, RS + fused GD + AG
+            try:
+                import numpy as np
+                init = np.zeros(elems, np.float32)
+                ps = ono_amd.ShardedParamServer(ring, init, ono_amd.GradientDescent(0.1))
+                params = torch.empty(elems, dtype=torch.float32, device="cuda")
+                refill()
+                ring.timing(False)
+                el, _ = timed_region(lambda i: ps.step(residuals[i], params, stream), args.steps, args.warmup,
+                                     torch.cuda.synchronize, ctl)
+                line["alt_schedules"]["ps:gd"] = {
+                    "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
+                    "ms_per_step": round(el / args.steps * 1e3, 4),
+                    "workload": "ShardedParamServer.step: reduce-scatter(sum) -> fused /n + GD on the owned "
+                                "shard -> all-gather(params), 256 MiB gradient per GPU"}
+                ps.close()
+                del params
+            except Exception as e:
+                line["alt_schedules"]["ps:gd"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        dog.cancel()
+        for w, r in rings.items():
+            if r is not ring:
+                r.close()
+
     ring.close()
     ctl.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0
+
+
+def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: str, algo: str) -> dict:
+    """N > 1: the exchange is xGMI-bound.  achieved = bytes each rank sends per
+    step / the step's collective time (HIP events on the launch stream); peak =
+    the N-1 direct links a rank can drive at once, 76.8 GB/s each per direction.
+    For the RCCL ring all-reduce the bytes are its busBW bytes 2(N-1)/N x bucket."""
+    wb = 2 if wire == "f16" else 4
+    if algo in ("allreduce", "auto") and wire == "f32":
+        bytes_out, colls = 2 * (world - 1) / world * bucket_bytes, 1           # ring all-reduce
+    elif algo == "direct":
+        bytes_out, colls = (world - 1) / world * (bucket_bytes + elems * wb), 2  # all-to-all f32 + all-gather
+    else:
+        bytes_out, colls = 2 * (world - 1) / world * elems * wb, 2 * (world - 1)  # n-1 + n-1 hops
+    n = max(tim["collectives"], 1)
+    step_coll_ms = tim["collective_ms"] * colls / n
+    ach = bytes_out / (step_coll_ms * 1e-3) / 1e9 if step_coll_ms > 0 else None
+    peak = XGMI_LINK_GBS * (world - 1)
+    kern_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
+    return {
+        "bound": "xgmi", "schedule": f"{algo}:{wire}",
+        "achieved": round(ach, 1) if ach else None, "peak": round(peak, 1), "unit": "GB/s",
+        "frac": round(ach / peak, 4) if ach else None, "traffic": None,
+        "wire_bytes_per_rank_per_step": int(bytes_out),
+        "collective_ms_per_step": round(step_coll_ms, 4),
+        "peak_note": "bytes each rank sends per step / collective time, vs (N-1) direct xGMI links x 76.8 GB/s "
+                     "per direction (153.6 GB/s bidirectional spec per link)",
+        "kernel_avg_us": round(kern_ms * 1e3, 2), "kernel_launches": tim["kernels"],
+    }
 
 
 if __name__ == "__main__":

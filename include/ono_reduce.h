@@ -180,6 +180,17 @@ typedef struct {
     float beta1, beta2, eps; /* Adam */
 } ono_opt_spec;
 
+/* The all-reduce consumer (worker/src/workers/all_reduce.rs:126-132):
+ * ParamManager::optimize (param_manager.rs:148-165) + zero_grad (:168-172) +
+ * `optimization_params.copy_from_slice(&params)` as ONE fused kernel:
+ * params = opt(params, grad); grad = 0; params_copy = params (when non-NULL).
+ * The optimizer state (velocity / Adam moments and powers) lives in HBM.     */
+typedef struct ono_optimizer ono_optimizer;
+int ono_optimizer_create(ono_optimizer **out, const ono_opt_spec *opt, size_t n, int device);
+int ono_optimizer_destroy(ono_optimizer *opt);
+int ono_optimizer_step(ono_optimizer *opt, float *params_dev, float *grad_dev, float *params_copy_dev,
+                       size_t n, void *stream);
+
 typedef enum { ONO_STORE_BLOCKING = 0, ONO_STORE_WILD = 1 } ono_store_kind;
 typedef struct ono_store ono_store;
 

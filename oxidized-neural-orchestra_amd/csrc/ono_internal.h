@@ -78,6 +78,6 @@ struct OptLaunch {
     bool plus_zero = true;
 };
 hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_,
-                             size_t n, bool zero_grad, hipStream_t st);
+                             size_t n, bool zero_grad, hipStream_t st, float *w_copy = nullptr);
 
 }  // namespace ono

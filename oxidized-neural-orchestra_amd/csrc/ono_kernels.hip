@@ -6,9 +6,10 @@
 //   * 16-B per lane f32 accesses (global_load_dwordx4 / global_store_dwordx4),
 //     8-B per lane for f16 wire buffers, one 64-lane wave = 1 KiB per f32
 //     instruction, consecutive lanes on consecutive addresses;
-//   * U independent vectors per thread issued before any is consumed (the
-//     loads of all U iterations are in flight together), grid-stride over a
-//     grid capped at a few workgroups per CU (256 CUs, 8 XCDs);
+//   * one vector per thread, one-wave workgroups, a one-shot grid: the
+//     hardware keeps the bytes in flight through wave count (measured, see
+//     the skeleton below and tools/stream_variants.hip);
+//   * non-temporal stores for outputs, non-temporal loads for read-once inputs;
 //   * misaligned chunk starts (split_chunks offsets are arbitrary) are handled
 //     by a <= 3-element scalar head and tail, so the body stays vectorised
 //     whenever all operands share the same 4-element phase;
@@ -439,6 +440,7 @@ struct SynthOp {
 // (gradient_descent.rs:44-47, gradient_descent_with_momentum.rs:56-62, adam.rs:76-91).
 template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
     float *g, *w, *v, *s;
+    float *w2;  // optional copy of the updated parameters (all_reduce.rs:132), may be NULL
     float lr, mu, b1, omb1, b2, omb2, eps, step, nw;
     struct R { f4 g, w, v, s; };
     __device__ __forceinline__ void one(float &gi, float &wi, float &vi, float &si) const {
@@ -464,6 +466,7 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         one(gi, wi, vi, si);
         g[i] = gi;
         w[i] = wi;
+        if (w2) w2[i] = wi;
         if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) v[i] = vi;
         if constexpr (KIND == ONO_OPT_ADAM) s[i] = si;
     }
@@ -482,6 +485,7 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         for (int j = 0; j < 4; j++) one(gg[j], ww[j], vv[j], ss[j]);
         st_nt((f4 *)(g + i), f4{gg[0], gg[1], gg[2], gg[3]});
         st_nt((f4 *)(w + i), f4{ww[0], ww[1], ww[2], ww[3]});
+        if (w2) st_nt((f4 *)(w2 + i), f4{ww[0], ww[1], ww[2], ww[3]});
         if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) st_nt((f4 *)(v + i), f4{vv[0], vv[1], vv[2], vv[3]});
         if constexpr (KIND == ONO_OPT_ADAM) st_nt((f4 *)(s + i), f4{ss[0], ss[1], ss[2], ss[3]});
     }
@@ -525,14 +529,14 @@ hipError_t sum_scale_dispatch(int k, float *out, const Ptrs &p, size_t n, const 
 }
 
 template <int KIND, bool ZERO>
-hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_, size_t n,
+hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_, float *w2, size_t n,
                     hipStream_t st) {
     Scale sc = make_scale(o.nworkers);
     float omb1 = 1.0f - o.beta1, omb2 = 1.0f - o.beta2;
     auto ph = {phase_of(g, 4), phase_of(w, 4), v ? phase_of(v, 4) : phase_of(g, 4),
-               s_ ? phase_of(s_, 4) : phase_of(g, 4)};
+               s_ ? phase_of(s_, 4) : phase_of(g, 4), w2 ? phase_of(w2, 4) : phase_of(g, 4)};
 #define ONO_OPT_OP(MODE, PZ) \
-    OptOp<KIND, MODE, ZERO, PZ>{g, w, v, s_, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
+    OptOp<KIND, MODE, ZERO, PZ>{g, w, v, s_, w2, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
     if (o.plus_zero) {
         switch (sc.mode) {
         case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE, true), n, ph, st);
@@ -695,18 +699,19 @@ ONO_INST(float)
 #undef ONO_INST
 
 hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_, size_t n,
-                             bool zero_grad, hipStream_t st) {
+                             bool zero_grad, hipStream_t st, float *w_copy) {
+#define ONO_OPT_CASE(KIND)                                                                     \
+    case KIND:                                                                                 \
+        return zero_grad ? opt_kind<KIND, true>(o, g, w, v, s_, w_copy, n, st)                 \
+                         : opt_kind<KIND, false>(o, g, w, v, s_, w_copy, n, st);
     switch (o.kind) {
-    case ONO_OPT_GD: return zero_grad ? opt_kind<ONO_OPT_GD, true>(o, g, w, v, s_, n, st)
-                                      : opt_kind<ONO_OPT_GD, false>(o, g, w, v, s_, n, st);
-    case ONO_OPT_MOMENTUM: return zero_grad ? opt_kind<ONO_OPT_MOMENTUM, true>(o, g, w, v, s_, n, st)
-                                            : opt_kind<ONO_OPT_MOMENTUM, false>(o, g, w, v, s_, n, st);
-    case ONO_OPT_ADAM: return zero_grad ? opt_kind<ONO_OPT_ADAM, true>(o, g, w, v, s_, n, st)
-                                        : opt_kind<ONO_OPT_ADAM, false>(o, g, w, v, s_, n, st);
-    case ONO_OPT_ADD: return zero_grad ? opt_kind<ONO_OPT_ADD, true>(o, g, w, v, s_, n, st)
-                                       : opt_kind<ONO_OPT_ADD, false>(o, g, w, v, s_, n, st);
+        ONO_OPT_CASE(ONO_OPT_GD)
+        ONO_OPT_CASE(ONO_OPT_MOMENTUM)
+        ONO_OPT_CASE(ONO_OPT_ADAM)
+        ONO_OPT_CASE(ONO_OPT_ADD)
     default: return hipErrorInvalidValue;
     }
+#undef ONO_OPT_CASE
 }
 
 }  // namespace ono

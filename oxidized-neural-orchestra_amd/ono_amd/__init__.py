@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede the library load; see above)
 from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, OnoError, RcclError,
                    SizeMismatch, header_functions, lib)
 from . import kernels
-from .ring import ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id
+from .ring import DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id
 from .store import (Adam, AddOptimizer, BarrierSync, BlockingStore, DynBarrier, GradientDescent,
                     GradientDescentWithMomentum, NoBlockingSync, WildStore, shard_size_for)
 from .ps import ShardedParamServer
@@ -23,7 +23,7 @@ lib()  # fail loudly at import when the native library is missing
 
 __all__ = [
     "Aborted", "HipError", "InvalidArgument", "InvalidWorkerEvent", "OnoError", "RcclError",
-    "SizeMismatch", "header_functions", "lib", "kernels", "ParamManager", "WorkerRingManager",
+    "SizeMismatch", "header_functions", "lib", "kernels", "DeviceOptimizer", "ParamManager", "WorkerRingManager",
     "local_ring_pull_grads", "unique_id", "Adam", "AddOptimizer", "BarrierSync", "BlockingStore",
     "DynBarrier", "GradientDescent", "GradientDescentWithMomentum", "NoBlockingSync", "WildStore",
     "shard_size_for", "ShardedParamServer",

@@ -104,7 +104,10 @@ _SIGS = {
                                   C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ono_local_ring_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
     "ono_local_direct_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
-    "ono_store_create": (_i, [C.POINTER(C.c_void_p), _i, _fp, _sz, _sz, _sz, C.POINTER(OptSpec), _i]),
+    "ono_optimizer_create": (_i, [C.POINTER(C.c_void_p), C.POINTER(OptSpec), _sz, _i]),
+    "ono_optimizer_destroy": (_i, [_vp]),
+    "ono_optimizer_step": (_i, [_vp, _fp, _fp, _fp, _sz, _vp]),
+    "ono_store_create":(_i, [C.POINTER(C.c_void_p), _i, _fp, _sz, _sz, _sz, C.POINTER(OptSpec), _i]),
     "ono_store_destroy": (_i, [_vp]),
     "ono_store_len": (_sz, [_vp]),
     "ono_store_accumulate": (_i, [_vp, _fp, _sz]),

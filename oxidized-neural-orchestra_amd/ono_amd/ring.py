@@ -50,6 +50,42 @@ class ParamManager:
         """param_manager.rs:168-172."""
         self.grad.zero_()
 
+    def optimize(self, optimizer: "DeviceOptimizer", params_copy: torch.Tensor | None = None,
+                 stream=None) -> None:
+        """ParamManager::optimize + zero_grad + the optimization_params copy of
+        all_reduce.rs:126-132, fused into one kernel."""
+        optimizer.step(self.params, self.grad, params_copy, stream)
+
+
+class DeviceOptimizer:
+    """GradientDescent / WithMomentum / Adam for the all-reduce consumer, with
+    its state in HBM (ono_optimizer_*)."""
+
+    def __init__(self, optimizer, n: int, device: int | None = None):
+        from ._lib import OptSpec  # noqa: F401
+        spec = optimizer.spec()
+        h = C.c_void_p()
+        dev = torch.cuda.current_device() if device is None else device
+        call("ono_optimizer_create", C.byref(h), C.byref(spec), n, dev)
+        self._h, self.n = h, n
+
+    def step(self, params: torch.Tensor, grad: torch.Tensor, params_copy: torch.Tensor | None = None,
+             stream=None) -> None:
+        call("ono_optimizer_step", self._h, kernels.f32_ptr(params), kernels.f32_ptr(grad),
+             kernels.f32_ptr(params_copy) if params_copy is not None else None, params.numel(),
+             kernels.stream_handle(stream))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            call("ono_optimizer_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
 
 class WorkerRingManager:
     """worker_ring.rs:10-56.  `addrs` is the worker list (only its length is
@@ -64,6 +100,7 @@ class WorkerRingManager:
         self.amount_of_layers = amount_of_layers
         self.device = torch.cuda.current_device() if device is None else device
         self.wire = wire
+        self.algo = "auto"
         h = C.c_void_p()
         call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
         self._h = h
