@@ -97,6 +97,24 @@ int ono_f16_add_encode_zero(uint16_t *out, float *acc, const uint16_t *in, size_
 /* gather receive: out = f32(in) / divisor         (worker_ring.rs:200 + :101-105) */
 int ono_f16_decode_scale(float *out, const uint16_t *in, size_t n, float divisor, void *stream);
 
+/* Sparse top-(1-r) gradient codec (comms/src/sparse/protocol.rs:33-144), the
+ * SparseCapable serializer's wire format, byte-exact:
+ *   [u64 LE total_len] { [u32 LE offset][u32 LE run_len][f16 LE x run_len] }*
+ * The threshold is the caller's (the reference samples it with rand 0.9.4
+ * StdRng, protocol.rs:33-49).  drop: g_dev -> buf_dev, *nbytes = encoded
+ * length (blocking; ONO_E_SIZE if it exceeds cap; ono_sparse_max_bytes(n)
+ * always suffices).  lift: host bytes (as received from comms/) -> g_dev of
+ * *out_len = total_len values (zero-filled, then the runs); malformed input ->
+ * ONO_E_PROTO with the reference's message.  mask: the ring's sparse
+ * bookkeeping — zero_kept=1: g = 0 where |g| >= t (worker_ring.rs:128-131),
+ * zero_kept=0: g = 0 where |g| < t (:183-187).                               */
+size_t ono_sparse_max_bytes(size_t n);
+int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
+                    float threshold, void *stream);
+int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
+                    void *stream);
+int ono_sparse_mask(float *g_dev, size_t n, float threshold, int zero_kept, void *stream);
+
 /* synthetic gradient bucket (SURVEY.md §8(d) distribution), bit-identical to
  * the CPU oracle's generator: out[j] = synth(seed, rank, offset + j)          */
 int ono_synth_f32(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset, void *stream);

@@ -1,0 +1,68 @@
+"""Sparse top-(1-r) gradient codec on the device (comms/src/sparse/protocol.rs).
+
+grad_drop(g, threshold) -> bytes   (protocol.rs:57-86, byte-exact wire format)
+grad_lift(buf) -> device tensor     (protocol.rs:96-144)
+mask_sent / mask_unsent             (the ring's sparse bookkeeping, worker_ring.rs:128-131, 183-187)
+The threshold is the caller's: the reference draws it from a rand 0.9.4 StdRng
+sample (protocol.rs:33-49); for gradients of <= 16384 values that sample is
+the whole gradient and `threshold_full` reproduces it exactly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import kernels
+from ._lib import call, lib
+
+SAMPLE_SIZE_MAX = 1 << 14
+MIN_POSITIVE_F16 = np.float32(6.103515625e-05)
+
+
+def threshold_full(g: np.ndarray, r: float) -> float:
+    """calculate_threshold for len(g) <= 16384 (sample = every value)."""
+    g = np.asarray(g, dtype=np.float32)
+    if g.size == 0:
+        return 0.0
+    if g.size > SAMPLE_SIZE_MAX:
+        raise ValueError("above 16384 values the reference threshold depends on rand 0.9.4 StdRng sampling")
+    a = np.sort(np.abs(g).view(np.uint32)).view(np.float32)   # total_cmp order of non-negative floats
+    k = int(np.float32(g.size) * (np.float32(1.0) - np.float32(r)))
+    k = min(max(k, 0), g.size - 1)
+    return float(max(a[k], MIN_POSITIVE_F16))
+
+
+def grad_drop(g: torch.Tensor, threshold: float, stream=None) -> bytes:
+    n = g.numel()
+    cap = lib().ono_sparse_max_bytes(n)
+    buf = torch.empty(cap + 8, dtype=torch.uint8, device=g.device)
+    nb = C.c_size_t(0)
+    call("ono_sparse_drop", buf.data_ptr(), cap, C.byref(nb), kernels.f32_ptr(g), n, float(threshold),
+         kernels.stream_handle(stream))
+    return bytes(buf[: nb.value].cpu().numpy())
+
+
+def grad_lift(buf: bytes, cap: int | None = None, device: str = "cuda", stream=None) -> torch.Tensor:
+    b = np.frombuffer(bytes(buf), dtype=np.uint8)
+    total = int.from_bytes(bytes(buf[:8]), "little") if len(buf) >= 8 else 0
+    cap = total if cap is None else cap
+    out = torch.empty(max(cap, 1), dtype=torch.float32, device=device)
+    ln = C.c_size_t(0)
+    call("ono_sparse_lift", kernels.f32_ptr(out), cap, C.byref(ln), b.ctypes.data if b.size else None, b.size,
+         kernels.stream_handle(stream))
+    torch.cuda.synchronize()
+    return out[: ln.value]
+
+
+def mask_sent(g: torch.Tensor, threshold: float, stream=None) -> torch.Tensor:
+    """Scatter side: the values just sent (|g| >= t) leave the residual."""
+    call("ono_sparse_mask", kernels.f32_ptr(g), g.numel(), float(threshold), 1, kernels.stream_handle(stream))
+    return g
+
+
+def mask_unsent(g: torch.Tensor, threshold: float, stream=None) -> torch.Tensor:
+    """Gather side: only the values that were sent (|g| >= t) stay."""
+    call("ono_sparse_mask", kernels.f32_ptr(g), g.numel(), float(threshold), 0, kernels.stream_handle(stream))
+    return g
