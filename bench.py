@@ -189,6 +189,8 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
     from oracle import oracle as O  # noqa: WPS433 (cpu_baseline leg only)
 
     r = O.cpu_ring(ranks, bucket_elems, rounds, check=False, pin=True, timeout=900)
+    hop = O.cpu_ps("hop", bucket_elems // ranks, rounds=rounds)
+    ps = O.cpu_ps("ps", bucket_elems, threads=16, workers=ranks, rounds=rounds)
     return {
         "value": round(r["gib_s"], 4),
         "unit": "GiB/s",
@@ -199,6 +201,12 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
                    f"{rounds} pull_grads rounds, {r['s_per_round']:.3f} s/round; C -O3 default x86-64"),
         "host_cpu": _cpu_model(),
         "host_nproc": os.cpu_count(),
+        # SURVEY §8(d) items (i) and (iii), same host, same run
+        "hop_compute_1core": {"gib_s": hop["gib_s"], "s_per_hop": hop["s_per_hop"],
+                              "sample": f"{hop['len']} elems: f16 encode + decode + f32 add, 1 core"},
+        "ps_accumulate_update": {"gib_s": ps["gib_s"], "s_per_round": ps["s_per_round"], "cores": ps["threads"],
+                                 "sample": f"BlockingStore: {ps['workers']} accumulates + 1 update (÷n, GD) of "
+                                           f"{ps['len']} params, {ps['shards']} shards on {ps['threads']} pinned cores"},
     }
 
 

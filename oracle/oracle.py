@@ -239,6 +239,21 @@ class WildStore:
         return out
 
 
+def cpu_ps(mode: str, length: int, threads: int = 16, workers: int = 2, rounds: int = 3,
+           timeout: float = 600) -> dict:
+    """oracle/ono_cpu_ps.c: 'hop' = one scatter hop's compute on one core,
+    'ps' = BlockingStore accumulate + update on `threads` cores (2 x threads shards)."""
+    import json
+
+    exe = os.path.join(BUILD, "ono_cpu_ps")
+    if not os.path.exists(exe):
+        build()
+    cmd = [exe, "--mode", mode, "--len", str(length), "--threads", str(threads), "--workers", str(workers),
+           "--rounds", str(rounds)]
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
 def cpu_ring(ranks: int, length: int, rounds: int, seed: int = 0x0402026, check: bool = False,
              pin: bool = True, timeout: float = 600) -> dict:
     """Run the TCP-loopback reference-style CPU ring (oracle/ono_cpu_ring.c)."""

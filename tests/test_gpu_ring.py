@@ -256,6 +256,35 @@ def test_local_direct_full_size_f16_n8_equals_hops():
     torch.cuda.empty_cache()
 
 
+def test_full_size_1gib_local_direct_f32_n8():
+    """BASELINE config 4 shape: 1 GiB bucket per rank, n = 8 (16 GiB in HBM).
+    Size-independent property: every rank's chunk c equals sum_scale of the
+    n slices taken in the reference order c, c+1, ..., c+7, divided by 8;
+    residuals are zeroed; a strided sample matches the oracle."""
+    n, n_el = 8, 1 << 28
+    res = [torch.empty(n_el, dtype=torch.float32, device=DEV) for _ in range(n)]
+    for r, t in enumerate(res):
+        ono_amd.kernels.synth(t, SEED + 5, r)
+    chunks = O.split_chunks(n_el, n)
+    expect = torch.empty(n_el, dtype=torch.float32, device=DEV)
+    for c, (lo, hi) in enumerate(chunks):
+        ono_amd.kernels.sum_scale(expect[lo:hi], [res[(c + k) % n][lo:hi] for k in range(n)], float(n))
+    grads = [torch.empty_like(res[0]) for _ in range(n)]
+    ono_amd.local_ring_pull_grads(res, grads, "f32", algo="direct")
+    torch.cuda.synchronize()
+    for r in range(n):
+        assert torch.equal(grads[r].view(torch.int32), expect.view(torch.int32)), r
+        assert int(torch.count_nonzero(res[r].view(torch.int32))) == 0
+    idx = np.arange(0, n_el, 1 << 20)
+    hs = [np.array([O.synth(1, SEED + 5, r, int(i))[0] for i in idx], np.float32) for r in range(n)]
+    ge = host(grads[3])[idx]
+    for j, i in enumerate(idx):
+        c = next(k for k, (lo, hi) in enumerate(chunks) if lo <= i < hi)
+        assert_bitexact(ge[j:j + 1], O.sum_scale([hs[(c + k) % n][j:j + 1] for k in range(n)], float(n)))
+    del res, grads, expect
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("algo", ["allreduce", "hops", "direct"])
 def test_ring_set_algo_n1(algo):
     ring = ono_amd.WorkerRingManager(0, 1, 1000, algo=algo)
