@@ -24,6 +24,8 @@ Extra objects on the JSON line:
   roofline      the step's dominant kernel, achieved vs peak, from HIP events
                 recorded on the launch stream inside the timed region
   local_reduce  BASELINE config 2: the 64 MiB sum-and-scale kernel, k = 2, 4, 8
+  host_fed      PCIe-inclusive pull_grads from host buffers (registered / pageable)
+  tcp_edge      MI355X workers in a loopback-TCP ring speaking the reference's frames
   cpu_baseline  the reference-style CPU ring (TCP loopback, f16 wire, one pinned
                 core per worker) on the same host, rank 0 at N = 1 only
 """
@@ -67,6 +69,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-local-reduce", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
+    ap.add_argument("--no-tcp-edge", action="store_true")
     ap.add_argument("--cpu-ranks", type=int, default=2)
     ap.add_argument("--cpu-rounds", type=int, default=3)
     return ap.parse_args(argv)
@@ -290,6 +293,71 @@ def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
             "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
 
 
+def tcp_edge(ono_amd, elems: int, rounds: int, ranks: int = 2) -> dict:
+    """The TCP edge (never `value`): `ranks` MI355X workers on
+    this one GPU, one thread each, in a loopback-TCP ring speaking the
+    reference's frames — the same transport, rank count and bucket as the
+    reference CPU ring of `cpu_baseline`, so the two rates compare directly.
+    Per round each worker refills its residual in HBM (untimed), then all run
+    pull_grads between two barriers.  Reports the per-worker bucket rate."""
+    import socket
+    import threading
+
+    import torch
+
+    lis = [socket.create_server(("127.0.0.1", 0)) for _ in range(ranks)]
+    ports = [s.getsockname()[1] for s in lis]
+    bar = threading.Barrier(ranks)
+    times, errs = [], []
+
+    def worker(r):
+        nxt = prev = ring = None
+        try:
+            torch.cuda.set_device(torch.cuda.current_device())
+            nxt = socket.create_connection(("127.0.0.1", ports[(r + 1) % ranks]), timeout=60)
+            nxt.settimeout(None)
+            nxt.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            prev, _ = lis[r].accept()
+            s = torch.cuda.Stream()
+            ring = ono_amd.WorkerRingManager.over_tcp(r, ranks, elems, prev, nxt)
+            with torch.cuda.stream(s):
+                src = torch.randn(elems, device="cuda") * 0.01
+            for k in range(rounds + 1):
+                with torch.cuda.stream(s):
+                    ring.residual.copy_(src)
+                s.synchronize()
+                bar.wait()
+                t0 = time.perf_counter()
+                ring.pull_grads(stream=s)
+                s.synchronize()
+                bar.wait()
+                if r == 0 and k:
+                    times.append(time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001 — reported in the line
+            errs.append(repr(e))
+            bar.abort()
+        finally:
+            if ring is not None:
+                ring.close()
+            for sk in (nxt, prev):
+                if sk is not None:
+                    sk.close()
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(ranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    for s in lis:
+        s.close()
+    if errs or not times:
+        return {"error": errs[0] if errs else "timed out"}
+    t = sorted(times)[len(times) // 2]
+    return {"workload": f"pull_grads over loopback TCP, {ranks} workers on one GPU, "
+                        f"{elems * 4 >> 20} MiB bucket each, f16 reference frames",
+            "ranks": ranks, "ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 3)}
+
+
 # ------------------------------------------------------------------- main
 def main(argv=None) -> int:
     args = parse_args(argv)
@@ -374,6 +442,8 @@ def main(argv=None) -> int:
 
     if rank == 0 and world == 1 and not args.no_host_fed:
         extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
+    if rank == 0 and world == 1 and not args.no_tcp_edge:
+        extra["tcp_edge"] = tcp_edge(ono_amd, elems, 3)
     if rank == 0 and world == 1 and not args.no_local_reduce:
         extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -42,7 +42,8 @@ typedef enum {
     ONO_E_ABORTED = 5, /* ono_ring_abort() — the reference drops the ring future in select!
                           (worker/src/workers/all_reduce.rs:73-75) */
     ONO_E_ARG = 6,     /* invalid argument (NULL handle, bad enum, k out of range) */
-    ONO_E_OTHER = 7    /* ParamServerErr::Other */
+    ONO_E_OTHER = 7,   /* ParamServerErr::Other */
+    ONO_E_IO = 8       /* socket error on a TCP ring (the reference's io::Error from comms/) */
 } ono_status;
 
 /* Wire type of the ring.  F16 reproduces the reference exactly: gradients
@@ -133,6 +134,15 @@ int ono_ring_unique_id(uint8_t uid[ONO_UID_BYTES]);
  * `device`.  nranks == 1 needs no uid (may be NULL).                        */
 int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device,
                     const uint8_t *uid, int wire);
+/* The TCP edge: the same manager over the worker's own sockets — fd_prev the
+ * accepted connection from the previous worker, fd_next the connection to the
+ * next (worker/src/builder.rs:272-311; the caller keeps ownership).  Frames
+ * are the reference's byte for byte ([u64 BE len][u32 BE kind=1][f16 LE],
+ * comms/src/protocol/msg.rs:120-191), so MI355X workers and reference Rust
+ * workers can form one ring.  f16 wire, hop schedule; the hop arithmetic runs
+ * in HBM (fused codec kernels), one D2H + H2D of the chunk per hop.          */
+int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
+                        int fd_next);
 int ono_ring_destroy(ono_ring *ring);
 /* the owned buckets (device pointers): grad = WorkerRingManager.grad,
  * residual = WorkerRingManager.residual                                      */

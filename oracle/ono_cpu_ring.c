@@ -16,6 +16,14 @@
  *
  * usage: ono_cpu_ring --ranks N --len L --rounds R [--seed S] [--check] [--no-pin]
  * prints one JSON line: {"ranks":..,"len":..,"rounds":..,"s_per_round":..,"gib_s":..,"check":..}
+ *
+ * single-worker mode (one reference-style worker of a ring whose other members
+ * run elsewhere — e.g. MI355X workers on ono_ring_create_tcp):
+ *   ono_cpu_ring --rank R --ranks N --len L --next-port P [--listen-port Q] [--rounds R]
+ *                [--seed S] [--out FILE]
+ * prints {"port": Q} once listening, then runs like one thread above (its input is
+ * ono_ref_synth(seed, rank R, round 0) every round) and writes grad ++ residual
+ * (f32, 2*L values) of the last round to FILE.
  */
 #include "ono_oracle.h"
 
@@ -38,7 +46,7 @@ typedef struct {
     int rank, n, rounds, pin;
     size_t len;
     uint64_t seed;
-    int listen_fd, port_next;
+    int listen_fd, port_next, timer;
     float *residual, *pristine, *grad;
     double elapsed;
 } worker_t;
@@ -92,10 +100,13 @@ static int connect_to(int port) {
     a.sin_family = AF_INET;
     a.sin_port = htons((uint16_t)port);
     a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-    for (int tries = 0; tries < 2000; tries++) {
+    for (int tries = 0; tries < 30000; tries++) {  /* 30 s: peers may start late */
         if (connect(fd, (struct sockaddr *)&a, sizeof a) == 0) return fd;
+        close(fd);
+        fd = socket(AF_INET, SOCK_STREAM, 0);
         usleep(1000);
     }
+    close(fd);
     return -1;
 }
 
@@ -134,7 +145,7 @@ static void *worker_main(void *arg) {
     for (int round = 0; round < w->rounds; round++) {
         memcpy(w->residual, w->pristine, w->len * sizeof(float));
         pthread_barrier_wait(&g_bar);
-        if (w->rank == 0) g_t0 = now();
+        if (w->timer) g_t0 = now();
         /* ---- scatter ---- */
         int i = w->rank;
         for (int s = 0; s < n - 1; s++) {
@@ -178,7 +189,7 @@ static void *worker_main(void *arg) {
             ono_ref_normalize(w->grad, w->len, (size_t)n);
         }
         pthread_barrier_wait(&g_bar);
-        if (w->rank == 0) g_total += now() - g_t0;
+        if (w->timer) g_total += now() - g_t0;
     }
     if (fd_next >= 0) close(fd_next);
     if (fd_prev >= 0) close(fd_prev);
@@ -186,12 +197,63 @@ static void *worker_main(void *arg) {
     return NULL;
 }
 
+static int listen_on(int port, int *bound) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    struct sockaddr_in a = {0};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (bind(fd, (struct sockaddr *)&a, sizeof a) || listen(fd, 4)) return -1;
+    socklen_t sl = sizeof a;
+    getsockname(fd, (struct sockaddr *)&a, &sl);
+    *bound = ntohs(a.sin_port);
+    return fd;
+}
+
+/* one worker of a ring whose other members are other processes */
+static int single_worker(int rank, int n, size_t len, int rounds, uint64_t seed, int listen_port,
+                         int next_port, const char *out) {
+    worker_t w = {0};
+    int port = 0;
+    w.listen_fd = listen_on(listen_port, &port);
+    if (w.listen_fd < 0) { perror("bind"); return 2; }
+    printf("{\"port\": %d}\n", port);
+    fflush(stdout);
+    w.rank = rank; w.n = n; w.rounds = rounds; w.pin = 0; w.timer = 1;
+    w.len = len; w.seed = seed; w.port_next = next_port;
+    w.residual = (float *)malloc(len * sizeof(float));
+    w.pristine = (float *)malloc(len * sizeof(float));
+    w.grad = (float *)calloc(len, sizeof(float));
+    ono_ref_synth(w.pristine, len, seed, (uint64_t)rank, 0);
+    pthread_barrier_init(&g_bar, NULL, 1);
+    worker_main(&w);
+    if (out) {
+        FILE *f = fopen(out, "wb");
+        if (!f || fwrite(w.grad, sizeof(float), len, f) != len ||
+            fwrite(w.residual, sizeof(float), len, f) != len) { perror("out"); return 5; }
+        fclose(f);
+    }
+    double spr = g_total / rounds;
+    printf("{\"rank\": %d, \"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"s_per_round\": %.9f}\n",
+           rank, n, len, rounds, spr);
+    close(w.listen_fd);
+    free(w.residual); free(w.pristine); free(w.grad);
+    return 0;
+}
+
 int main(int argc, char **argv) {
-    int n = 2, rounds = 3, check = 0, pin = 1;
+    int n = 2, rounds = 3, check = 0, pin = 1, rank = -1, listen_port = 0, next_port = -1;
     size_t len = 109386;
     uint64_t seed = 0x0402026;
+    const char *out = NULL;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--rank") && a + 1 < argc) rank = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--listen-port") && a + 1 < argc) listen_port = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--next-port") && a + 1 < argc) next_port = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--out") && a + 1 < argc) out = argv[++a];
         else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = (size_t)strtoull(argv[++a], 0, 10);
         else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--seed") && a + 1 < argc) seed = strtoull(argv[++a], 0, 0);
@@ -200,23 +262,18 @@ int main(int argc, char **argv) {
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
     if (n < 1 || len < (size_t)n || rounds < 1) { fprintf(stderr, "need len >= ranks >= 1\n"); return 1; }
+    if (rank >= 0) {
+        if (rank >= n || (n > 1 && next_port <= 0)) { fprintf(stderr, "need rank < ranks, --next-port\n"); return 1; }
+        return single_worker(rank, n, len, rounds, seed, listen_port, next_port, out);
+    }
     worker_t *w = (worker_t *)calloc((size_t)n, sizeof(worker_t));
     int *ports = (int *)calloc((size_t)n, sizeof(int));
     for (int r = 0; r < n; r++) {
-        int fd = socket(AF_INET, SOCK_STREAM, 0);
-        int one = 1;
-        setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-        struct sockaddr_in a = {0};
-        a.sin_family = AF_INET;
-        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-        if (bind(fd, (struct sockaddr *)&a, sizeof a) || listen(fd, 4)) { perror("bind"); return 2; }
-        socklen_t sl = sizeof a;
-        getsockname(fd, (struct sockaddr *)&a, &sl);
-        ports[r] = ntohs(a.sin_port);
-        w[r].listen_fd = fd;
+        w[r].listen_fd = listen_on(0, &ports[r]);
+        if (w[r].listen_fd < 0) { perror("bind"); return 2; }
     }
     for (int r = 0; r < n; r++) {
-        w[r].rank = r; w[r].n = n; w[r].rounds = rounds; w[r].pin = pin;
+        w[r].rank = r; w[r].n = n; w[r].rounds = rounds; w[r].pin = pin; w[r].timer = r == 0;
         w[r].len = len; w[r].seed = seed; w[r].port_next = ports[(r + 1) % n];
         w[r].residual = (float *)malloc(len * sizeof(float));
         w[r].pristine = (float *)malloc(len * sizeof(float));

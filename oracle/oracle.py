@@ -269,3 +269,50 @@ def cpu_ring(ranks: int, length: int, rounds: int, seed: int = 0x0402026, check:
         cmd.append("--no-pin")
     out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
     return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+class CpuRingWorker:
+    """One reference-style ring worker as its own process (ono_cpu_ring.c single
+    mode): listens on an ephemeral loopback port (`.port`), connects to
+    `next_port`, runs `rounds` pull_grads rounds over the reference framing on
+    input synth(length, seed, rank), and leaves grad and residual of the last
+    round in `result()`.  Test infrastructure: the peer that proves an MI355X
+    worker and a reference worker can share one ring."""
+
+    def __init__(self, rank: int, ranks: int, length: int, next_port: int, rounds: int = 1,
+                 seed: int = 0x0402026, listen_port: int = 0):
+        import json
+        import tempfile
+
+        if not os.path.exists(CPU_RING):
+            build()
+        self.length = length
+        fd, self.out = tempfile.mkstemp(suffix=".bin")
+        os.close(fd)
+        self.proc = subprocess.Popen(
+            [CPU_RING, "--rank", str(rank), "--ranks", str(ranks), "--len", str(length),
+             "--next-port", str(next_port), "--listen-port", str(listen_port), "--rounds", str(rounds),
+             "--seed", str(seed), "--out", self.out], stdout=subprocess.PIPE, text=True)
+        self.port = json.loads(self.proc.stdout.readline())["port"]
+
+    def result(self, timeout: float = 120):
+        """(grad, residual) of the last round; raises if the worker failed."""
+        import json
+
+        try:
+            tail = self.proc.stdout.read()
+            rc = self.proc.wait(timeout)
+            if rc != 0:
+                raise RuntimeError(f"ono_cpu_ring worker exited with {rc}")
+            data = np.fromfile(self.out, dtype=np.float32)
+            info = json.loads(tail.strip().splitlines()[-1])
+            return data[:self.length].copy(), data[self.length:].copy(), info
+        finally:
+            self.close()
+
+    def close(self):
+        if self.proc.poll() is None:
+            self.proc.kill()
+            self.proc.wait()
+        if os.path.exists(self.out):
+            os.unlink(self.out)

@@ -16,8 +16,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <poll.h>
+#include <sys/socket.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -124,6 +128,11 @@ struct ono_ring {
     hipStream_t zstream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     ncclComm_t comm = nullptr;
+    // TCP transport (ono_ring_create_tcp): the caller's connected sockets to the
+    // previous and next worker, pinned frame buffers (rx 4-B aligned, source.rs:43-50)
+    int fd_prev = -1, fd_next = -1;
+    uint8_t *tx = nullptr, *rx = nullptr;
+    size_t frame_cap = 0;
     std::atomic<bool> aborted{false};
     std::mutex mu;  // serialises host-form calls and the timer
     // host-fed pipeline (ono_ring_pull_grads_host): H2D on hstream, reduce on
@@ -155,6 +164,68 @@ template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
 template <> ncclDataType_t nccl_type<float>() { return ncclFloat32; }
 
 // One pull_grads round of rank `pos`, exact reference hop order, wire W.
+// One hop over the reference's TCP wire (the TCP edge):
+// the f16 payload comes down from HBM into a pinned frame
+//   [u64 BE len = 4 + payload][u32 BE kind = 1: DenseGrad, is_last = false][f16 LE ...]
+// (msg.rs:120-151, sink.rs:37-58, worker.rs:157-174), is sent to `next` while
+// the previous worker's frame is read (try_join!, worker_ring.rs:122-123;
+// source.rs:34-57), validated as a DenseGrad of the expected length, and goes
+// up to HBM for the next fused kernel.  Frames are byte-identical to the
+// reference's, so MI355X workers and reference Rust workers can share a ring.
+int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_dev, size_t recv_bytes,
+             hipStream_t s) {
+    uint8_t *tx = r->tx, *rx = r->rx;
+    ONO_HIP(hipMemcpyAsync(tx + 12, send_dev, send_bytes, hipMemcpyDeviceToHost, s));
+    ONO_HIP(hipStreamSynchronize(s));
+    const uint64_t flen = 4 + (uint64_t)send_bytes;
+    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
+    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
+    const size_t out = 12 + send_bytes;
+    size_t sent = 0, got = 0, need = 8;
+    bool have_len = false;
+    while (sent < out || got < need) {
+        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        struct pollfd p[2];
+        int np = 0, is = -1, ir = -1;
+        if (sent < out) { p[np].fd = r->fd_next; p[np].events = POLLOUT; p[np].revents = 0; is = np++; }
+        if (got < need) { p[np].fd = r->fd_prev; p[np].events = POLLIN; p[np].revents = 0; ir = np++; }
+        int pr = poll(p, (nfds_t)np, 1000);
+        if (pr < 0 && errno != EINTR) return set_error(ONO_E_IO, "poll: %s", strerror(errno));
+        if (pr <= 0) continue;  // re-check the abort flag once a second
+        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP))) {
+            ssize_t k = send(r->fd_next, tx + sent, out - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
+            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
+                return set_error(ONO_E_IO, "send to next worker: %s", strerror(errno));
+            if (k > 0) sent += (size_t)k;
+        }
+        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP))) {
+            ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
+            if (k == 0) return set_error(ONO_E_IO, "previous worker closed the connection");
+            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
+                return set_error(ONO_E_IO, "recv from previous worker: %s", strerror(errno));
+            if (k > 0) got += (size_t)k;
+            if (!have_len && got >= 8) {
+                uint64_t l = 0;
+                for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
+                if (l < 4 || 8 + l > r->frame_cap)
+                    return set_error(ONO_E_PROTO, "Received an invalid worker event (frame of %llu bytes)",
+                                     (unsigned long long)l);
+                need = 8 + (size_t)l;
+                have_len = true;
+            }
+        }
+    }
+    const uint8_t kind = rx[11];  // Header::from_be_bytes(..) as u8 (msg.rs:168)
+    const size_t payload = need - 12;
+    if (kind != 1 && kind != 2)   // only a DenseGrad is a valid event here (worker_ring.rs:136-138)
+        return set_error(ONO_E_PROTO, "Received an invalid worker event (kind %u)", kind);
+    if (payload != recv_bytes)
+        return set_error(ONO_E_PROTO, "Received an invalid worker event (%zu payload bytes, expected %zu)",
+                         payload, recv_bytes);
+    ONO_HIP(hipMemcpyAsync(recv_dev, rx + 12, recv_bytes, hipMemcpyHostToDevice, s));
+    return ONO_OK;  // rx is reused only after the next hop's stream synchronisation
+}
+
 template <class W>
 int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
     const int n = r->n, pos = r->pos;
@@ -165,6 +236,10 @@ int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
     const float fn = (float)n;
     auto xchg = [&](int bs, int cs, int br, int cr) -> int {
         if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        if (r->fd_next >= 0)
+            return timed(r, s, 1, [&]() -> int {
+                return tcp_xchg(r, slot(bs, cs), len(cs) * sizeof(W), slot(br, cr), len(cr) * sizeof(W), s);
+            });
         return timed(r, s, 1, [&]() -> int {
             ONO_NCCL(ncclGroupStart());
             ONO_NCCL(ncclSend(slot(bs, cs), len(cs), nccl_type<W>(), next, r->comm, s));
@@ -326,14 +401,59 @@ int ono_ring_unique_id(uint8_t uid[ONO_UID_BYTES]) {
     return ONO_OK;
 }
 
-int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device,
-                    const uint8_t *uid, int wire) {
+static int ring_validate(ono_ring **out, int pos, int nranks, size_t size, int wire) {
     if (!out) return set_error(ONO_E_ARG, "out is NULL");
     *out = nullptr;
     if (nranks < 1 || pos < 0 || pos >= nranks) return set_error(ONO_E_ARG, "pos=%d nranks=%d", pos, nranks);
     if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
     if (size < (size_t)nranks)  // reference: chunks[pos] out of bounds (worker_ring.rs:120-122)
         return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, nranks);
+    return ONO_OK;
+}
+
+// The reference's ring over its own TCP connections (builder.rs:272-311 hands
+// the worker an accepted `prev` and a connected `next` stream): f16 wire, hop
+// schedule, the arithmetic in HBM, the frames on the caller's sockets.
+int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
+                        int fd_next) {
+    int rc = ring_validate(out, pos, nranks, size, ONO_WIRE_F16);
+    if (rc) return rc;
+    if (nranks > 1 && (fd_prev < 0 || fd_next < 0)) return set_error(ONO_E_ARG, "sockets required for nranks > 1");
+    // reuse the common allocation path (nranks == 1 needs neither sockets nor an id)
+    static const uint8_t no_uid[ONO_UID_BYTES] = {0};
+    rc = ono_ring_create(out, 0, 1, size, device, no_uid, ONO_WIRE_F16);
+    if (rc) return rc;
+    ono_ring *r = *out;
+    if (nranks == 1) return ONO_OK;
+    *out = nullptr;
+    r->n = nranks;
+    r->pos = pos;
+    r->off = split_chunks(size, (size_t)nranks);
+    r->maxc = r->off[1] - r->off[0];
+    r->algo = ONO_ALGO_HOPS;
+    r->fd_prev = fd_prev;
+    r->fd_next = fd_next;
+    r->frame_cap = 12 + 2 * (r->maxc + 4);
+    DeviceGuard g(device);
+    hipError_t e;
+    for (int b = 0; b < 2; b++)
+        if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(float))) != hipSuccess) {
+            ono_ring_destroy(r);
+            return hip_error(e, "wire buffer allocation", __FILE__, __LINE__);
+        }
+    if ((e = hipHostMalloc((void **)&r->tx, r->frame_cap, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&r->rx, r->frame_cap, hipHostMallocDefault)) != hipSuccess) {
+        ono_ring_destroy(r);
+        return hip_error(e, "frame buffer allocation", __FILE__, __LINE__);
+    }
+    *out = r;
+    return ONO_OK;
+}
+
+int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device,
+                    const uint8_t *uid, int wire) {
+    int vrc = ring_validate(out, pos, nranks, size, wire);
+    if (vrc) return vrc;
     if (nranks > 1 && !uid) return set_error(ONO_E_ARG, "uid required for nranks > 1");
     ono_ring *r = new ono_ring();
     r->pos = pos; r->n = nranks; r->size = size; r->device = device; r->wire = wire;
@@ -386,6 +506,8 @@ int ono_ring_destroy(ono_ring *r) {
             if (st) (void)hipStreamSynchronize(st);
         if (r->pin_in) (void)hipHostFree(r->pin_in);
         if (r->pin_out) (void)hipHostFree(r->pin_out);
+        if (r->tx) (void)hipHostFree(r->tx);
+        if (r->rx) (void)hipHostFree(r->rx);
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);
@@ -600,8 +722,10 @@ int ono_ring_set_algo(ono_ring *r, int algo) {
         return set_error(ONO_E_ARG, "an RCCL all-reduce cannot carry the f16 wire semantics");
     if (algo == ONO_ALGO_DIRECT && r->n > ONO_MAX_INPUTS)
         return set_error(ONO_E_ARG, "direct schedule supports up to %d ranks", ONO_MAX_INPUTS);
+    if (r->fd_next >= 0 && algo != ONO_ALGO_HOPS && algo != ONO_ALGO_AUTO)
+        return set_error(ONO_E_ARG, "a TCP ring runs the reference hop schedule only");
     std::lock_guard<std::mutex> lk(r->mu);
-    r->algo = algo;
+    r->algo = r->fd_next >= 0 ? ONO_ALGO_HOPS : algo;
     return ONO_OK;
 }
 
@@ -780,6 +904,7 @@ int ono_ps_create(ono_ps **out, ono_ring *ring, const float *init, size_t nparam
     if (!out || !ring || !init || !opt) return set_error(ONO_E_ARG, "NULL argument");
     if (opt->kind < ONO_OPT_GD || opt->kind > ONO_OPT_ADD) return set_error(ONO_E_ARG, "optimizer kind %d", opt->kind);
     *out = nullptr;
+    if (ring->fd_next >= 0) return set_error(ONO_E_ARG, "the sharded PS needs an RCCL ring, not a TCP ring");
     DeviceGuard g(ring->device);
     ono_ps *p = new ono_ps();
     p->ring = ring;

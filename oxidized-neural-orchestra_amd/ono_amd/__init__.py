@@ -11,8 +11,8 @@ objects, so torch tensors, torch streams and the library share one runtime.
 """
 import torch  # noqa: F401  (must precede the library load; see above)
 
-from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, OnoError, RcclError,
-                   SizeMismatch, header_functions, lib)
+from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, IoError, OnoError,
+                   RcclError, SizeMismatch, header_functions, lib)
 from . import kernels, sparse
 from .ring import DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id
 from .store import (Adam, AddOptimizer, BarrierSync, BlockingStore, DynBarrier, GradientDescent,
@@ -22,7 +22,7 @@ from .ps import ShardedParamServer
 lib()  # fail loudly at import when the native library is missing
 
 __all__ = [
-    "Aborted", "HipError", "InvalidArgument", "InvalidWorkerEvent", "OnoError", "RcclError",
+    "Aborted", "HipError", "InvalidArgument", "InvalidWorkerEvent", "IoError", "OnoError", "RcclError",
     "SizeMismatch", "header_functions", "lib", "kernels", "DeviceOptimizer", "ParamManager", "WorkerRingManager",
     "local_ring_pull_grads", "unique_id", "Adam", "AddOptimizer", "BarrierSync", "BlockingStore",
     "DynBarrier", "GradientDescent", "GradientDescentWithMomentum", "NoBlockingSync", "WildStore",

@@ -14,7 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libono_reduce.so")
 HEADER = os.path.normpath(os.path.join(HERE, "..", "..", "include", "ono_reduce.h"))
 
-ONO_OK, ONO_E_SIZE, ONO_E_PROTO, ONO_E_HIP, ONO_E_RCCL, ONO_E_ABORTED, ONO_E_ARG, ONO_E_OTHER = range(8)
+(ONO_OK, ONO_E_SIZE, ONO_E_PROTO, ONO_E_HIP, ONO_E_RCCL, ONO_E_ABORTED, ONO_E_ARG, ONO_E_OTHER,
+ ONO_E_IO) = range(9)
 WIRE = {"f32": 0, "f16": 1}
 ALGO = {"auto": 0, "allreduce": 1, "hops": 2, "direct": 3}
 OPT_KIND = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
@@ -56,8 +57,13 @@ class InvalidArgument(OnoError, ValueError):
     pass
 
 
+class IoError(OnoError, OSError):
+    """Socket failure on a TCP ring (the reference's io::Error from comms/)."""
+
+
 _ERR = {ONO_E_SIZE: SizeMismatch, ONO_E_PROTO: InvalidWorkerEvent, ONO_E_HIP: HipError,
-        ONO_E_RCCL: RcclError, ONO_E_ABORTED: Aborted, ONO_E_ARG: InvalidArgument}
+        ONO_E_RCCL: RcclError, ONO_E_ABORTED: Aborted, ONO_E_ARG: InvalidArgument,
+        ONO_E_IO: IoError}
 
 
 class OptSpec(C.Structure):
@@ -90,6 +96,7 @@ _SIGS = {
     "ono_sparse_mask": (_i, [_fp, _sz, C.c_float, _i, _vp]),
     "ono_ring_unique_id": (_i, [C.c_char_p]),
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
+    "ono_ring_create_tcp": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i, _i]),
     "ono_ring_destroy": (_i, [_vp]),
     "ono_ring_grad": (C.c_void_p, [_vp]),
     "ono_ring_residual": (C.c_void_p, [_vp]),

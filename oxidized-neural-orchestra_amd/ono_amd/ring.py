@@ -101,11 +101,35 @@ class WorkerRingManager:
         self.device = torch.cuda.current_device() if device is None else device
         self.wire = wire
         self.algo = "auto"
+        self._socks = ()
         h = C.c_void_p()
-        call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
+        if isinstance(uid, tuple):  # (fd_prev, fd_next): the TCP edge, see over_tcp()
+            call("ono_ring_create_tcp", C.byref(h), pos, nranks, size, self.device, *uid)
+        else:
+            call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
         self._h = h
         if algo != "auto":
             self.set_algo(algo)
+        self._bind()
+
+    @classmethod
+    def over_tcp(cls, pos: int, addrs, size: int, prev_sock, next_sock, amount_of_layers: int = 1,
+                 *, device: int | None = None) -> "WorkerRingManager":
+        """The TCP edge: the manager over the worker's own connections
+        (worker/src/builder.rs:272-311 — `prev_sock` accepted from the previous
+        worker, `next_sock` connected to the next), speaking the reference's
+        frames byte for byte (comms/src/protocol/msg.rs:120-191).  Always the
+        f16 wire and the hop schedule.  The sockets stay owned by the caller
+        and must outlive the manager."""
+        nranks = addrs if isinstance(addrs, int) else len(addrs)
+        fds = (-1, -1) if nranks == 1 else (prev_sock.fileno(), next_sock.fileno())
+        self = cls(pos, nranks, size, amount_of_layers, uid=fds, wire="f16", device=device)
+        self._socks = (prev_sock, next_sock)
+        self.algo = "hops"
+        return self
+
+    def _bind(self):
+        h, size = self._h, self.size
         dev = f"cuda:{self.device}"
         self.grad = torch.as_tensor(_DevArray(lib().ono_ring_grad(h), size), device=dev)
         self.residual = torch.as_tensor(_DevArray(lib().ono_ring_residual(h), size), device=dev)

@@ -1,0 +1,255 @@
+"""GPU parity of the TCP edge (ono_ring_create_tcp).
+
+The ring runs over the worker's own stream sockets and speaks the reference's
+frames byte for byte ([u64 BE len][u32 BE kind=1][f16 LE], msg.rs:120-191),
+with the hop arithmetic in HBM.  Several ranks share the one GPU of the box,
+one Python thread each (the C ABI releases the GIL while it blocks on its
+sockets):
+
+* all-GPU rings over socket pairs: bit-exact with the oracle, device and
+  host-fed forms, several rounds;
+* mixed rings over loopback TCP: MI355X workers and reference-style CPU
+  workers (oracle/ono_cpu_ring.c single mode, one process per rank) in ONE
+  ring — wire compatibility with the reference;
+* the bytes an MI355X worker puts on the wire equal the reference framing of
+  the reference's f16 encoding of its chunk;
+* the reference's failure behaviour: an invalid event is InvalidWorkerEvent
+  (worker_ring.rs:136-138), a closed peer is an io error, abort() unblocks.
+"""
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import ono_amd
+from conftest import SEED, assert_bitexact
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def socketpair_links(n):
+    """links[r] = (prev_sock, next_sock) of rank r; pair i carries i -> i+1."""
+    pairs = [socket.socketpair() for _ in range(n)]
+    return [(pairs[(r - 1) % n][1], pairs[r][0]) for r in range(n)], pairs
+
+
+def close_all(socks):
+    for s in socks:
+        s.close()
+
+
+class GpuWorker(threading.Thread):
+    """One MI355X ring worker on its own stream: per round, residual <- input,
+    pull_grads (device or host-fed form); keeps the last round's results."""
+
+    def __init__(self, rank, n, length, inputs, prev=None, nxt=None, connect=None, listener=None,
+                 host_fed=False):
+        super().__init__(daemon=True)
+        self.rank, self.n, self.length, self.inputs = rank, n, length, inputs
+        self.prev, self.nxt, self.connect, self.listener = prev, nxt, connect, listener
+        self.host_fed = host_fed
+        self.err = None
+        self.grad = self.residual = None
+        self.ring = None
+        self.ready = threading.Event()
+
+    def run(self):
+        try:
+            torch.cuda.set_device(0)
+            if self.connect is not None:  # builder.rs:272-311: connect to next, accept prev
+                self.nxt = socket.create_connection(("127.0.0.1", self.connect()), timeout=60)
+                self.nxt.settimeout(None)
+                self.prev, _ = self.listener.accept()
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                self.ring = ono_amd.WorkerRingManager.over_tcp(self.rank, self.n, self.length,
+                                                               self.prev, self.nxt)
+                self.ready.set()
+                for x in self.inputs:
+                    if self.host_fed:
+                        res = np.array(x, dtype=np.float32, copy=True)
+                        grad = np.full_like(res, 7.0)
+                        self.ring.pull_grads_host(res, grad)
+                        self.grad, self.residual = grad, res
+                    else:
+                        self.ring.residual.copy_(torch.from_numpy(x).to(DEV))
+                        self.ring.pull_grads(stream=s)
+                        s.synchronize()
+                        self.grad = self.ring.grad.cpu().numpy()
+                        self.residual = self.ring.residual.cpu().numpy()
+        except Exception as e:  # reported by the test thread
+            self.err = e
+        finally:
+            self.ready.set()
+            if self.ring is not None:
+                self.ring.close()
+
+
+def join_all(workers, timeout=300):
+    for w in workers:
+        w.join(timeout)
+        assert not w.is_alive(), f"rank {w.rank} did not finish"
+    for w in workers:
+        if w.err is not None:
+            raise w.err
+
+
+def inputs_for(n, length, rounds, seed):
+    return [[O.synth(length, seed + 100 * k, r) for r in range(n)] for k in range(rounds)]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5])
+@pytest.mark.parametrize("length", [109386, 4099, 2 ** 16 + 3])
+@pytest.mark.parametrize("host_fed", [False, True])
+def test_tcp_ring_socketpairs_vs_oracle(n, length, host_fed):
+    rounds = 2
+    ins = inputs_for(n, length, rounds, SEED + 21)
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(rounds)], *links[r], host_fed=host_fed)
+          for r in range(n)]
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        close_all(s for p in pairs for s in p)
+    eg, er = O.ring_pull_grads(ins[-1], "f16")
+    for r in range(n):
+        assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
+
+
+def test_tcp_ring_single_worker():
+    """nranks == 1: no sockets; pull_grads = copy + zero (worker_ring.rs:82-94)."""
+    x = O.synth(5000, SEED, 0)
+    ring = ono_amd.WorkerRingManager.over_tcp(0, 1, x.size, None, None)
+    try:
+        ring.residual.copy_(torch.from_numpy(x).to(DEV))
+        ring.pull_grads()
+        torch.cuda.synchronize()
+        assert_bitexact(ring.grad.cpu().numpy(), x, "grad")
+        assert not ring.residual.cpu().numpy().view(np.uint32).any()
+    finally:
+        ring.close()
+
+
+@pytest.mark.parametrize("n,cpu_ranks,length", [(2, (1,), 109386), (3, (1,), 10007),
+                                                (4, (1, 3), 65539), (5, (2, 3), 4099)])
+def test_tcp_ring_mixed_with_reference_workers(n, cpu_ranks, length):
+    """MI355X workers and reference-style CPU workers in one loopback TCP ring:
+    every rank's grad and residual are bit-exact with the oracle."""
+    rounds, seed = 2, SEED + 7
+    assert 0 not in cpu_ranks  # rank n-1 connects to rank 0, whose port must exist first
+    listeners, ports = {}, {}
+    for r in range(n):
+        if r not in cpu_ranks:
+            listeners[r] = socket.create_server(("127.0.0.1", 0))
+            ports[r] = listeners[r].getsockname()[1]
+    cpu, gpu = {}, []
+    try:
+        for r in sorted(cpu_ranks, reverse=True):  # a CPU rank's next is already listening
+            cpu[r] = O.CpuRingWorker(r, n, length, ports[(r + 1) % n], rounds=rounds, seed=seed)
+            ports[r] = cpu[r].port
+        # the CPU workers feed the same input every round: synth(seed, rank)
+        x = [O.synth(length, seed, r) for r in range(n)]
+        gpu = [GpuWorker(r, n, length, [x[r]] * rounds, connect=lambda r=r: ports[(r + 1) % n],
+                         listener=listeners[r]) for r in range(n) if r not in cpu_ranks]
+        for w in gpu:
+            w.start()
+        join_all(gpu)
+        got = {w.rank: (w.grad, w.residual) for w in gpu}
+        for r, c in cpu.items():
+            g, res, _ = c.result()
+            got[r] = (g, res)
+    finally:
+        for c in cpu.values():
+            c.close()
+        close_all(listeners.values())
+        for w in gpu:
+            for s in (w.prev, w.nxt):
+                if s is not None:
+                    s.close()
+    eg, er = O.ring_pull_grads(x, "f16")
+    for r in range(n):
+        assert_bitexact(got[r][0], eg[r], f"grad rank {r}")
+        assert_bitexact(got[r][1], er[r], f"residual rank {r}")
+
+
+def recv_frame(sock):
+    head = b""
+    while len(head) < 8:
+        head += sock.recv(8 - len(head))
+    ln = int.from_bytes(head, "big")
+    body = b""
+    while len(body) < ln:
+        body += sock.recv(ln - len(body))
+    return head + body
+
+
+def start_two_rank(length, x):
+    """Rank 0 on the GPU; rank 1 is the test itself on the other socket ends."""
+    links, pairs = socketpair_links(2)
+    w = GpuWorker(0, 2, length, [x], *links[0])
+    w.start()
+    return w, links[1], pairs
+
+
+def test_tcp_ring_wire_bytes_and_invalid_kind():
+    length = 10001
+    x = O.synth(length, SEED + 1, 0)
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, x)
+    try:
+        frame = recv_frame(from_gpu)
+        (a, b) = O.split_chunks(length, 2)[0]
+        assert frame == O.frame_dense(O.f16_encode(x[a:b]))  # byte for byte the reference's
+        bad = bytearray(O.frame_dense(O.f16_encode(np.zeros(length - b, np.float32))))
+        bad[11] = 3  # a Control frame where a DenseGrad is required
+        to_gpu.sendall(bytes(bad))
+        w.join(60)
+        assert isinstance(w.err, ono_amd.InvalidWorkerEvent), w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+
+
+def test_tcp_ring_wrong_length_is_invalid_event():
+    length = 10001
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
+    try:
+        recv_frame(from_gpu)
+        to_gpu.sendall(O.frame_dense(np.zeros(7, np.uint16)))
+        w.join(60)
+        assert isinstance(w.err, ono_amd.InvalidWorkerEvent), w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+
+
+def test_tcp_ring_peer_closed_is_io_error():
+    length = 10001
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
+    try:
+        recv_frame(from_gpu)
+        to_gpu.close()
+        w.join(60)
+        assert isinstance(w.err, ono_amd.IoError), w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+
+
+def test_tcp_ring_abort_unblocks():
+    length = 10001
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
+    try:
+        recv_frame(from_gpu)  # the peer never answers
+        w.ready.wait(60)
+        time.sleep(0.2)
+        w.ring.abort()
+        w.join(30)
+        assert not w.is_alive()
+        assert isinstance(w.err, ono_amd.Aborted), w.err
+    finally:
+        close_all(s for p in pairs for s in p)

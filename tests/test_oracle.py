@@ -170,6 +170,31 @@ def test_cpu_tcp_ring_matches_oracle(n, length):
     assert r["check"] == 1
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n,length", [(2, 5003), (3, 10007)])
+def test_cpu_ring_single_worker_processes(n, length):
+    """The single-worker mode (one process per rank, the peer the TCP-edge GPU
+    tests mix into their rings) forms a ring with itself and is bit-exact."""
+    p0 = free_port()
+    ws = {}
+    nxt = p0
+    for r in range(n - 1, 0, -1):
+        ws[r] = O.CpuRingWorker(r, n, length, nxt, rounds=2, seed=SEED + 3)
+        nxt = ws[r].port
+    ws[0] = O.CpuRingWorker(0, n, length, nxt, rounds=2, seed=SEED + 3, listen_port=p0)
+    got = {r: w.result() for r, w in ws.items()}
+    eg, er = O.ring_pull_grads([O.synth(length, SEED + 3, r) for r in range(n)], "f16")
+    for r in range(n):
+        assert_bitexact(got[r][0], eg[r], f"grad rank {r}")
+        assert_bitexact(got[r][1], er[r], f"residual rank {r}")
+
+
 # --------------------------------------------------------- store KATs
 def _store(impl, params, shard, nworkers, kind="add", **hp):
     if impl == "c":
