@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ono_internal.h"
@@ -133,6 +134,8 @@ struct ono_ring {
     int fd_prev = -1, fd_next = -1;
     uint8_t *tx = nullptr, *rx = nullptr;
     size_t frame_cap = 0;
+    size_t tcp_block = 0;           // pipelining piece of a frame (tcp_block_bytes())
+    std::vector<hipEvent_t> tx_ev;  // one per piece of a frame's D2H
     std::atomic<bool> aborted{false};
     std::mutex mu;  // serialises host-form calls and the timer
     // host-fed pipeline (ono_ring_pull_grads_host): H2D on hstream, reduce on
@@ -163,69 +166,153 @@ template <class W> ncclDataType_t nccl_type();
 template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
 template <> ncclDataType_t nccl_type<float>() { return ncclFloat32; }
 
-// One pull_grads round of rank `pos`, exact reference hop order, wire W.
-// One hop over the reference's TCP wire (the TCP edge):
-// the f16 payload comes down from HBM into a pinned frame
+// One hop over the reference's TCP wire (the TCP edge).
+// The f16 payload comes down from HBM into a pinned frame
 //   [u64 BE len = 4 + payload][u32 BE kind = 1: DenseGrad, is_last = false][f16 LE ...]
-// (msg.rs:120-151, sink.rs:37-58, worker.rs:157-174), is sent to `next` while
-// the previous worker's frame is read (try_join!, worker_ring.rs:122-123;
+// (msg.rs:120-151, sink.rs:37-58, worker.rs:157-174) and is sent to `next`
+// while the previous worker's frame is read (try_join!, worker_ring.rs:122-123;
 // source.rs:34-57), validated as a DenseGrad of the expected length, and goes
 // up to HBM for the next fused kernel.  Frames are byte-identical to the
 // reference's, so MI355X workers and reference Rust workers can share a ring.
-int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_dev, size_t recv_bytes,
-             hipStream_t s) {
-    uint8_t *tx = r->tx, *rx = r->rx;
-    ONO_HIP(hipMemcpyAsync(tx + 12, send_dev, send_bytes, hipMemcpyDeviceToHost, s));
-    ONO_HIP(hipStreamSynchronize(s));
-    const uint64_t flen = 4 + (uint64_t)send_bytes;
-    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
-    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
-    const size_t out = 12 + send_bytes;
-    size_t sent = 0, got = 0, need = 8;
-    bool have_len = false;
-    while (sent < out || got < need) {
-        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-        struct pollfd p[2];
-        int np = 0, is = -1, ir = -1;
-        if (sent < out) { p[np].fd = r->fd_next; p[np].events = POLLOUT; p[np].revents = 0; is = np++; }
-        if (got < need) { p[np].fd = r->fd_prev; p[np].events = POLLIN; p[np].revents = 0; ir = np++; }
-        int pr = poll(p, (nfds_t)np, 1000);
-        if (pr < 0 && errno != EINTR) return set_error(ONO_E_IO, "poll: %s", strerror(errno));
-        if (pr <= 0) continue;  // re-check the abort flag once a second
-        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP))) {
-            ssize_t k = send(r->fd_next, tx + sent, out - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
-            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
-                return set_error(ONO_E_IO, "send to next worker: %s", strerror(errno));
+//
+// Pipelined in r->tcp_block pieces: the D2H of piece b+1 overlaps the send of
+// piece b (a sender thread waits on per-piece events), and each received
+// piece goes up to HBM while the next one is still on the socket.  Sending and
+// receiving run on two threads, so the two kernel-side socket copies overlap.
+size_t tcp_block_bytes() {  // env ONO_TCP_BLOCK_KIB (default 4 MiB), read once per ring
+    const char *v = getenv("ONO_TCP_BLOCK_KIB");
+    long k = v ? atol(v) : 0;
+    return k > 0 ? (size_t)k << 10 : size_t(4) << 20;
+}
+constexpr int kTcpPollMs = 100;  // abort / peer-failure latency
+
+struct TcpErr {
+    int code = ONO_OK;
+    char msg[160] = {0};
+};
+
+// Wait until `fd` is ready for `ev`; false (with e set) on abort, stop or poll error.
+bool tcp_wait(ono_ring *r, int fd, short ev, const std::atomic<bool> &stop, TcpErr &e) {
+    for (;;) {
+        if (r->aborted.load()) { e.code = ONO_E_ABORTED; snprintf(e.msg, sizeof e.msg, "ring aborted"); return false; }
+        if (stop.load()) { e.code = ONO_E_OTHER; return false; }  // the other side already failed
+        struct pollfd p = {fd, ev, 0};
+        int pr = poll(&p, 1, kTcpPollMs);
+        if (pr < 0 && errno != EINTR) {
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "poll: %s", strerror(errno)); return false;
+        }
+        if (pr > 0) return true;
+    }
+}
+
+void tcp_send_frame(ono_ring *r, size_t payload, const std::atomic<bool> &stop, TcpErr &e) {
+    const size_t blk = r->tcp_block;
+    const size_t out = 12 + payload;
+    size_t sent = 0;
+    for (size_t b = 0; sent < out; b++) {
+        const size_t ready = std::min(out, 12 + (b + 1) * blk);
+        if (payload) {
+            hipError_t he = hipEventSynchronize(r->tx_ev[b]);
+            if (he != hipSuccess) {
+                e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "D2H of a frame: %s", hipGetErrorString(he));
+                return;
+            }
+        }
+        while (sent < ready) {
+            if (!tcp_wait(r, r->fd_next, POLLOUT, stop, e)) return;
+            ssize_t k = send(r->fd_next, r->tx + sent, ready - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
+            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+                e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "send to next worker: %s", strerror(errno));
+                return;
+            }
             if (k > 0) sent += (size_t)k;
         }
-        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP))) {
-            ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
-            if (k == 0) return set_error(ONO_E_IO, "previous worker closed the connection");
-            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
-                return set_error(ONO_E_IO, "recv from previous worker: %s", strerror(errno));
-            if (k > 0) got += (size_t)k;
-            if (!have_len && got >= 8) {
-                uint64_t l = 0;
-                for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
-                if (l < 4 || 8 + l > r->frame_cap)
-                    return set_error(ONO_E_PROTO, "Received an invalid worker event (frame of %llu bytes)",
-                                     (unsigned long long)l);
-                need = 8 + (size_t)l;
-                have_len = true;
+    }
+}
+
+void tcp_recv_frame(ono_ring *r, uint8_t *recv_dev, size_t payload, hipStream_t s,
+                    const std::atomic<bool> &stop, TcpErr &e) {
+    uint8_t *rx = r->rx;
+    const size_t blk = r->tcp_block;
+    size_t got = 0, need = 12, issued = 0;
+    bool have_hdr = false;
+    while (got < need) {
+        if (!tcp_wait(r, r->fd_prev, POLLIN, stop, e)) return;
+        ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
+        if (k == 0) { e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "previous worker closed the connection"); return; }
+        if (k < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) continue;
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "recv from previous worker: %s", strerror(errno));
+            return;
+        }
+        got += (size_t)k;
+        if (!have_hdr && got >= 12) {
+            uint64_t l = 0;
+            for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
+            const uint32_t kind = (uint32_t)rx[8] << 24 | (uint32_t)rx[9] << 16 | (uint32_t)rx[10] << 8 | rx[11];
+            // only a DenseGrad of this hop's chunk is a valid event (worker_ring.rs:136-138)
+            if ((kind & 0xFF) != 1 && (kind & 0xFF) != 2) {  // Header::from_be_bytes(..) as u8 (msg.rs:168)
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind & 0xFF);
+                return;
+            }
+            if (l != 4 + (uint64_t)payload) {
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
+                         (unsigned long long)(l < 4 ? 0 : l - 4), payload);
+                return;
+            }
+            need = 12 + payload;
+            have_hdr = true;
+        }
+        if (have_hdr) {  // each complete piece goes up while the next is still arriving
+            const size_t avail = got - 12;
+            while (issued < avail && (avail - issued >= blk || avail == payload)) {
+                const size_t c = std::min(blk, payload - issued);
+                hipError_t he = hipMemcpyAsync(recv_dev + issued, rx + 12 + issued, c, hipMemcpyHostToDevice, s);
+                if (he != hipSuccess) {
+                    e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "H2D of a frame: %s", hipGetErrorString(he));
+                    return;
+                }
+                issued += c;
             }
         }
     }
-    const uint8_t kind = rx[11];  // Header::from_be_bytes(..) as u8 (msg.rs:168)
-    const size_t payload = need - 12;
-    if (kind != 1 && kind != 2)   // only a DenseGrad is a valid event here (worker_ring.rs:136-138)
-        return set_error(ONO_E_PROTO, "Received an invalid worker event (kind %u)", kind);
-    if (payload != recv_bytes)
-        return set_error(ONO_E_PROTO, "Received an invalid worker event (%zu payload bytes, expected %zu)",
-                         payload, recv_bytes);
-    ONO_HIP(hipMemcpyAsync(recv_dev, rx + 12, recv_bytes, hipMemcpyHostToDevice, s));
-    return ONO_OK;  // rx is reused only after the next hop's stream synchronisation
 }
 
+int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_dev, size_t recv_bytes,
+             hipStream_t s) {
+    uint8_t *tx = r->tx;
+    const size_t blk = r->tcp_block;
+    const uint64_t flen = 4 + (uint64_t)send_bytes;
+    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
+    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
+    const size_t nblk = (send_bytes + blk - 1) / blk;
+    if (nblk > r->tx_ev.size()) return set_error(ONO_E_ARG, "frame of %zu bytes exceeds the ring's chunk", send_bytes);
+    for (size_t b = 0; b < nblk; b++) {
+        const size_t o = b * blk, c = std::min(blk, send_bytes - o);
+        ONO_HIP(hipMemcpyAsync(tx + 12 + o, static_cast<const uint8_t *>(send_dev) + o, c, hipMemcpyDeviceToHost, s));
+        ONO_HIP(hipEventRecord(r->tx_ev[b], s));
+    }
+    // rx is free once the previous hop's H2D pieces ran: they precede piece 0's D2H on s
+    if (nblk) ONO_HIP(hipEventSynchronize(r->tx_ev[0]));
+    else ONO_HIP(hipStreamSynchronize(s));
+    std::atomic<bool> stop_send{false}, stop_recv{false};
+    TcpErr es, er;
+    std::thread sender([&] {
+        tcp_send_frame(r, send_bytes, stop_send, es);
+        if (es.code) stop_recv.store(true);
+    });
+    tcp_recv_frame(r, static_cast<uint8_t *>(recv_dev), recv_bytes, s, stop_recv, er);
+    if (er.code) stop_send.store(true);
+    sender.join();
+    // report the root cause, not the "other side failed" stop
+    const TcpErr &e = (er.code && er.code != ONO_E_OTHER) ? er : (es.code && es.code != ONO_E_OTHER) ? es : er;
+    if (e.code) return set_error(e.code, "%s", e.msg);
+    return ONO_OK;
+}
+
+// One pull_grads round of rank `pos`, exact reference hop order, wire W.
 template <class W>
 int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
     const int n = r->n, pos = r->pos;
@@ -446,6 +533,13 @@ int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int de
         ono_ring_destroy(r);
         return hip_error(e, "frame buffer allocation", __FILE__, __LINE__);
     }
+    r->tcp_block = tcp_block_bytes();
+    r->tx_ev.assign((2 * (r->maxc + 4) + r->tcp_block - 1) / r->tcp_block, nullptr);
+    for (auto &ev : r->tx_ev)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
+            ono_ring_destroy(r);
+            return hip_error(e, "frame event creation", __FILE__, __LINE__);
+        }
     *out = r;
     return ONO_OK;
 }
@@ -506,6 +600,7 @@ int ono_ring_destroy(ono_ring *r) {
             if (st) (void)hipStreamSynchronize(st);
         if (r->pin_in) (void)hipHostFree(r->pin_in);
         if (r->pin_out) (void)hipHostFree(r->pin_out);
+        for (hipEvent_t ev : r->tx_ev) (void)hipEventDestroy(ev);
         if (r->tx) (void)hipHostFree(r->tx);
         if (r->rx) (void)hipHostFree(r->rx);
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
