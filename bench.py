@@ -60,8 +60,11 @@ def parse_args(argv=None):
     ap.add_argument("--bucket-mib", type=int, default=256)
     ap.add_argument("--wire", choices=["f32", "f16"], default="f32")
     ap.add_argument("--algo", choices=["auto", "allreduce", "hops", "direct"], default="auto")
-    ap.add_argument("--alt-schedules", default="direct:f32,direct:f16,hops:f16",
-                    help="N > 1 only: extra schedules measured after the main line (algo:wire,...; '' = none)")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="f32 all-reduce pipeline segments (0 = library default: ONO_AR_SEGMENTS or 4)")
+    ap.add_argument("--alt-schedules", default="allreduce:f32:1,direct:f32,direct:f16,hops:f16",
+                    help="N > 1 only: extra schedules measured after the main line "
+                         "(algo:wire[:segments],...; '' = none)")
     ap.add_argument("--alt-timeout", type=float, default=240.0)
     ap.add_argument("--alt-at-n1", action="store_true", help="exercise the alternative-schedule plumbing at N = 1")
     ap.add_argument("--no-ps-mode", dest="ps_mode", action="store_false",
@@ -382,6 +385,7 @@ def main(argv=None) -> int:
         return ono_amd.WorkerRingManager(rank, world, elems, uid=uid, wire=wire, device=local_rank, algo=algo)
 
     ring = new_ring(args.wire, args.algo)
+    ring.set_pipeline(args.segments)
 
     nb = args.warmup + args.steps
     residuals = [torch.empty(elems, dtype=torch.float32, device="cuda") for _ in range(nb)]
@@ -453,6 +457,8 @@ def main(argv=None) -> int:
     line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
                       bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
     line["config"]["schedule"] = ring.algo
+    if world > 1 and args.wire == "f32" and ring.algo in ("auto", "allreduce"):
+        line["config"]["allreduce_segments"] = args.segments or "library default (ONO_AR_SEGMENTS or 4)"
 
     # Informational: the other exchange schedules at N > 1 (never `value`).
     # A watchdog keeps an untested-at-scale schedule from costing the main line.
@@ -470,14 +476,17 @@ def main(argv=None) -> int:
         dog.daemon = True
         dog.start()
         rings = {args.wire: ring}
-        for algo, wire in alts:
-            key = f"{algo}:{wire}"
+        for alt in alts:
+            algo, wire, seg = alt[0], alt[1], int(alt[2]) if len(alt) > 2 else args.segments
+            key = ":".join(alt)
             try:
                 if wire not in rings:
                     rings[wire] = new_ring(wire, "auto")
                 r = rings[wire]
                 r.set_algo(algo)
+                r.set_pipeline(seg)
                 el, t = measure(r)
+                r.set_pipeline(args.segments)
                 line["alt_schedules"][key] = {
                     "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
                     "ms_per_step": round(el / args.steps * 1e3, 4),

@@ -174,6 +174,12 @@ int ono_ring_unregister_host(ono_ring *ring, void *ptr);
  *              all-gather; bit-exact for both wires; n <= ONO_MAX_INPUTS     */
 typedef enum { ONO_ALGO_AUTO = 0, ONO_ALGO_ALLREDUCE = 1, ONO_ALGO_HOPS = 2, ONO_ALGO_DIRECT = 3 } ono_algo;
 int ono_ring_set_algo(ono_ring *ring, int algo);
+/* Segments of the f32 all-reduce schedule (ONO_ALGO_ALLREDUCE): with k > 1
+ * the fused finaliser (÷n, residual = 0) of segment j overlaps the RCCL
+ * all-reduce of segment j+1; 1 = one all-reduce then one finaliser; 0 = the
+ * default (env ONO_AR_SEGMENTS, else 4).  At least 16 MiB per segment.  Results do
+ * not depend on it beyond RCCL's own summation order.                       */
+int ono_ring_set_pipeline(ono_ring *ring, int segments);
 /* in-place averaged all-reduce of a device buffer (buf = sum_r buf_r / n) */
 int ono_ring_allreduce_avg_dev(ono_ring *ring, float *buf_dev, size_t n, void *stream);
 /* Cancellation: makes the in-flight and every later call fail with

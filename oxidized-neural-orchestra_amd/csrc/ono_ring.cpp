@@ -136,6 +136,12 @@ struct ono_ring {
     size_t frame_cap = 0;
     size_t tcp_block = 0;           // pipelining piece of a frame (tcp_block_bytes())
     std::vector<hipEvent_t> tx_ev;  // one per piece of a frame's D2H
+    // segmented f32 all-reduce (ono_ring_set_pipeline): the finaliser of
+    // segment k runs on astream while segment k+1 is still on the wire
+    int segments = 0;  // 0 = unresolved: env ONO_AR_SEGMENTS, default 4
+    hipStream_t astream = nullptr;
+    std::vector<hipEvent_t> ev_seg;
+    hipEvent_t ev_ajoin = nullptr;
     std::atomic<bool> aborted{false};
     std::mutex mu;  // serialises host-form calls and the timer
     // host-fed pipeline (ono_ring_pull_grads_host): H2D on hstream, reduce on
@@ -451,22 +457,78 @@ int resolved_algo(const ono_ring *r) {
     return r->wire == ONO_WIRE_F32 ? ONO_ALGO_ALLREDUCE : ONO_ALGO_HOPS;
 }
 
-int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
-    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-    if (r->n == 1) {  // worker_ring.rs:166-171: grad = residual; residual = 0; no ÷
-        ONO_K(r, s, launch_scale_zero(grad, res, r->size, 1.0f, res, s));
-        return ONO_OK;
+int ar_segments(ono_ring *r) {
+    if (r->segments <= 0) {
+        const char *v = getenv("ONO_AR_SEGMENTS");
+        const int k = v ? atoi(v) : 0;
+        r->segments = k > 0 ? k : 4;
     }
-    switch (resolved_algo(r)) {
-    case ONO_ALGO_ALLREDUCE: {
-        int rc = timed(r, s, 1, [&]() -> int {
+    const size_t by_size = std::max<size_t>(1, r->size / (size_t(4) << 20));  // >= 16 MiB per segment
+    return (int)std::min<size_t>((size_t)r->segments, by_size);
+}
+
+// n == 1 with ONO_ALGO_ALLREDUCE (tests, bench plumbing): a one-rank communicator
+int ensure_comm(ono_ring *r) {
+    if (r->comm) return ONO_OK;
+    ncclUniqueId id;
+    ONO_NCCL(ncclGetUniqueId(&id));
+    ONO_NCCL(ncclCommInitRank(&r->comm, 1, id, 0));
+    return ONO_OK;
+}
+
+// grad = (sum over ranks of res) / n, res = 0: RCCL all-reduce + fused finaliser.
+// With k > 1 segments the finaliser of segment j (on astream) overlaps the
+// all-reduce of segment j+1 (on s); every element still sees one all-reduce and
+// one finaliser, so the result is the unsegmented one.
+int allreduce_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    int rc = ensure_comm(r);
+    if (rc) return rc;
+    const float fn = (float)r->n;
+    const int nseg = ar_segments(r);
+    if (nseg <= 1) {
+        rc = timed(r, s, 1, [&]() -> int {
             ONO_NCCL(ncclAllReduce(res, grad, r->size, ncclFloat32, ncclSum, r->comm, s));
             return ONO_OK;
         });
         if (rc) return rc;
-        ONO_K(r, s, launch_scale_zero(grad, grad, r->size, (float)r->n, res, s));
+        ONO_K(r, s, launch_scale_zero(grad, grad, r->size, fn, res, s));
         return ONO_OK;
     }
+    if (!r->astream) {
+        ONO_HIP(hipStreamCreateWithFlags(&r->astream, hipStreamNonBlocking));
+        ONO_HIP(hipEventCreateWithFlags(&r->ev_ajoin, hipEventDisableTiming));
+    }
+    while (r->ev_seg.size() < (size_t)nseg) {
+        hipEvent_t ev;
+        ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        r->ev_seg.push_back(ev);
+    }
+    const size_t seg = ((r->size + nseg - 1) / nseg + 63) & ~size_t(63);  // 256-B aligned segments
+    for (int k = 0; k < nseg && (size_t)k * seg < r->size; k++) {
+        const size_t lo = (size_t)k * seg, len = std::min(seg, r->size - lo);
+        rc = timed(r, s, 1, [&]() -> int {
+            ONO_NCCL(ncclAllReduce(res + lo, grad + lo, len, ncclFloat32, ncclSum, r->comm, s));
+            return ONO_OK;
+        });
+        if (rc) return rc;
+        ONO_HIP(hipEventRecord(r->ev_seg[k], s));
+        ONO_HIP(hipStreamWaitEvent(r->astream, r->ev_seg[k], 0));
+        ONO_K(r, r->astream, launch_scale_zero(grad + lo, grad + lo, len, fn, res + lo, r->astream));
+    }
+    ONO_HIP(hipEventRecord(r->ev_ajoin, r->astream));
+    ONO_HIP(hipStreamWaitEvent(s, r->ev_ajoin, 0));
+    return ONO_OK;
+}
+
+int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    if (r->n == 1 && r->algo != ONO_ALGO_ALLREDUCE) {  // worker_ring.rs:166-171: grad = residual; residual = 0; no ÷
+        ONO_K(r, s, launch_scale_zero(grad, res, r->size, 1.0f, res, s));
+        return ONO_OK;
+    }
+    switch (resolved_algo(r)) {
+    case ONO_ALGO_ALLREDUCE:
+        return allreduce_impl(r, res, grad, s);
     case ONO_ALGO_HOPS:
         return r->wire == ONO_WIRE_F16 ? ring_hops<uint16_t>(r, res, grad, s) : ring_hops<float>(r, res, grad, s);
     case ONO_ALGO_DIRECT:
@@ -607,12 +669,15 @@ int ono_ring_destroy(ono_ring *r) {
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);
         if (r->zstream) (void)hipStreamSynchronize(r->zstream);
+        if (r->astream) (void)hipStreamSynchronize(r->astream);
+        for (hipEvent_t ev : r->ev_seg) (void)hipEventDestroy(ev);
+        if (r->ev_ajoin) (void)hipEventDestroy(r->ev_ajoin);
         (void)hipFree(r->rbuf);
         (void)hipFree(r->gstage);
         (void)hipFree(r->msg);
         for (hipEvent_t ev : {r->ev_fork, r->ev_join})
             if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t st : {r->hstream, r->cstream, r->dstream, r->zstream})
+        for (hipStream_t st : {r->hstream, r->cstream, r->dstream, r->zstream, r->astream})
             if (st) (void)hipStreamDestroy(st);
     }
     delete r;
@@ -821,6 +886,14 @@ int ono_ring_set_algo(ono_ring *r, int algo) {
         return set_error(ONO_E_ARG, "a TCP ring runs the reference hop schedule only");
     std::lock_guard<std::mutex> lk(r->mu);
     r->algo = r->fd_next >= 0 ? ONO_ALGO_HOPS : algo;
+    return ONO_OK;
+}
+
+int ono_ring_set_pipeline(ono_ring *r, int segments) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    if (segments < 0) return set_error(ONO_E_ARG, "segments %d", segments);
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->segments = segments;  // 0: back to the default
     return ONO_OK;
 }
 

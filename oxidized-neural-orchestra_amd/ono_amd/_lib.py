@@ -98,6 +98,7 @@ _SIGS = {
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
     "ono_ring_create_tcp": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i, _i]),
     "ono_ring_destroy": (_i, [_vp]),
+    "ono_ring_set_pipeline": (_i, [_vp, _i]),
     "ono_ring_grad": (C.c_void_p, [_vp]),
     "ono_ring_residual": (C.c_void_p, [_vp]),
     "ono_ring_size": (_sz, [_vp]),

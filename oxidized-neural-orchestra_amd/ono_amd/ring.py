@@ -175,6 +175,11 @@ class WorkerRingManager:
         call("ono_ring_set_algo", self._h, ALGO[algo])
         self.algo = algo
 
+    def set_pipeline(self, segments: int) -> None:
+        """Segments of the f32 all-reduce schedule (finaliser of segment j
+        overlaps the all-reduce of segment j+1); 1 = unsegmented, 0 = default."""
+        call("ono_ring_set_pipeline", self._h, segments)
+
     def abort(self) -> None:
         call("ono_ring_abort", self._h)
 

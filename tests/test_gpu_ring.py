@@ -297,3 +297,29 @@ def test_ring_set_algo_n1(algo):
     with pytest.raises(ono_amd.InvalidArgument):
         f16ring.set_algo("allreduce")
     f16ring.close()
+
+
+@pytest.mark.parametrize("segments", [1, 2, 4, 7])
+def test_allreduce_pipeline_segments_n1(segments):
+    """The segmented f32 all-reduce schedule (finaliser of segment j on a side
+    stream, overlapping the all-reduce of segment j+1) through a real one-rank
+    RCCL communicator: every round's grad is its own residual, bit for bit, and
+    every residual ends zeroed — a finaliser that ran ahead of its all-reduce
+    would leave zeros or a stale round in grad."""
+    length = (1 << 25) + 37
+    ring = ono_amd.WorkerRingManager(0, 1, length, algo="allreduce")
+    ring.set_pipeline(segments)
+    s = torch.cuda.Stream()
+    grad = torch.full((length,), 7.0, device=DEV)
+    xs = [to_dev(O.synth(length, SEED + 40 + k, 0)) for k in range(3)]
+    res = [x.clone() for x in xs]
+    try:
+        with torch.cuda.stream(s):
+            for k in range(3):
+                ring.pull_grads_dev(res[k], grad, s)
+                out = grad.clone()
+                torch.cuda.current_stream().synchronize()
+                assert torch.equal(out.view(torch.int32), xs[k].view(torch.int32)), f"round {k}"
+                assert not res[k].view(torch.int32).any()
+    finally:
+        ring.close()
