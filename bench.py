@@ -230,7 +230,9 @@ def _cpu_model() -> str:
 # ---------------------------------------------------------- local reduce
 def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
     """BASELINE config 2: ono_sum_scale_f32 over k 64 MiB buckets (÷k),
-    device time from HIP events on the launch stream.  Launches rotate over
+    device time from one HIP event pair on the launch stream around the K
+    back-to-back launches (per-launch event pairs add ~2 us to a 30 us
+    kernel, tools/stream_variants.hip "pull" mode).  Launches rotate over
     enough input/output sets that every launch reads from HBM (the working
     set exceeds the 256 MiB Infinity Cache by > 4x)."""
     n = 16 << 20
@@ -247,14 +249,15 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
         for i in range(warmup):
             ins, dst = sets[i % nsets]
             ono_amd.kernels.sum_scale(dst, ins, float(k))
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-        for i, (a, b) in enumerate(evs):
-            ins, dst = sets[(warmup + i) % nsets]
-            a.record(stream)
-            ono_amd.kernels.sum_scale(dst, ins, float(k))
-            b.record(stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
-        ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+        a.record(stream)
+        for i in range(steps):
+            ins, dst = sets[(warmup + i) % nsets]
+            ono_amd.kernels.sum_scale(dst, ins, float(k))
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / steps
         nbytes = (k + 1) * 4 * n
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[f"k{k}"] = {"bytes_per_launch": nbytes, "us_per_launch": round(ms * 1e3, 2),
@@ -263,6 +266,7 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
         del sets
         torch.cuda.empty_cache()
     return {"workload": "sum_scale_f32, 64 MiB buckets, out = (sum of k inputs) / k", "hbm_peak_gbs": HBM_PEAK_GBS,
+            "timing": "one HIP event pair around K back-to-back launches (inter-kernel gaps included)",
             **out}
 
 

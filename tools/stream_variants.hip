@@ -260,6 +260,21 @@ int main(int argc, char **argv) {
             for (int B : {256, 64})
                 for (bool fx : {true, false})
                     for (bool pe : {false, true}) pull_shape(P, s, fx, pe, B);
+    } else if (mode[0] == 'k') {  // sum_scale block size with nt loads (config 2 shape)
+        for (int rep = 0; rep < 2; rep++) {
+            row2<2, false, 64, 1, true>(P, s, "sum2 2R1W");
+            row2<2, false, 128, 1, true>(P, s, "sum2 2R1W");
+            row2<2, false, 256, 1, true>(P, s, "sum2 2R1W");
+            row2<4, false, 64, 1, true>(P, s, "sum4 4R1W");
+            row2<4, false, 128, 1, true>(P, s, "sum4 4R1W");
+            row2<4, false, 256, 1, true>(P, s, "sum4 4R1W");
+            row2<4, false, 512, 1, true>(P, s, "sum4 4R1W");
+            row2<8, false, 64, 1, true>(P, s, "sum8 8R1W");
+            row2<8, false, 128, 1, true>(P, s, "sum8 8R1W");
+            row2<8, false, 256, 1, true>(P, s, "sum8 8R1W");
+            row2<8, false, 512, 1, true>(P, s, "sum8 8R1W");
+            row2<8, false, 256, 2, true>(P, s, "sum8 8R1W");
+        }
     } else if (mode[0] == 'a') {
         sweep<1, false>(P, cus, s, "copy 1R1W");
         sweep<1, true>(P, cus, s, "copy+zero 1R2W");
