@@ -25,6 +25,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -114,6 +117,98 @@ inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to 
 
 }  // namespace
 
+namespace {
+
+// Host-side copy pool for the pageable host-fed form: the CPU copies between
+// the caller's pageable buckets and the pinned bounce slots (and the residual
+// zeroing) are split over T threads, so they keep up with PCIe Gen5 DMA.
+// T = env ONO_HOST_THREADS (default 8, at most the hardware threads).
+class HostPool {
+public:
+    explicit HostPool(int t) : nt_(std::max(1, t)) {
+        for (int i = 1; i < nt_; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int threads() const { return nt_; }
+    // f(part, nparts) on every thread (the caller runs part 0); returns when all are done
+    void run(const std::function<void(int, int)> &f) {
+        if (nt_ == 1) { f(0, 1); return; }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f;
+            pending_ = nt_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0, nt_);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    void copy(void *dst, const void *src, size_t bytes) {
+        run([&](int i, int k) {
+            size_t lo, len;
+            part(bytes, i, k, lo, len);
+            if (len) memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
+        });
+    }
+    void zero(void *dst, size_t bytes) {
+        run([&](int i, int k) {
+            size_t lo, len;
+            part(bytes, i, k, lo, len);
+            if (len) memset(static_cast<char *>(dst) + lo, 0, len);
+        });
+    }
+
+private:
+    static void part(size_t bytes, int i, int k, size_t &lo, size_t &len) {
+        size_t per = ((bytes + k - 1) / k + 4095) & ~size_t(4095);  // page-aligned pieces
+        lo = std::min(bytes, per * i);
+        len = std::min(bytes - lo, per);
+    }
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int, int)> *f;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(i, nt_);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    int nt_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int, int)> *job_ = nullptr;
+    int pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+int host_threads() {
+    const char *e = getenv("ONO_HOST_THREADS");
+    long t = e ? atol(e) : 8;
+    long hw = (long)std::thread::hardware_concurrency();
+    if (hw > 0) t = std::min(t, hw);
+    return (int)std::max(1L, t);
+}
+
+}  // namespace
+
 struct ono_ring {
     int pos = 0, n = 1, device = 0, wire = ONO_WIRE_F32;
     size_t size = 0;
@@ -148,6 +243,7 @@ struct ono_ring {
     // cstream, D2H on dstream; pinned bounce slots for unregistered buffers
     hipStream_t hstream = nullptr, cstream = nullptr, dstream = nullptr;
     float *pin_in = nullptr, *pin_out = nullptr;  // kSlots x chunk elements each
+    std::unique_ptr<HostPool> pool;               // CPU copies of the bounce path
     std::vector<hipEvent_t> ev_h, ev_c, ev_d;
     std::vector<std::pair<void *, size_t>> registered;  // ono_ring_register_host
     Timer timer;
@@ -805,6 +901,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const size_t nch = (n + CH - 1) / CH;
     int rc = ensure_events(r, nch);
     if (rc) return rc;
+    if (!r->pool) r->pool.reset(new HostPool(host_threads()));
     if (!reg && !r->pin_in) {
         ONO_HIP(hipHostMalloc((void **)&r->pin_in, kSlots * CH * sizeof(float), hipHostMallocDefault));
         ONO_HIP(hipHostMalloc((void **)&r->pin_out, kSlots * CH * sizeof(float), hipHostMallocDefault));
@@ -813,7 +910,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     auto len_of = [&](size_t c) { return std::min(CH, n - c * CH); };
     auto drain_out = [&](size_t c) -> int {  // bounce path: wait D2H of chunk c, copy to caller
         ONO_HIP(hipEventSynchronize(r->ev_d[c]));
-        memcpy(grad_host + lo_of(c), r->pin_out + (c % kSlots) * CH, len_of(c) * sizeof(float));
+        r->pool->copy(grad_host + lo_of(c), r->pin_out + (c % kSlots) * CH, len_of(c) * sizeof(float));
         return ONO_OK;
     };
     for (size_t c = 0; c < nch; c++) {
@@ -823,7 +920,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
         if (!reg) {
             if (c >= (size_t)kSlots && (rc = drain_out(c - kSlots))) return rc;  // slot free again
             float *slot_in = r->pin_in + (c % kSlots) * CH;
-            memcpy(slot_in, src, cb);
+            r->pool->copy(slot_in, src, cb);
             src = slot_in;
             dst = r->pin_out + (c % kSlots) * CH;
         }
@@ -836,15 +933,15 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
         ONO_HIP(hipMemcpyAsync(dst, r->grad + lo, cb, hipMemcpyDeviceToHost, r->dstream));
         ONO_HIP(hipEventRecord(r->ev_d[c], r->dstream));
         if (!reg) {
-            memset(res_host + lo, 0, cb);  // already copied to the bounce slot
+            r->pool->zero(res_host + lo, cb);  // already copied to the bounce slot
         } else if (c > 0) {
             ONO_HIP(hipEventSynchronize(r->ev_h[c - 1]));  // chunk c-1 has reached HBM
-            memset(res_host + lo_of(c - 1), 0, len_of(c - 1) * sizeof(float));
+            r->pool->zero(res_host + lo_of(c - 1), len_of(c - 1) * sizeof(float));
         }
     }
     if (reg) {
         ONO_HIP(hipEventSynchronize(r->ev_h[nch - 1]));
-        memset(res_host + lo_of(nch - 1), 0, len_of(nch - 1) * sizeof(float));
+        r->pool->zero(res_host + lo_of(nch - 1), len_of(nch - 1) * sizeof(float));
         ONO_HIP(hipStreamSynchronize(r->dstream));
     } else {
         for (size_t c = nch > (size_t)kSlots ? nch - kSlots : 0; c < nch; c++)
