@@ -446,7 +446,7 @@ def main(argv=None) -> int:
         if pmc:
             extra["roofline"]["traffic_source"] = pmc["source"]
     else:
-        extra["roofline"] = xgmi_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo)
+        extra["roofline"] = xgmi_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo, args.steps)
 
     if rank == 0 and world == 1 and not args.no_host_fed:
         extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
@@ -494,7 +494,7 @@ def main(argv=None) -> int:
                 line["alt_schedules"][key] = {
                     "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
                     "ms_per_step": round(el / args.steps * 1e3, 4),
-                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo)}
+                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps)}
             except Exception as e:  # recorded, never fatal for the main line
                 line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if args.ps_mode:  # BASELINE config 5: sharded synchronizer, RS + fused GD + AG
@@ -528,20 +528,20 @@ def main(argv=None) -> int:
     return 0
 
 
-def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: str, algo: str) -> dict:
+def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: str, algo: str,
+                  steps: int) -> dict:
     """N > 1: the exchange is xGMI-bound.  achieved = bytes each rank sends per
     step / the step's collective time (HIP events on the launch stream); peak =
     the N-1 direct links a rank can drive at once, 76.8 GB/s each per direction.
     For the RCCL ring all-reduce the bytes are its busBW bytes 2(N-1)/N x bucket."""
     wb = 2 if wire == "f16" else 4
     if algo in ("allreduce", "auto") and wire == "f32":
-        bytes_out, colls = 2 * (world - 1) / world * bucket_bytes, 1           # ring all-reduce
+        bytes_out = 2 * (world - 1) / world * bucket_bytes            # ring all-reduce (any segmentation)
     elif algo == "direct":
-        bytes_out, colls = (world - 1) / world * (bucket_bytes + elems * wb), 2  # all-to-all f32 + all-gather
+        bytes_out = (world - 1) / world * (bucket_bytes + elems * wb)  # all-to-all f32 + all-gather
     else:
-        bytes_out, colls = 2 * (world - 1) / world * elems * wb, 2 * (world - 1)  # n-1 + n-1 hops
-    n = max(tim["collectives"], 1)
-    step_coll_ms = tim["collective_ms"] * colls / n
+        bytes_out = 2 * (world - 1) / world * elems * wb              # n-1 + n-1 hops
+    step_coll_ms = tim["collective_ms"] / max(steps, 1)  # timing is enabled for the K timed steps only
     ach = bytes_out / (step_coll_ms * 1e-3) / 1e9 if step_coll_ms > 0 else None
     peak = XGMI_LINK_GBS * (world - 1)
     kern_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
