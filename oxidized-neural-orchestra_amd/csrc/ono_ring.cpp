@@ -122,7 +122,9 @@ namespace {
 // Host-side copy pool for the pageable host-fed form: the CPU copies between
 // the caller's pageable buckets and the pinned bounce slots (and the residual
 // zeroing) are split over T threads, so they keep up with PCIe Gen5 DMA.
-// T = env ONO_HOST_THREADS (default 8, at most the hardware threads).
+// T = env ONO_HOST_THREADS (default 16, at most the hardware threads).  The
+// registered form does not use it: its only CPU work is zeroing the residual,
+// and a single thread there leaves the host memory bandwidth to the DMA.
 class HostPool {
 public:
     explicit HostPool(int t) : nt_(std::max(1, t)) {
@@ -201,7 +203,7 @@ private:
 
 int host_threads() {
     const char *e = getenv("ONO_HOST_THREADS");
-    long t = e ? atol(e) : 8;
+    long t = e ? atol(e) : 16;
     long hw = (long)std::thread::hardware_concurrency();
     if (hw > 0) t = std::min(t, hw);
     return (int)std::max(1L, t);
@@ -901,7 +903,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const size_t nch = (n + CH - 1) / CH;
     int rc = ensure_events(r, nch);
     if (rc) return rc;
-    if (!r->pool) r->pool.reset(new HostPool(host_threads()));
+    if (!reg && !r->pool) r->pool.reset(new HostPool(host_threads()));
     if (!reg && !r->pin_in) {
         ONO_HIP(hipHostMalloc((void **)&r->pin_in, kSlots * CH * sizeof(float), hipHostMallocDefault));
         ONO_HIP(hipHostMalloc((void **)&r->pin_out, kSlots * CH * sizeof(float), hipHostMallocDefault));
@@ -936,12 +938,13 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
             r->pool->zero(res_host + lo, cb);  // already copied to the bounce slot
         } else if (c > 0) {
             ONO_HIP(hipEventSynchronize(r->ev_h[c - 1]));  // chunk c-1 has reached HBM
-            r->pool->zero(res_host + lo_of(c - 1), len_of(c - 1) * sizeof(float));
+            memset(res_host + lo_of(c - 1), 0, len_of(c - 1) * sizeof(float));  // one thread: leaves the
+                                                                                 // host memory to the DMA
         }
     }
     if (reg) {
         ONO_HIP(hipEventSynchronize(r->ev_h[nch - 1]));
-        r->pool->zero(res_host + lo_of(nch - 1), len_of(nch - 1) * sizeof(float));
+        memset(res_host + lo_of(nch - 1), 0, len_of(nch - 1) * sizeof(float));
         ONO_HIP(hipStreamSynchronize(r->dstream));
     } else {
         for (size_t c = nch > (size_t)kSlots ? nch - kSlots : 0; c < nch; c++)
