@@ -1,8 +1,10 @@
 // ono_harness.cpp — a C++ host program driving libono_reduce.so through its
 // C ABI only (include/ono_reduce.h), the way the reference's Rust crates would
 // bind it.  It plays one WorkerRingManager round (n = 1 on this box: the
-// device path of pull_grads) on host buckets, a BlockingStore + BarrierSync
-// round with three worker threads, and checks both against the C oracle.
+// device path of pull_grads) on host buckets, a three-worker ring over the
+// TCP edge (socket pairs, one thread per worker, host buckets), and a
+// BlockingStore + BarrierSync round with three worker threads, and checks all
+// three against the C oracle.
 //
 //   make -C tools harness && tools/ono_harness [n_elems]
 // exit 0 = bit-exact, 1 = mismatch, 2 = library error.
@@ -10,6 +12,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+
+#include <sys/socket.h>
+#include <unistd.h>
 #include <vector>
 
 #include "ono_oracle.h"
@@ -48,6 +53,41 @@ int main(int argc, char **argv) {
     CHECK(ono_ring_unregister_host(ring, grad.data()));
     CHECK(ono_ring_destroy(ring));
     printf("ring pull_grads_host (n=1, %zu elems): %s\n", n, ok ? "bit-exact" : "MISMATCH");
+
+    // ---- TCP edge: three workers in one ring over socket pairs (builder.rs:272-311
+    // hands each worker its prev/next connections), host buckets, f16 frames
+    const int nr = 3;
+    const size_t nt = 300007;
+    int sp[nr][2];  // pair i carries worker i -> worker i+1
+    for (auto &p : sp)
+        if (socketpair(AF_UNIX, SOCK_STREAM, 0, p)) { perror("socketpair"); return 2; }
+    std::vector<std::vector<float>> tres(nr, std::vector<float>(nt)), tgrad(nr, std::vector<float>(nt, 7.0f));
+    for (int r = 0; r < nr; r++) ono_ref_synth(tres[r].data(), nt, seed + 9, (uint64_t)r, 0);
+    std::vector<std::vector<float>> eres = tres, egrad(nr, std::vector<float>(nt));
+    std::vector<int> trc(nr, ONO_OK);
+    std::vector<std::thread> tw;
+    for (int r = 0; r < nr; r++)
+        tw.emplace_back([&, r] {
+            ono_ring *tr = nullptr;
+            int rc = ono_ring_create_tcp(&tr, r, nr, nt, 0, sp[(r + nr - 1) % nr][1], sp[r][0]);
+            if (rc == ONO_OK) rc = ono_ring_pull_grads_host(tr, tres[r].data(), tgrad[r].data(), nt);
+            if (rc != ONO_OK) fprintf(stderr, "worker %d: %s\n", r, ono_last_error());
+            if (tr) ono_ring_destroy(tr);
+            trc[r] = rc;
+        });
+    for (auto &t : tw) t.join();
+    for (auto &p : sp) { close(p[0]); close(p[1]); }
+    for (int rc : trc)
+        if (rc != ONO_OK) return 2;
+    {
+        std::vector<float *> rp(nr), gp(nr);
+        for (int r = 0; r < nr; r++) { rp[r] = eres[r].data(); gp[r] = egrad[r].data(); }
+        ono_ref_ring_pull_grads(rp.data(), gp.data(), nr, nt, 0);
+    }
+    bool ok3 = true;
+    for (int r = 0; r < nr; r++) ok3 &= same(tgrad[r].data(), egrad[r].data(), nt) && same(tres[r].data(), eres[r].data(), nt);
+    printf("TCP edge ring (3 workers, socket pairs, %zu elems, host buckets): %s\n", nt, ok3 ? "bit-exact" : "MISMATCH");
+    ok &= ok3;
 
     // ---- PS: BlockingStore + BarrierSync, three worker threads, Adam
     const int nw = 3, rounds = 4;
