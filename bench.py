@@ -406,13 +406,13 @@ def main(argv=None) -> int:
         N = 1: a step is exactly one kernel, so one HIP event pair around the
         timed region gives its average launch duration without per-launch
         events (which add ~6 % to a 130 us stream, tools/stream_variants.hip
-        "pull" mode).  N > 1: per-launch events split collectives and kernels."""
+        "pull" mode).  N > 1: the timed run has no per-launch events; a second
+        run of the same K steps records them to split collectives and kernels
+        for the roofline."""
         refill()
         span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
 
         def on_start():
-            if world > 1:
-                r.timing(True)
             span[0].record(stream)
 
         def step(i: int) -> None:
@@ -422,11 +422,16 @@ def main(argv=None) -> int:
 
         el, _ = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl, on_start=on_start)
         span_ms = span[0].elapsed_time(span[1])
-        tim = (r.timing_read() if world > 1 else
-               {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0})
+        if world == 1:
+            return el, {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0}
+        refill()
+        timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl, on_start=lambda: r.timing(True))
+        tim = r.timing_read()
         r.timing(False)
         return el, tim
 
+    link = xgmi_link_probe(torch) if (world > 1 and rank == 0) else None
+    ctl.barrier()
     elapsed, tim = measure(ring)
 
     extra = {}
@@ -447,6 +452,11 @@ def main(argv=None) -> int:
             extra["roofline"]["traffic_source"] = pmc["source"]
     else:
         extra["roofline"] = xgmi_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo, args.steps)
+        if link:
+            extra["roofline"]["link_probe"] = link
+            if extra["roofline"]["achieved"] and link.get("gbs"):
+                extra["roofline"]["frac_of_measured_links"] = round(
+                    extra["roofline"]["achieved"] / (link["gbs"] * (world - 1)), 4)
 
     if rank == 0 and world == 1 and not args.no_host_fed:
         extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
@@ -526,6 +536,36 @@ def main(argv=None) -> int:
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0
+
+
+def xgmi_link_probe(torch) -> dict | None:
+    """calibrate the xGMI denominator with a measured one-link
+    copy.  Rank 0 (alone, the other ranks wait at a barrier) copies 256 MiB
+    from its GPU to the next one (hipMemcpyPeerAsync under torch), 10 times;
+    None when this process sees a single device."""
+    try:
+        if torch.cuda.device_count() < 2:
+            return None
+        src_dev = torch.cuda.current_device()
+        dst_dev = (src_dev + 1) % torch.cuda.device_count()
+        a = torch.ones(1 << 26, dtype=torch.float32, device=f"cuda:{src_dev}")
+        b = torch.empty(1 << 26, dtype=torch.float32, device=f"cuda:{dst_dev}")
+        for _ in range(2):
+            b.copy_(a)
+        torch.cuda.synchronize(src_dev)
+        torch.cuda.synchronize(dst_dev)
+        t0 = time.perf_counter()
+        for _ in range(10):
+            b.copy_(a)
+        torch.cuda.synchronize(src_dev)
+        torch.cuda.synchronize(dst_dev)
+        t = (time.perf_counter() - t0) / 10
+        del a, b
+        torch.cuda.empty_cache()
+        return {"gbs": round((1 << 28) / t / 1e9, 1), "bytes": 1 << 28,
+                "what": f"cuda:{src_dev} -> cuda:{dst_dev} device copy, one direction, 10 x 256 MiB"}
+    except Exception as e:  # informational only
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
 
 
 def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: str, algo: str,
