@@ -65,7 +65,9 @@ def parse_args(argv=None):
     ap.add_argument("--alt-schedules", default="allreduce:f32:1,direct:f32,direct:f16,hops:f16",
                     help="N > 1 only: extra schedules measured after the main line "
                          "(algo:wire[:segments],...; '' = none)")
-    ap.add_argument("--alt-timeout", type=float, default=240.0)
+    ap.add_argument("--sweep-mib", default="1,4,16,64,256,1024",
+                    help="N > 1 (or --alt-at-n1): bucket-size sweep of the main schedule, MiB list ('' = none)")
+    ap.add_argument("--alt-timeout", type=float, default=300.0)
     ap.add_argument("--alt-at-n1", action="store_true", help="exercise the alternative-schedule plumbing at N = 1")
     ap.add_argument("--no-ps-mode", dest="ps_mode", action="store_false",
                     help="skip the N > 1 parameter-server (RS + update + AG) measurement")
@@ -197,6 +199,17 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
     r = O.cpu_ring(ranks, bucket_elems, rounds, check=False, pin=True, timeout=900)
     hop = O.cpu_ps("hop", bucket_elems // ranks, rounds=rounds)
     ps = O.cpu_ps("ps", bucket_elems, threads=16, workers=ranks, rounds=rounds)
+    try:  # -march=native variants, compiled here for this host (BASELINE.md CPU plan)
+        import tempfile
+        with tempfile.TemporaryDirectory() as d:
+            exes = O.build_native(d)
+            rn = O.cpu_ring(ranks, bucket_elems, rounds, check=False, pin=True, timeout=900,
+                            exe=exes["ono_cpu_ring"])
+            hn = O.cpu_ps("hop", bucket_elems // ranks, rounds=rounds, exe=exes["ono_cpu_ps"])
+        native = {"ring_gib_s": round(rn["gib_s"], 4), "hop_compute_1core_gib_s": hn["gib_s"],
+                  "flags": "-O3 -march=native (built on this host)"}
+    except Exception as e:  # reported, never fatal
+        native = {"error": f"{type(e).__name__}: {e}"[:200]}
     return {
         "value": round(r["gib_s"], 4),
         "unit": "GiB/s",
@@ -213,6 +226,7 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
         "ps_accumulate_update": {"gib_s": ps["gib_s"], "s_per_round": ps["s_per_round"], "cores": ps["threads"],
                                  "sample": f"BlockingStore: {ps['workers']} accumulates + 1 update (÷n, GD) of "
                                            f"{ps['len']} params, {ps['shards']} shards on {ps['threads']} pinned cores"},
+        "march_native": native,
     }
 
 
@@ -383,10 +397,10 @@ def main(argv=None) -> int:
     elems = args.bucket_mib * (1 << 20) // 4
     bucket_bytes = elems * 4
 
-    def new_ring(wire: str, algo: str):
+    def new_ring(wire: str, algo: str, size: int = elems):
         uid = ono_amd.unique_id() if (world > 1 and rank == 0) else None
         uid = ctl.bcast_bytes(uid) if world > 1 else None
-        return ono_amd.WorkerRingManager(rank, world, elems, uid=uid, wire=wire, device=local_rank, algo=algo)
+        return ono_amd.WorkerRingManager(rank, world, size, uid=uid, wire=wire, device=local_rank, algo=algo)
 
     ring = new_ring(args.wire, args.algo)
     ring.set_pipeline(args.segments)
@@ -476,8 +490,9 @@ def main(argv=None) -> int:
 
     # Informational: the other exchange schedules at N > 1 (never `value`).
     # A watchdog keeps an untested-at-scale schedule from costing the main line.
-    alts = [a.split(":") for a in args.alt_schedules.split(",") if a] if (world > 1 or args.alt_at_n1) else []
-    if alts:
+    extras = world > 1 or args.alt_at_n1
+    alts = [a.split(":") for a in args.alt_schedules.split(",") if a] if extras else []
+    if extras:
         line["alt_schedules"] = {}
 
         def fire():
@@ -507,6 +522,8 @@ def main(argv=None) -> int:
                     "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps)}
             except Exception as e:  # recorded, never fatal for the main line
                 line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if args.sweep_mib:  # BASELINE config 4: the bandwidth-vs-bucket-size curve, main schedule
+            line["size_sweep"] = size_sweep(torch, ono_amd, ctl, new_ring, args, world, rank, stream)
         if args.ps_mode:  # BASELINE config 5: sharded synchronizer, RS + fused GD + AG
             try:
                 import numpy as np
@@ -536,6 +553,34 @@ def main(argv=None) -> int:
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0
+
+
+def size_sweep(torch, ono_amd, ctl, new_ring, args, world: int, rank: int, stream) -> dict:
+    """pull_grads of the main schedule over bucket sizes
+    1 MiB … 1 GiB (10 timed + 3 warmup steps each, a fresh bucket per step,
+    max over ranks).  Informational; `value` stays the 256 MiB line."""
+    out = {}
+    for mib in [int(x) for x in args.sweep_mib.split(",") if x]:
+        try:
+            e = mib << 18
+            r = new_ring(args.wire, args.algo, e)
+            r.set_pipeline(args.segments)
+            k, w = 10, 3
+            bufs = [torch.empty(e, dtype=torch.float32, device="cuda") for _ in range(k + w)]
+            for i, t in enumerate(bufs):
+                ono_amd.kernels.synth(t, SEED + i, rank)
+            g = torch.empty(e, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            el, _ = timed_region(lambda i: r.pull_grads_dev(bufs[i], g, stream), k, w, torch.cuda.synchronize, ctl)
+            alg = e * 4 * k / el / GIB
+            out[f"{mib}MiB"] = {"ms_per_step": round(el / k * 1e3, 4), "algbw_gib_s": round(alg, 3),
+                                "busbw_gib_s": round(alg * 2 * (world - 1) / world, 3) if world > 1 else None}
+            r.close()
+            del bufs, g
+            torch.cuda.empty_cache()
+        except Exception as ex:  # recorded, never fatal
+            out[f"{mib}MiB"] = {"error": f"{type(ex).__name__}: {ex}"[:200]}
+    return {"workload": "pull_grads_dev of the main schedule per bucket size (config 4 curve)", "sizes": out}
 
 
 def xgmi_link_probe(torch) -> dict | None:

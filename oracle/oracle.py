@@ -239,15 +239,31 @@ class WildStore:
         return out
 
 
+def build_native(out_dir: str) -> dict:
+    """The -march=native variants of the CPU baselines ("also
+    report a -march=native variant"), compiled on the host that runs them
+    (a binary tuned for this container's CPU may not run on the GPU box's)."""
+    os.makedirs(out_dir, exist_ok=True)
+    flags = ["-O3", "-march=native", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-D_GNU_SOURCE"]
+    exes = {}
+    for name in ("ono_cpu_ring", "ono_cpu_ps"):
+        exe = os.path.join(out_dir, name)
+        subprocess.run(["gcc", *flags, "-o", exe, os.path.join(HERE, name + ".c"),
+                        os.path.join(HERE, "ono_oracle.c"), "-lm", "-lpthread"], check=True)
+        exes[name] = exe
+    return exes
+
+
 def cpu_ps(mode: str, length: int, threads: int = 16, workers: int = 2, rounds: int = 3,
-           timeout: float = 600) -> dict:
+           timeout: float = 600, exe: str | None = None) -> dict:
     """oracle/ono_cpu_ps.c: 'hop' = one scatter hop's compute on one core,
     'ps' = BlockingStore accumulate + update on `threads` cores (2 x threads shards)."""
     import json
 
-    exe = os.path.join(BUILD, "ono_cpu_ps")
-    if not os.path.exists(exe):
-        build()
+    if exe is None:
+        exe = os.path.join(BUILD, "ono_cpu_ps")
+        if not os.path.exists(exe):
+            build()
     cmd = [exe, "--mode", mode, "--len", str(length), "--threads", str(threads), "--workers", str(workers),
            "--rounds", str(rounds)]
     out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
@@ -255,13 +271,15 @@ def cpu_ps(mode: str, length: int, threads: int = 16, workers: int = 2, rounds: 
 
 
 def cpu_ring(ranks: int, length: int, rounds: int, seed: int = 0x0402026, check: bool = False,
-             pin: bool = True, timeout: float = 600) -> dict:
+             pin: bool = True, timeout: float = 600, exe: str | None = None) -> dict:
     """Run the TCP-loopback reference-style CPU ring (oracle/ono_cpu_ring.c)."""
     import json
 
-    if not os.path.exists(CPU_RING):
-        build()
-    cmd = [CPU_RING, "--ranks", str(ranks), "--len", str(length), "--rounds", str(rounds),
+    if exe is None:
+        exe = CPU_RING
+        if not os.path.exists(CPU_RING):
+            build()
+    cmd = [exe, "--ranks", str(ranks), "--len", str(length), "--rounds", str(rounds),
            "--seed", str(seed)]
     if check:
         cmd.append("--check")
