@@ -50,6 +50,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-le
 XGMI_LINK_GBS = 153.6 / 2      # per direction; 153.6 GB/s bidirectional per link (spec)
 GIB = float(1 << 30)
 SEED = 0x0402026
+CONFIG1_ELEMS = (784 + 1) * 128 + (128 + 1) * 64 + (64 + 1) * 10  # 109,386: MLP 784-128-64-10
 
 
 def parse_args(argv=None):
@@ -314,6 +315,26 @@ def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
             "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
 
 
+def tcp_edge_native(elems: int, rounds: int, ranks: int = 2) -> dict | None:
+    """The TCP edge driven from a plain C++ host (tools/ono_tcp_bench: worker
+    threads on this GPU, ono_ring_create_tcp over loopback TCP, pthread
+    barriers) — the way a native Rust worker drives it, without the Python
+    threading overhead of tcp_edge().  None if the tool is not built."""
+    exe = os.path.join(ROOT, "tools", "ono_tcp_bench")
+    if not os.path.exists(exe):
+        return None
+    import subprocess
+    try:
+        out = subprocess.run([exe, "--ranks", str(ranks), "--len", str(elems), "--rounds", str(rounds)],
+                             capture_output=True, text=True, timeout=300, check=True)
+        d = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 — reported in the line
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+    return {"workload": f"pull_grads over loopback TCP, {ranks} workers (C++ host threads) on one GPU, "
+                        f"{elems} f32 each, f16 reference frames",
+            "ranks": ranks, "ms": round(d["s_per_round"] * 1e3, 4), "gib_s": round(d["gib_s"], 3)}
+
+
 def tcp_edge(ono_amd, elems: int, rounds: int, ranks: int = 2) -> dict:
     """The TCP edge (never `value`): `ranks` MI355X workers on
     this one GPU, one thread each, in a loopback-TCP ring speaking the
@@ -475,7 +496,17 @@ def main(argv=None) -> int:
     if rank == 0 and world == 1 and not args.no_host_fed:
         extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
     if rank == 0 and world == 1 and not args.no_tcp_edge:
-        extra["tcp_edge"] = tcp_edge(ono_amd, elems, 3)
+        extra["tcp_edge"] = tcp_edge_native(elems, 10) or tcp_edge(ono_amd, elems, 3)
+        # BASELINE config 1: the reference's own case — 2 loopback workers, the
+        # MLP 784-128-64-10 bucket (109,386 f32) — TCP edge vs CPU ring
+        small = {"2_ranks": tcp_edge_native(CONFIG1_ELEMS, 200) or tcp_edge(ono_amd, CONFIG1_ELEMS, 50),
+                 "4_ranks": tcp_edge_native(CONFIG1_ELEMS, 200, 4) or tcp_edge(ono_amd, CONFIG1_ELEMS, 50, 4)}
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O  # noqa: WPS433 (cpu_baseline leg only)
+            for k, nr in (("2_ranks", 2), ("4_ranks", 4)):
+                cr = O.cpu_ring(nr, CONFIG1_ELEMS, 50, check=False, pin=True, timeout=300)
+                small[k]["cpu_ring_ms"] = round(cr["s_per_round"] * 1e3, 4)
+        extra["tcp_edge"]["config1"] = small
     if rank == 0 and world == 1 and not args.no_local_reduce:
         extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -232,6 +232,10 @@ struct ono_ring {
     uint8_t *tx = nullptr, *rx = nullptr;
     size_t frame_cap = 0;
     size_t tcp_block = 0;           // pipelining piece of a frame (tcp_block_bytes())
+    // small-frame TCP rings: the wire buffers are pinned host frames the codec
+    // kernels read and write in place (no D2H / H2D per hop); zc[b] + 16 is the
+    // payload base, so a frame's 12-byte header sits just before its payload
+    uint8_t *zc[2] = {nullptr, nullptr};
     std::vector<hipEvent_t> tx_ev;  // one per piece of a frame's D2H
     // segmented f32 all-reduce (ono_ring_set_pipeline): the finaliser of
     // segment k runs on astream while segment k+1 is still on the wire
@@ -289,6 +293,7 @@ size_t tcp_block_bytes() {  // env ONO_TCP_BLOCK_KIB (default 4 MiB), read once 
     return k > 0 ? (size_t)k << 10 : size_t(4) << 20;
 }
 constexpr int kTcpPollMs = 100;  // abort / peer-failure latency
+constexpr size_t kTcpInline = size_t(256) << 10;  // frames up to this go through one poll loop
 
 struct TcpErr {
     int code = ONO_OK;
@@ -309,6 +314,71 @@ bool tcp_wait(ono_ring *r, int fd, short ev, const std::atomic<bool> &stop, TcpE
     }
 }
 
+// One send(2) of the frame's ready bytes; false (e set) on a socket error.
+bool tcp_send_some(ono_ring *r, const uint8_t *tx, size_t &sent, size_t ready, TcpErr &e) {
+    ssize_t k = send(r->fd_next, tx + sent, ready - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
+    if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+        e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "send to next worker: %s", strerror(errno));
+        return false;
+    }
+    if (k > 0) sent += (size_t)k;
+    return true;
+}
+
+// Receive side of one hop: header validation, then each complete piece of the
+// payload goes up to HBM while the next one is still on the socket.
+struct TcpRecv {
+    uint8_t *rx;  // where the frame lands (header, then payload)
+    size_t got = 0, need = 12, issued = 0;
+    bool have_hdr = false;
+    explicit TcpRecv(uint8_t *frame) : rx(frame) {}
+    bool done() const { return got >= need && have_hdr; }
+    // one recv(2); false (e set) on a socket or protocol error.  recv_dev ==
+    // nullptr: the payload stays where it landed (zero-copy frames).
+    bool step(ono_ring *r, uint8_t *recv_dev, size_t payload, hipStream_t s, TcpErr &e) {
+        ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
+        if (k == 0) { e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "previous worker closed the connection"); return false; }
+        if (k < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) return true;
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "recv from previous worker: %s", strerror(errno));
+            return false;
+        }
+        got += (size_t)k;
+        if (!have_hdr && got >= 12) {
+            uint64_t l = 0;
+            for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
+            const uint32_t kind = (uint32_t)rx[8] << 24 | (uint32_t)rx[9] << 16 | (uint32_t)rx[10] << 8 | rx[11];
+            // only a DenseGrad of this hop's chunk is a valid event (worker_ring.rs:136-138)
+            if ((kind & 0xFF) != 1 && (kind & 0xFF) != 2) {  // Header::from_be_bytes(..) as u8 (msg.rs:168)
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind & 0xFF);
+                return false;
+            }
+            if (l != 4 + (uint64_t)payload) {
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
+                         (unsigned long long)(l < 4 ? 0 : l - 4), payload);
+                return false;
+            }
+            need = 12 + payload;
+            have_hdr = true;
+        }
+        if (have_hdr && recv_dev) {
+            const size_t blk = r->tcp_block, avail = got - 12;
+            while (issued < avail && (avail - issued >= blk || avail == payload)) {
+                const size_t c = std::min(blk, payload - issued);
+                hipError_t he = hipMemcpyAsync(recv_dev + issued, rx + 12 + issued, c, hipMemcpyHostToDevice, s);
+                if (he != hipSuccess) {
+                    e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "H2D of a frame: %s", hipGetErrorString(he));
+                    return false;
+                }
+                issued += c;
+            }
+        }
+        return true;
+    }
+};
+
 void tcp_send_frame(ono_ring *r, size_t payload, const std::atomic<bool> &stop, TcpErr &e) {
     const size_t blk = r->tcp_block;
     const size_t out = 12 + payload;
@@ -322,66 +392,42 @@ void tcp_send_frame(ono_ring *r, size_t payload, const std::atomic<bool> &stop, 
                 return;
             }
         }
-        while (sent < ready) {
-            if (!tcp_wait(r, r->fd_next, POLLOUT, stop, e)) return;
-            ssize_t k = send(r->fd_next, r->tx + sent, ready - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
-            if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
-                e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "send to next worker: %s", strerror(errno));
-                return;
-            }
-            if (k > 0) sent += (size_t)k;
-        }
+        while (sent < ready)
+            if (!tcp_wait(r, r->fd_next, POLLOUT, stop, e) || !tcp_send_some(r, r->tx, sent, ready, e)) return;
     }
 }
 
 void tcp_recv_frame(ono_ring *r, uint8_t *recv_dev, size_t payload, hipStream_t s,
                     const std::atomic<bool> &stop, TcpErr &e) {
-    uint8_t *rx = r->rx;
-    const size_t blk = r->tcp_block;
-    size_t got = 0, need = 12, issued = 0;
-    bool have_hdr = false;
-    while (got < need) {
-        if (!tcp_wait(r, r->fd_prev, POLLIN, stop, e)) return;
-        ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
-        if (k == 0) { e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "previous worker closed the connection"); return; }
-        if (k < 0) {
-            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) continue;
-            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "recv from previous worker: %s", strerror(errno));
-            return;
-        }
-        got += (size_t)k;
-        if (!have_hdr && got >= 12) {
-            uint64_t l = 0;
-            for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
-            const uint32_t kind = (uint32_t)rx[8] << 24 | (uint32_t)rx[9] << 16 | (uint32_t)rx[10] << 8 | rx[11];
-            // only a DenseGrad of this hop's chunk is a valid event (worker_ring.rs:136-138)
-            if ((kind & 0xFF) != 1 && (kind & 0xFF) != 2) {  // Header::from_be_bytes(..) as u8 (msg.rs:168)
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind & 0xFF);
-                return;
-            }
-            if (l != 4 + (uint64_t)payload) {
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
-                         (unsigned long long)(l < 4 ? 0 : l - 4), payload);
-                return;
-            }
-            need = 12 + payload;
-            have_hdr = true;
-        }
-        if (have_hdr) {  // each complete piece goes up while the next is still arriving
-            const size_t avail = got - 12;
-            while (issued < avail && (avail - issued >= blk || avail == payload)) {
-                const size_t c = std::min(blk, payload - issued);
-                hipError_t he = hipMemcpyAsync(recv_dev + issued, rx + 12 + issued, c, hipMemcpyHostToDevice, s);
-                if (he != hipSuccess) {
-                    e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "H2D of a frame: %s", hipGetErrorString(he));
-                    return;
-                }
-                issued += c;
-            }
-        }
+    TcpRecv rv(r->rx);
+    while (!rv.done())
+        if (!tcp_wait(r, r->fd_prev, POLLIN, stop, e) || !rv.step(r, recv_dev, payload, s, e)) return;
+}
+
+// Small frames: one thread drives both directions from one poll loop (a
+// thread hand-off costs more than the transfer); the whole frame is already
+// down in tx.
+int tcp_xchg_inline(ono_ring *r, const uint8_t *tx, size_t send_bytes, uint8_t *rx, uint8_t *recv_dev,
+                    size_t recv_bytes, hipStream_t s) {
+    const size_t out = 12 + send_bytes;
+    size_t sent = 0;
+    TcpRecv rv(rx);
+    TcpErr e;
+    while (sent < out || !rv.done()) {
+        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        struct pollfd p[2];
+        int np = 0, is = -1, ir = -1;
+        if (sent < out) { p[np] = {r->fd_next, POLLOUT, 0}; is = np++; }
+        if (!rv.done()) { p[np] = {r->fd_prev, POLLIN, 0}; ir = np++; }
+        int pr = poll(p, (nfds_t)np, kTcpPollMs);
+        if (pr < 0 && errno != EINTR) return set_error(ONO_E_IO, "poll: %s", strerror(errno));
+        if (pr <= 0) continue;
+        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP)) && !tcp_send_some(r, tx, sent, out, e))
+            return set_error(e.code, "%s", e.msg);
+        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP)) && !rv.step(r, recv_dev, recv_bytes, s, e))
+            return set_error(e.code, "%s", e.msg);
     }
+    return ONO_OK;
 }
 
 int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_dev, size_t recv_bytes,
@@ -401,6 +447,8 @@ int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_de
     // rx is free once the previous hop's H2D pieces ran: they precede piece 0's D2H on s
     if (nblk) ONO_HIP(hipEventSynchronize(r->tx_ev[0]));
     else ONO_HIP(hipStreamSynchronize(s));
+    if (send_bytes <= kTcpInline && recv_bytes <= kTcpInline)  // small: no thread hand-off
+        return tcp_xchg_inline(r, r->tx, send_bytes, r->rx, static_cast<uint8_t *>(recv_dev), recv_bytes, s);
     std::atomic<bool> stop_send{false}, stop_recv{false};
     TcpErr es, er;
     std::thread sender([&] {
@@ -416,17 +464,60 @@ int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_de
     return ONO_OK;
 }
 
+// Zero-copy hop (small frames): the payload to send was written by the codec
+// kernel straight into pinned host memory at send_pay, the frame arrives in
+// place at recv_pay - 12 and the next kernel reads it there.
+int tcp_xchg_zc(ono_ring *r, void *send_pay, size_t send_bytes, void *recv_pay, size_t recv_bytes, hipStream_t s) {
+    uint8_t *tx = static_cast<uint8_t *>(send_pay) - 12;
+    const uint64_t flen = 4 + (uint64_t)send_bytes;
+    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
+    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
+    // the producing kernel has written the payload, and the kernel that read
+    // the receive buffer in the previous hop has finished with it
+    ONO_HIP(hipStreamSynchronize(s));
+    uint8_t *rx = static_cast<uint8_t *>(recv_pay) - 12;
+    if (send_bytes <= kTcpInline && recv_bytes <= kTcpInline)
+        return tcp_xchg_inline(r, tx, send_bytes, rx, nullptr, recv_bytes, s);
+    // larger frames: send and receive on two threads (two kernel socket copies at once)
+    std::atomic<bool> stop_send{false}, stop_recv{false};
+    TcpErr es, er;
+    std::thread sender([&] {
+        size_t sent = 0;
+        while (sent < 12 + send_bytes)
+            if (!tcp_wait(r, r->fd_next, POLLOUT, stop_send, es) || !tcp_send_some(r, tx, sent, 12 + send_bytes, es)) {
+                stop_recv.store(true);
+                return;
+            }
+    });
+    TcpRecv rv(rx);
+    while (!rv.done())
+        if (!tcp_wait(r, r->fd_prev, POLLIN, stop_recv, er) || !rv.step(r, nullptr, recv_bytes, s, er)) {
+            stop_send.store(true);
+            break;
+        }
+    sender.join();
+    const TcpErr &e = (er.code && er.code != ONO_E_OTHER) ? er : (es.code && es.code != ONO_E_OTHER) ? es : er;
+    if (e.code) return set_error(e.code, "%s", e.msg);
+    return ONO_OK;
+}
+
 // One pull_grads round of rank `pos`, exact reference hop order, wire W.
 template <class W>
 int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
     const int n = r->n, pos = r->pos;
     const auto &off = r->off;
     auto len = [&](int c) { return off[c + 1] - off[c]; };
-    auto slot = [&](int b, int c) { return static_cast<W *>(r->wbuf[b]) + ph(off[c]); };
+    auto slot = [&](int b, int c) {
+        return (r->zc[0] ? reinterpret_cast<W *>(r->zc[b] + 16) : static_cast<W *>(r->wbuf[b])) + ph(off[c]);
+    };
     const int next = (pos + 1) % n, prev = (pos + n - 1) % n;
     const float fn = (float)n;
     auto xchg = [&](int bs, int cs, int br, int cr) -> int {
         if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        if (r->zc[0])
+            return timed(r, s, 1, [&]() -> int {
+                return tcp_xchg_zc(r, slot(bs, cs), len(cs) * sizeof(W), slot(br, cr), len(cr) * sizeof(W), s);
+            });
         if (r->fd_next >= 0)
             return timed(r, s, 1, [&]() -> int {
                 return tcp_xchg(r, slot(bs, cs), len(cs) * sizeof(W), slot(br, cr), len(cr) * sizeof(W), s);
@@ -693,6 +784,15 @@ int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int de
         ono_ring_destroy(r);
         return hip_error(e, "frame buffer allocation", __FILE__, __LINE__);
     }
+    // zero-copy frames up to ONO_TCP_ZEROCOPY KiB of payload (default 256; 0 = off)
+    const char *zc_env = getenv("ONO_TCP_ZEROCOPY");
+    const size_t zc_max = zc_env ? (size_t)atol(zc_env) << 10 : kTcpInline;
+    if (2 * (r->maxc + 4) <= zc_max)
+        for (int b = 0; b < 2; b++)
+            if ((e = hipHostMalloc((void **)&r->zc[b], 16 + 2 * (r->maxc + 4), hipHostMallocCoherent)) != hipSuccess) {
+                ono_ring_destroy(r);
+                return hip_error(e, "zero-copy frame allocation", __FILE__, __LINE__);
+            }
     r->tcp_block = tcp_block_bytes();
     r->tx_ev.assign((2 * (r->maxc + 4) + r->tcp_block - 1) / r->tcp_block, nullptr);
     for (auto &ev : r->tx_ev)
@@ -761,6 +861,8 @@ int ono_ring_destroy(ono_ring *r) {
         if (r->pin_in) (void)hipHostFree(r->pin_in);
         if (r->pin_out) (void)hipHostFree(r->pin_out);
         for (hipEvent_t ev : r->tx_ev) (void)hipEventDestroy(ev);
+        for (uint8_t *z : r->zc)
+            if (z) (void)hipHostFree(z);
         if (r->tx) (void)hipHostFree(r->tx);
         if (r->rx) (void)hipHostFree(r->rx);
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);

@@ -106,12 +106,43 @@ def inputs_for(n, length, rounds, seed):
 @pytest.mark.parametrize("n", [2, 3, 4, 5])
 @pytest.mark.parametrize("length", [109386, 4099, 2 ** 16 + 3])
 @pytest.mark.parametrize("host_fed", [False, True])
-def test_tcp_ring_socketpairs_vs_oracle(n, length, host_fed):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_tcp_ring_socketpairs_vs_oracle(n, length, host_fed, zero_copy, monkeypatch):
+    """Frames of these sizes are small: by default the codec kernels read and
+    write them in pinned host memory (zero-copy); ONO_TCP_ZEROCOPY=0 stages
+    them through HBM wire buffers with D2H / H2D copies instead."""
+    if not zero_copy:
+        monkeypatch.setenv("ONO_TCP_ZEROCOPY", "0")
     rounds = 2
     ins = inputs_for(n, length, rounds, SEED + 21)
     links, pairs = socketpair_links(n)
     ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(rounds)], *links[r], host_fed=host_fed)
           for r in range(n)]
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        close_all(s for p in pairs for s in p)
+    eg, er = O.ring_pull_grads(ins[-1], "f16")
+    for r in range(n):
+        assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
+
+
+@pytest.mark.parametrize("n,length,piece_kib", [(2, 2 ** 20 + 7, 64), (3, 3 * 2 ** 19 + 5, 128),
+                                                (4, 2 ** 21 + 3, 4096)])
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_tcp_ring_pipelined_pieces(n, length, piece_kib, zero_copy, monkeypatch):
+    """Frames above the inline size go through the two-thread exchange: staged
+    through HBM in pipelined D2H / H2D pieces (ONO_TCP_BLOCK_KIB, read at ring
+    creation), or — with the zero-copy limit raised — read and written by the
+    codec kernels in pinned host memory.  Bit-exact either way."""
+    monkeypatch.setenv("ONO_TCP_BLOCK_KIB", str(piece_kib))
+    monkeypatch.setenv("ONO_TCP_ZEROCOPY", "65536" if zero_copy else "0")
+    ins = inputs_for(n, length, 2, SEED + 31)
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(2)], *links[r]) for r in range(n)]
     try:
         for w in ws:
             w.start()

@@ -1,0 +1,123 @@
+// ono_tcp_bench.cpp — the TCP edge timed from a plain C++ host (no Python in
+// the process), the way the reference's Rust workers would drive it: n worker
+// threads on one GPU, each an ono_ring_create_tcp manager over loopback TCP
+// connections set up as the reference does (accept prev, connect next), each
+// round = refill the residual in HBM (untimed) -> barrier -> pull_grads ->
+// barrier.  Prints one JSON line with the median round time.
+//
+//   make -C tools tcp_bench && tools/ono_tcp_bench --ranks 2 --len 109386 --rounds 200
+#include <hip/hip_runtime.h>
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <pthread.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "ono_reduce.h"
+
+namespace {
+
+int listen_any(int *port) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (bind(fd, (sockaddr *)&a, sizeof a) || listen(fd, 4)) return -1;
+    socklen_t sl = sizeof a;
+    getsockname(fd, (sockaddr *)&a, &sl);
+    *port = ntohs(a.sin_port);
+    return fd;
+}
+
+int connect_to(int port) {
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    for (int t = 0; t < 5000; t++) {
+        int fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (connect(fd, (sockaddr *)&a, sizeof a) == 0) return fd;
+        close(fd);
+        usleep(1000);
+    }
+    return -1;
+}
+
+void nodelay(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    int n = 2, rounds = 100;
+    size_t len = 109386;
+    for (int a = 1; a < argc; a++) {
+        if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = strtoull(argv[++a], nullptr, 10);
+        else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
+        else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
+    }
+    if (n < 2 || rounds < 1 || len < (size_t)n) { fprintf(stderr, "need ranks >= 2, len >= ranks\n"); return 1; }
+    std::vector<int> lfd(n), port(n);
+    for (int r = 0; r < n; r++)
+        if ((lfd[r] = listen_any(&port[r])) < 0) { perror("listen"); return 2; }
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, nullptr, (unsigned)n);
+    std::vector<double> t(rounds, 0.0);
+    std::vector<int> rc(n, ONO_OK);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; r++)
+        th.emplace_back([&, r] {
+            int nxt = connect_to(port[(r + 1) % n]);
+            int prv = accept(lfd[r], nullptr, nullptr);
+            if (nxt < 0 || prv < 0) { fprintf(stderr, "worker %d: connect failed\n", r); _exit(2); }
+            nodelay(nxt);
+            nodelay(prv);
+            (void)hipSetDevice(0);
+            hipStream_t s;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) _exit(2);
+            ono_ring *ring = nullptr;
+            int e = ono_ring_create_tcp(&ring, r, n, len, 0, prv, nxt);
+            for (int k = 0; k <= rounds && e == ONO_OK; k++) {  // round 0 is warmup
+                e = ono_synth_f32(ono_ring_residual(ring), len, 0x0402026 + k, (uint64_t)r, 0, s);
+                if (e == ONO_OK) e = hipStreamSynchronize(s) == hipSuccess ? ONO_OK : ONO_E_HIP;
+                pthread_barrier_wait(&bar);
+                auto t0 = std::chrono::steady_clock::now();
+                if (e == ONO_OK) e = ono_ring_pull_grads(ring, s);
+                if (e == ONO_OK) e = hipStreamSynchronize(s) == hipSuccess ? ONO_OK : ONO_E_HIP;
+                pthread_barrier_wait(&bar);
+                if (r == 0 && k > 0)
+                    t[k - 1] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            }
+            if (e != ONO_OK) {  // the peers would wait for this worker's frames: end the tool
+                fprintf(stderr, "worker %d: %s\n", r, ono_last_error());
+                _exit(2);
+            }
+            rc[r] = e;
+            if (ring) ono_ring_destroy(ring);
+            (void)hipStreamDestroy(s);
+            close(nxt);
+            close(prv);
+        });
+    for (auto &x : th) x.join();
+    for (int r = 0; r < n; r++) close(lfd[r]);
+    for (int e : rc)
+        if (e != ONO_OK) return 2;
+    std::sort(t.begin(), t.end());
+    const double med = t[t.size() / 2];
+    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"s_per_round\": %.9f, \"gib_s\": %.6f}\n", n, len,
+           rounds, med, (double)len * 4.0 / med / (double)(1ull << 30));
+    return 0;
+}
