@@ -275,9 +275,11 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
         ms = a.elapsed_time(b) / steps
         nbytes = (k + 1) * 4 * n
         gbs = nbytes / (ms * 1e-3) / 1e9
+        pmc = pmc_traffic(f"SumScaleOp<{k},", n)
         out[f"k{k}"] = {"bytes_per_launch": nbytes, "us_per_launch": round(ms * 1e3, 2),
                         "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
-                        "rotating_sets": nsets}
+                        "rotating_sets": nsets,
+                        "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
         del sets
         torch.cuda.empty_cache()
     return {"workload": "sum_scale_f32, 64 MiB buckets, out = (sum of k inputs) / k", "hbm_peak_gbs": HBM_PEAK_GBS,

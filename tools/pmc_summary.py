@@ -21,6 +21,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 
 
@@ -44,6 +45,8 @@ def main() -> int:
     ap.add_argument("--out", required=True)
     ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp"])
     ap.add_argument("--algo-bytes-per-elem", type=float, default=12.0)
+    ap.add_argument("--local-elems", type=int, default=16 << 20,
+                    help="bucket length of bench.py's local_reduce (SumScaleOp<k> kernels: (k+1) x 4 B/elem)")
     a = ap.parse_args()
     fetch, write = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     kernels = []
@@ -52,13 +55,18 @@ def main() -> int:
             continue
         f_kb, w_kb = statistics.median(fetch[name]), statistics.median(write[name])
         rd, wr = 2.0 * f_kb * 1024, w_kb * 1024
+        m = re.search(r"SumScaleOp<(\d+),", name)
+        if m:  # config 2: k inputs read, one output written
+            elems, algo = a.local_elems, (int(m.group(1)) + 1) * 4.0 * a.local_elems
+        else:
+            elems, algo = a.elems, a.algo_bytes_per_elem * a.elems
         kernels.append({
-            "name": name, "elems": a.elems, "launches_fetch": len(fetch[name]), "launches_write": len(write[name]),
+            "name": name, "elems": elems, "launches_fetch": len(fetch[name]), "launches_write": len(write[name]),
             "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
             "hbm_bytes_per_launch": rd + wr,
-            "algorithmic_bytes_per_launch": a.algo_bytes_per_elem * a.elems,
-            "traffic_over_algorithmic": (rd + wr) / (a.algo_bytes_per_elem * a.elems),
+            "algorithmic_bytes_per_launch": algo,
+            "traffic_over_algorithmic": (rd + wr) / algo,
         })
     doc = {"note": "median over launches; read = 2 x FETCH_SIZE x 1 KiB (gfx950 half-count), write = WRITE_SIZE x 1 KiB",
            "kernels": kernels}
