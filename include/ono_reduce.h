@@ -172,8 +172,31 @@ int ono_ring_unregister_host(ono_ring *ring, void *ptr);
  *   DIRECT     all-to-all of chunk slices over every xGMI link at once, the
  *              owner replays the reference chain in one fused kernel, then an
  *              all-gather; bit-exact for both wires; n <= ONO_MAX_INPUTS     */
-typedef enum { ONO_ALGO_AUTO = 0, ONO_ALGO_ALLREDUCE = 1, ONO_ALGO_HOPS = 2, ONO_ALGO_DIRECT = 3 } ono_algo;
+typedef enum {
+    ONO_ALGO_AUTO = 0,
+    ONO_ALGO_ALLREDUCE = 1,
+    ONO_ALGO_HOPS = 2,
+    ONO_ALGO_DIRECT = 3,
+    ONO_ALGO_XGMI = 4
+} ono_algo;
+/*   XGMI       the direct schedule's arithmetic with no collective library in
+ *              the data path: each rank maps its peers' exchange regions (IPC,
+ *              uncached HBM) and the kernels push slices into the owners'
+ *              receive slots and pull the owners' results over xGMI, with
+ *              device-side flag barriers (timeout: env ONO_XGMI_TIMEOUT_S,
+ *              default 30 s -> ONO_E_IO).  Bit-exact for both wires; ranks of
+ *              one node; n <= ONO_MAX_INPUTS.  On an RCCL ring the exchange
+ *              regions are connected over the communicator on first use.    */
 int ono_ring_set_algo(ono_ring *ring, int algo);
+/* A ring with no collective library at all (ONO_ALGO_XGMI only): create,
+ * export this rank's handle, pass every rank's handle (nranks x
+ * ONO_XGMI_HANDLE_BYTES, rank order) to connect.  The handles travel out of
+ * band, like the RCCL id.  Destroy is collective (a final barrier keeps this
+ * rank's region mapped until every peer is done with it).                    */
+#define ONO_XGMI_HANDLE_BYTES 64 /* sizeof(hipIpcMemHandle_t) */
+int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
+int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
+int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
 /* Segments of the f32 all-reduce schedule (ONO_ALGO_ALLREDUCE): with k > 1
  * the fused finaliser (÷n, residual = 0) of segment j overlaps the RCCL
  * all-reduce of segment j+1; 1 = one all-reduce then one finaliser; 0 = the

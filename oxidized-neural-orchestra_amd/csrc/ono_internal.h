@@ -58,11 +58,40 @@ template <class W> hipError_t launch_add_finish(float *grad, W *out, float *acc,
 
 // Chunk owner's reduction of the direct schedule (ono_kernels.hip DirectOp):
 // ins[k] = rank (c+k)'s slice of chunk c (owner's own residual last);
-// grad = chain(ins) / divisor; out = wire(chain) (f16 wire; NULL for f32);
+// grad = chain(ins) / divisor; out = wire(chain) (f16 wire) or a copy of grad
+// (f32 wire; NULL = none);
 // zero the last input, or every input when zero_all.
 template <class W>
 hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, size_t n, float divisor,
                          bool zero_all, hipStream_t s);
+
+// ---- xGMI peer-access schedule (ono_xgmi.hip) ----
+// One peer's part of a push or pull launch: n elements from src to dst.
+// head = scalar elements before the first 16-B vector (all operands share the
+// phase), or kScalarOnly when their phases differ.  tiles is filled in by the
+// launcher.
+constexpr uint32_t kScalarOnly = 0xFFFFFFFFu;
+struct XSeg {
+    const void *src;  // push: local residual slice (f32, zeroed after the read); pull: peer obuf (f32 / f16)
+    void *dst;        // push: peer receive slot (f32); pull: local grad (f32)
+    uint64_t n;
+    uint32_t head;
+    uint32_t tiles;
+};
+struct XSegs {
+    XSeg s[ONO_MAX_INPUTS];
+    int nseg;
+};
+struct XBarrier {
+    uint64_t *peer_flags[ONO_MAX_INPUTS];  // peer q's flag array (mapped), this rank writes slot `pos`
+    uint64_t *my_flags;                    // this rank's flag array, slot q written by peer q
+    uint32_t *err;                         // host-mapped error word, set on timeout
+    uint64_t epoch, timeout_ticks;
+    int n, pos;
+};
+hipError_t launch_xgmi_push(const XSegs &g, hipStream_t s);
+hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s);
+hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s);
 
 // PS shard update (storage/blocking/shard.rs:74-92 + optimization/*.rs), fused:
 //   g /= nworkers (if > 1); optimizer step on w (state v, s); g = 0 when zero_grad

@@ -219,7 +219,8 @@ template <int K, int M, bool NTL> struct SumScaleOp {
 // reproduces the reference's hop chain (worker_ring.rs:122-143: each hop adds
 // the received wire value into the local f32 chunk), wire() being the f16
 // round trip (f16 wire) or the identity (f32 wire).  Then grad = p / d (:166 +
-// :101-105), out = enc(p) for the all-gather (f16 wire only), and the slices
+// :101-105), out = enc(p) for the all-gather (f16 wire; f32 wire: a copy of
+// grad when out is set — the xGMI schedule's exchange buffer), and the slices
 // that were "sent" are zeroed (:133, :191-193): the own one, or all of them
 // when every rank is co-resident (zall).  Scale mode and zall are uniform
 // run-time flags (uniform branches, no divergence).
@@ -238,8 +239,10 @@ template <int K, class W> struct DirectOp {
         float p = in.p[0][i];
 #pragma unroll
         for (int k = 1; k < K; k++) p = in.p[k][i] + wq(p);
-        grad[i] = mode == SCALE_RECIP ? p * v : p / v;
+        const float gv = mode == SCALE_RECIP ? p * v : p / v;
+        grad[i] = gv;
         if constexpr (sizeof(W) == 2) out[i] = Wire<W>::enc(p);
+        else if (out) out[i] = gv;
         if (zall) {
 #pragma unroll
             for (int k = 0; k < K; k++) const_cast<float *>(in.p[k])[i] = 0.0f;
@@ -258,8 +261,10 @@ template <int K, class W> struct DirectOp {
         return p;
     }
     __device__ __forceinline__ void store(size_t i, R p) const {
-        st_nt((f4 *)(grad + i), mode == SCALE_RECIP ? p * v : p / v);
+        const f4 gv = mode == SCALE_RECIP ? p * v : p / v;
+        st_nt((f4 *)(grad + i), gv);
         if constexpr (sizeof(W) == 2) st_nt((WV *)(out + i), Wire<W>::enc4(p));
+        else if (out) st_nt((f4 *)(out + i), gv);
         const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
         if (zall) {
 #pragma unroll

@@ -33,91 +33,14 @@
 #include <vector>
 
 #include "ono_internal.h"
+#include "ono_ring_impl.h"
+
 
 using namespace ono;
 
-#define ONO_NCCL(expr)                                                                        \
-    do {                                                                                      \
-        ncclResult_t ono_r_ = (expr);                                                         \
-        if (ono_r_ != ncclSuccess)                                                            \
-            return set_error(ONO_E_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(ono_r_), \
-                             __FILE__, __LINE__);                                             \
-    } while (0)
-
 static_assert(sizeof(ncclUniqueId) == ONO_UID_BYTES, "ncclUniqueId size");
 
-namespace {
-
-struct EventPair {
-    hipEvent_t a = nullptr, b = nullptr;
-    int kind = 0;  // 0 = library kernel, 1 = collective
-};
-
-// HIP-event timer for the library's own launches (on the launch stream).
-struct Timer {
-    bool on = false;
-    std::vector<EventPair> pending, pool;
-    double kernel_ms = 0, coll_ms = 0;
-    int64_t kernels = 0, colls = 0;
-
-    hipError_t begin(hipStream_t s, EventPair &p, int kind) {
-        if (!pool.empty()) {
-            p = pool.back();
-            pool.pop_back();
-        } else {
-            hipError_t e = hipEventCreate(&p.a);
-            if (e != hipSuccess) return e;
-            e = hipEventCreate(&p.b);
-            if (e != hipSuccess) return e;
-        }
-        p.kind = kind;
-        return hipEventRecord(p.a, s);
-    }
-    hipError_t end(hipStream_t s, EventPair &p) {
-        hipError_t e = hipEventRecord(p.b, s);
-        pending.push_back(p);
-        return e;
-    }
-    hipError_t drain() {
-        for (auto &p : pending) {
-            hipError_t e = hipEventSynchronize(p.b);
-            if (e != hipSuccess) return e;
-            float ms = 0;
-            e = hipEventElapsedTime(&ms, p.a, p.b);
-            if (e != hipSuccess) return e;
-            if (p.kind == 0) { kernel_ms += ms; kernels++; }
-            else { coll_ms += ms; colls++; }
-            pool.push_back(p);
-        }
-        pending.clear();
-        return hipSuccess;
-    }
-    void destroy() {
-        for (auto &p : pending) pool.push_back(p);
-        pending.clear();
-        for (auto &p : pool) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
-        pool.clear();
-    }
-};
-
-// RAII device guard: run on the ring's device, restore the caller's afterwards.
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to chunk starts
-
-}  // namespace
-
-namespace {
+namespace ono {
 
 // Host-side copy pool for the pageable host-fed form: the CPU copies between
 // the caller's pageable buckets and the pinned bounce slots (and the residual
@@ -209,66 +132,9 @@ int host_threads() {
     return (int)std::max(1L, t);
 }
 
-}  // namespace
-
-struct ono_ring {
-    int pos = 0, n = 1, device = 0, wire = ONO_WIRE_F32;
-    size_t size = 0;
-    float *grad = nullptr, *residual = nullptr;
-    std::vector<size_t> off;
-    size_t maxc = 0;
-    void *wbuf[2] = {nullptr, nullptr};  // hop-ring wire buffers, (maxc + 4) x 4 B each
-    int algo = ONO_ALGO_AUTO;
-    // direct schedule: all-to-all receive slots, all-gather staging (f16),
-    // the owner's f16 message; zstream zeroes the residual beside the all-gather
-    float *rbuf = nullptr;
-    uint16_t *gstage = nullptr, *msg = nullptr;
-    hipStream_t zstream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    ncclComm_t comm = nullptr;
-    // TCP transport (ono_ring_create_tcp): the caller's connected sockets to the
-    // previous and next worker, pinned frame buffers (rx 4-B aligned, source.rs:43-50)
-    int fd_prev = -1, fd_next = -1;
-    uint8_t *tx = nullptr, *rx = nullptr;
-    size_t frame_cap = 0;
-    size_t tcp_block = 0;           // pipelining piece of a frame (tcp_block_bytes())
-    // small-frame TCP rings: the wire buffers are pinned host frames the codec
-    // kernels read and write in place (no D2H / H2D per hop); zc[b] + 16 is the
-    // payload base, so a frame's 12-byte header sits just before its payload
-    uint8_t *zc[2] = {nullptr, nullptr};
-    std::vector<hipEvent_t> tx_ev;  // one per piece of a frame's D2H
-    // segmented f32 all-reduce (ono_ring_set_pipeline): the finaliser of
-    // segment k runs on astream while segment k+1 is still on the wire
-    int segments = 0;  // 0 = unresolved: env ONO_AR_SEGMENTS, default 4
-    hipStream_t astream = nullptr;
-    std::vector<hipEvent_t> ev_seg;
-    hipEvent_t ev_ajoin = nullptr;
-    std::atomic<bool> aborted{false};
-    std::mutex mu;  // serialises host-form calls and the timer
-    // host-fed pipeline (ono_ring_pull_grads_host): H2D on hstream, reduce on
-    // cstream, D2H on dstream; pinned bounce slots for unregistered buffers
-    hipStream_t hstream = nullptr, cstream = nullptr, dstream = nullptr;
-    float *pin_in = nullptr, *pin_out = nullptr;  // kSlots x chunk elements each
-    std::unique_ptr<HostPool> pool;               // CPU copies of the bounce path
-    std::vector<hipEvent_t> ev_h, ev_c, ev_d;
-    std::vector<std::pair<void *, size_t>> registered;  // ono_ring_register_host
-    Timer timer;
-};
+}  // namespace ono
 
 namespace {
-
-template <class F>
-int timed(ono_ring *r, hipStream_t s, int kind, F &&f) {
-    EventPair p;
-    if (r->timer.on) ONO_HIP(r->timer.begin(s, p, kind));
-    int rc = f();
-    if (rc != ONO_OK) return rc;
-    if (r->timer.on) ONO_HIP(r->timer.end(s, p));
-    return ONO_OK;
-}
-
-#define ONO_K(ring, s, expr) \
-    do { int rc_ = timed(ring, s, 0, [&]() -> int { ONO_HIP(expr); return ONO_OK; }); if (rc_) return rc_; } while (0)
 
 template <class W> ncclDataType_t nccl_type();
 template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
@@ -722,6 +588,8 @@ int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
         return r->wire == ONO_WIRE_F16 ? ring_hops<uint16_t>(r, res, grad, s) : ring_hops<float>(r, res, grad, s);
     case ONO_ALGO_DIRECT:
         return r->wire == ONO_WIRE_F16 ? direct_impl<uint16_t>(r, res, grad, s) : direct_impl<float>(r, res, grad, s);
+    case ONO_ALGO_XGMI:
+        return xgmi_pull_grads(r, res, grad, s);
     default:
         return set_error(ONO_E_ARG, "algo %d", r->algo);
     }
@@ -846,6 +714,7 @@ int ono_ring_destroy(ono_ring *r) {
     if (!r) return ONO_OK;
     {
         DeviceGuard g(r->device);
+        xgmi_free(r);
         if (r->hstream) (void)hipStreamSynchronize(r->hstream);
         if (r->comm) {
             if (r->aborted.load()) ncclCommAbort(r->comm);
@@ -1079,7 +948,14 @@ int ono_ring_allreduce_avg_dev(ono_ring *r, float *buf, size_t n, void *stream) 
 
 int ono_ring_set_algo(ono_ring *r, int algo) {
     if (!r) return set_error(ONO_E_ARG, "ring is NULL");
-    if (algo < ONO_ALGO_AUTO || algo > ONO_ALGO_DIRECT) return set_error(ONO_E_ARG, "algo %d", algo);
+    if (algo < ONO_ALGO_AUTO || algo > ONO_ALGO_XGMI) return set_error(ONO_E_ARG, "algo %d", algo);
+    if (r->n > 1 && !r->comm && r->fd_next < 0) {  // ono_ring_create_xgmi: no communicator
+        if (algo != ONO_ALGO_XGMI && algo != ONO_ALGO_AUTO)
+            return set_error(ONO_E_ARG, "an xGMI ring (no RCCL communicator) runs the xGMI schedule only");
+        return ONO_OK;
+    }
+    if (algo == ONO_ALGO_XGMI && r->n > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "xGMI schedule supports up to %d ranks", ONO_MAX_INPUTS);
     if (algo == ONO_ALGO_ALLREDUCE && r->wire == ONO_WIRE_F16)
         return set_error(ONO_E_ARG, "an RCCL all-reduce cannot carry the f16 wire semantics");
     if (algo == ONO_ALGO_DIRECT && r->n > ONO_MAX_INPUTS)
@@ -1102,6 +978,7 @@ int ono_ring_set_pipeline(ono_ring *r, int segments) {
 int ono_ring_abort(ono_ring *r) {
     if (!r) return set_error(ONO_E_ARG, "ring is NULL");
     r->aborted.store(true);
+    xgmi_abort(r);
     return ONO_OK;
 }
 

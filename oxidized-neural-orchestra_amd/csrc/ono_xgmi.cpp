@@ -1,0 +1,293 @@
+// ono_xgmi.cpp — the xGMI peer-access schedule of the ring (ONO_ALGO_XGMI).
+//
+// The same round as the direct schedule (worker_ring.rs:112-204 restated as
+// "every slice of chunk c reaches its owner, the owner replays the hop chain
+// c, c+1, ..., c+n-1, the result goes back to everyone"), but with no
+// collective library in the data path: every rank exports one exchange region
+// of uncached HBM (IPC), maps its peers' regions, and the kernels move the
+// bytes with vector loads and stores over the node's xGMI links:
+//
+//   1. push     for every peer q: my slice of q's chunk -> q.rbuf[k], my slice
+//               zeroed in the same pass (k = my place in that chunk's chain)
+//   2. barrier  all slices have landed
+//   3. owner    DirectOp: grad[c] = chain(rbuf[0..n-2], own slice) / n, own
+//               slice zeroed, the result (f32 wire: grad[c]; f16 wire: the
+//               f16 message the reference forwards) into my obuf
+//   4. barrier  all owners' results are ready
+//   5. pull     for every peer q: grad[chunk of q] = dec(q.obuf) (/ n for f16)
+//
+// Bit-exact with the reference hop order for both wires (the chain is the
+// direct schedule's, tested against the oracle).  Bytes per rank on the links:
+// (n-1)/n 4N out in step 1, (n-1)/n 4N (f32) or 2N (f16) in step 5, all n-1
+// links at once.  No stream synchronisation or host round trip per round: the
+// barriers are device-side flag exchanges with a timeout.
+//
+// Reuse safety without a third barrier: a rank writes peer q's rbuf in round
+// r+1 only after passing barrier 4 of round r, which q reaches after its step 3
+// (the only reader of its rbuf); it overwrites its own obuf (round r+1 step 3)
+// only after barrier 2 of round r+1, which every peer reaches after its round-r
+// step 5 (the only remote reader of obuf).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "ono_internal.h"
+#include "ono_ring_impl.h"
+
+static_assert(sizeof(hipIpcMemHandle_t) == ONO_XGMI_HANDLE_BYTES, "IPC handle size");
+
+namespace ono {
+
+constexpr size_t kFlagBytes = 4096;  // flag slots (n x u64) at the start of the region
+
+struct XgmiState {
+    uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
+    size_t slot = 0;                  // elements per receive slot (multiple of 64: 256-B aligned slots)
+    size_t obuf_off = 0;              // byte offset of the owner's result buffer
+    std::vector<uint8_t *> peer;      // every rank's region as mapped here (peer[pos] = xbuf)
+    bool connected = false;
+    uint64_t epoch = 0;               // barriers issued so far (the same sequence on every rank)
+    uint32_t *err = nullptr;          // host-mapped: set by a barrier that timed out
+    uint32_t *err_dev = nullptr;
+    uint64_t timeout_ticks = 0;
+};
+
+}  // namespace ono
+
+using namespace ono;
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int xgmi_alloc(ono_ring *r) {
+    if (r->xgmi) return ONO_OK;
+    if (r->n > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "xGMI schedule supports up to %d ranks", ONO_MAX_INPUTS);
+    DeviceGuard g(r->device);
+    auto *x = new XgmiState();
+    r->xgmi = x;
+    x->slot = align_up(r->maxc + 4, 64);
+    const size_t rb = (size_t)std::max(r->n - 1, 1) * x->slot * sizeof(float);
+    x->obuf_off = align_up(kFlagBytes + rb, 256);
+    const size_t bytes = x->obuf_off + x->slot * sizeof(float);
+    ONO_HIP(hipExtMallocWithFlags((void **)&x->xbuf, bytes, hipDeviceMallocUncached));
+    ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0
+    ONO_HIP(hipDeviceSynchronize());              // zeroed before the handle leaves this process
+    x->peer.assign(r->n, nullptr);
+    x->peer[r->pos] = x->xbuf;
+    ONO_HIP(hipHostMalloc((void **)&x->err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    *x->err = 0;
+    ONO_HIP(hipHostGetDevicePointer((void **)&x->err_dev, x->err, 0));
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, r->device) != hipSuccess || khz <= 0)
+        khz = 100000;  // MI300-class constant 100 MHz wall clock
+    const char *e = getenv("ONO_XGMI_TIMEOUT_S");
+    const double secs = e && atof(e) > 0 ? atof(e) : 30.0;
+    x->timeout_ticks = (uint64_t)(secs * khz * 1000.0);
+    return ONO_OK;
+}
+
+uint64_t *flags_of(uint8_t *region) { return reinterpret_cast<uint64_t *>(region); }
+float *rbuf_of(const XgmiState *x, uint8_t *region, int k) {
+    return reinterpret_cast<float *>(region + kFlagBytes) + (size_t)k * x->slot;
+}
+uint8_t *obuf_of(const XgmiState *x, uint8_t *region) { return region + x->obuf_off; }
+
+int xgmi_connect(ono_ring *r, const uint8_t *handles) {
+    XgmiState *x = r->xgmi;
+    if (x->connected) return ONO_OK;
+    DeviceGuard g(r->device);
+    for (int q = 0; q < r->n; q++) {
+        if (q == r->pos) continue;
+        hipIpcMemHandle_t h;
+        memcpy(&h, handles + (size_t)q * ONO_XGMI_HANDLE_BYTES, sizeof h);
+        void *p = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
+        x->peer[q] = static_cast<uint8_t *>(p);
+    }
+    x->connected = true;
+    return ONO_OK;
+}
+
+// An RCCL ring switched to ONO_ALGO_XGMI exchanges the handles over its own
+// communicator on first use (every rank is inside pull_grads together).
+int xgmi_connect_over_rccl(ono_ring *r, hipStream_t s) {
+    int rc = xgmi_alloc(r);
+    if (rc) return rc;
+    if (!r->comm) return set_error(ONO_E_ARG, "xGMI ring not connected: call ono_ring_xgmi_connect first");
+    const size_t H = ONO_XGMI_HANDLE_BYTES;
+    std::vector<uint8_t> all((size_t)r->n * H);
+    hipIpcMemHandle_t h;
+    ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
+    memcpy(all.data() + (size_t)r->pos * H, &h, H);
+    uint8_t *d = nullptr;
+    ONO_HIP(hipMalloc((void **)&d, all.size()));
+    hipError_t e = hipMemcpyAsync(d + (size_t)r->pos * H, all.data() + (size_t)r->pos * H, H, hipMemcpyHostToDevice, s);
+    ncclResult_t nr = e == hipSuccess ? ncclAllGather(d + (size_t)r->pos * H, d, H, ncclUint8, r->comm, s) : ncclSuccess;
+    if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpyAsync(all.data(), d, all.size(), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (nr != ncclSuccess) return set_error(ONO_E_RCCL, "handle all-gather: %s", ncclGetErrorString(nr));
+    if (e != hipSuccess) return hip_error(e, "handle exchange", __FILE__, __LINE__);
+    return xgmi_connect(r, all.data());
+}
+
+int barrier(ono_ring *r, hipStream_t s) {
+    XgmiState *x = r->xgmi;
+    XBarrier b{};
+    for (int q = 0; q < r->n; q++) b.peer_flags[q] = flags_of(x->peer[q]);
+    b.my_flags = flags_of(x->xbuf);
+    b.err = x->err_dev;
+    b.epoch = ++x->epoch;
+    b.timeout_ticks = x->timeout_ticks;
+    b.n = r->n;
+    b.pos = r->pos;
+    return timed(r, s, 1, [&]() -> int {
+        ONO_HIP(launch_xgmi_barrier(b, s));
+        return ONO_OK;
+    });
+}
+
+uint32_t head_of(const void *a, size_t esz_a, const void *b, size_t esz_b) {
+    const unsigned pa = (unsigned)(((uintptr_t)a / esz_a) & 3u), pb = (unsigned)(((uintptr_t)b / esz_b) & 3u);
+    return pa == pb ? (4u - pa) & 3u : kScalarOnly;
+}
+
+template <class W>
+int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    XgmiState *x = r->xgmi;
+    const int n = r->n, pos = r->pos, c = (pos + 1) % n;
+    const auto &off = r->off;
+    auto len = [&](int q) { return off[q + 1] - off[q]; };
+    constexpr bool f16 = sizeof(W) == 2;
+    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
+        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+
+    XSegs push{};  // 1. my slice of every peer's chunk -> that owner's receive slot
+    for (int d = 1; d < n; d++) {
+        const int q = (pos + d) % n, cq = (q + 1) % n, k = (pos - cq + n) % n;
+        XSeg &sg = push.s[push.nseg++];
+        sg.src = res + off[cq];
+        sg.dst = rbuf_of(x, x->peer[q], k) + ph(off[cq]);
+        sg.n = len(cq);
+        sg.head = head_of(sg.src, 4, sg.dst, 4);
+    }
+    int rc = timed(r, s, 1, [&]() -> int {
+        ONO_HIP(launch_xgmi_push(push, s));
+        return ONO_OK;
+    });
+    if (rc || (rc = barrier(r, s))) return rc;  // 2.
+
+    const float *ins[ONO_MAX_INPUTS];  // 3. the chain of my chunk, reference order
+    for (int k = 0; k < n - 1; k++) ins[k] = rbuf_of(x, x->xbuf, k) + ph(off[c]);
+    ins[n - 1] = res + off[c];
+    W *out = reinterpret_cast<W *>(obuf_of(x, x->xbuf)) + ph(off[c]);
+    ONO_K(r, s, launch_direct<W>(grad + off[c], out, ins, n, len(c), (float)n, false, s));
+    if ((rc = barrier(r, s))) return rc;  // 4.
+
+    XSegs pull{};  // 5. every owner's result -> my grad
+    for (int d = 1; d < n; d++) {
+        const int q = (pos + d) % n, cq = (q + 1) % n;
+        XSeg &sg = pull.s[pull.nseg++];
+        sg.src = reinterpret_cast<const W *>(obuf_of(x, x->peer[q])) + ph(off[cq]);
+        sg.dst = grad + off[cq];
+        sg.n = len(cq);
+        sg.head = head_of(sg.src, sizeof(W), sg.dst, 4);
+    }
+    return timed(r, s, 1, [&]() -> int {
+        ONO_HIP(launch_xgmi_pull(pull, f16, f16 ? (float)n : 1.0f, s));
+        return ONO_OK;
+    });
+}
+
+}  // namespace
+
+namespace ono {
+
+int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    if (!r->xgmi || !r->xgmi->connected) {
+        int rc = xgmi_connect_over_rccl(r, s);
+        if (rc) return rc;
+    }
+    return r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, res, grad, s) : xgmi_round<float>(r, res, grad, s);
+}
+
+// ono_ring_abort: barriers still spinning on the device give up (they poll
+// the host-mapped error word), so an aborted round drains instead of waiting
+// for the timeout.
+void xgmi_abort(ono_ring *r) {
+    if (r->xgmi && r->xgmi->err) __atomic_store_n(r->xgmi->err, 2u, __ATOMIC_RELEASE);
+}
+
+// Teardown is collective: a final barrier keeps this rank's region mapped
+// until every peer has finished reading it (a peer still pulling from a freed
+// region would fault).  A peer that never arrives costs the timeout, no more.
+void xgmi_free(ono_ring *r) {
+    XgmiState *x = r->xgmi;
+    if (!x) return;
+    DeviceGuard g(r->device);
+    if (x->connected && !__atomic_load_n(x->err, __ATOMIC_ACQUIRE)) {
+        (void)hipDeviceSynchronize();
+        if (barrier(r, r->cstream) == ONO_OK) (void)hipStreamSynchronize(r->cstream);
+    }
+    for (int q = 0; q < (int)x->peer.size(); q++)
+        if (q != r->pos && x->peer[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
+    (void)hipFree(x->xbuf);
+    if (x->err) (void)hipHostFree(x->err);
+    delete x;
+    r->xgmi = nullptr;
+}
+
+}  // namespace ono
+
+extern "C" {
+
+int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire) {
+    if (!out) return set_error(ONO_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (nranks < 1 || nranks > ONO_MAX_INPUTS || pos < 0 || pos >= nranks)
+        return set_error(ONO_E_ARG, "pos=%d nranks=%d (xGMI schedule: 1..%d ranks)", pos, nranks, ONO_MAX_INPUTS);
+    if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
+    if (size < (size_t)nranks)  // reference: chunks[pos] out of bounds (worker_ring.rs:120-122)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, nranks);
+    ono_ring *r = nullptr;
+    int rc = ono_ring_create(&r, 0, 1, size, device, nullptr, wire);  // buckets + streams, no communicator
+    if (rc) return rc;
+    r->n = nranks;
+    r->pos = pos;
+    r->off = split_chunks(size, (size_t)nranks);
+    r->maxc = r->off[1] - r->off[0];
+    r->algo = ONO_ALGO_XGMI;
+    if (nranks > 1 && (rc = xgmi_alloc(r))) {
+        ono_ring_destroy(r);
+        return rc;
+    }
+    *out = r;
+    return ONO_OK;
+}
+
+int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
+    if (!r || !handle) return set_error(ONO_E_ARG, "NULL argument");
+    memset(handle, 0, ONO_XGMI_HANDLE_BYTES);
+    if (r->n == 1) return ONO_OK;
+    int rc = xgmi_alloc(r);
+    if (rc) return rc;
+    DeviceGuard g(r->device);
+    hipIpcMemHandle_t h;
+    ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
+    memcpy(handle, &h, sizeof h);
+    return ONO_OK;
+}
+
+int ono_ring_xgmi_connect(ono_ring *r, const uint8_t *handles) {
+    if (!r || !handles) return set_error(ONO_E_ARG, "NULL argument");
+    if (r->n == 1) return ONO_OK;
+    int rc = xgmi_alloc(r);
+    if (rc) return rc;
+    return xgmi_connect(r, handles);
+}
+
+}  // extern "C"

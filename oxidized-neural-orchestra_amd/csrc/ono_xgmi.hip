@@ -1,0 +1,192 @@
+// ono_xgmi.hip — gfx950 kernels of the xGMI peer-access schedule (ONO_ALGO_XGMI).
+//
+// The ranks of one node map each other's exchange region (IPC, uncached HBM)
+// and move chunk slices with plain vector loads and stores over xGMI — no
+// RCCL, no staging copies.  One launch drives every peer link at once: the
+// workgroups of a launch are dealt round-robin over the peers' segments
+// (blockIdx % nseg), so all n-1 links carry traffic from the first wave on.
+//
+//   push  (scatter)  x = residual slice; peer.rbuf[k] = x; residual slice = 0
+//                    (worker_ring.rs:122, :133 — the slice leaves and is zeroed)
+//   pull  (gather)   grad[chunk of q] = dec(peer_q.obuf) / d
+//                    (worker_ring.rs:200 + the ÷n of param_manager.rs:183-188)
+//   barrier          every rank stores the round's epoch into every peer's flag
+//                    slot, then waits for all n-1 flags of its own (bounded:
+//                    a rank that never arrives sets the ring's error word
+//                    after ~timeout instead of hanging the grid)
+//
+// The owner's chain between the two (DirectOp in ono_kernels.hip) is the
+// reference arithmetic; these kernels only move bytes, HBM- and link-bound.
+#include <hip/hip_runtime.h>
+
+#include "ono_internal.h"
+
+namespace ono {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint16_t h4 __attribute__((ext_vector_type(4)));
+
+constexpr int kXBlock = 64;  // one wave per workgroup, one 16-B vector per lane (as ew_kernel)
+
+// half 2.7.1 f16_to_f32 (same rule as ono_kernels.hip from_f16)
+__device__ __forceinline__ float x_from_f16(uint16_t b) {
+    float f = (float)__builtin_bit_cast(_Float16, b);
+    uint32_t nb = ((uint32_t)(b & 0x8000u) << 16) | 0x7FC00000u | ((uint32_t)(b & 0x3FFu) << 13);
+    bool nan = ((b & 0x7C00u) == 0x7C00u) && (b & 0x3FFu);
+    return nan ? __builtin_bit_cast(float, nb) : f;
+}
+
+template <int M> __device__ __forceinline__ float xs(float x, float v) {
+    if constexpr (M == SCALE_NONE) return x;
+    else if constexpr (M == SCALE_RECIP) return x * v;
+    else return x / v;
+}
+
+// Element geometry of one segment: [0, head) scalar, [head, head + 4 nvec)
+// 4-wide, tail scalar; head == kScalarOnly: the operands' 4-element phases
+// differ, every element goes through the scalar path.
+__device__ __forceinline__ void seg_geometry(const XSeg &s, uint32_t t, int lane, bool &vec_ok, size_t &v,
+                                             size_t &nvec) {
+    nvec = (s.n - s.head) / 4;
+    v = (size_t)t * kXBlock + lane;
+    vec_ok = v < nvec;
+}
+
+struct PushOp {  // f32 slice -> peer receive slot, then zero the slice
+    __device__ __forceinline__ static void scalar(const XSeg &s, size_t i) {
+        float *src = (float *)s.src;
+        ((float *)s.dst)[i] = src[i];
+        src[i] = 0.0f;
+    }
+    __device__ __forceinline__ static void vec(const XSeg &s, size_t i) {
+        f4 *src = (f4 *)((float *)s.src + i);
+        f4 x = *src;  // plain load: the same lines are rewritten (zeroed) below
+        __builtin_nontemporal_store(x, (f4 *)((float *)s.dst + i));
+        __builtin_nontemporal_store(f4{0.0f, 0.0f, 0.0f, 0.0f}, src);
+    }
+};
+
+template <int M> struct PullF32Op {  // owner's f32 result (already ÷n) -> grad
+    float v;
+    __device__ __forceinline__ void scalar(const XSeg &s, size_t i) const {
+        ((float *)s.dst)[i] = xs<M>(((const float *)s.src)[i], v);
+    }
+    __device__ __forceinline__ void vec(const XSeg &s, size_t i) const {
+        f4 x = __builtin_nontemporal_load((const f4 *)((const float *)s.src + i));
+        if constexpr (M == SCALE_RECIP) x = x * v;
+        else if constexpr (M == SCALE_DIV) x = x / v;
+        __builtin_nontemporal_store(x, (f4 *)((float *)s.dst + i));
+    }
+};
+
+template <int M> struct PullF16Op {  // owner's f16 message -> grad = f32(h) / d
+    float v;
+    __device__ __forceinline__ void scalar(const XSeg &s, size_t i) const {
+        ((float *)s.dst)[i] = xs<M>(x_from_f16(((const uint16_t *)s.src)[i]), v);
+    }
+    __device__ __forceinline__ void vec(const XSeg &s, size_t i) const {
+        h4 h = __builtin_nontemporal_load((const h4 *)((const uint16_t *)s.src + i));
+        f4 x = {xs<M>(x_from_f16(h.x), v), xs<M>(x_from_f16(h.y), v), xs<M>(x_from_f16(h.z), v),
+                xs<M>(x_from_f16(h.w), v)};
+        __builtin_nontemporal_store(x, (f4 *)((float *)s.dst + i));
+    }
+};
+
+template <class Op>
+__global__ __launch_bounds__(kXBlock) void xseg_kernel(Op op, XSegs g) {
+    const int j = (int)(blockIdx.x % (unsigned)g.nseg);
+    const uint32_t t = blockIdx.x / (unsigned)g.nseg;
+    const XSeg s = g.s[j];
+    if (t >= s.tiles) return;
+    const int lane = threadIdx.x;
+    if (s.head == kScalarOnly) {  // 256 elements per tile, 4 per lane
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            size_t i = (size_t)t * (4 * kXBlock) + (size_t)u * kXBlock + lane;
+            if (i < s.n) op.scalar(s, i);
+        }
+        return;
+    }
+    bool vec_ok;
+    size_t v, nvec;
+    seg_geometry(s, t, lane, vec_ok, v, nvec);
+    if (t == 0) {
+        const size_t tail0 = s.head + 4 * nvec;
+        if ((size_t)lane < s.head) op.scalar(s, lane);
+        if ((size_t)lane < s.n - tail0) op.scalar(s, tail0 + lane);
+    }
+    if (vec_ok) op.vec(s, s.head + 4 * v);
+}
+
+// One workgroup; lane q < n signals peer q and waits for q's signal.
+__global__ __launch_bounds__(64) void xbarrier_kernel(XBarrier b) {
+    const int q = threadIdx.x;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // (system scope) earlier launches' stores first
+    if (q < b.n && q != b.pos)
+        __hip_atomic_store(b.peer_flags[q] + b.pos, b.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (q < b.n && q != b.pos) {
+        const uint64_t t0 = wall_clock64();
+        uint32_t spins = 0;
+        while (__hip_atomic_load(b.my_flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < b.epoch) {
+            if (wall_clock64() - t0 > b.timeout_ticks) {
+                __hip_atomic_store(b.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            if ((++spins & 63u) == 0 && __hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                break;  // timed out elsewhere, or ono_ring_abort()
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+}
+
+template <class Op>
+hipError_t launch_segs(const Op &op, XSegs g, hipStream_t s) {
+    uint32_t tiles = 0;
+    for (int j = 0; j < g.nseg; j++) {
+        XSeg &x = g.s[j];
+        if (x.head != kScalarOnly) {
+            if (x.head > x.n) x.head = (uint32_t)x.n;
+            size_t nvec = (x.n - x.head) / 4;
+            x.tiles = (uint32_t)std::max<size_t>(1, (nvec + kXBlock - 1) / kXBlock);
+        } else {
+            x.tiles = (uint32_t)((x.n + 4 * kXBlock - 1) / (4 * kXBlock));
+        }
+        if (x.n == 0) x.tiles = 0;
+        tiles = std::max(tiles, x.tiles);
+    }
+    if (g.nseg == 0 || tiles == 0) return hipSuccess;
+    const size_t blocks = (size_t)tiles * (size_t)g.nseg;
+    if (blocks > 0x7FFFFFFFu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xseg_kernel<Op>, dim3((unsigned)blocks), dim3(kXBlock), 0, s, op, g);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_xgmi_push(const XSegs &g, hipStream_t s) { return launch_segs(PushOp{}, g, s); }
+
+hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s) {
+    Scale sc = make_scale(divisor);
+    if (f16) {
+        switch (sc.mode) {
+        case SCALE_NONE: return launch_segs(PullF16Op<SCALE_NONE>{sc.v}, g, s);
+        case SCALE_RECIP: return launch_segs(PullF16Op<SCALE_RECIP>{sc.v}, g, s);
+        default: return launch_segs(PullF16Op<SCALE_DIV>{sc.v}, g, s);
+        }
+    }
+    switch (sc.mode) {
+    case SCALE_NONE: return launch_segs(PullF32Op<SCALE_NONE>{sc.v}, g, s);
+    case SCALE_RECIP: return launch_segs(PullF32Op<SCALE_RECIP>{sc.v}, g, s);
+    default: return launch_segs(PullF32Op<SCALE_DIV>{sc.v}, g, s);
+    }
+}
+
+hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s) {
+    if (b.n < 1 || b.n > ONO_MAX_INPUTS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xbarrier_kernel, dim3(1), dim3(64), 0, s, b);
+    return hipGetLastError();
+}
+
+}  // namespace ono

@@ -17,11 +17,12 @@ HEADER = os.path.normpath(os.path.join(HERE, "..", "..", "include", "ono_reduce.
 (ONO_OK, ONO_E_SIZE, ONO_E_PROTO, ONO_E_HIP, ONO_E_RCCL, ONO_E_ABORTED, ONO_E_ARG, ONO_E_OTHER,
  ONO_E_IO) = range(9)
 WIRE = {"f32": 0, "f16": 1}
-ALGO = {"auto": 0, "allreduce": 1, "hops": 2, "direct": 3}
+ALGO = {"auto": 0, "allreduce": 1, "hops": 2, "direct": 3, "xgmi": 4}
 OPT_KIND = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
 STORE_KIND = {"blocking": 0, "wild": 1}
 SYNC_KIND = {"barrier": 0, "nonblocking": 1}
 UID_BYTES = 128
+XGMI_HANDLE_BYTES = 64
 MAX_INPUTS = 16
 
 
@@ -97,6 +98,9 @@ _SIGS = {
     "ono_ring_unique_id": (_i, [C.c_char_p]),
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
     "ono_ring_create_tcp": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i, _i]),
+    "ono_ring_create_xgmi": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i]),
+    "ono_ring_xgmi_handle": (_i, [_vp, C.c_char_p]),
+    "ono_ring_xgmi_connect": (_i, [_vp, C.c_char_p]),
     "ono_ring_destroy": (_i, [_vp]),
     "ono_ring_set_pipeline": (_i, [_vp, _i]),
     "ono_ring_grad": (C.c_void_p, [_vp]),

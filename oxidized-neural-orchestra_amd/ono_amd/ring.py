@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import kernels
-from ._lib import ALGO, UID_BYTES, WIRE, call, lib
+from ._lib import ALGO, UID_BYTES, WIRE, XGMI_HANDLE_BYTES, call, lib
 
 
 class _DevArray:
@@ -105,6 +105,8 @@ class WorkerRingManager:
         h = C.c_void_p()
         if isinstance(uid, tuple):  # (fd_prev, fd_next): the TCP edge, see over_tcp()
             call("ono_ring_create_tcp", C.byref(h), pos, nranks, size, self.device, *uid)
+        elif uid == "xgmi":  # no communicator, see over_xgmi()
+            call("ono_ring_create_xgmi", C.byref(h), pos, nranks, size, self.device, WIRE[wire])
         else:
             call("ono_ring_create", C.byref(h), pos, nranks, size, self.device, uid, WIRE[wire])
         self._h = h
@@ -126,6 +128,26 @@ class WorkerRingManager:
         self = cls(pos, nranks, size, amount_of_layers, uid=fds, wire="f16", device=device)
         self._socks = (prev_sock, next_sock)
         self.algo = "hops"
+        return self
+
+    @classmethod
+    def over_xgmi(cls, pos: int, addrs, size: int, allgather, amount_of_layers: int = 1, *,
+                  wire: str = "f32", device: int | None = None) -> "WorkerRingManager":
+        """The xGMI peer-access schedule with no collective library: every rank
+        exports its exchange region and maps its peers' (ONO_ALGO_XGMI).
+        `allgather(bytes) -> list[bytes]` moves the 64-byte handles between the
+        ranks in rank order — any control channel (the reference's ring links,
+        a gloo group, a pipe).  Every rank must construct (and close) together."""
+        nranks = addrs if isinstance(addrs, int) else len(addrs)
+        self = cls(pos, nranks, size, amount_of_layers, uid="xgmi", wire=wire, device=device)
+        self.algo = "xgmi"
+        if nranks > 1:
+            buf = C.create_string_buffer(XGMI_HANDLE_BYTES)
+            call("ono_ring_xgmi_handle", self._h, buf)
+            handles = allgather(buf.raw)
+            if len(handles) != nranks or any(len(x) != XGMI_HANDLE_BYTES for x in handles):
+                raise ValueError("allgather must return one 64-byte handle per rank")
+            call("ono_ring_xgmi_connect", self._h, b"".join(handles))
         return self
 
     def _bind(self):
@@ -171,7 +193,7 @@ class WorkerRingManager:
         call("ono_ring_acc_residual", self._h, kernels.f32_ptr(grad), kernels.stream_handle(stream))
 
     def set_algo(self, algo: str) -> None:
-        """n > 1 exchange schedule: "allreduce" | "hops" | "direct" | "auto"."""
+        """n > 1 exchange schedule: "allreduce" | "hops" | "direct" | "xgmi" | "auto"."""
         call("ono_ring_set_algo", self._h, ALGO[algo])
         self.algo = algo
 

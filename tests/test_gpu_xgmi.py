@@ -1,0 +1,79 @@
+"""GPU parity of the xGMI peer-access schedule (ONO_ALGO_XGMI) against the oracle.
+
+n ranks run as n processes (tests/xgmi_worker.py), each owning a ring created
+with ono_ring_create_xgmi and connected through the 64-byte IPC handles of its
+peers — the production multi-process path.  On the one-GPU box every rank
+lives on cuda:0, so the mapped peer regions are IPC imports of the same
+device.  Checked bit for bit against the oracle's reference ring
+(worker_ring.rs:112-204, both wires), several rounds per ring (barrier epochs
+and buffer reuse), owned buckets and caller buffers at mismatched 4-element
+phases, ragged and tiny buckets, and the barrier timeout (a missing peer ends
+in IoError, not a hang).  Tolerance: 0 ulp.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(n: int, cases: list, timeout: float = 240.0) -> list:
+    port = _port()
+    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), str(port),
+                               json.dumps(cases)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(n)]
+    outs = []
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=timeout)
+            assert p.returncode == 0, f"rank exited {p.returncode}: {err[-2000:]}"
+            outs.append(json.loads(out.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return outs
+
+
+def check(outs):
+    bad = [(o["rank"], r["case"], r["msg"]) for o in outs for r in o["results"] if not r["ok"]]
+    assert not bad, bad[:6]
+
+
+def cases_for(n: int) -> list:
+    c = []
+    for wire in ("f32", "f16"):
+        c += [{"length": 109386, "wire": wire, "rounds": 3},                      # BASELINE config 1 bucket
+              {"length": 2 ** 18 + 5, "wire": wire, "form": "dev"},               # ragged chunks
+              {"length": 100003, "wire": wire, "form": "dev_offset", "seed": 7},  # phase mismatch paths
+              {"length": n, "wire": wire, "seed": 3},                             # one element per chunk
+              {"length": 4 * n + 3, "wire": wire, "seed": 5}]
+    return c
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_xgmi_ring_vs_oracle(n):
+    check(run_ranks(n, cases_for(n)))
+
+
+def test_xgmi_ring_large_ragged():
+    """64 MiB bucket + 5 elements over 4 ranks, both wires (chunk starts at
+    every phase; many tiles per peer segment)."""
+    check(run_ranks(4, [{"length": 2 ** 24 + 5, "wire": w, "rounds": 1} for w in ("f32", "f16")], 400.0))
+
+
+def test_xgmi_barrier_timeout_is_an_error_not_a_hang():
+    check(run_ranks(2, [{"kind": "timeout"}], 120.0))

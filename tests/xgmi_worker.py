@@ -1,0 +1,131 @@
+"""One rank of a multi-process xGMI-schedule test (tests/test_gpu_xgmi.py).
+
+Every rank is its own process (as on an 8-GPU node: one process per GPU); on
+the one-GPU test box all ranks share cuda:0, so the peer regions they map are
+IPC imports of the same device — the same code path (export, import, peer
+loads/stores, flag barriers), with HBM standing in for the xGMI links.  The
+64-byte handles travel over a gloo group (the control channel the reference
+would use is its ring TCP links).
+
+usage: python xgmi_worker.py RANK NRANKS PORT CASES_JSON
+Prints one JSON line: {"rank": r, "results": [{"case": ..., "ok": bool, "msg": str}, ...]}.
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "oxidized-neural-orchestra_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ono_amd  # noqa: E402
+from oracle import oracle as O  # noqa: E402  (checker only)
+
+SEED = 0x0402026
+
+
+def allgather(b: bytes) -> list:
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, b)
+    return out
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def run_case(rank: int, n: int, case: dict) -> str | None:
+    """None when the case passes, else a message."""
+    length, wire, rounds = case["length"], case["wire"], case.get("rounds", 2)
+    form = case.get("form", "owned")  # owned | dev | dev_offset
+    ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
+    try:
+        for rd in range(rounds):
+            ins = [O.synth(length, SEED + 100 * rd + case.get("seed", 0), r) for r in range(n)]
+            expect, _ = O.ring_pull_grads(ins, wire)
+            if form == "owned":
+                ring.residual.copy_(torch.from_numpy(ins[rank]))
+                ring.pull_grads()
+                torch.cuda.synchronize()
+                got, res_after = ring.grad.cpu().numpy(), ring.residual.cpu().numpy()
+            else:  # caller device buffers; dev_offset: views at different 4-element phases
+                ro, go = (1, 2) if form == "dev_offset" else (0, 0)
+                rbase = torch.zeros(length + 8, dtype=torch.float32, device="cuda")
+                gbase = torch.full((length + 8,), 7.0, dtype=torch.float32, device="cuda")
+                res, grad = rbase[ro:ro + length], gbase[go:go + length]
+                res.copy_(torch.from_numpy(ins[rank]))
+                ring.pull_grads_dev(res, grad)
+                torch.cuda.synchronize()
+                got, res_after = grad.cpu().numpy(), res.cpu().numpy()
+                if gbase[:go].ne(7.0).any().item() or gbase[go + length:].ne(7.0).any().item():
+                    return f"round {rd}: write outside the grad view"
+                if rbase[:ro].ne(0).any().item() or rbase[ro + length:].ne(0).any().item():
+                    return f"round {rd}: write outside the residual view"
+            bad = np.flatnonzero(bits(got) != bits(expect[rank]))
+            if bad.size:
+                i = bad[0]
+                return (f"round {rd}: {bad.size}/{length} differ, first at {i}: "
+                        f"0x{bits(got)[i]:08x} vs 0x{bits(expect[rank])[i]:08x}")
+            if bits(res_after).any():
+                return f"round {rd}: residual not zeroed ({np.count_nonzero(bits(res_after))} left)"
+        return None
+    finally:
+        ring.close()
+
+
+def run_timeout(rank: int, n: int) -> str | None:
+    """Rank 0 starts a round alone: its barrier gives up after the timeout and
+    the next call fails with IoError instead of hanging; the late rank's
+    teardown is bounded too."""
+    os.environ["ONO_XGMI_TIMEOUT_S"] = "2"  # read when the ring's region is allocated
+    try:
+        ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, 4096, allgather, wire="f32")
+    finally:
+        os.environ["ONO_XGMI_TIMEOUT_S"] = "10"
+    try:
+        if rank == 0:
+            t0 = time.time()
+            ring.pull_grads()
+            torch.cuda.synchronize()
+            waited = time.time() - t0
+            try:
+                ring.pull_grads()
+            except ono_amd.IoError:
+                pass
+            else:
+                return "second pull_grads after a timed-out barrier did not raise IoError"
+            if not 1.0 <= waited <= 30.0:
+                return f"barrier waited {waited:.1f} s (timeout 2 s)"
+        dist.barrier()
+        return None
+    finally:
+        ring.close()
+
+
+def main() -> int:
+    rank, n, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    cases = json.loads(sys.argv[4])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=n, init_method=f"tcp://127.0.0.1:{port}")
+    results = []
+    for case in cases:
+        try:
+            msg = run_timeout(rank, n) if case.get("kind") == "timeout" else run_case(rank, n, case)
+        except Exception as e:  # reported, the parent asserts
+            msg = f"{type(e).__name__}: {e}"
+        results.append({"case": case, "ok": msg is None, "msg": msg or ""})
+        dist.barrier()
+    print(json.dumps({"rank": rank, "results": results}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
