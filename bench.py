@@ -60,7 +60,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bucket-mib", type=int, default=256)
     ap.add_argument("--wire", choices=["f32", "f16"], default="f32")
-    ap.add_argument("--algo", choices=["auto", "allreduce", "hops", "direct"], default="auto")
+    ap.add_argument("--algo", choices=["auto", "allreduce", "hops", "direct", "xgmi"], default="auto")
     ap.add_argument("--segments", type=int, default=0,
                     help="f32 all-reduce pipeline segments (0 = library default: ONO_AR_SEGMENTS or 4)")
     ap.add_argument("--alt-schedules", default="allreduce:f32:1,direct:f32,direct:f16,hops:f16",
@@ -76,6 +76,13 @@ def parse_args(argv=None):
     ap.add_argument("--no-local-reduce", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true")
     ap.add_argument("--no-tcp-edge", action="store_true")
+    ap.add_argument("--no-xgmi", dest="xgmi", action="store_false",
+                    help="N > 1: skip the xGMI peer-access schedule (measured in child processes)")
+    ap.add_argument("--xgmi-timeout", type=float, default=240.0)
+    ap.add_argument("--xgmi-coresident", type=int, default=0,
+                    help="N = 1 rehearsal: run the xGMI schedule with this many ranks as processes on one GPU "
+                         "(HBM stands in for the links; informational)")
+    ap.add_argument("--xgmi-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-ranks", type=int, default=2)
     ap.add_argument("--cpu-rounds", type=int, default=3)
     return ap.parse_args(argv)
@@ -113,6 +120,13 @@ class Ctl:
         obj = [b]
         self.dist.broadcast_object_list(obj, src=0)
         return obj[0]
+
+    def allgather_bytes(self, b: bytes) -> list:
+        if not self.dist:
+            return [b]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, b)
+        return out
 
     def close(self) -> None:
         if self.dist and self.dist.is_initialized():
@@ -402,9 +416,91 @@ def tcp_edge(ono_amd, elems: int, rounds: int, ranks: int = 2) -> dict:
             "ranks": ranks, "ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 3)}
 
 
+
+# ------------------------------------------------------------- the step loop
+class Runner:
+    """W + K pull_grads rounds of a ring, each over its own freshly generated
+    bucket already resident in HBM (W + K buckets of the bench size), output
+    into one grad bucket."""
+
+    def __init__(self, torch, ono_amd, args, ctl: Ctl, world: int, rank: int, elems: int):
+        self.torch, self.ono_amd, self.args, self.ctl = torch, ono_amd, args, ctl
+        self.world, self.rank, self.elems = world, rank, elems
+        self.nb = args.warmup + args.steps
+        self.residuals = [torch.empty(elems, dtype=torch.float32, device="cuda") for _ in range(self.nb)]
+        self.grad = torch.empty(elems, dtype=torch.float32, device="cuda")
+        self.stream = torch.cuda.current_stream()
+
+    def refill(self) -> None:  # a fresh, distinct bucket for every step (untimed)
+        for i, t in enumerate(self.residuals):
+            self.ono_amd.kernels.synth(t, SEED + i, self.rank)
+        self.torch.cuda.synchronize()
+
+    def measure(self, r) -> tuple[float, dict]:
+        """W + K pull_grads rounds with ring r; (max-over-ranks seconds, timing).
+        N = 1: a step is exactly one kernel, so one HIP event pair around the
+        timed region gives its average launch duration without per-launch
+        events (which add ~6 % to a 130 us stream, tools/stream_variants.hip
+        "pull" mode).  N > 1: the timed run has no per-launch events; a second
+        run of the same K steps records them to split collectives and kernels
+        for the roofline."""
+        torch, args, nb = self.torch, self.args, self.nb
+        self.refill()
+        span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
+        def on_start():
+            span[0].record(self.stream)
+
+        def step(i: int) -> None:
+            r.pull_grads_dev(self.residuals[i], self.grad, self.stream)
+            if i == nb - 1:
+                span[1].record(self.stream)
+
+        el, _ = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, self.ctl, on_start=on_start)
+        span_ms = span[0].elapsed_time(span[1])
+        if self.world == 1:
+            return el, {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0}
+        self.refill()
+        timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, self.ctl,
+                     on_start=lambda: r.timing(True))
+        tim = r.timing_read()
+        r.timing(False)
+        return el, tim
+
+    def verify(self, wire: str) -> dict:
+        """Check the last measured step against the exact average: every rank
+        regenerates all N inputs of that step (counter-based generator) and
+        bounds |grad - sum/N| by the summation-order term 2(N-1) 2^-24 sum|g| / N
+        (f16 wire: + N 2^-11 sum|g| / N + N 2^-25 for the N f16 roundings);
+        the residual must be all zero.  ratio = max err / bound over all ranks
+        (<= 1 passes; 0 where the bound is 0 means bit-exact)."""
+        torch, n, i = self.torch, self.world, self.nb - 1
+        tmp = torch.empty(self.elems, dtype=torch.float32, device="cuda")
+        acc = torch.zeros(self.elems, dtype=torch.float64, device="cuda")
+        mag = torch.zeros(self.elems, dtype=torch.float64, device="cuda")
+        for r in range(n):
+            self.ono_amd.kernels.synth(tmp, SEED + i, r)
+            acc += tmp.double()
+            mag += tmp.abs().double()
+        bound = mag * (2 * (n - 1) * 2.0 ** -24 / n)
+        if wire == "f16":
+            bound += mag * 2.0 ** -11 + n * 2.0 ** -25
+        err = (self.grad.double() - acc / n).abs()
+        over = err > bound
+        ratio = float((err / bound.clamp_min(1e-300)).max().item()) if bool(bound.gt(0).any()) else 0.0
+        bad = int(over.sum().item())
+        left = int(self.residuals[i].count_nonzero().item())
+        del tmp, acc, mag, bound, err, over
+        self.torch.cuda.empty_cache()
+        ratio, bad, left = self.ctl.max(ratio), int(self.ctl.max(bad)), int(self.ctl.max(left))
+        return {"ok": bad == 0 and left == 0, "max_err_over_bound": round(ratio, 4), "elems_over_bound": bad,
+                "residual_nonzero": left}
+
 # ------------------------------------------------------------------- main
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.xgmi_child:
+        return xgmi_child_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -427,51 +523,14 @@ def main(argv=None) -> int:
 
     ring = new_ring(args.wire, args.algo)
     ring.set_pipeline(args.segments)
-
-    nb = args.warmup + args.steps
-    residuals = [torch.empty(elems, dtype=torch.float32, device="cuda") for _ in range(nb)]
-    grad = torch.empty(elems, dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream()
-
-    def refill() -> None:  # a fresh, distinct bucket for every step (untimed)
-        for i, t in enumerate(residuals):
-            ono_amd.kernels.synth(t, SEED + i, rank)
-        torch.cuda.synchronize()
-
-    def measure(r) -> tuple[float, dict]:
-        """W + K pull_grads rounds with ring r; (max-over-ranks seconds, timing).
-        N = 1: a step is exactly one kernel, so one HIP event pair around the
-        timed region gives its average launch duration without per-launch
-        events (which add ~6 % to a 130 us stream, tools/stream_variants.hip
-        "pull" mode).  N > 1: the timed run has no per-launch events; a second
-        run of the same K steps records them to split collectives and kernels
-        for the roofline."""
-        refill()
-        span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-
-        def on_start():
-            span[0].record(stream)
-
-        def step(i: int) -> None:
-            r.pull_grads_dev(residuals[i], grad, stream)
-            if i == nb - 1:
-                span[1].record(stream)
-
-        el, _ = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl, on_start=on_start)
-        span_ms = span[0].elapsed_time(span[1])
-        if world == 1:
-            return el, {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0}
-        refill()
-        timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, ctl, on_start=lambda: r.timing(True))
-        tim = r.timing_read()
-        r.timing(False)
-        return el, tim
+    run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
+    measure, stream = run.measure, run.stream
 
     link = xgmi_link_probe(torch) if (world > 1 and rank == 0) else None
     ctl.barrier()
     elapsed, tim = measure(ring)
 
-    extra = {}
+    extra = {"check": run.verify(args.wire)}
     if world == 1:
         avg_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
         per_launch = 12 * elems  # read residual, write grad, write zeros (SURVEY §8(d): 12 N)
@@ -527,6 +586,8 @@ def main(argv=None) -> int:
     alts = [a.split(":") for a in args.alt_schedules.split(",") if a] if extras else []
     if extras:
         line["alt_schedules"] = {}
+        if world > 1 and args.xgmi:  # in child processes: a fault there cannot take the main line down
+            line["alt_schedules"].update(xgmi_spawn(args, ctl, world, rank, local_rank))
 
         def fire():
             line["alt_schedules"]["error"] = f"watchdog: alternative schedules exceeded {args.alt_timeout:.0f} s"
@@ -552,7 +613,8 @@ def main(argv=None) -> int:
                 line["alt_schedules"][key] = {
                     "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
                     "ms_per_step": round(el / args.steps * 1e3, 4),
-                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps)}
+                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps),
+                    "check": run.verify(wire)}
             except Exception as e:  # recorded, never fatal for the main line
                 line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if args.sweep_mib:  # BASELINE config 4: the bandwidth-vs-bucket-size curve, main schedule
@@ -563,9 +625,9 @@ def main(argv=None) -> int:
                 init = np.zeros(elems, np.float32)
                 ps = ono_amd.ShardedParamServer(ring, init, ono_amd.GradientDescent(0.1))
                 params = torch.empty(elems, dtype=torch.float32, device="cuda")
-                refill()
+                run.refill()
                 ring.timing(False)
-                el, _ = timed_region(lambda i: ps.step(residuals[i], params, stream), args.steps, args.warmup,
+                el, _ = timed_region(lambda i: ps.step(run.residuals[i], params, stream), args.steps, args.warmup,
                                      torch.cuda.synchronize, ctl)
                 line["alt_schedules"]["ps:gd"] = {
                     "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
@@ -581,10 +643,96 @@ def main(argv=None) -> int:
             if r is not ring:
                 r.close()
 
+    if world == 1 and args.xgmi_coresident > 1:
+        line["xgmi_coresident"] = xgmi_spawn(args, ctl, world, rank, local_rank, coresident=args.xgmi_coresident)
+
     ring.close()
     ctl.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
+    return 0
+
+
+# ------------------------------------------------ xGMI schedule (children)
+def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresident: int = 0) -> dict:
+    """Measure the xGMI peer-access schedule (ONO_ALGO_XGMI) in child
+    processes: each rank starts one child on its GPU (coresident = R: rank 0
+    starts R children on its one GPU — a rehearsal with HBM standing in for
+    the links).  The children form their own ring (ono_ring_create_xgmi, IPC
+    handles over their own gloo group) and time both wires; a child that hangs
+    or faults is killed at --xgmi-timeout and recorded, the parent's line
+    survives.  Returns {"xgmi:f32": {...}, "xgmi:f16": {...}} from child rank 0."""
+    import socket
+    import subprocess
+
+    n = coresident or world
+    port = None
+    if rank == 0:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = str(sk.getsockname()[1]).encode()
+    port = ctl.bcast_bytes(port).decode()
+    import torch
+    torch.cuda.synchronize()
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--xgmi-child", "--gpus", str(n), "--steps",
+           str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib)]
+    procs = []
+    for r in (range(n) if coresident else [rank]):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    deadline = time.time() + args.xgmi_timeout
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=max(1.0, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+            err = f"killed after {args.xgmi_timeout:.0f} s; " + (err or "")
+        outs.append((p.returncode, out, err))
+    ctl.barrier()
+    if rank != 0:
+        return {}
+    rc, out, err = outs[0]
+    try:
+        res = json.loads(out.strip().splitlines()[-1])
+        if coresident:
+            res["note"] = (f"co-resident rehearsal: {n} ranks as processes on ONE GPU, peer regions are IPC "
+                           "imports of the same HBM; the xGMI roofline fields do not apply")
+        return res
+    except (ValueError, IndexError):
+        return {"xgmi": {"error": f"child rank 0 exited {rc}: {(err or '').strip()[-300:]}"}}
+
+
+def xgmi_child_main(args) -> int:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import ono_amd
+
+    torch.cuda.set_device(local_rank)
+    ctl = Ctl(world, rank)
+    elems = args.bucket_mib * (1 << 20) // 4
+    run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
+    out = {}
+    for wire in ("f32", "f16"):
+        key = f"xgmi:{wire}"
+        try:
+            ring = ono_amd.WorkerRingManager.over_xgmi(rank, world, elems, ctl.allgather_bytes, wire=wire,
+                                                       device=local_rank)
+            el, t = run.measure(ring)
+            out[key] = {"value": round(world * elems * 4 * args.steps / el / GIB, 3),
+                        "ms_per_step": round(el / args.steps * 1e3, 4),
+                        "roofline": xgmi_roofline(t, elems * 4, elems, world, wire, "xgmi", args.steps),
+                        "check": run.verify(wire)}
+            ring.close()
+        except Exception as e:  # recorded
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    ctl.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     return 0
 
 
@@ -655,7 +803,7 @@ def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: st
     wb = 2 if wire == "f16" else 4
     if algo in ("allreduce", "auto") and wire == "f32":
         bytes_out = 2 * (world - 1) / world * bucket_bytes            # ring all-reduce (any segmentation)
-    elif algo == "direct":
+    elif algo in ("direct", "xgmi"):
         bytes_out = (world - 1) / world * (bucket_bytes + elems * wb)  # all-to-all f32 + all-gather
     else:
         bytes_out = 2 * (world - 1) / world * elems * wb              # n-1 + n-1 hops
