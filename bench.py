@@ -727,6 +727,20 @@ def xgmi_child_main(args) -> int:
                         "ms_per_step": round(el / args.steps * 1e3, 4),
                         "roofline": xgmi_roofline(t, elems * 4, elems, world, wire, "xgmi", args.steps),
                         "check": run.verify(wire)}
+            if wire == "f32":  # BASELINE config 5 over the same regions: push -> sum + fused GD -> pull
+                import numpy as np
+                ps = ono_amd.ShardedParamServer(ring, np.zeros(elems, np.float32), ono_amd.GradientDescent(0.1))
+                params = torch.empty(elems, dtype=torch.float32, device="cuda")
+                run.refill()
+                el, _ = timed_region(lambda i: ps.step(run.residuals[i], params, run.stream), args.steps,
+                                     args.warmup, torch.cuda.synchronize, ctl)
+                out["xgmi-ps:gd"] = {
+                    "value": round(world * elems * 4 * args.steps / el / GIB, 3),
+                    "ms_per_step": round(el / args.steps * 1e3, 4),
+                    "workload": "ShardedParamServer.step over the xGMI exchange regions: push gradient slices -> "
+                                "worker-order sum + fused /n + GD on the owned shard -> pull params"}
+                ps.close()
+                del params
             ring.close()
         except Exception as e:  # recorded
             out[key] = {"error": f"{type(e).__name__}: {e}"[:300]}

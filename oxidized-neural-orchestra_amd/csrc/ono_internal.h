@@ -72,7 +72,7 @@ hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, si
 // launcher.
 constexpr uint32_t kScalarOnly = 0xFFFFFFFFu;
 struct XSeg {
-    const void *src;  // push: local residual slice (f32, zeroed after the read); pull: peer obuf (f32 / f16)
+    const void *src;  // push: local slice (f32; a ring residual is zeroed after the read); pull: peer obuf
     void *dst;        // push: peer receive slot (f32); pull: local grad (f32)
     uint64_t n;
     uint32_t head;
@@ -89,7 +89,7 @@ struct XBarrier {
     uint64_t epoch, timeout_ticks;
     int n, pos;
 };
-hipError_t launch_xgmi_push(const XSegs &g, hipStream_t s);
+hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s);
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s);
 hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s);
 

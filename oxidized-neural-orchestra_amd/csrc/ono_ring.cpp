@@ -1198,6 +1198,8 @@ int ono_ps_step(ono_ps *p, const float *grad, float *params, void *stream) {
         float bc1 = 1.0f - p->beta1_t, bc2 = 1.0f - p->beta2_t;
         p->opt.step_size = p->opt.lr * (std::sqrt(bc2) / bc1);
     }
+    if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // peer-access form, no padding needed
+        return xgmi_ps_step(r, grad, params, N, C, p->gshard, p->ppad + (size_t)r->pos * C, p->opt, p->v, p->s, s);
     const float *gsrc = grad;
     if (p->padded != N) {
         ONO_HIP(hipMemcpyAsync(p->gpad, grad, N * sizeof(float), hipMemcpyDeviceToDevice, s));

@@ -176,7 +176,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
         sg.head = head_of(sg.src, 4, sg.dst, 4);
     }
     int rc = timed(r, s, 1, [&]() -> int {
-        ONO_HIP(launch_xgmi_push(push, s));
+        ONO_HIP(launch_xgmi_push(push, true, s));
         return ONO_OK;
     });
     if (rc || (rc = barrier(r, s))) return rc;  // 2.
@@ -203,15 +203,87 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
     });
 }
 
+int ensure_connected(ono_ring *r, hipStream_t s) {
+    if (r->xgmi && r->xgmi->connected) return ONO_OK;
+    return xgmi_connect_over_rccl(r, s);
+}
+
 }  // namespace
 
 namespace ono {
 
-int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
-    if (!r->xgmi || !r->xgmi->connected) {
-        int rc = xgmi_connect_over_rccl(r, s);
-        if (rc) return rc;
+// Multi-GPU parameter-server step over the same exchange regions (BASELINE
+// config 5; the RCCL form is ono_ps_step's reduce-scatter + all-gather).
+// Shard q = [q C, min(N, (q+1) C)) lives on rank q (store.rs:84-124 with one
+// shard server per GPU):
+//   1. push     my gradient slice of every peer's shard -> that owner's slot
+//               for my worker index (the gradient itself is left untouched)
+//   2. barrier
+//   3. owner    acc = g_0 + g_1 + ... + g_{n-1} in worker order (the
+//               BlockingStore accumulate order when workers arrive in rank
+//               order, store.rs:84-91), then the fused (+0, ÷n, optimizer,
+//               zero_grad) shard update (shard.rs:74-92) that also writes the
+//               new shard into my result buffer
+//   4. barrier
+//   5. pull     every shard's parameters -> params (store.rs:110-124)
+// Bit-exact with the store oracle fed in worker order.
+int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t C, float *gshard, float *wshard,
+                 const OptLaunch &opt, float *v, float *s_, hipStream_t s) {
+    int rc = ensure_connected(r, s);
+    if (rc) return rc;
+    XgmiState *x = r->xgmi;
+    if (C + 4 > x->slot)
+        return set_error(ONO_E_SIZE, "PS shard of %zu elements exceeds the ring's exchange slot (%zu)", C, x->slot - 4);
+    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
+        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    const int n = r->n, pos = r->pos;
+    auto lo = [&](int q) { return std::min(N, (size_t)q * C); };
+    auto len = [&](int q) { return std::min(N, lo(q) + C) - lo(q); };
+    auto slot_of = [&](int w, int owner) { return w < owner ? w : w - 1; };  // worker order, owner excluded
+
+    XSegs push{};
+    for (int d = 1; d < n; d++) {
+        const int q = (pos + d) % n;
+        XSeg &sg = push.s[push.nseg++];
+        sg.src = grad + lo(q);
+        sg.dst = rbuf_of(x, x->peer[q], slot_of(pos, q)) + ph(lo(q));
+        sg.n = len(q);
+        sg.head = head_of(sg.src, 4, sg.dst, 4);
     }
+    rc = timed(r, s, 1, [&]() -> int {
+        ONO_HIP(launch_xgmi_push(push, false, s));
+        return ONO_OK;
+    });
+    if (rc || (rc = barrier(r, s))) return rc;
+
+    float *out = reinterpret_cast<float *>(obuf_of(x, x->xbuf)) + ph(lo(pos));
+    if (len(pos) > 0) {
+        const float *ins[ONO_MAX_INPUTS];
+        for (int w = 0; w < n; w++)
+            ins[w] = w == pos ? grad + lo(pos) : rbuf_of(x, x->xbuf, slot_of(w, pos)) + ph(lo(pos));
+        ONO_K(r, s, launch_sum_scale(gshard, ins, n, len(pos), 1.0f, s));
+        ONO_K(r, s, launch_opt_update(opt, gshard, wshard, v, s_, len(pos), true, s, out));
+    }
+    if ((rc = barrier(r, s))) return rc;
+
+    XSegs pull{};
+    for (int d = 0; d < n; d++) {
+        const int q = (pos + d) % n;
+        XSeg &sg = pull.s[pull.nseg++];
+        sg.src = reinterpret_cast<const float *>(obuf_of(x, x->peer[q])) + ph(lo(q));
+        sg.dst = params + lo(q);
+        sg.n = len(q);
+        sg.head = head_of(sg.src, 4, sg.dst, 4);
+    }
+    return timed(r, s, 1, [&]() -> int {
+        ONO_HIP(launch_xgmi_pull(pull, false, 1.0f, s));
+        return ONO_OK;
+    });
+}
+
+int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    int rc = ensure_connected(r, s);
+    if (rc) return rc;
     return r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, res, grad, s) : xgmi_round<float>(r, res, grad, s);
 }
 

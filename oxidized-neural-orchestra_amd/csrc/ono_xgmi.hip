@@ -53,17 +53,23 @@ __device__ __forceinline__ void seg_geometry(const XSeg &s, uint32_t t, int lane
     vec_ok = v < nvec;
 }
 
-struct PushOp {  // f32 slice -> peer receive slot, then zero the slice
+// f32 slice -> peer receive slot; ZERO: then zero the slice (the ring's
+// residual); without: a plain copy (the PS mode's gradient stays the caller's)
+template <bool ZERO> struct PushOp {
     __device__ __forceinline__ static void scalar(const XSeg &s, size_t i) {
         float *src = (float *)s.src;
         ((float *)s.dst)[i] = src[i];
-        src[i] = 0.0f;
+        if constexpr (ZERO) src[i] = 0.0f;
     }
     __device__ __forceinline__ static void vec(const XSeg &s, size_t i) {
         f4 *src = (f4 *)((float *)s.src + i);
-        f4 x = *src;  // plain load: the same lines are rewritten (zeroed) below
-        __builtin_nontemporal_store(x, (f4 *)((float *)s.dst + i));
-        __builtin_nontemporal_store(f4{0.0f, 0.0f, 0.0f, 0.0f}, src);
+        if constexpr (ZERO) {
+            f4 x = *src;  // plain load: the same lines are rewritten (zeroed) below
+            __builtin_nontemporal_store(x, (f4 *)((float *)s.dst + i));
+            __builtin_nontemporal_store(f4{0.0f, 0.0f, 0.0f, 0.0f}, src);
+        } else {
+            __builtin_nontemporal_store(__builtin_nontemporal_load(src), (f4 *)((float *)s.dst + i));
+        }
     }
 };
 
@@ -165,7 +171,9 @@ hipError_t launch_segs(const Op &op, XSegs g, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_xgmi_push(const XSegs &g, hipStream_t s) { return launch_segs(PushOp{}, g, s); }
+hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s) {
+    return zero_src ? launch_segs(PushOp<true>{}, g, s) : launch_segs(PushOp<false>{}, g, s);
+}
 
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s) {
     Scale sc = make_scale(divisor);

@@ -75,5 +75,16 @@ def test_xgmi_ring_large_ragged():
     check(run_ranks(4, [{"length": 2 ** 24 + 5, "wire": w, "rounds": 1} for w in ("f32", "f16")], 400.0))
 
 
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_xgmi_sharded_ps_vs_store_oracle(n):
+    """BASELINE config 5 over the exchange regions: push gradient slices to the
+    shard owners, worker-order sum + fused (+0, /n, optimizer) update, pull the
+    parameters; bit-exact with the BlockingStore oracle for GD, momentum, Adam,
+    ragged and tiny shards."""
+    cases = [{"kind": "ps", "length": 100003, "opt": k} for k in ("gd", "momentum", "adam")]
+    cases += [{"kind": "ps", "length": n + 1, "opt": "gd", "steps": 2}]
+    check(run_ranks(n, cases))
+
+
 def test_xgmi_barrier_timeout_is_an_error_not_a_hang():
     check(run_ranks(2, [{"kind": "timeout"}], 120.0))

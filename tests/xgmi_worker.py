@@ -80,6 +80,40 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
         ring.close()
 
 
+def run_ps(rank: int, n: int, case: dict) -> str | None:
+    """ShardedParamServer over the xGMI ring (BASELINE config 5): every rank
+    is a worker and the server of shard `rank`; after each step all ranks
+    hold the parameters the BlockingStore oracle computes when the n workers'
+    gradients arrive in rank order."""
+    nparams, kind, steps = case["length"], case["opt"], case.get("steps", 3)
+    opt = {"gd": ono_amd.GradientDescent(0.1), "momentum": ono_amd.GradientDescentWithMomentum(0.1, 0.9),
+           "adam": ono_amd.Adam(0.1, 0.9, 0.999, 1e-8)}[kind]
+    init = O.synth(nparams, SEED, 99)
+    ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, nparams, allgather)
+    ps = ono_amd.ShardedParamServer(ring, init, opt)
+    ref = O.Store(init, 1000, n, kind, lr=0.1, momentum=0.9, beta1=0.9, beta2=0.999, eps=1e-8)
+    try:
+        params = torch.empty(nparams, device="cuda")
+        for st in range(steps):
+            gs = [O.synth(nparams, SEED + 10 * st, w) for w in range(n)]
+            g = torch.from_numpy(gs[rank]).cuda()
+            ps.step(g, params)
+            for w in range(n):
+                ref.accumulate(gs[w])
+            ref.update_params()
+            torch.cuda.synchronize()
+            if not np.array_equal(bits(g.cpu().numpy()), bits(gs[rank])):
+                return f"step {st}: the worker's gradient was modified"
+            got, exp = bits(params.cpu().numpy()), bits(ref.pull_params())
+            bad = np.flatnonzero(got != exp)
+            if bad.size:
+                return f"step {st}: {bad.size}/{nparams} differ, first at {bad[0]}"
+        return None
+    finally:
+        ps.close()
+        ring.close()
+
+
 def run_timeout(rank: int, n: int) -> str | None:
     """Rank 0 starts a round alone: its barrier gives up after the timeout and
     the next call fails with IoError instead of hanging; the late rank's
@@ -117,7 +151,9 @@ def main() -> int:
     results = []
     for case in cases:
         try:
-            msg = run_timeout(rank, n) if case.get("kind") == "timeout" else run_case(rank, n, case)
+            kind = case.get("kind", "ring")
+            msg = run_timeout(rank, n) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
+                run_case(rank, n, case)
         except Exception as e:  # reported, the parent asserts
             msg = f"{type(e).__name__}: {e}"
         results.append({"case": case, "ok": msg is None, "msg": msg or ""})
