@@ -673,7 +673,8 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
             port = str(sk.getsockname()[1]).encode()
     port = ctl.bcast_bytes(port).decode()
     import torch
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()  # nothing of the parent's in flight while the children run
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--xgmi-child", "--gpus", str(n), "--steps",
            str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib)]
     procs = []

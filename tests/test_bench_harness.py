@@ -87,3 +87,37 @@ def test_build_line_contract():
 def test_gpus_mismatch_is_an_error(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "1")
     assert bench.main(["--gpus", "2"]) == 2
+
+
+XGMI_SPAWN = r"""
+import json, os, sys, types
+sys.path.insert(0, {root!r})
+import bench
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+ctl = bench.Ctl(world, rank)
+args = types.SimpleNamespace(steps=2, warmup=1, bucket_mib=1, xgmi_timeout=90.0)
+res = bench.xgmi_spawn(args, ctl, world, rank, rank)
+print(json.dumps({{"rank": rank, "res": res}}), flush=True)
+ctl.close()
+"""
+
+
+def test_xgmi_children_failing_is_recorded_not_fatal():
+    """bench.py's N > 1 xGMI leg runs in child processes; when they fail (here:
+    no GPU) every parent returns, rank 0 records the child's error, nobody hangs."""
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, "-c", XGMI_SPAWN.format(root=ROOT)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        out, err = p.communicate(timeout=180)
+        assert p.returncode == 0, err
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    r0 = [o for o in outs if o["rank"] == 0][0]["res"]
+    r1 = [o for o in outs if o["rank"] == 1][0]["res"]
+    assert r1 == {}
+    assert "error" in r0.get("xgmi", {}) or all("error" in v for v in r0.values())
