@@ -618,7 +618,12 @@ def main(argv=None) -> int:
             except Exception as e:  # recorded, never fatal for the main line
                 line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if args.sweep_mib:  # BASELINE config 4: the bandwidth-vs-bucket-size curve, main schedule
-            line["size_sweep"] = size_sweep(torch, ono_amd, ctl, new_ring, args, world, rank, stream)
+            def sweep_ring(e):
+                r = new_ring(args.wire, args.algo, e)
+                r.set_pipeline(args.segments)
+                return r
+            line["size_sweep"] = size_sweep(torch, ono_amd, ctl, sweep_ring, sweep_sizes(args.sweep_mib), world,
+                                            rank, stream)
         if args.ps_mode:  # BASELINE config 5: sharded synchronizer, RS + fused GD + AG
             try:
                 import numpy as np
@@ -676,7 +681,8 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
     if torch.cuda.is_available():
         torch.cuda.synchronize()  # nothing of the parent's in flight while the children run
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--xgmi-child", "--gpus", str(n), "--steps",
-           str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib)]
+           str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib),
+           "--sweep-mib", getattr(args, "sweep_mib", "")]
     procs = []
     for r in (range(n) if coresident else [rank]):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
@@ -745,22 +751,27 @@ def xgmi_child_main(args) -> int:
             ring.close()
         except Exception as e:  # recorded
             out[key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if args.sweep_mib:  # config 4 curve + the config-1 bucket, f32 wire
+        out["xgmi:f32_size_sweep"] = size_sweep(
+            torch, ono_amd, ctl, lambda e: ono_amd.WorkerRingManager.over_xgmi(
+                rank, world, e, ctl.allgather_bytes, wire="f32", device=local_rank),
+            sweep_sizes(args.sweep_mib), world, rank, run.stream)
     ctl.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     return 0
 
 
-def size_sweep(torch, ono_amd, ctl, new_ring, args, world: int, rank: int, stream) -> dict:
-    """pull_grads of the main schedule over bucket sizes
-    1 MiB … 1 GiB (10 timed + 3 warmup steps each, a fresh bucket per step,
-    max over ranks).  Informational; `value` stays the 256 MiB line."""
+def size_sweep(torch, ono_amd, ctl, make_ring, sizes, world: int, rank: int, stream) -> dict:
+    """pull_grads over bucket sizes (10 timed + 3
+    warmup steps each, a fresh bucket per step, max over ranks), plus the
+    reference's own config-1 bucket (the MLP's 109,386 f32, latency-bound).
+    `sizes` = [(label, elems)], `make_ring(elems)` builds the schedule's ring.
+    Informational; `value` stays the 256 MiB line."""
     out = {}
-    for mib in [int(x) for x in args.sweep_mib.split(",") if x]:
+    for label, e in sizes:
         try:
-            e = mib << 18
-            r = new_ring(args.wire, args.algo, e)
-            r.set_pipeline(args.segments)
+            r = make_ring(e)
             k, w = 10, 3
             bufs = [torch.empty(e, dtype=torch.float32, device="cuda") for _ in range(k + w)]
             for i, t in enumerate(bufs):
@@ -769,14 +780,18 @@ def size_sweep(torch, ono_amd, ctl, new_ring, args, world: int, rank: int, strea
             torch.cuda.synchronize()
             el, _ = timed_region(lambda i: r.pull_grads_dev(bufs[i], g, stream), k, w, torch.cuda.synchronize, ctl)
             alg = e * 4 * k / el / GIB
-            out[f"{mib}MiB"] = {"ms_per_step": round(el / k * 1e3, 4), "algbw_gib_s": round(alg, 3),
-                                "busbw_gib_s": round(alg * 2 * (world - 1) / world, 3) if world > 1 else None}
+            out[label] = {"ms_per_step": round(el / k * 1e3, 4), "algbw_gib_s": round(alg, 3),
+                          "busbw_gib_s": round(alg * 2 * (world - 1) / world, 3) if world > 1 else None}
             r.close()
             del bufs, g
             torch.cuda.empty_cache()
         except Exception as ex:  # recorded, never fatal
-            out[f"{mib}MiB"] = {"error": f"{type(ex).__name__}: {ex}"[:200]}
-    return {"workload": "pull_grads_dev of the main schedule per bucket size (config 4 curve)", "sizes": out}
+            out[label] = {"error": f"{type(ex).__name__}: {ex}"[:200]}
+    return {"workload": "pull_grads_dev per bucket size (config 4 curve; config1 = the MLP bucket)", "sizes": out}
+
+
+def sweep_sizes(sweep_mib: str) -> list:
+    return [("config1", CONFIG1_ELEMS)] + [(f"{int(m)}MiB", int(m) << 18) for m in sweep_mib.split(",") if m]
 
 
 def xgmi_link_probe(torch) -> dict | None:
