@@ -724,8 +724,9 @@ def xgmi_child_main(args) -> int:
     elems = args.bucket_mib * (1 << 20) // 4
     run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
     out = {}
-    for wire in ("f32", "f16"):
-        key = f"xgmi:{wire}"
+    for gather, wire in (("pull", "f32"), ("pull", "f16"), ("push", "f32"), ("push", "f16")):
+        key = f"xgmi:{wire}" if gather == "pull" else f"xgmi-pushgather:{wire}"
+        os.environ["ONO_XGMI_GATHER"] = gather  # read when the ring's exchange region is made
         try:
             ring = ono_amd.WorkerRingManager.over_xgmi(rank, world, elems, ctl.allgather_bytes, wire=wire,
                                                        device=local_rank)
@@ -734,7 +735,7 @@ def xgmi_child_main(args) -> int:
                         "ms_per_step": round(el / args.steps * 1e3, 4),
                         "roofline": xgmi_roofline(t, elems * 4, elems, world, wire, "xgmi", args.steps),
                         "check": run.verify(wire)}
-            if wire == "f32":  # BASELINE config 5 over the same regions: push -> sum + fused GD -> pull
+            if wire == "f32" and gather == "pull":  # BASELINE config 5 over the same regions: push -> sum + GD -> pull
                 import numpy as np
                 ps = ono_amd.ShardedParamServer(ring, np.zeros(elems, np.float32), ono_amd.GradientDescent(0.1))
                 params = torch.empty(elems, dtype=torch.float32, device="cuda")
@@ -751,6 +752,7 @@ def xgmi_child_main(args) -> int:
             ring.close()
         except Exception as e:  # recorded
             out[key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    os.environ["ONO_XGMI_GATHER"] = "pull"
     if args.sweep_mib:  # config 4 curve + the config-1 bucket, f32 wire
         out["xgmi:f32_size_sweep"] = size_sweep(
             torch, ono_amd, ctl, lambda e: ono_amd.WorkerRingManager.over_xgmi(

@@ -16,6 +16,12 @@
 //   4. barrier  all owners' results are ready
 //   5. pull     for every peer q: grad[chunk of q] = dec(q.obuf) (/ n for f16)
 //
+// Gather variant (env ONO_XGMI_GATHER=push, read when the region is made):
+// step 3 also stores the owner's result into every peer's gather slot over
+// xGMI (remote writes instead of remote reads), and step 5 unpacks the local
+// gather slots.  Same bytes on the links, one extra local pass; which one the
+// links prefer is measured by bench.py at N > 1.
+//
 // Bit-exact with the reference hop order for both wires (the chain is the
 // direct schedule's, tested against the oracle).  Bytes per rank on the links:
 // (n-1)/n 4N out in step 1, (n-1)/n 4N (f32) or 2N (f16) in step 5, all n-1
@@ -46,6 +52,8 @@ struct XgmiState {
     uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
     size_t slot = 0;                  // elements per receive slot (multiple of 64: 256-B aligned slots)
     size_t obuf_off = 0;              // byte offset of the owner's result buffer
+    bool push_gather = false;         // env ONO_XGMI_GATHER=push: owners store results into peers' gather slots
+    size_t gat_off = 0;               // byte offset of the n-1 gather slots (push_gather only)
     std::vector<uint8_t *> peer;      // every rank's region as mapped here (peer[pos] = xbuf)
     bool connected = false;
     uint64_t epoch = 0;               // barriers issued so far (the same sequence on every rank)
@@ -71,7 +79,10 @@ int xgmi_alloc(ono_ring *r) {
     x->slot = align_up(r->maxc + 4, 64);
     const size_t rb = (size_t)std::max(r->n - 1, 1) * x->slot * sizeof(float);
     x->obuf_off = align_up(kFlagBytes + rb, 256);
-    const size_t bytes = x->obuf_off + x->slot * sizeof(float);
+    x->gat_off = align_up(x->obuf_off + x->slot * sizeof(float), 256);
+    const char *gm = getenv("ONO_XGMI_GATHER");
+    x->push_gather = gm && strcmp(gm, "push") == 0;
+    const size_t bytes = x->push_gather ? x->gat_off + rb : x->gat_off;
     ONO_HIP(hipExtMallocWithFlags((void **)&x->xbuf, bytes, hipDeviceMallocUncached));
     ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0
     ONO_HIP(hipDeviceSynchronize());              // zeroed before the handle leaves this process
@@ -94,6 +105,10 @@ float *rbuf_of(const XgmiState *x, uint8_t *region, int k) {
     return reinterpret_cast<float *>(region + kFlagBytes) + (size_t)k * x->slot;
 }
 uint8_t *obuf_of(const XgmiState *x, uint8_t *region) { return region + x->obuf_off; }
+// receiver q's gather slot for owner o's result (push_gather), slots in owner order without q
+uint8_t *gslot_of(const XgmiState *x, uint8_t *region_q, int o, int q) {
+    return region_q + x->gat_off + (size_t)(o < q ? o : o - 1) * x->slot * sizeof(float);
+}
 
 int xgmi_connect(ono_ring *r, const uint8_t *handles) {
     XgmiState *x = r->xgmi;
@@ -184,6 +199,30 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
     const float *ins[ONO_MAX_INPUTS];  // 3. the chain of my chunk, reference order
     for (int k = 0; k < n - 1; k++) ins[k] = rbuf_of(x, x->xbuf, k) + ph(off[c]);
     ins[n - 1] = res + off[c];
+    if (x->push_gather) {  // 3'. owner chain + its result stored straight into every peer's gather slot
+        W *outs[ONO_MAX_INPUTS];
+        int no = 0;
+        for (int d = 1; d < n; d++) {
+            const int q = (pos + d) % n;
+            outs[no++] = reinterpret_cast<W *>(gslot_of(x, x->peer[q], pos, q)) + ph(off[c]);
+        }
+        rc = timed(r, s, 1, [&]() -> int {
+            ONO_HIP(launch_direct_multi<W>(grad + off[c], outs, no, ins, n, len(c), (float)n, false, s));
+            return ONO_OK;
+        });
+        if (rc || (rc = barrier(r, s))) return rc;
+        XSegs unpack{};  // 5'. local: every owner's result from my gather slots -> my grad
+        for (int d = 1; d < n; d++) {
+            const int q = (pos + d) % n, cq = (q + 1) % n;
+            XSeg &sg = unpack.s[unpack.nseg++];
+            sg.src = reinterpret_cast<const W *>(gslot_of(x, x->xbuf, q, pos)) + ph(off[cq]);
+            sg.dst = grad + off[cq];
+            sg.n = len(cq);
+            sg.head = head_of(sg.src, sizeof(W), sg.dst, 4);
+        }
+        ONO_K(r, s, launch_xgmi_pull(unpack, f16, f16 ? (float)n : 1.0f, s));
+        return ONO_OK;
+    }
     W *out = reinterpret_cast<W *>(obuf_of(x, x->xbuf)) + ph(off[c]);
     ONO_K(r, s, launch_direct<W>(grad + off[c], out, ins, n, len(c), (float)n, false, s));
     if ((rc = barrier(r, s))) return rc;  // 4.

@@ -28,9 +28,9 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(n: int, cases: list, timeout: float = 240.0) -> list:
+def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull") -> list:
     port = _port()
-    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1")
+    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), str(port),
                                json.dumps(cases)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for r in range(n)]
@@ -64,15 +64,21 @@ def cases_for(n: int) -> list:
     return c
 
 
+@pytest.mark.parametrize("gather", ["pull", "push"])
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
-def test_xgmi_ring_vs_oracle(n):
-    check(run_ranks(n, cases_for(n)))
+def test_xgmi_ring_vs_oracle(n, gather):
+    """gather "pull": replicas load the owners' results over the links;
+    "push" (ONO_XGMI_GATHER=push): owners store them into the replicas'
+    gather slots, replicas unpack locally."""
+    check(run_ranks(n, cases_for(n), gather=gather))
 
 
-def test_xgmi_ring_large_ragged():
+@pytest.mark.parametrize("gather", ["pull", "push"])
+def test_xgmi_ring_large_ragged(gather):
     """64 MiB bucket + 5 elements over 4 ranks, both wires (chunk starts at
     every phase; many tiles per peer segment)."""
-    check(run_ranks(4, [{"length": 2 ** 24 + 5, "wire": w, "rounds": 1} for w in ("f32", "f16")], 400.0))
+    check(run_ranks(4, [{"length": 2 ** 24 + 5, "wire": w, "rounds": 1} for w in ("f32", "f16")], 400.0,
+                    gather=gather))
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
