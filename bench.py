@@ -83,6 +83,9 @@ def parse_args(argv=None):
                     help="N = 1 rehearsal: run the xGMI schedule with this many ranks as processes on one GPU "
                          "(HBM stands in for the links; informational)")
     ap.add_argument("--xgmi-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on device 0 (with --algo xgmi, which needs no "
+                         "RCCL, the whole N > 1 flow runs: torchrun launch, rings, checks, children, JSON line)")
     ap.add_argument("--cpu-ranks", type=int, default=2)
     ap.add_argument("--cpu-rounds", type=int, default=3)
     return ap.parse_args(argv)
@@ -503,7 +506,7 @@ def main(argv=None) -> int:
         return xgmi_child_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
@@ -517,6 +520,9 @@ def main(argv=None) -> int:
     bucket_bytes = elems * 4
 
     def new_ring(wire: str, algo: str, size: int = elems):
+        if algo == "xgmi" and world > 1:  # no communicator: IPC handles over the control plane
+            return ono_amd.WorkerRingManager.over_xgmi(rank, world, size, ctl.allgather_bytes, wire=wire,
+                                                       device=local_rank)
         uid = ono_amd.unique_id() if (world > 1 and rank == 0) else None
         uid = ctl.bcast_bytes(uid) if world > 1 else None
         return ono_amd.WorkerRingManager(rank, world, size, uid=uid, wire=wire, device=local_rank, algo=algo)
@@ -577,6 +583,8 @@ def main(argv=None) -> int:
     line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
                       bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
     line["config"]["schedule"] = ring.algo
+    if world > 1 and ring.algo == "xgmi":
+        line["config"]["collective"] = "xGMI peer-access kernels over IPC-mapped peer HBM (no RCCL)"
     if world > 1 and args.wire == "f32" and ring.algo in ("auto", "allreduce"):
         line["config"]["allreduce_segments"] = args.segments or "library default (ONO_AR_SEGMENTS or 4)"
 
@@ -684,8 +692,12 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
            str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib),
            "--sweep-mib", getattr(args, "sweep_mib", "")]
     procs = []
+    # The children rendezvous on their own port with rank 0 hosting the store:
+    # drop torchrun's agent-store settings (TORCHELASTIC_USE_AGENT_STORE=True
+    # would make every child a client of a store nobody serves on that port).
+    base_env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     for r in (range(n) if coresident else [rank]):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
+        env = dict(base_env, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     deadline = time.time() + args.xgmi_timeout
@@ -717,12 +729,18 @@ def xgmi_child_main(args) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    import ono_amd
 
-    torch.cuda.set_device(local_rank)
-    ctl = Ctl(world, rank)
-    elems = args.bucket_mib * (1 << 20) // 4
-    run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
+    ctl = Ctl(world, rank)  # rendezvous first: a GPU failure below is then reported, not a hang
+    try:
+        import ono_amd
+        torch.cuda.set_device(local_rank)
+        elems = args.bucket_mib * (1 << 20) // 4
+        run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
+    except Exception as e:
+        ctl.close()
+        if rank == 0:
+            print(json.dumps({"xgmi": {"error": f"{type(e).__name__}: {e}"[:300]}}), flush=True)
+        return 0
     out = {}
     for gather, wire in (("pull", "f32"), ("pull", "f16"), ("push", "f32"), ("push", "f16")):
         key = f"xgmi:{wire}" if gather == "pull" else f"xgmi-pushgather:{wire}"
