@@ -179,7 +179,8 @@ def build_line(*, value, n_gpus, steps, warmup, elapsed, bucket_bytes, wire, ext
             "parallelism": f"dp{n_gpus}",
             "wire": wire,
             "collective": "none (n == 1)" if n_gpus == 1 else ("RCCL all-reduce over xGMI" if wire == "f32"
-                                                                 else "reference f16 hop ring over RCCL p2p"),
+                                                                 else "reference f16 arithmetic, DIRECT all-to-all "
+                                                                      "over RCCL p2p"),
         },
         "algbw_gib_s": round(algbw, 3),
         "busbw_gib_s": round(algbw * 2 * (n_gpus - 1) / n_gpus, 3) if n_gpus > 1 else None,
@@ -851,7 +852,9 @@ def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: st
     the N-1 direct links a rank can drive at once, 76.8 GB/s each per direction.
     For the RCCL ring all-reduce the bytes are its busBW bytes 2(N-1)/N x bucket."""
     wb = 2 if wire == "f16" else 4
-    if algo in ("allreduce", "auto") and wire == "f32":
+    if algo == "auto":  # the library's AUTO resolution (ono_ring.cpp resolved_algo)
+        algo = "allreduce" if wire == "f32" else "direct"
+    if algo == "allreduce" and wire == "f32":
         bytes_out = 2 * (world - 1) / world * bucket_bytes            # ring all-reduce (any segmentation)
     elif algo in ("direct", "xgmi"):
         bytes_out = (world - 1) / world * (bucket_bytes + elems * wb)  # all-to-all f32 + all-gather

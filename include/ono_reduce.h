@@ -165,7 +165,8 @@ int ono_ring_pull_grads_host(ono_ring *ring, float *residual_host, float *grad_h
  * place; unregistered buffers are staged through pinned bounce slots.       */
 int ono_ring_register_host(ono_ring *ring, void *ptr, size_t bytes);
 int ono_ring_unregister_host(ono_ring *ring, void *ptr);
-/* Schedule of the n > 1 exchange (default AUTO: F32 -> ALLREDUCE, F16 -> HOPS).
+/* Schedule of the n > 1 exchange (default AUTO: F32 -> ALLREDUCE, F16 -> DIRECT
+ * for n <= ONO_MAX_INPUTS, else HOPS; a TCP ring always runs HOPS).
  *   ALLREDUCE  ncclAllReduce + fused ÷n / residual reset (f32 wire only)
  *   HOPS       the reference hop ring (n-1 scatter + n-1 gather hops) over
  *              ncclSend/ncclRecv, bit-exact for both wires

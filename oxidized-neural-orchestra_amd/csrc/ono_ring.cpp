@@ -507,9 +507,14 @@ int direct_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
     return ONO_OK;
 }
 
+// AUTO: the f32 wire is one RCCL all-reduce; the f16 wire (the reference's
+// exact arithmetic) takes the DIRECT schedule — bit-identical to the hop ring
+// but over every link at once instead of 2(n-1) dependent single-link hops —
+// up to ONO_MAX_INPUTS ranks, the hop ring beyond (and always on a TCP ring).
 int resolved_algo(const ono_ring *r) {
     if (r->algo != ONO_ALGO_AUTO) return r->algo;
-    return r->wire == ONO_WIRE_F32 ? ONO_ALGO_ALLREDUCE : ONO_ALGO_HOPS;
+    if (r->wire == ONO_WIRE_F32) return ONO_ALGO_ALLREDUCE;
+    return (r->fd_next < 0 && r->n <= ONO_MAX_INPUTS) ? ONO_ALGO_DIRECT : ONO_ALGO_HOPS;
 }
 
 int ar_segments(ono_ring *r) {

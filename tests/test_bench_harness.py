@@ -120,7 +120,11 @@ def test_xgmi_children_under_torchrun_rendezvous_and_report():
     finally:
         os.remove(script)
     assert r.returncode == 0, r.stderr[-3000:]
-    outs = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    outs, dec, text, i = [], json.JSONDecoder(), r.stdout, 0  # the two ranks' lines may interleave
+    while (i := text.find('{"rank"', i)) >= 0:
+        obj, end = dec.raw_decode(text, i)
+        outs.append(obj)
+        i = end
     r0 = [o for o in outs if o["rank"] == 0][0]["res"]
     r1 = [o for o in outs if o["rank"] == 1][0]["res"]
     assert r1 == {}
