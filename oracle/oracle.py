@@ -143,6 +143,30 @@ def synth(n: int, seed: int, rank: int, offset: int = 0) -> np.ndarray:
     return out
 
 
+def synth_special(n: int, seed: int, rank: int) -> np.ndarray:
+    """synth() with IEEE special values planted at rank-dependent strides:
+    quiet NaNs with payloads, +-inf, -0, f16-overflowing 7e4, f16-subnormal /
+    underflowing 1e-8 and 3e38 (an f32 sum of two overflows).  Test input."""
+    x = synth(n, seed, rank)
+    u = x.view(np.uint32)
+    u[rank % 97::97] = 0x7FC01234 + rank
+    x[(rank + 3) % 101::101] = np.inf if rank % 2 == 0 else -np.inf
+    u[(rank + 5) % 103::103] = 0x80000000
+    x[(rank + 7) % 107::107] = 7.0e4
+    x[(rank + 11) % 109::109] = 1.0e-8
+    x[(rank + 13) % 113::113] = 3.0e38
+    return x
+
+
+def same_or_both_nan(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Element mask: bit-identical, or NaN in both (NaN payload propagation
+    through a + b is not pinned by IEEE-754 nor by the reference's compiler,
+    which may commute the operands)."""
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+
+
 def frame_dense(h: np.ndarray, is_last: bool = False) -> bytes:
     h = np.ascontiguousarray(h, dtype=np.uint16)
     buf = np.empty(12 + 2 * h.size, np.uint8)

@@ -323,3 +323,25 @@ def test_allreduce_pipeline_segments_n1(segments):
                 assert not res[k].view(torch.int32).any()
     finally:
         ring.close()
+
+
+@pytest.mark.parametrize("algo", ["hops", "direct"])
+@pytest.mark.parametrize("wire", ["f16", "f32"])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_local_ring_special_values(n, wire, algo):
+    """NaN (with payloads), +-inf, -0, f16 overflow/underflow and f32 overflow
+    through the whole round: bit-exact with the oracle wherever the oracle is
+    not NaN, NaN exactly where the oracle is NaN (payload propagation through
+    a + b is compiler-dependent in the reference itself)."""
+    length = 100003
+    ins = [O.synth_special(length, SEED + 17, r) for r in range(n)]
+    eg, _ = O.ring_pull_grads(ins, wire)
+    res = [to_dev(x) for x in ins]
+    grads = [torch.full_like(r, 7.0) for r in res]
+    ono_amd.local_ring_pull_grads(res, grads, wire, algo=algo)
+    for r in range(n):
+        got = host(grads[r])
+        ok = O.same_or_both_nan(got, eg[r])
+        assert ok.all(), f"rank {r}: {np.count_nonzero(~ok)} differ, first at {np.flatnonzero(~ok)[0]}"
+        assert np.isnan(eg[r]).any() and np.isinf(eg[r]).any()  # the specials did reach the output
+        assert not host(res[r]).view(np.uint32).any()

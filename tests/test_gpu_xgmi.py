@@ -8,7 +8,8 @@ device.  Checked bit for bit against the oracle's reference ring
 (worker_ring.rs:112-204, both wires), several rounds per ring (barrier epochs
 and buffer reuse), owned buckets and caller buffers at mismatched 4-element
 phases, ragged and tiny buckets, and the barrier timeout (a missing peer ends
-in IoError, not a hang).  Tolerance: 0 ulp.
+in IoError, not a hang).  Tolerance: 0 ulp (NaN outputs: NaN where the oracle
+is NaN — payload propagation through a + b is compiler-defined in the reference).
 """
 import json
 import os
@@ -60,7 +61,8 @@ def cases_for(n: int) -> list:
               {"length": 2 ** 18 + 5, "wire": wire, "form": "dev"},               # ragged chunks
               {"length": 100003, "wire": wire, "form": "dev_offset", "seed": 7},  # phase mismatch paths
               {"length": n, "wire": wire, "seed": 3},                             # one element per chunk
-              {"length": 4 * n + 3, "wire": wire, "seed": 5}]
+              {"length": 4 * n + 3, "wire": wire, "seed": 5},
+              {"length": 50021, "wire": wire, "seed": 9, "special": True}]     # NaN/inf/-0/overflow
     return c
 
 

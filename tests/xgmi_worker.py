@@ -48,7 +48,8 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
     ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
     try:
         for rd in range(rounds):
-            ins = [O.synth(length, SEED + 100 * rd + case.get("seed", 0), r) for r in range(n)]
+            gen = O.synth_special if case.get("special") else O.synth
+            ins = [gen(length, SEED + 100 * rd + case.get("seed", 0), r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, wire)
             if form == "owned":
                 ring.residual.copy_(torch.from_numpy(ins[rank]))
@@ -68,7 +69,7 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
                     return f"round {rd}: write outside the grad view"
                 if rbase[:ro].ne(0).any().item() or rbase[ro + length:].ne(0).any().item():
                     return f"round {rd}: write outside the residual view"
-            bad = np.flatnonzero(bits(got) != bits(expect[rank]))
+            bad = np.flatnonzero(~O.same_or_both_nan(got, expect[rank]))
             if bad.size:
                 i = bad[0]
                 return (f"round {rd}: {bad.size}/{length} differ, first at {i}: "
