@@ -335,6 +335,46 @@ def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
             "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
 
 
+def ps_host_fed(ono_amd, elems: int, rounds: int = 3, workers: int = 2) -> dict:
+    """The parameter server's own hot path (SURVEY §8(a) BlockingStore rows):
+    gradients arrive in host memory from comms/, the device store accumulates
+    them, the leader updates (÷n + GD), params go back to host.  Same round
+    as cpu_baseline.ps_accumulate_update (workers accumulates + 1 update;
+    GiB/s = workers x 4N / t), plus the pull.  Never `value`."""
+    import numpy as np
+
+    params = np.zeros(elems, np.float32)
+    grads = [np.random.default_rng(w).standard_normal(elems, dtype=np.float32) * np.float32(0.01)
+             for w in range(workers)]
+    out = np.empty(elems, np.float32)
+    store = ono_amd.BlockingStore(max(1, elems // 32), workers, params, ono_amd.GradientDescent(0.1))
+    res = {}
+    for form in ("pageable", "registered"):
+        if form == "registered":
+            if not hasattr(store, "register_host"):
+                break
+            for g in grads + [out]:
+                store.register_host(g)
+        ts, tp = [], []
+        for r in range(rounds + 1):
+            t0 = time.perf_counter()
+            for g in grads:
+                store.accumulate(g)
+            store.update_params()
+            t1 = time.perf_counter()
+            store.pull_params(out)
+            t2 = time.perf_counter()
+            if r:
+                ts.append(t1 - t0)
+                tp.append(t2 - t1)
+        t, p = sorted(ts)[len(ts) // 2], sorted(tp)[len(tp) // 2]
+        res[form] = {"accumulate_update_ms": round(t * 1e3, 3), "gib_s": round(workers * elems * 4 / t / GIB, 3),
+                     "pull_ms": round(p * 1e3, 3), "pull_gib_s": round(elems * 4 / p / GIB, 3)}
+    store.close()
+    return {"workload": f"BlockingStore on the device fed from host buffers: {workers} accumulates + 1 update "
+                        f"(/n, GD) of {elems} params, then pull_params to host", **res}
+
+
 def tcp_edge_native(elems: int, rounds: int, ranks: int = 2) -> dict | None:
     """The TCP edge driven from a plain C++ host (tools/ono_tcp_bench: worker
     threads on this GPU, ono_ring_create_tcp over loopback TCP, pthread
@@ -575,6 +615,8 @@ def main(argv=None) -> int:
                 cr = O.cpu_ring(nr, CONFIG1_ELEMS, 50, check=False, pin=True, timeout=300)
                 small[k]["cpu_ring_ms"] = round(cr["s_per_round"] * 1e3, 4)
         extra["tcp_edge"]["config1"] = small
+    if rank == 0 and world == 1 and not args.no_host_fed:
+        extra["ps_host_fed"] = ps_host_fed(ono_amd, elems)
     if rank == 0 and world == 1 and not args.no_local_reduce:
         extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
