@@ -263,6 +263,12 @@ size_t ono_store_len(const ono_store *store);
 /* Store::accumulate (store.rs:84-91): thread-safe; ONO_E_SIZE on length mismatch */
 int ono_store_accumulate(ono_store *store, const float *grad_host, size_t n);
 int ono_store_accumulate_dev(ono_store *store, const float *grad_dev, size_t n);
+/* The same from the reference's wire form: the worker's f16 gradient payload
+ * (ParamServerHandle::push_grad, comms/src/handles/parameter_server.rs:92-107)
+ * crosses PCIe as f16 and is decoded inside the accumulate kernel — the
+ * server's CPU decode (handles/worker.rs:82-101) + accumulate, fused.        */
+int ono_store_accumulate_f16(ono_store *store, const uint16_t *grad_f16_host, size_t n);
+int ono_store_accumulate_f16_dev(ono_store *store, const uint16_t *grad_f16_dev, size_t n);
 /* Store::update_params (store.rs:93-108): CAS-guarded; a concurrent second
  * caller returns immediately without updating.                              */
 int ono_store_update_params(ono_store *store);
@@ -286,6 +292,9 @@ int ono_sync_release(ono_sync *sync);
  * accumulate(grad); [barrier: last arriver runs update_params]; pull_params(params) */
 int ono_sync_step(ono_sync *sync, ono_store *store, const float *grad_host, float *params_host,
                   size_t n);
+/* the same with the gradient as the f16 payload it arrives in (fused decode) */
+int ono_sync_step_f16(ono_sync *sync, ono_store *store, const uint16_t *grad_f16_host, float *params_host,
+                      size_t n);
 
 /* DynBarrier (synchronization/dyn_barrier.rs:47-106), exposed for the host tests */
 typedef struct ono_barrier ono_barrier;

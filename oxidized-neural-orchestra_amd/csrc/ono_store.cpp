@@ -126,11 +126,49 @@ static int accumulate(ono_store *st, const float *grad, size_t n, hipMemcpyKind 
     return ONO_OK;
 }
 
+// The reference's wire form: the worker sends its gradient as f16
+// (ParamServerHandle::push_grad, comms/src/handles/parameter_server.rs:92-107)
+// and the server decodes it on the CPU before accumulating
+// (WorkerHandle::recv_event, handles/worker.rs:82-101).  Here the f16 payload
+// itself crosses PCIe (half the bytes) and the decode is fused into the
+// accumulate kernel: acc += f32(h), exact widening with half 2.7.1's NaN rule.
+static int accumulate_f16(ono_store *st, const uint16_t *grad, size_t n, hipMemcpyKind kind) {
+    if (!st || (!grad && n)) return set_error(ONO_E_ARG, "NULL argument");
+    if (n != st->nparams) return set_error(ONO_E_SIZE, "gradient of %zu elements, store of %zu", n, st->nparams);
+    std::lock_guard<std::mutex> lk(st->mu);
+    DeviceGuard g(st->device);
+    hipStream_t s = st->stream;
+    if (n == 0) return ONO_OK;
+    uint16_t *h = reinterpret_cast<uint16_t *>(st->scratch);  // 4N bytes hold the 2N-byte payload
+    ONO_HIP(hipMemcpyAsync(h, grad, n * sizeof(uint16_t), kind, s));
+    if (st->kind == ONO_STORE_WILD) {
+        adam_advance(st);
+        OptLaunch o = st->opt;
+        o.nworkers = 1.0f;
+        o.plus_zero = false;
+        float *g32 = st->grads[0];  // unused by the wild store: the decoded gradient
+        ONO_HIP(launch_decode_scale<uint16_t>(g32, h, n, 1.0f, s));
+        ONO_HIP(launch_opt_update(o, g32, st->params, st->v, st->s, n, false, s));
+    } else {
+        int active = st->active_idx.load(std::memory_order_acquire);
+        ONO_HIP(launch_decode_add<uint16_t>(st->grads[active], h, n, s));
+    }
+    ONO_HIP(hipStreamSynchronize(s));
+    return ONO_OK;
+}
+
 int ono_store_accumulate(ono_store *st, const float *grad, size_t n) {
     return accumulate(st, grad, n, hipMemcpyHostToDevice);
 }
 int ono_store_accumulate_dev(ono_store *st, const float *grad, size_t n) {
     return accumulate(st, grad, n, hipMemcpyDeviceToDevice);
+}
+
+int ono_store_accumulate_f16(ono_store *st, const uint16_t *grad, size_t n) {
+    return accumulate_f16(st, grad, n, hipMemcpyHostToDevice);
+}
+int ono_store_accumulate_f16_dev(ono_store *st, const uint16_t *grad, size_t n) {
+    return accumulate_f16(st, grad, n, hipMemcpyDeviceToDevice);
 }
 
 int ono_store_update_params(ono_store *st) {
@@ -282,9 +320,10 @@ int ono_sync_release(ono_sync *s) {
     return ONO_OK;
 }
 
-int ono_sync_step(ono_sync *s, ono_store *st, const float *grad, float *params, size_t n) {
+static int sync_step(ono_sync *s, ono_store *st, const void *grad, bool f16, float *params, size_t n) {
     if (!s || !st) return set_error(ONO_E_ARG, "NULL argument");
-    int rc = ono_store_accumulate(st, grad, n);
+    int rc = f16 ? ono_store_accumulate_f16(st, static_cast<const uint16_t *>(grad), n)
+                 : ono_store_accumulate(st, static_cast<const float *>(grad), n);
     if (rc) return rc;
     if (s->kind == ONO_SYNC_BARRIER) {
         int urc = ONO_OK;
@@ -295,6 +334,13 @@ int ono_sync_step(ono_sync *s, ono_store *st, const float *grad, float *params, 
         if (rc) return rc;
     }
     return ono_store_pull_params(st, params, n);
+}
+
+int ono_sync_step(ono_sync *s, ono_store *st, const float *grad, float *params, size_t n) {
+    return sync_step(s, st, grad, false, params, n);
+}
+int ono_sync_step_f16(ono_sync *s, ono_store *st, const uint16_t *grad, float *params, size_t n) {
+    return sync_step(s, st, grad, true, params, n);
 }
 
 }  // extern "C"

@@ -128,6 +128,8 @@ _SIGS = {
     "ono_store_len": (_sz, [_vp]),
     "ono_store_accumulate": (_i, [_vp, _fp, _sz]),
     "ono_store_accumulate_dev": (_i, [_vp, _fp, _sz]),
+    "ono_store_accumulate_f16": (_i, [_vp, _vp, _sz]),
+    "ono_store_accumulate_f16_dev": (_i, [_vp, _vp, _sz]),
     "ono_store_update_params": (_i, [_vp]),
     "ono_store_pull_params": (_i, [_vp, _fp, _sz]),
     "ono_store_pull_params_dev": (_i, [_vp, _fp, _sz]),
@@ -137,6 +139,7 @@ _SIGS = {
     "ono_sync_clone": (_i, [_vp]),
     "ono_sync_release": (_i, [_vp]),
     "ono_sync_step": (_i, [_vp, _vp, _fp, _fp, _sz]),
+    "ono_sync_step_f16": (_i, [_vp, _vp, _vp, _fp, _sz]),
     "ono_barrier_create": (_i, [C.POINTER(C.c_void_p), _sz]),
     "ono_barrier_destroy": (_i, [_vp]),
     "ono_barrier_wait_with": (_i, [_vp, LEADER_FN, _vp]),

@@ -13,6 +13,7 @@ import os
 from dataclasses import dataclass
 
 import numpy as np
+import torch
 
 from ._lib import LEADER_FN, OPT_KIND, STORE_KIND, SYNC_KIND, OptSpec, call, lib
 
@@ -91,6 +92,19 @@ class _Store:
     def accumulate(self, grad) -> None:
         g = _f32(grad)
         call("ono_store_accumulate", self._h, g.ctypes.data if g.size else None, g.size)
+
+    def accumulate_f16(self, grad_f16) -> None:
+        """accumulate() from the reference's wire form: the worker's f16
+        payload (uint16 bit patterns), decoded inside the accumulate kernel."""
+        if isinstance(grad_f16, torch.Tensor):
+            if grad_f16.dtype not in (torch.float16, torch.int16) or not grad_f16.is_cuda:
+                raise ValueError("device payload must be a float16/int16 CUDA tensor")
+            call("ono_store_accumulate_f16_dev", self._h, grad_f16.data_ptr(), grad_f16.numel())
+            return
+        h = np.ascontiguousarray(grad_f16)
+        if h.dtype not in (np.uint16, np.float16):
+            raise ValueError("host payload must be uint16 (f16 bit patterns) or float16")
+        call("ono_store_accumulate_f16", self._h, h.ctypes.data if h.size else None, h.size)
 
     def update_params(self) -> None:
         call("ono_store_update_params", self._h)
@@ -187,6 +201,16 @@ class _Sync:
             raise ValueError("params must be a contiguous float32 array")
         call("ono_sync_step", self._h, store._h, g.ctypes.data if g.size else None,
              params.ctypes.data if params.size else None, g.size)
+
+    def step_f16(self, store: _Store, grad_f16, params: np.ndarray) -> None:
+        """step() with the gradient as the f16 payload it arrives in (uint16 bit patterns)."""
+        h = np.ascontiguousarray(grad_f16)
+        if h.dtype not in (np.uint16, np.float16):
+            raise ValueError("payload must be uint16 (f16 bit patterns) or float16")
+        if params.dtype != np.float32 or not params.flags.c_contiguous:
+            raise ValueError("params must be a contiguous float32 array")
+        call("ono_sync_step_f16", self._h, store._h, h.ctypes.data if h.size else None,
+             params.ctypes.data if params.size else None, h.size)
 
 
 class BarrierSync(_Sync):

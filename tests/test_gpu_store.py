@@ -217,3 +217,50 @@ def test_sharded_ps_single_gpu(kind):
         assert_bitexact(params.cpu().numpy(), ref.pull_params(), f"round {r}")
     ps.close()
     ring.close()
+
+
+@pytest.mark.parametrize("kind", ["gd", "momentum", "adam"])
+@pytest.mark.parametrize("nparams", [1, 4099, 1 << 20])
+def test_store_accumulate_f16_wire(kind, nparams):
+    """The PS server's receive path fused: the worker's f16 payload
+    (ParamServerHandle::push_grad) is decoded inside the accumulate kernel.
+    Equal to the oracle fed the CPU decode of the same payload (worker.rs:
+    82-101), host and device payloads, specials included."""
+    init = O.synth(nparams, SEED + 1, 9)
+    s = ono_amd.BlockingStore(ono_amd.shard_size_for(nparams), 2, init, OPTS[kind])
+    ref = O.Store(init, 7, 2, kind, lr=0.1, momentum=0.9, beta1=0.9, beta2=0.999, eps=1e-8)
+    for rnd in range(4):
+        for w in range(2):
+            h = O.f16_encode(O.synth_special(nparams, SEED + rnd, w) if nparams > 200 else
+                             O.synth(nparams, SEED + rnd, w))
+            if w == 0:
+                s.accumulate_f16(h)
+            else:
+                s.accumulate_f16(torch.from_numpy(h.view(np.int16)).cuda())
+            ref.accumulate(O.f16_decode(h))
+        s.update_params()
+        ref.update_params()
+        ok = O.same_or_both_nan(s.pull_params(), ref.pull_params())
+        assert ok.all(), f"{kind} round {rnd}: {np.count_nonzero(~ok)} differ"
+
+
+def test_wild_store_and_sync_step_f16():
+    init = O.synth(5000, SEED, 2)
+    s = ono_amd.WildStore(100, init, OPTS["adam"])
+    ref = O.WildStore(init, 100, "adam", lr=0.1, momentum=0.9, beta1=0.9, beta2=0.999, eps=1e-8)
+    for rnd in range(4):
+        h = O.f16_encode(O.synth(5000, SEED + rnd, 1))
+        s.accumulate_f16(h)
+        ref.accumulate(O.f16_decode(h))
+    assert_bitexact(s.pull_params(), ref.pull_params(), "wild f16")
+    b = ono_amd.BlockingStore(50, 1, init, GradientDescentWithMomentum(0.1, 0.9))
+    sync = ono_amd.NoBlockingSync()
+    rb = O.Store(init, 50, 1, "momentum", lr=0.1, momentum=0.9)
+    p = np.empty(5000, np.float32)
+    for r in range(3):
+        h = O.f16_encode(O.synth(5000, SEED + r, 4))
+        sync.step_f16(b, h, p)
+        rb.accumulate(O.f16_decode(h))
+        rb.update_params()
+        assert_bitexact(p, rb.pull_params(), f"sync f16 round {r}")
+    sync.drop()
