@@ -509,6 +509,7 @@ class Runner:
         timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, self.ctl,
                      on_start=lambda: r.timing(True))
         tim = r.timing_read()
+        tim["phases"] = r.timing_phases()
         r.timing(False)
         return el, tim
 
@@ -907,8 +908,16 @@ def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: st
     ach = bytes_out / (step_coll_ms * 1e-3) / 1e9 if step_coll_ms > 0 else None
     peak = XGMI_LINK_GBS * (world - 1)
     kern_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
+    phases = {k: round(v[0] / max(steps, 1), 4) for k, v in tim.get("phases", {}).items() if v[1]}
+    per_link = {}
+    if algo == "xgmi" and world > 1 and phases:
+        # one peer segment per link: the scatter moves 4 N/n bytes to each peer, the gather wire N/n
+        for ph, b in (("xgmi_scatter", 4 * elems / world), ("xgmi_gather", wb * elems / world)):
+            if phases.get(ph):
+                per_link[ph] = round(b / (phases[ph] * 1e-3) / 1e9, 1)
     return {
         "bound": "xgmi", "schedule": f"{algo}:{wire}",
+        "phases_ms_per_step": phases, "per_link_gbs": per_link or None,
         "achieved": round(ach, 1) if ach else None, "peak": round(peak, 1), "unit": "GB/s",
         "frac": round(ach / peak, 4) if ach else None, "traffic": None,
         "wire_bytes_per_rank_per_step": int(bytes_out),

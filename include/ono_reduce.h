@@ -215,6 +215,19 @@ int ono_ring_abort(ono_ring *ring);
 int ono_ring_timing_enable(ono_ring *ring, int enable);
 int ono_ring_timing_read(ono_ring *ring, double *kernel_ms, int64_t *launches,
                          double *collective_ms, int64_t *collectives);
+/* The same split by phase (ms[ONO_PHASES], count[ONO_PHASES]): local kernels,
+ * RCCL calls, and the xGMI schedule's scatter (push), barriers and gather
+ * (pull, or owner chain + remote stores with ONO_XGMI_GATHER=push).  The
+ * collective total of ono_ring_timing_read is phases 1..4.                  */
+typedef enum {
+    ONO_PHASE_KERNEL = 0,
+    ONO_PHASE_RCCL = 1,
+    ONO_PHASE_XGMI_SCATTER = 2,
+    ONO_PHASE_XGMI_BARRIER = 3,
+    ONO_PHASE_XGMI_GATHER = 4,
+    ONO_PHASES = 5
+} ono_phase;
+int ono_ring_timing_phases(ono_ring *ring, double *ms, int64_t *count);
 
 /* n virtual ranks co-resident on ONE device (the device analog of the
  * reference's loopback workers): residuals[r], grads[r] are device buckets of

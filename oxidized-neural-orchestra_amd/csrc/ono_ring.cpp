@@ -993,8 +993,19 @@ int ono_ring_timing_enable(ono_ring *r, int enable) {
     DeviceGuard g(r->device);
     ONO_HIP(r->timer.drain());
     r->timer.on = enable != 0;
-    r->timer.kernel_ms = r->timer.coll_ms = 0;
-    r->timer.kernels = r->timer.colls = 0;
+    r->timer.reset();
+    return ONO_OK;
+}
+
+int ono_ring_timing_phases(ono_ring *r, double *ms, int64_t *count) {
+    if (!r || !ms || !count) return set_error(ONO_E_ARG, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    DeviceGuard g(r->device);
+    ONO_HIP(r->timer.drain());
+    for (int i = 0; i < ONO_PHASES; i++) {
+        ms[i] = r->timer.phase_ms[i];
+        count[i] = r->timer.phase_n[i];
+    }
     return ONO_OK;
 }
 

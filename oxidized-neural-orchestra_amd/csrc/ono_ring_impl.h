@@ -30,7 +30,7 @@ struct XgmiState;  // ono_xgmi.cpp
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
-    int kind = 0;  // 0 = library kernel, 1 = collective
+    int kind = 0;  // ono_phase: 0 = library kernel, 1 = RCCL collective, 2..4 = xGMI phases
 };
 
 // HIP-event timer for the library's own launches (on the launch stream).
@@ -39,6 +39,8 @@ struct Timer {
     std::vector<EventPair> pending, pool;
     double kernel_ms = 0, coll_ms = 0;
     int64_t kernels = 0, colls = 0;
+    double phase_ms[ONO_PHASES] = {};
+    int64_t phase_n[ONO_PHASES] = {};
 
     hipError_t begin(hipStream_t s, EventPair &p, int kind) {
         if (!pool.empty()) {
@@ -67,10 +69,16 @@ struct Timer {
             if (e != hipSuccess) return e;
             if (p.kind == 0) { kernel_ms += ms; kernels++; }
             else { coll_ms += ms; colls++; }
+            if (p.kind >= 0 && p.kind < ONO_PHASES) { phase_ms[p.kind] += ms; phase_n[p.kind]++; }
             pool.push_back(p);
         }
         pending.clear();
         return hipSuccess;
+    }
+    void reset() {
+        kernel_ms = coll_ms = 0;
+        kernels = colls = 0;
+        for (int i = 0; i < ONO_PHASES; i++) { phase_ms[i] = 0; phase_n[i] = 0; }
     }
     void destroy() {
         for (auto &p : pending) pool.push_back(p);

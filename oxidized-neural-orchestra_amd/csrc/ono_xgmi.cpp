@@ -160,7 +160,7 @@ int barrier(ono_ring *r, hipStream_t s) {
     b.timeout_ticks = x->timeout_ticks;
     b.n = r->n;
     b.pos = r->pos;
-    return timed(r, s, 1, [&]() -> int {
+    return timed(r, s, ONO_PHASE_XGMI_BARRIER, [&]() -> int {
         ONO_HIP(launch_xgmi_barrier(b, s));
         return ONO_OK;
     });
@@ -190,7 +190,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
         sg.n = len(cq);
         sg.head = head_of(sg.src, 4, sg.dst, 4);
     }
-    int rc = timed(r, s, 1, [&]() -> int {
+    int rc = timed(r, s, ONO_PHASE_XGMI_SCATTER, [&]() -> int {
         ONO_HIP(launch_xgmi_push(push, true, s));
         return ONO_OK;
     });
@@ -206,7 +206,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
             const int q = (pos + d) % n;
             outs[no++] = reinterpret_cast<W *>(gslot_of(x, x->peer[q], pos, q)) + ph(off[c]);
         }
-        rc = timed(r, s, 1, [&]() -> int {
+        rc = timed(r, s, ONO_PHASE_XGMI_GATHER, [&]() -> int {
             ONO_HIP(launch_direct_multi<W>(grad + off[c], outs, no, ins, n, len(c), (float)n, false, s));
             return ONO_OK;
         });
@@ -236,7 +236,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
         sg.n = len(cq);
         sg.head = head_of(sg.src, sizeof(W), sg.dst, 4);
     }
-    return timed(r, s, 1, [&]() -> int {
+    return timed(r, s, ONO_PHASE_XGMI_GATHER, [&]() -> int {
         ONO_HIP(launch_xgmi_pull(pull, f16, f16 ? (float)n : 1.0f, s));
         return ONO_OK;
     });
@@ -289,7 +289,7 @@ int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t
         sg.n = len(q);
         sg.head = head_of(sg.src, 4, sg.dst, 4);
     }
-    rc = timed(r, s, 1, [&]() -> int {
+    rc = timed(r, s, ONO_PHASE_XGMI_SCATTER, [&]() -> int {
         ONO_HIP(launch_xgmi_push(push, false, s));
         return ONO_OK;
     });
@@ -314,7 +314,7 @@ int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t
         sg.n = len(q);
         sg.head = head_of(sg.src, 4, sg.dst, 4);
     }
-    return timed(r, s, 1, [&]() -> int {
+    return timed(r, s, ONO_PHASE_XGMI_GATHER, [&]() -> int {
         ONO_HIP(launch_xgmi_pull(pull, false, 1.0f, s));
         return ONO_OK;
     });

@@ -24,6 +24,7 @@ SYNC_KIND = {"barrier": 0, "nonblocking": 1}
 UID_BYTES = 128
 XGMI_HANDLE_BYTES = 64
 MAX_INPUTS = 16
+PHASES = ("kernel", "rccl", "xgmi_scatter", "xgmi_barrier", "xgmi_gather")  # ono_phase
 
 
 class OnoError(RuntimeError):
@@ -118,6 +119,7 @@ _SIGS = {
     "ono_ring_timing_enable": (_i, [_vp, _i]),
     "ono_ring_timing_read": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                   C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "ono_ring_timing_phases": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ono_local_ring_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
     "ono_local_direct_pull_grads": (_i, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _i, _sz, _i, _vp]),
     "ono_optimizer_create": (_i, [C.POINTER(C.c_void_p), C.POINTER(OptSpec), _sz, _i]),

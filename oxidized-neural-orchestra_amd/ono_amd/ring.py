@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import kernels
-from ._lib import ALGO, UID_BYTES, WIRE, XGMI_HANDLE_BYTES, call, lib
+from ._lib import ALGO, PHASES, UID_BYTES, WIRE, XGMI_HANDLE_BYTES, call, lib
 
 
 class _DevArray:
@@ -212,6 +212,13 @@ class WorkerRingManager:
         km, kn, cm, cn = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
         call("ono_ring_timing_read", self._h, C.byref(km), C.byref(kn), C.byref(cm), C.byref(cn))
         return {"kernel_ms": km.value, "kernels": kn.value, "collective_ms": cm.value, "collectives": cn.value}
+
+    def timing_phases(self) -> dict:
+        """{phase: (ms, launches)} — local kernels, RCCL calls, xGMI scatter /
+        barrier / gather (ono_ring_timing_phases)."""
+        ms, cnt = (C.c_double * len(PHASES))(), (C.c_int64 * len(PHASES))()
+        call("ono_ring_timing_phases", self._h, ms, cnt)
+        return {p: (ms[i], cnt[i]) for i, p in enumerate(PHASES)}
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -94,5 +94,9 @@ def test_xgmi_sharded_ps_vs_store_oracle(n):
     check(run_ranks(n, cases))
 
 
+def test_xgmi_timing_phases():
+    check(run_ranks(3, [{"kind": "timing"}]))
+
+
 def test_xgmi_barrier_timeout_is_an_error_not_a_hang():
     check(run_ranks(2, [{"kind": "timeout"}], 120.0))

@@ -115,6 +115,31 @@ def run_ps(rank: int, n: int, case: dict) -> str | None:
         ring.close()
 
 
+def run_timing(rank: int, n: int) -> str | None:
+    """ono_ring_timing_phases on the xGMI schedule: per round one scatter, two
+    barriers, one gather and one local kernel (the owner chain); the RCCL
+    phase stays empty; ono_ring_timing_read's collective total = phases 1..4."""
+    ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, 1 << 16, allgather, wire="f16")
+    try:
+        ring.timing(True)
+        for _ in range(3):
+            ring.pull_grads()
+        torch.cuda.synchronize()
+        ph, tot = ring.timing_phases(), ring.timing_read()
+        want = {"kernel": 3, "rccl": 0, "xgmi_scatter": 3, "xgmi_barrier": 6, "xgmi_gather": 3}
+        got = {k: v[1] for k, v in ph.items()}
+        if got != want:
+            return f"phase counts {got} != {want}"
+        coll = sum(v[0] for k, v in ph.items() if k != "kernel")
+        if abs(coll - tot["collective_ms"]) > 1e-6 or tot["collectives"] != 12 or tot["kernels"] != 3:
+            return f"timing_read {tot} inconsistent with phases {ph}"
+        if not all(v[0] > 0 for k, v in ph.items() if k != "rccl"):
+            return f"empty phase time {ph}"
+        return None
+    finally:
+        ring.close()
+
+
 def run_timeout(rank: int, n: int) -> str | None:
     """Rank 0 starts a round alone: its barrier gives up after the timeout and
     the next call fails with IoError instead of hanging; the late rank's
@@ -154,7 +179,7 @@ def main() -> int:
         try:
             kind = case.get("kind", "ring")
             msg = run_timeout(rank, n) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
-                run_case(rank, n, case)
+                run_timing(rank, n) if kind == "timing" else run_case(rank, n, case)
         except Exception as e:  # reported, the parent asserts
             msg = f"{type(e).__name__}: {e}"
         results.append({"case": case, "ok": msg is None, "msg": msg or ""})
