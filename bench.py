@@ -920,6 +920,9 @@ def xgmi_roofline(tim: dict, bucket_bytes: int, elems: int, world: int, wire: st
         "phases_ms_per_step": phases, "per_link_gbs": per_link or None,
         "achieved": round(ach, 1) if ach else None, "peak": round(peak, 1), "unit": "GB/s",
         "frac": round(ach / peak, 4) if ach else None, "traffic": None,
+        # BASELINE.md's primary denominator: one xGMI link (153.6 GB/s, the single-ring per-link bound);
+        # `frac` above uses the stricter every-link peak of a fully connected node
+        "frac_of_one_link_153gbs": round(ach / (2 * XGMI_LINK_GBS), 4) if ach else None,
         "wire_bytes_per_rank_per_step": int(bytes_out),
         "collective_ms_per_step": round(step_coll_ms, 4),
         "peak_note": "bytes each rank sends per step / collective time, vs (N-1) direct xGMI links x 76.8 GB/s "
