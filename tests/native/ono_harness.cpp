@@ -6,7 +6,7 @@
 // BlockingStore + BarrierSync round with three worker threads, and checks all
 // three against the C oracle.
 //
-//   make -C tools harness && tools/ono_harness [n_elems]
+//   make -C tests/native ono_harness && tests/native/ono_harness [n_elems]
 // exit 0 = bit-exact, 1 = mismatch, 2 = library error.
 #include <cstdio>
 #include <cstdlib>

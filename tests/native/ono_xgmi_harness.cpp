@@ -9,7 +9,7 @@
 // (ono_ring_pull_grads_host on registered host buckets, both wires), each
 // checked bit for bit against the C oracle of the reference ring.
 //
-//   make -C tools xgmi_harness && tools/ono_xgmi_harness [nranks] [n_elems] [device_stride]
+//   make -C tests/native ono_xgmi_harness && tests/native/ono_xgmi_harness [nranks] [n_elems] [device_stride]
 // device_stride 0 puts every rank on device 0 (one-GPU box), 1 gives rank r device r.
 // exit 0 = every rank bit-exact, 1 = mismatch, 2 = library / process error.
 #include <sys/wait.h>
