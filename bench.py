@@ -502,6 +502,7 @@ class Runner:
                 span[1].record(self.stream)
 
         el, _ = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize, self.ctl, on_start=on_start)
+        r.check()  # an xGMI barrier timeout would make the timed rounds invalid
         span_ms = span[0].elapsed_time(span[1])
         if self.world == 1:
             return el, {"kernel_ms": span_ms, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0}

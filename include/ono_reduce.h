@@ -198,6 +198,11 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
 int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
+/* Health of the rounds already enqueued: call after synchronizing the stream.
+ * ONO_E_IO when an xGMI barrier timed out (that round's results are invalid,
+ * and every later call fails the same way), ONO_E_ABORTED after
+ * ono_ring_abort, else ONO_OK.                                               */
+int ono_ring_check(const ono_ring *ring);
 /* Segments of the f32 all-reduce schedule (ONO_ALGO_ALLREDUCE): with k > 1
  * the fused finaliser (÷n, residual = 0) of segment j overlaps the RCCL
  * all-reduce of segment j+1; 1 = one all-reduce then one finaliser; 0 = the

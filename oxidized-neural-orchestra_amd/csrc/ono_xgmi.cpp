@@ -393,6 +393,14 @@ int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
     return ONO_OK;
 }
 
+int ono_ring_check(const ono_ring *r) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    if (r->xgmi && r->xgmi->err && __atomic_load_n(r->xgmi->err, __ATOMIC_ACQUIRE) == 1u)
+        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    return ONO_OK;
+}
+
 int ono_ring_xgmi_connect(ono_ring *r, const uint8_t *handles) {
     if (!r || !handles) return set_error(ONO_E_ARG, "NULL argument");
     if (r->n == 1) return ONO_OK;

@@ -202,6 +202,11 @@ class WorkerRingManager:
         overlaps the all-reduce of segment j+1); 1 = unsegmented, 0 = default."""
         call("ono_ring_set_pipeline", self._h, segments)
 
+    def check(self) -> None:
+        """Raise if the rounds enqueued so far are invalid (synchronize first):
+        IoError after an xGMI barrier timeout, Aborted after abort()."""
+        call("ono_ring_check", self._h)
+
     def abort(self) -> None:
         call("ono_ring_abort", self._h)
 

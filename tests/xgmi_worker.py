@@ -156,6 +156,12 @@ def run_timeout(rank: int, n: int) -> str | None:
             torch.cuda.synchronize()
             waited = time.time() - t0
             try:
+                ring.check()
+            except ono_amd.IoError:
+                pass
+            else:
+                return "check() after a timed-out barrier did not raise IoError"
+            try:
                 ring.pull_grads()
             except ono_amd.IoError:
                 pass
