@@ -79,9 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-xgmi", dest="xgmi", action="store_false",
                     help="N > 1: skip the xGMI peer-access schedule (measured in child processes)")
     ap.add_argument("--xgmi-timeout", type=float, default=240.0)
-    ap.add_argument("--xgmi-coresident", type=int, default=0,
-                    help="N = 1 rehearsal: run the xGMI schedule with this many ranks as processes on one GPU "
-                         "(HBM stands in for the links; informational)")
+    ap.add_argument("--xgmi-coresident", type=int, default=2,
+                    help="N = 1: also run the xGMI schedule with this many ranks as processes on the one GPU "
+                         "(HBM stands in for the links; informational; 0 = off)")
     ap.add_argument("--xgmi-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a one-GPU box: every rank on device 0 (with --algo xgmi, which needs no "
@@ -762,9 +762,14 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
     rc, out, err = outs[0]
     try:
         res = json.loads(out.strip().splitlines()[-1])
-        if coresident:
+        if coresident:  # no links here: keep the timings, drop the link roofline
+            for v in res.values():
+                rl = v.get("roofline") if isinstance(v, dict) else None
+                if rl:
+                    v["roofline"] = {k: rl[k] for k in ("schedule", "phases_ms_per_step", "kernel_avg_us")
+                                     if k in rl}
             res["note"] = (f"co-resident rehearsal: {n} ranks as processes on ONE GPU, peer regions are IPC "
-                           "imports of the same HBM; the xGMI roofline fields do not apply")
+                           "imports of the same HBM (no xGMI links involved; timings only)")
         return res
     except (ValueError, IndexError):
         return {"xgmi": {"error": f"child rank 0 exited {rc}: {(err or '').strip()[-300:]}"}}
