@@ -305,6 +305,124 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
             **out}
 
 
+def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
+    """SURVEY §8(f) rows 1, 2 and 4 at the measurement bar: the remaining
+    kernels of the path, each timed as one HIP event pair around K
+    back-to-back launches over rotating buffer sets (> 1 GiB, so the Infinity
+    Cache cannot serve re-reads), against the 8 TB/s HBM roofline:
+      acc_residual       residual += grad (param_manager.rs:191-197)          12 B/elem
+      f16_add_encode_zero  the hop kernel: acc + dec(in) -> enc -> out, acc = 0  12 B/elem
+                         (worker_ring.rs:141-143 + :122, :133; the TCP edge's per-hop work)
+      f16_decode_scale   gather receive (:200 + /n)                             6 B/elem
+      consumer_{gd,momentum,adam}  optimize + zero_grad + params copy        20/28/36 B/elem
+                         (all_reduce.rs:126-132, param_manager.rs:148-172)
+    64 MiB f32 buckets (16 M elements)."""
+    n = 16 << 20
+    stream = torch.cuda.current_stream()
+    f32 = lambda: torch.empty(n, dtype=torch.float32, device="cuda")  # noqa: E731
+    u16 = lambda: torch.empty(n, dtype=torch.int16, device="cuda")  # noqa: E731
+    out = {}
+
+    def timed(name, per_elem, make_set, launch, nsets):
+        sets = [make_set(i) for i in range(nsets)]
+        torch.cuda.synchronize()
+        for i in range(warmup):
+            launch(sets[i % nsets])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(stream)
+        for i in range(steps):
+            launch(sets[(warmup + i) % nsets])
+        b.record(stream)
+        torch.cuda.synchronize()
+        us = a.elapsed_time(b) / steps * 1e3
+        gbs = per_elem * n / (us * 1e-6) / 1e9
+        out[name] = {"bytes_per_launch": per_elem * n, "us_per_launch": round(us, 2), "achieved_gbs": round(gbs, 1),
+                     "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        del sets
+        torch.cuda.empty_cache()
+
+    def filled(i, r):
+        return ono_amd.kernels.synth(f32(), SEED + i, r)
+
+    timed("acc_residual", 12, lambda i: (filled(i, 0), filled(i, 1)),
+          lambda st: ono_amd.kernels.acc(st[0], st[1]), 6)
+
+    def hop_set(i):
+        h = u16()
+        ono_amd.kernels.f16_encode(h, filled(i, 2))
+        return (u16(), filled(i, 0), h)
+    timed("f16_add_encode_zero", 12, hop_set, lambda st: ono_amd.kernels.f16_add_encode_zero(*st), 8)
+
+    def dec_set(i):
+        h = u16()
+        ono_amd.kernels.f16_encode(h, filled(i, 3))
+        return (f32(), h)
+    timed("f16_decode_scale", 6, dec_set, lambda st: ono_amd.kernels.f16_decode_scale(st[0], st[1], 8.0), 12)
+
+    for name, opt, per in (("gd", ono_amd.GradientDescent(0.1), 20),
+                           ("momentum", ono_amd.GradientDescentWithMomentum(0.1, 0.9), 28),
+                           ("adam", ono_amd.Adam(1e-3, 0.9, 0.999, 1e-8), 36)):
+        dev_opt = ono_amd.DeviceOptimizer(opt, n)
+        timed(f"consumer_{name}", per, lambda i: (filled(i, 4), filled(i, 5), f32()),
+              lambda st, o=dev_opt: o.step(st[0], st[1], st[2]), 4)
+        dev_opt.close()
+    return {"workload": "the path's other kernels on 64 MiB f32 buckets (16 M elements), device-resident",
+            "hbm_peak_gbs": HBM_PEAK_GBS,
+            "timing": "one HIP event pair around K back-to-back launches over rotating sets", **out}
+
+
+def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
+    """the device top-k codec (comms/src/sparse/protocol.rs:57-144) on a 64 MiB
+    gradient with the threshold at the 90th |g| percentile (~10 % of the values kept, the
+    reference's r = 0.9).  Drop = count pass + scan + write pass + headers, a blocking call (the
+    wire length is needed on the host); bytes = 8 N read + the wire written.  Lift parses the
+    run headers on the host and expands on the device (host buffer in)."""
+    import ctypes as C
+
+    n = 16 << 20
+    g = ono_amd.kernels.synth(torch.empty(n, dtype=torch.float32, device="cuda"), SEED, 7)
+    t = float(torch.quantile(g[: 1 << 20].abs().float(), 0.9).item())
+    L = ono_amd.lib()
+    cap = L.ono_sparse_max_bytes(n)
+    buf = torch.empty(cap + 8, dtype=torch.uint8, device="cuda")
+    nb = C.c_size_t(0)
+    stream = torch.cuda.current_stream()
+    ts, tev = [], []
+    for r in range(rounds + 1):  # device-resident: gradient in, wire buffer out, both in HBM
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        a.record(stream)
+        ono_amd._lib.call("ono_sparse_drop", buf.data_ptr(), cap, C.byref(nb), g.data_ptr(), n, t,
+                          stream.cuda_stream)
+        b.record(stream)
+        t1 = time.perf_counter()
+        if r:
+            ts.append(t1 - t0)
+            b.synchronize()
+            tev.append(a.elapsed_time(b) * 1e-3)
+    td, tdev = sorted(ts)[len(ts) // 2], sorted(tev)[len(tev) // 2]
+    wire = bytes(buf[: nb.value].cpu().numpy())
+    tl = []
+    for r in range(rounds + 1):
+        t0 = time.perf_counter()
+        back = ono_amd.sparse.grad_lift(wire, n)
+        if r:
+            tl.append(time.perf_counter() - t0)
+    lt = sorted(tl)[len(tl) // 2]
+    kept = int(torch.count_nonzero(back).item())
+    drop_bytes = 8 * n + len(wire)
+    return {"workload": "sparse grad_drop / grad_lift, 64 MiB f32 gradient, threshold = 90th |g| percentile",
+            "kept_values": kept, "wire_bytes": len(wire),
+            "drop": {"ms": round(td * 1e3, 3), "device_ms": round(tdev * 1e3, 3), "algorithmic_bytes": drop_bytes,
+                     "achieved_gbs": round(drop_bytes / tdev / 1e9, 1),
+                     "frac_of_hbm_peak": round(drop_bytes / tdev / 1e9 / HBM_PEAK_GBS, 4),
+                     "note": "ms = wall time of the blocking C call; device_ms = HIP events around it on its "
+                             "stream (count + scan + host read of the totals + write + headers)"},
+            "lift": {"ms": round(lt * 1e3, 3), "note": "host wire buffer in: header parse on the host + H2D + expand"}}
+
+
 def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
     """PCIe-inclusive pull_grads from host buffers (never
     `value`): the reference's buckets live in host memory and arrive from
@@ -622,6 +740,8 @@ def main(argv=None) -> int:
         extra["ps_host_fed"] = ps_host_fed(ono_amd, elems)
     if rank == 0 and world == 1 and not args.no_local_reduce:
         extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
+        extra["path_kernels"] = path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
+        extra["sparse_codec"] = sparse_codec(torch, ono_amd)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         extra["cpu_baseline"] = cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds)
 

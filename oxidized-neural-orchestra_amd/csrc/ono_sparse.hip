@@ -12,13 +12,17 @@
 //   offset_j = U(s_j) - U(s_{j-1}),  U(i) = i - F(i)  (unkept values before i)
 //   len_j    = F(s_{j+1}) - F(s_j)   (F_total for the last run).
 // Four launches: per-tile counts -> tile scan -> write (block-wide scan with
-// wave shuffles + LDS; values written, run starts record U and F) -> headers.
+// wave shuffles + LDS; values written, run starts record U and F) -> headers,
+// back to back on the stream (the totals stay on the device; the host reads
+// them once, at the end, for the wire length).
 // Decoding walks the run headers on the host (a sequential parse, as in the
 // reference, over R records) and expands all values on the device.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "ono_internal.h"
@@ -48,28 +52,43 @@ __device__ __forceinline__ float from_f16_sp(uint16_t b) {
 __device__ __forceinline__ bool kept(float x, float t) { return fabsf(x) >= t; }
 
 // Flags of a thread's kEPT elements: bit e = kept, plus whether each starts a run.
+// The kEPT = 8 values come in as two 16-B loads (g is 16-B aligned on the fast
+// path; `vec` = false uses scalar loads); whether the element before the
+// thread's first one is kept comes from the neighbouring lane (a shuffle), and
+// only lane 0 of each wave reads it from memory.
 struct Bits {
     uint32_t keep = 0, start = 0;
 };
-__device__ __forceinline__ Bits thread_bits(const float *g, size_t n, float t, size_t base) {
+typedef float f4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Bits thread_bits(const float *g, size_t n, float t, size_t base, bool vec,
+                                            float (&x)[kEPT]) {
     Bits b;
-    bool prev = base > 0 && base - 1 < n ? kept(g[base - 1], t) : false;
+    if (vec && base + kEPT <= n) {
+        f4s a = __builtin_nontemporal_load((const f4s *)(g + base));
+        f4s c = __builtin_nontemporal_load((const f4s *)(g + base + 4));
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < kEPT; e++) {
-        size_t i = base + e;
-        bool k = i < n && kept(g[i], t);
-        if (k) b.keep |= 1u << e;
-        if (k && !prev) b.start |= 1u << e;
-        prev = k;
+        for (int e = 0; e < kEPT; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
     }
+#pragma unroll
+    for (int e = 0; e < kEPT; e++)
+        if (base + e < n && kept(x[e], t)) b.keep |= 1u << e;
+    // kept(element base-1): the previous lane's last flag; lane 0 loads it
+    const int lane = threadIdx.x & 63;
+    uint32_t last = (b.keep >> (kEPT - 1)) & 1u;
+    uint32_t prev = __shfl_up(last, 1, 64);
+    if (lane == 0) prev = base > 0 && base - 1 < n ? (kept(g[base - 1], t) ? 1u : 0u) : 0u;
+    b.start = b.keep & ~((b.keep << 1) | prev);
     return b;
 }
 
 // Exclusive block-wide scan of (a, b) pairs: wave-level shuffles (64 lanes),
 // then the 4 wave totals through LDS.  Returns the block totals too.
+template <int NT = kSB>
 __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea, uint32_t &eb, uint32_t &ta,
                                             uint32_t &tb) {
-    __shared__ uint32_t wa[kSB / 64], wb[kSB / 64];
+    __shared__ uint32_t wa[NT / 64], wb[NT / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t ia = a, ib = b;  // inclusive wave scan
 #pragma unroll
@@ -82,7 +101,7 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
     uint32_t pa = 0, pb = 0;
     ta = 0; tb = 0;
 #pragma unroll
-    for (int w = 0; w < kSB / 64; w++) {
+    for (int w = 0; w < NT / 64; w++) {
         if (w < wave) { pa += wa[w]; pb += wb[w]; }
         ta += wa[w];
         tb += wb[w];
@@ -91,70 +110,130 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
     eb = pb + ib - b;
 }
 
-__global__ __launch_bounds__(kSB) void sp_count(const float *g, size_t n, float t, uint32_t *tileF, uint32_t *tileS) {
-    Bits b = thread_bits(g, n, t, (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT);
+__global__ __launch_bounds__(kSB) void sp_count(const float *g, size_t n, float t, uint32_t *tileF, uint32_t *tileS,
+                                                bool vec) {
+    float x[kEPT];
+    Bits b = thread_bits(g, n, t, (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT, vec, x);
     uint32_t ea, eb, ta, tb;
     block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
     if (threadIdx.x == 0) { tileF[blockIdx.x] = ta; tileS[blockIdx.x] = tb; }
 }
 
-// Exclusive scan of the tile counts in place (one block, running carry);
+// Exclusive scan of the tile counts in place, one block of kScanT threads,
+// in chunks of kScanT x kScanPer tiles staged through LDS: coalesced global
+// loads into LDS, each thread scans its kScanPer contiguous tiles there, one
+// block-wide scan of the per-thread sums, coalesced stores back.
 // totals[0] = kept values, totals[1] = runs.
-__global__ __launch_bounds__(kSB) void sp_scan_tiles(uint32_t *tileF, uint32_t *tileS, size_t ntiles,
-                                                     uint64_t *totals) {
-    __shared__ uint32_t carryF, carryS;
-    if (threadIdx.x == 0) { carryF = 0; carryS = 0; }
-    __syncthreads();
-    for (size_t base = 0; base < ntiles; base += kSB) {
-        size_t i = base + threadIdx.x;
-        uint32_t f = i < ntiles ? tileF[i] : 0, s = i < ntiles ? tileS[i] : 0;
-        uint32_t ea, eb, ta, tb;
-        block_scan2(f, s, ea, eb, ta, tb);
-        uint32_t cf = carryF, cs = carryS;
-        if (i < ntiles) { tileF[i] = cf + ea; tileS[i] = cs + eb; }
+constexpr int kScanT = 1024, kScanPer = 8, kScanChunk = kScanT * kScanPer;
+__global__ __launch_bounds__(kScanT) void sp_scan_tiles(uint32_t *tileF, uint32_t *tileS, size_t ntiles,
+                                                        uint64_t *totals) {
+    __shared__ uint32_t lf[kScanChunk], ls[kScanChunk];
+    __shared__ uint32_t carry[2];
+    if (threadIdx.x == 0) { carry[0] = 0; carry[1] = 0; }
+    for (size_t c0 = 0; c0 < ntiles; c0 += kScanChunk) {
+        const size_t m = ntiles - c0 < (size_t)kScanChunk ? ntiles - c0 : (size_t)kScanChunk;
+        for (size_t i = threadIdx.x; i < kScanChunk; i += kScanT) {
+            lf[i] = i < m ? tileF[c0 + i] : 0u;
+            ls[i] = i < m ? tileS[c0 + i] : 0u;
+        }
         __syncthreads();
-        if (threadIdx.x == 0) { carryF = cf + ta; carryS = cs + tb; }
+        const int lo = threadIdx.x * kScanPer;
+        uint32_t sf = 0, ss = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; k++) { sf += lf[lo + k]; ss += ls[lo + k]; }
+        uint32_t ef, es, tf, ts;
+        block_scan2<kScanT>(sf, ss, ef, es, tf, ts);
+        ef += carry[0];
+        es += carry[1];
+#pragma unroll
+        for (int k = 0; k < kScanPer; k++) {
+            const uint32_t a = lf[lo + k], b = ls[lo + k];
+            lf[lo + k] = ef;
+            ls[lo + k] = es;
+            ef += a;
+            es += b;
+        }
+        __syncthreads();
+        for (size_t i = threadIdx.x; i < m; i += kScanT) {
+            tileF[c0 + i] = lf[i];
+            tileS[c0 + i] = ls[i];
+        }
+        if (threadIdx.x == 0) { carry[0] += tf; carry[1] += ts; }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { totals[0] = carryF; totals[1] = carryS; }
+    if (threadIdx.x == 0) { totals[0] = carry[0]; totals[1] = carry[1]; }
 }
 
+// A tile's output is one contiguous byte range of the wire, from
+// 8 + 8 S0 + 2 F0 to 8 + 8 (S0 + runs) + 2 (F0 + kept) (S0, F0: the tile's
+// prefix).  Values are placed in an LDS image of that range first, then the
+// block writes the range out with consecutive 2-byte stores (coalesced,
+// instead of one scattered store per kept value).  Header slots in the image
+// are left as they are; sp_headers writes them afterwards.
+constexpr int kStageU16 = (8 * (kTile / 2 + 1) + 2 * kTile) / 2;  // worst case: alternating kept/unkept
 __global__ __launch_bounds__(kSB) void sp_write(const float *g, size_t n, float t, const uint32_t *tileF,
-                                                const uint32_t *tileS, uint8_t *buf, uint32_t *RU, uint32_t *RF) {
+                                                const uint32_t *tileS, uint8_t *buf, uint32_t *RU, uint32_t *RF,
+                                                bool vec) {
+    __shared__ uint16_t stage[kStageU16];
+    __shared__ uint32_t su[kTile / 2 + 1], sf[kTile / 2 + 1];  // the tile's run table rows
     const size_t base = (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT;
-    Bits b = thread_bits(g, n, t, base);
+    float x[kEPT];  // the values stay in registers from the flag pass (g is read once here)
+    Bits b = thread_bits(g, n, t, base, vec, x);
     uint32_t ea, eb, ta, tb;
     block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
-    uint32_t F = tileF[blockIdx.x] + ea;   // kept values before this thread's first element
-    uint32_t S = tileS[blockIdx.x] + eb;   // runs started before it
+    const uint32_t F0 = tileF[blockIdx.x], S0 = tileS[blockIdx.x];
+    uint32_t f = ea, sl = eb;  // this thread's kept values / runs before it, within the tile
+    if (b.keep) {
 #pragma unroll
-    for (int e = 0; e < kEPT; e++) {
-        if (!(b.keep >> e & 1u)) continue;
-        size_t i = base + e;
-        if (b.start >> e & 1u) {
-            RU[S] = (uint32_t)(i - F);  // U(s_j): unkept values before the run
-            RF[S] = F;                  // F(s_j)
-            S++;
+        for (int e = 0; e < kEPT; e++) {
+            if (!(b.keep >> e & 1u)) continue;
+            if (b.start >> e & 1u) {
+                const size_t i = base + e;
+                su[sl] = (uint32_t)(i - (F0 + f));  // U(s_j): unkept values before the run
+                sf[sl] = F0 + f;                    // F(s_j)
+                sl++;
+            }
+            stage[4 * sl + f] = to_f16_sp(x[e]);  // byte 8 sl + 2 f of the tile's range
+            f++;
         }
-        *(uint16_t *)(buf + 8 + 8 * (size_t)S + 2 * (size_t)F) = to_f16_sp(g[i]);
-        F++;
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < tb; k += kSB) {  // run table rows, coalesced
+        RU[S0 + k] = su[k];
+        RF[S0 + k] = sf[k];
+    }
+    // the range, 4 bytes per store where aligned (it starts 2-B aligned)
+    const uint32_t nu16 = 4 * tb + ta;  // the range's length in 2-byte units
+    uint16_t *dst = (uint16_t *)(buf + 8 + 8 * (size_t)S0 + 2 * (size_t)F0);
+    const uint32_t h = (uint32_t)(((uintptr_t)dst >> 1) & 1u) < nu16 ? (uint32_t)(((uintptr_t)dst >> 1) & 1u) : nu16;
+    if (threadIdx.x == 0 && h) dst[0] = stage[0];
+    const uint32_t npair = (nu16 - h) / 2;
+    uint32_t *d32 = (uint32_t *)(dst + h);
+    for (uint32_t k = threadIdx.x; k < npair; k += kSB)
+        d32[k] = (uint32_t)stage[h + 2 * k] | (uint32_t)stage[h + 2 * k + 1] << 16;
+    if (threadIdx.x == 0 && h + 2 * npair < nu16) dst[nu16 - 1] = stage[nu16 - 1];
 }
 
-__global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint32_t *RF, size_t R, uint32_t Ftot,
-                                                  uint64_t total_len, uint8_t *buf) {
-    size_t j = (size_t)blockIdx.x * kSB + threadIdx.x;
-    if (j == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
+// R and the kept total come from the device totals (no host round trip); a
+// grid-stride loop sized for the worst case idles past R.
+__global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint32_t *RF, const uint64_t *totals,
+                                                  uint64_t total_len, uint8_t *buf, uint64_t *host_tot) {
+    const size_t R = totals[1];
+    const uint32_t Ftot = (uint32_t)totals[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)(total_len >> (16 * q));
+        host_tot[0] = Ftot;  // the wire length's terms, for the caller (host-mapped)
+        host_tot[1] = R;
     }
-    if (j >= R) return;
-    uint32_t off = RU[j] - (j ? RU[j - 1] : 0u);
-    uint32_t len = (j + 1 < R ? RF[j + 1] : Ftot) - RF[j];
-    uint8_t *h = buf + 8 + 8 * j + 2 * (size_t)RF[j];
-    *(uint16_t *)(h + 0) = (uint16_t)off;
-    *(uint16_t *)(h + 2) = (uint16_t)(off >> 16);
-    *(uint16_t *)(h + 4) = (uint16_t)len;
-    *(uint16_t *)(h + 6) = (uint16_t)(len >> 16);
+    for (size_t j = (size_t)blockIdx.x * kSB + threadIdx.x; j < R; j += (size_t)gridDim.x * kSB) {
+        uint32_t off = RU[j] - (j ? RU[j - 1] : 0u);
+        uint32_t len = (j + 1 < R ? RF[j + 1] : Ftot) - RF[j];
+        uint8_t *h = buf + 8 + 8 * j + 2 * (size_t)RF[j];
+        *(uint16_t *)(h + 0) = (uint16_t)off;
+        *(uint16_t *)(h + 2) = (uint16_t)(off >> 16);
+        *(uint16_t *)(h + 4) = (uint16_t)len;
+        *(uint16_t *)(h + 6) = (uint16_t)(len >> 16);
+    }
 }
 
 // Lift: value v belongs to run j with cumF[j] <= v < cumF[j+1] (binary search);
@@ -186,6 +265,51 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
     }
 }
 
+// the totals into the host-mapped words (the exact-size path of a small buffer)
+__global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
+    host_tot[0] = totals[0];
+    host_tot[1] = totals[1];
+}
+
+// Scratch of the encoder (tile counts, run table, device totals, two host-
+// mapped words for the result), kept per device and grown on demand: the
+// stream-ordered allocations it replaces cost more than the kernels at 64 MiB.
+struct Scratch {
+    size_t tiles_cap = 0, runs_cap = 0;
+    uint32_t *tiles = nullptr, *runs = nullptr;
+    uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
+};
+std::mutex g_scratch_mu;
+Scratch g_scratch[64];
+
+int scratch_for(size_t ntiles, size_t maxruns, Scratch **out) {
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
+    Scratch &sc = g_scratch[dev];
+    if (!sc.totals_dev) {
+        ONO_HIP(hipMalloc((void **)&sc.totals_dev, 2 * sizeof(uint64_t)));
+        ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
+    }
+    if (2 * ntiles + 2 > sc.tiles_cap) {
+        (void)hipFree(sc.tiles);
+        sc.tiles = nullptr;
+        sc.tiles_cap = 0;
+        ONO_HIP(hipMalloc((void **)&sc.tiles, (2 * ntiles + 2) * sizeof(uint32_t)));
+        sc.tiles_cap = 2 * ntiles + 2;
+    }
+    if (2 * maxruns > sc.runs_cap) {
+        (void)hipFree(sc.runs);
+        sc.runs = nullptr;
+        sc.runs_cap = 0;
+        ONO_HIP(hipMalloc((void **)&sc.runs, 2 * maxruns * sizeof(uint32_t)));
+        sc.runs_cap = 2 * maxruns;
+    }
+    *out = &sc;
+    return ONO_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -200,42 +324,47 @@ int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, si
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
     const size_t maxruns = (n + 1) / 2 + 1;
-    uint32_t *tiles = nullptr, *runs = nullptr;
-    uint64_t *totals = nullptr;
-    ONO_HIP(hipMallocAsync((void **)&tiles, (2 * ntiles + 2) * sizeof(uint32_t), s));
-    ONO_HIP(hipMallocAsync((void **)&runs, 2 * maxruns * sizeof(uint32_t), s));
-    ONO_HIP(hipMallocAsync((void **)&totals, 2 * sizeof(uint64_t), s));
-    ONO_HIP(hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s));
-    uint32_t *tileF = tiles, *tileS = tiles + ntiles + 1, *RU = runs, *RF = runs + maxruns;
-    int rc = ONO_OK;
-    uint64_t tot[2] = {0, 0};
+    const bool vec = ((uintptr_t)g & 15u) == 0;
+    // A buffer of the worst-case size cannot overflow: count, scan, write and
+    // headers run back to back and the host reads the totals once at the end.
+    // A smaller buffer needs the exact size first (one extra host round trip).
+    const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);  // one call at a time per process owns the scratch
+    Scratch *sc = nullptr;
+    int rc = scratch_for(ntiles, maxruns, &sc);
+    if (rc) return rc;
+    uint32_t *tileF = sc->tiles, *tileS = sc->tiles + ntiles + 1, *RU = sc->runs, *RF = sc->runs + maxruns;
+    volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
+    tot[0] = tot[1] = 0;
+    uint64_t *totals = sc->totals_dev;
+    hipError_t e = hipSuccess;
     if (ntiles) {
-        hipLaunchKernelGGL(sp_count, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS);
-        hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kSB), 0, s, tileF, tileS, ntiles, totals);
-    }
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(tot, totals, sizeof tot, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    const size_t F = tot[0], R = tot[1], bytes = 8 + 8 * R + 2 * F;
-    if (e != hipSuccess) {
-        rc = hip_error(e, "sparse count", __FILE__, __LINE__);
-    } else if (bytes > cap) {
-        rc = set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu", bytes, cap);
+        hipLaunchKernelGGL(sp_count, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS, vec);
+        hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, tileF, tileS, ntiles, totals);
     } else {
-        if (ntiles)
-            hipLaunchKernelGGL(sp_write, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS, buf,
-                               RU, RF);
-        hipLaunchKernelGGL(sp_headers, dim3((unsigned)((R + kSB) / kSB)), dim3(kSB), 0, s, RU, RF, R, (uint32_t)F,
-                           (uint64_t)n, buf);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) rc = hip_error(e, "sparse write", __FILE__, __LINE__);
-        *nbytes = bytes;
+        e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s);
     }
-    (void)hipFreeAsync(tiles, s);
-    (void)hipFreeAsync(runs, s);
-    (void)hipFreeAsync(totals, s);
-    return rc;
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess && !worst_case_fits) {
+        hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(1), 0, s, totals, sc->host_tot_dev);
+        e = hipStreamSynchronize(s);
+        if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
+            return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu",
+                             (size_t)(8 + 8 * tot[1] + 2 * tot[0]), cap);
+    }
+    if (e != hipSuccess) return hip_error(e, "sparse count", __FILE__, __LINE__);
+    if (ntiles)
+        hipLaunchKernelGGL(sp_write, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS, buf, RU,
+                           RF, vec);
+    const size_t hdr_runs = worst_case_fits ? maxruns : (size_t)tot[1];
+    const size_t hblocks = std::min<size_t>(4096, (hdr_runs + kSB) / kSB);
+    hipLaunchKernelGGL(sp_headers, dim3((unsigned)hblocks), dim3(kSB), 0, s, RU, RF, totals, (uint64_t)n, buf,
+                       sc->host_tot_dev);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
+    *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
+    return ONO_OK;
 }
 
 int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, size_t nbytes, void *stream) {
