@@ -64,10 +64,11 @@ template <class W> hipError_t launch_add_finish(float *grad, W *out, float *acc,
 template <class W>
 hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, size_t n, float divisor,
                          bool zero_all, hipStream_t s);
-// the same with nout copies of the result (e.g. straight into every peer's gather slot)
+// the same with nout copies of the result (e.g. straight into every peer's gather
+// slot: sys_out = system-coherent stores for peer HBM)
 template <class W>
-hipError_t launch_direct_multi(float *grad, W *const *outs, int nout, const float *const *ins, int k, size_t n,
-                               float divisor, bool zero_all, hipStream_t s);
+hipError_t launch_direct_multi(float *grad, W *const *outs, int nout, bool sys_out, const float *const *ins, int k,
+                               size_t n, float divisor, bool zero_all, hipStream_t s);
 
 // ---- xGMI peer-access schedule (ono_xgmi.hip) ----
 // One peer's part of a push or pull launch: n elements from src to dst.

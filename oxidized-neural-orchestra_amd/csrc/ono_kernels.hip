@@ -233,6 +233,7 @@ template <int K, class W> struct DirectOp {
     float *grad;
     Outs out;  // nout copies of the result (f16 message / f32 grad value): local and/or peer HBM
     int nout;
+    int sys_out;  // outs are peer HBM: system-coherent (sc0 sc1) stores, see ono_xgmi.hip
     float v;
     int mode;  // SCALE_RECIP or SCALE_DIV
     int zall;
@@ -246,7 +247,10 @@ template <int K, class W> struct DirectOp {
         const float gv = mode == SCALE_RECIP ? p * v : p / v;
         grad[i] = gv;
         const W m = sizeof(W) == 2 ? Wire<W>::enc(p) : Wire<W>::enc(gv);
-        for (int j = 0; j < nout; j++) static_cast<W *>(out.p[j])[i] = m;
+        for (int j = 0; j < nout; j++) {
+            if (sys_out) *(volatile __attribute__((address_space(1))) W *)(static_cast<W *>(out.p[j]) + i) = m;
+            else static_cast<W *>(out.p[j])[i] = m;
+        }
         if (zall) {
 #pragma unroll
             for (int k = 0; k < K; k++) const_cast<float *>(in.p[k])[i] = 0.0f;
@@ -268,7 +272,10 @@ template <int K, class W> struct DirectOp {
         const f4 gv = mode == SCALE_RECIP ? p * v : p / v;
         st_nt((f4 *)(grad + i), gv);
         const WV m = sizeof(W) == 2 ? Wire<W>::enc4(p) : Wire<W>::enc4(gv);
-        for (int j = 0; j < nout; j++) st_nt((WV *)(static_cast<W *>(out.p[j]) + i), m);
+        for (int j = 0; j < nout; j++) {
+            if (sys_out) *(volatile __attribute__((address_space(1))) WV *)(static_cast<W *>(out.p[j]) + i) = m;
+            else st_nt((WV *)(static_cast<W *>(out.p[j]) + i), m);
+        }
         const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
         if (zall) {
 #pragma unroll
@@ -564,8 +571,8 @@ hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_,
 template <class W> unsigned wph(const W *p) { return phase_of(p, sizeof(W)); }
 
 template <int K, class W>
-hipError_t direct_k(float *grad, const Outs &out, int nout, const Ptrs &p, size_t n, const Scale &sc, bool zall,
-                    hipStream_t s) {
+hipError_t direct_k(float *grad, const Outs &out, int nout, bool sys_out, const Ptrs &p, size_t n, const Scale &sc,
+                    bool zall, hipStream_t s) {
     unsigned ph[2 * ONO_MAX_INPUTS + 1];
     int c = 0;
     ph[c++] = phase_of(grad, 4);
@@ -573,18 +580,18 @@ hipError_t direct_k(float *grad, const Outs &out, int nout, const Ptrs &p, size_
     for (int k = 0; k < K; k++) ph[c++] = phase_of(p.p[k], 4);
     // SCALE_NONE (d == 1) runs as a multiply by 1: the identity, -0 and NaN payloads included
     const int mode = sc.mode == SCALE_DIV ? SCALE_DIV : SCALE_RECIP;
-    DirectOp<K, W> op{p, grad, out, nout, sc.mode == SCALE_NONE ? 1.0f : sc.v, mode, zall ? 1 : 0};
+    DirectOp<K, W> op{p, grad, out, nout, sys_out ? 1 : 0, sc.mode == SCALE_NONE ? 1.0f : sc.v, mode, zall ? 1 : 0};
     return launch_ew_arr(op, n, ph, c, s);
 }
 
 template <int K, class W>
-hipError_t direct_dispatch(int k, float *grad, const Outs &out, int nout, const Ptrs &p, size_t n,
+hipError_t direct_dispatch(int k, float *grad, const Outs &out, int nout, bool sys_out, const Ptrs &p, size_t n,
                            const Scale &sc, bool zall, hipStream_t s) {
     if constexpr (K > ONO_MAX_INPUTS) {
         return hipErrorInvalidValue;
     } else {
-        if (k == K) return direct_k<K, W>(grad, out, nout, p, n, sc, zall, s);
-        return direct_dispatch<K + 1, W>(k, grad, out, nout, p, n, sc, zall, s);
+        if (k == K) return direct_k<K, W>(grad, out, nout, sys_out, p, n, sc, zall, s);
+        return direct_dispatch<K + 1, W>(k, grad, out, nout, sys_out, p, n, sc, zall, s);
     }
 }
 
@@ -623,28 +630,28 @@ hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n
 }
 
 template <class W>
-hipError_t launch_direct_multi(float *grad, W *const *outs, int nout, const float *const *ins, int k, size_t n,
-                               float divisor, bool zero_all, hipStream_t s) {
+hipError_t launch_direct_multi(float *grad, W *const *outs, int nout, bool sys_out, const float *const *ins, int k,
+                               size_t n, float divisor, bool zero_all, hipStream_t s) {
     if (k < 1 || k > ONO_MAX_INPUTS || nout < 0 || nout > ONO_MAX_INPUTS) return hipErrorInvalidValue;
     Ptrs p{};
     for (int j = 0; j < k; j++) p.p[j] = ins[j];
     Outs o{};
     for (int j = 0; j < nout; j++) o.p[j] = outs[j];
-    return direct_dispatch<1, W>(k, grad, o, nout, p, n, make_scale(divisor), zero_all, s);
+    return direct_dispatch<1, W>(k, grad, o, nout, sys_out, p, n, make_scale(divisor), zero_all, s);
 }
 template <class W>
 hipError_t launch_direct(float *grad, W *out, const float *const *ins, int k, size_t n, float divisor,
                          bool zero_all, hipStream_t s) {
-    return launch_direct_multi<W>(grad, &out, out ? 1 : 0, ins, k, n, divisor, zero_all, s);
+    return launch_direct_multi<W>(grad, &out, out ? 1 : 0, false, ins, k, n, divisor, zero_all, s);
 }
 template hipError_t launch_direct<uint16_t>(float *, uint16_t *, const float *const *, int, size_t, float, bool,
                                             hipStream_t);
 template hipError_t launch_direct<float>(float *, float *, const float *const *, int, size_t, float, bool,
                                          hipStream_t);
-template hipError_t launch_direct_multi<uint16_t>(float *, uint16_t *const *, int, const float *const *, int, size_t,
-                                                  float, bool, hipStream_t);
-template hipError_t launch_direct_multi<float>(float *, float *const *, int, const float *const *, int, size_t, float,
-                                               bool, hipStream_t);
+template hipError_t launch_direct_multi<uint16_t>(float *, uint16_t *const *, int, bool, const float *const *, int,
+                                                  size_t, float, bool, hipStream_t);
+template hipError_t launch_direct_multi<float>(float *, float *const *, int, bool, const float *const *, int, size_t,
+                                               float, bool, hipStream_t);
 
 hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s) {
     return launch_ew(AccOp{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);

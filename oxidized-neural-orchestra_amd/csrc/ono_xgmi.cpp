@@ -207,7 +207,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
             outs[no++] = reinterpret_cast<W *>(gslot_of(x, x->peer[q], pos, q)) + ph(off[c]);
         }
         rc = timed(r, s, ONO_PHASE_XGMI_GATHER, [&]() -> int {
-            ONO_HIP(launch_direct_multi<W>(grad + off[c], outs, no, ins, n, len(c), (float)n, false, s));
+            ONO_HIP(launch_direct_multi<W>(grad + off[c], outs, no, true, ins, n, len(c), (float)n, false, s));
             return ONO_OK;
         });
         if (rc || (rc = barrier(r, s))) return rc;
