@@ -722,10 +722,14 @@ def main(argv=None) -> int:
                 extra["roofline"]["frac_of_measured_links"] = round(
                     extra["roofline"]["achieved"] / (link["gbs"] * (world - 1)), 4)
 
-    if rank == 0 and world == 1 and not args.no_host_fed:
-        extra["host_fed"] = host_fed(ono_amd, ring, elems, 5)
-    if rank == 0 and world == 1 and not args.no_tcp_edge:
-        extra["tcp_edge"] = tcp_edge_native(elems, 10) or tcp_edge(ono_amd, elems, 3)
+    def leg(name, fn):  # informational legs: a failure is recorded in the line, never fatal to it
+        try:
+            extra[name] = fn()
+        except Exception as e:  # noqa: BLE001
+            extra[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+
+    def tcp_legs():
+        out = tcp_edge_native(elems, 10) or tcp_edge(ono_amd, elems, 3)
         # BASELINE config 1: the reference's own case — 2 loopback workers, the
         # MLP 784-128-64-10 bucket (109,386 f32) — TCP edge vs CPU ring
         small = {"2_ranks": tcp_edge_native(CONFIG1_ELEMS, 200) or tcp_edge(ono_amd, CONFIG1_ELEMS, 50),
@@ -735,15 +739,22 @@ def main(argv=None) -> int:
             for k, nr in (("2_ranks", 2), ("4_ranks", 4)):
                 cr = O.cpu_ring(nr, CONFIG1_ELEMS, 50, check=False, pin=True, timeout=300)
                 small[k]["cpu_ring_ms"] = round(cr["s_per_round"] * 1e3, 4)
-        extra["tcp_edge"]["config1"] = small
-    if rank == 0 and world == 1 and not args.no_host_fed:
-        extra["ps_host_fed"] = ps_host_fed(ono_amd, elems)
-    if rank == 0 and world == 1 and not args.no_local_reduce:
-        extra["local_reduce"] = local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
-        extra["path_kernels"] = path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2))
-        extra["sparse_codec"] = sparse_codec(torch, ono_amd)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        extra["cpu_baseline"] = cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds)
+        out["config1"] = small
+        return out
+
+    if rank == 0 and world == 1:
+        if not args.no_host_fed:
+            leg("host_fed", lambda: host_fed(ono_amd, ring, elems, 5))
+        if not args.no_tcp_edge:
+            leg("tcp_edge", tcp_legs)
+        if not args.no_host_fed:
+            leg("ps_host_fed", lambda: ps_host_fed(ono_amd, elems))
+        if not args.no_local_reduce:
+            leg("local_reduce", lambda: local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
+            leg("path_kernels", lambda: path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
+            leg("sparse_codec", lambda: sparse_codec(torch, ono_amd))
+        if not args.no_cpu_baseline:
+            leg("cpu_baseline", lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
 
     value = world * bucket_bytes * args.steps / elapsed / GIB
     line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,

@@ -91,3 +91,32 @@ def test_masks_match_ring_bookkeeping():
     e_unsent = np.where(np.abs(g) < t, np.float32(0), g)   # worker_ring.rs:183-187
     assert_bitexact(a.cpu().numpy(), e_sent)
     assert_bitexact(b.cpu().numpy(), e_unsent)
+
+
+@pytest.mark.parametrize("offset", [0, 1, 3])
+def test_drop_exact_size_buffer_and_unaligned_input(offset):
+    """The two host-visible paths of ono_sparse_drop: a buffer of exactly the
+    encoded size (the counts come back to the host before the write pass) and
+    one byte short (SizeMismatch), plus the worst-case buffer, on a 16-B aligned
+    gradient and on unaligned views (scalar loads instead of 16-B vectors)."""
+    import ctypes as C
+
+    n = 65536 + 17
+    g = O.synth(n, SEED + 5, 2)
+    t = float(np.quantile(np.abs(g), 0.8))
+    want = O.grad_drop(g, t)
+    base = torch.zeros(n + 8, dtype=torch.float32, device="cuda")
+    view = base[offset:offset + n]
+    view.copy_(torch.from_numpy(g))
+    assert SP.grad_drop(view, t) == want
+    L = ono_amd.lib()
+    for cap, ok in ((len(want), True), (len(want) - 1, False)):
+        buf = torch.empty(cap + 8, dtype=torch.uint8, device="cuda")
+        nb = C.c_size_t(0)
+        rc = L.ono_sparse_drop(buf.data_ptr(), cap, C.byref(nb), view.data_ptr(), n, t,
+                               torch.cuda.current_stream().cuda_stream)
+        if ok:
+            assert rc == 0 and nb.value == len(want)
+            assert bytes(buf[: nb.value].cpu().numpy()) == want
+        else:
+            assert rc == 1  # ONO_E_SIZE
