@@ -323,7 +323,7 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
     u16 = lambda: torch.empty(n, dtype=torch.int16, device="cuda")  # noqa: E731
     out = {}
 
-    def timed(name, per_elem, make_set, launch, nsets):
+    def timed(name, kernel, per_elem, make_set, launch, nsets):
         sets = [make_set(i) for i in range(nsets)]
         torch.cuda.synchronize()
         for i in range(warmup):
@@ -337,34 +337,38 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
         torch.cuda.synchronize()
         us = a.elapsed_time(b) / steps * 1e3
         gbs = per_elem * n / (us * 1e-6) / 1e9
+        pmc = pmc_traffic(kernel, n)
         out[name] = {"bytes_per_launch": per_elem * n, "us_per_launch": round(us, 2), "achieved_gbs": round(gbs, 1),
-                     "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+                     "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
         del sets
         torch.cuda.empty_cache()
 
     def filled(i, r):
         return ono_amd.kernels.synth(f32(), SEED + i, r)
 
-    timed("acc_residual", 12, lambda i: (filled(i, 0), filled(i, 1)),
+    timed("acc_residual", "AccOp", 12, lambda i: (filled(i, 0), filled(i, 1)),
           lambda st: ono_amd.kernels.acc(st[0], st[1]), 6)
 
     def hop_set(i):
         h = u16()
         ono_amd.kernels.f16_encode(h, filled(i, 2))
         return (u16(), filled(i, 0), h)
-    timed("f16_add_encode_zero", 12, hop_set, lambda st: ono_amd.kernels.f16_add_encode_zero(*st), 8)
+    timed("f16_add_encode_zero", "AddEncodeZeroOp<unsigned short>", 12, hop_set,
+          lambda st: ono_amd.kernels.f16_add_encode_zero(*st), 8)
 
     def dec_set(i):
         h = u16()
         ono_amd.kernels.f16_encode(h, filled(i, 3))
         return (f32(), h)
-    timed("f16_decode_scale", 6, dec_set, lambda st: ono_amd.kernels.f16_decode_scale(st[0], st[1], 8.0), 12)
+    timed("f16_decode_scale", "DecodeScaleOp<unsigned short", 6, dec_set,
+          lambda st: ono_amd.kernels.f16_decode_scale(st[0], st[1], 8.0), 12)
 
-    for name, opt, per in (("gd", ono_amd.GradientDescent(0.1), 20),
-                           ("momentum", ono_amd.GradientDescentWithMomentum(0.1, 0.9), 28),
-                           ("adam", ono_amd.Adam(1e-3, 0.9, 0.999, 1e-8), 36)):
+    for name, kind, opt, per in (("gd", 0, ono_amd.GradientDescent(0.1), 20),
+                                 ("momentum", 1, ono_amd.GradientDescentWithMomentum(0.1, 0.9), 28),
+                                 ("adam", 2, ono_amd.Adam(1e-3, 0.9, 0.999, 1e-8), 36)):
         dev_opt = ono_amd.DeviceOptimizer(opt, n)
-        timed(f"consumer_{name}", per, lambda i: (filled(i, 4), filled(i, 5), f32()),
+        timed(f"consumer_{name}", f"OptOp<{kind},", per, lambda i: (filled(i, 4), filled(i, 5), f32()),
               lambda st, o=dev_opt: o.step(st[0], st[1], st[2]), 4)
         dev_opt.close()
     return {"workload": "the path's other kernels on 64 MiB f32 buckets (16 M elements), device-resident",

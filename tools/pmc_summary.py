@@ -43,7 +43,8 @@ def main() -> int:
     ap.add_argument("--write", required=True)
     ap.add_argument("--elems", type=int, required=True)
     ap.add_argument("--out", required=True)
-    ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp"])
+    ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp", "AccOp", "AddEncodeZeroOp",
+                                                  "DecodeScaleOp", "OptOp"])
     ap.add_argument("--algo-bytes-per-elem", type=float, default=12.0)
     ap.add_argument("--local-elems", type=int, default=16 << 20,
                     help="bucket length of bench.py's local_reduce (SumScaleOp<k> kernels: (k+1) x 4 B/elem)")
@@ -56,10 +57,19 @@ def main() -> int:
         f_kb, w_kb = statistics.median(fetch[name]), statistics.median(write[name])
         rd, wr = 2.0 * f_kb * 1024, w_kb * 1024
         m = re.search(r"SumScaleOp<(\d+),", name)
+        o = re.search(r"OptOp<(\d+),", name)
         if m:  # config 2: k inputs read, one output written
             elems, algo = a.local_elems, (int(m.group(1)) + 1) * 4.0 * a.local_elems
+        elif o:  # bench.py path_kernels consumer: GD / momentum / Adam, params copy written too
+            elems, algo = a.local_elems, {0: 20.0, 1: 28.0, 2: 36.0}.get(int(o.group(1)), 0.0) * a.local_elems
+        elif "AccOp" in name or "AddEncodeZeroOp" in name:  # path_kernels: 12 B/elem each
+            elems, algo = a.local_elems, 12.0 * a.local_elems
+        elif "DecodeScaleOp" in name:  # path_kernels: f16 in, f32 out
+            elems, algo = a.local_elems, 6.0 * a.local_elems
         else:
             elems, algo = a.elems, a.algo_bytes_per_elem * a.elems
+        if not algo:
+            continue
         kernels.append({
             "name": name, "elems": elems, "launches_fetch": len(fetch[name]), "launches_write": len(write[name]),
             "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
