@@ -11,7 +11,8 @@ on every rank over a freshly produced 256 MiB residual bucket already
 resident in HBM: grad = (sum over ranks of residual) / N, residual = 0.
   N = 1   the reference's n == 1 round: grad = residual, residual = 0 (no
           division, worker_ring.rs:166-171) — one fused gfx950 kernel.
-  N > 1   RCCL all-reduce over xGMI + one fused kernel (grad /= N, residual = 0).
+  N > 1   RCCL all-reduce over xGMI + one fused kernel (grad /= N, residual = 0);
+          --algo selects another schedule (hops, direct, xgmi).
 Every timed step consumes its own pre-generated residual bucket (W + K buckets
 of 256 MiB in HBM), so no step reduces an already-zeroed bucket.
 
@@ -21,13 +22,27 @@ per GPU is fixed).  algbw_gib_s (bucket / time) and busbw_gib_s
 (algbw * 2(N-1)/N) are reported beside it.
 
 Extra objects on the JSON line:
-  roofline      the step's dominant kernel, achieved vs peak, from HIP events
-                recorded on the launch stream inside the timed region
+  check         the last timed step against the exact average of all N inputs
+                (regenerated on every rank), residual all zero
+  roofline      the step's dominant kernel (N = 1: HBM) or exchange (N > 1: xGMI
+                links), achieved vs peak, from HIP events on the launch stream;
+                N > 1 also splits the step by phase (ono_ring_timing_phases)
   local_reduce  BASELINE config 2: the 64 MiB sum-and-scale kernel, k = 2, 4, 8
+  path_kernels  the path's other kernels (acc_residual, hop codec, consumer
+                optimizers) against the HBM roofline, PMC traffic beside
+  sparse_codec  the device top-k codec (drop / lift) on a 64 MiB gradient
   host_fed      PCIe-inclusive pull_grads from host buffers (registered / pageable)
+  ps_host_fed   the device store fed from host buffers (f32 and f16 wire payloads)
   tcp_edge      MI355X workers in a loopback-TCP ring speaking the reference's frames
   cpu_baseline  the reference-style CPU ring (TCP loopback, f16 wire, one pinned
                 core per worker) on the same host, rank 0 at N = 1 only
+  xgmi_coresident  N = 1: the xGMI peer-access schedule as 2 processes on the GPU
+  alt_schedules N > 1: the other exchange schedules (RCCL single all-reduce,
+                DIRECT f32/f16, HOPS f16, PS mode) behind a watchdog, and the
+                xGMI schedule (pull / push gather, both wires, PS step) in child
+                processes that are killed if they hang
+  size_sweep    N > 1: the main schedule from the config-1 bucket to 1 GiB
+Every informational object records its own failure instead of ending the line.
 """
 from __future__ import annotations
 
