@@ -472,6 +472,41 @@ def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
             "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
 
 
+def host_fed_n(ono_amd, ring, elems: int, ctl, world: int, rounds: int = 5) -> dict:
+    """N > 1: the end-to-end round a worker of the reference runs — host buckets
+    in (registered once, as the manager's Vec<f32>s live as long as it does),
+    H2D, the main schedule across the N GPUs, D2H, residual zeroed — timed
+    between barriers, max over ranks.  GiB/s of one rank's bucket.  Never `value`."""
+    import numpy as np
+
+    try:
+        res, grad = np.empty(elems, np.float32), np.empty(elems, np.float32)
+        src = np.random.default_rng(ctl.rank).standard_normal(elems, dtype=np.float32) * np.float32(0.01)
+        ring.register_host(res)
+        ring.register_host(grad)
+        ts = []
+        for r in range(rounds + 1):
+            res[:] = src
+            ctl.barrier()
+            t0 = time.perf_counter()
+            ring.pull_grads_host(res, grad)
+            t = ctl.max(time.perf_counter() - t0)
+            if r:
+                ts.append(t)
+        ring.unregister_host(res)
+        ring.unregister_host(grad)
+        t = sorted(ts)[len(ts) // 2]
+        piped = ring.wire == "f32" and ring.algo in ("auto", "allreduce")
+        return {"workload": f"pull_grads_host on {world} GPUs: registered host buckets of {elems * 4 >> 20} MiB per "
+                            "rank, " + ("H2D || all-reduce || D2H in 16 MiB chunks" if piped else
+                                        f"whole bucket: H2D, {ring.algo} round, D2H") + f" ({ring.wire} wire)",
+                "ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 2)}
+    except Exception as e:  # noqa: BLE001 — informational
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    finally:
+        ring.close()
+
+
 def ps_host_fed(ono_amd, elems: int, rounds: int = 3, workers: int = 2) -> dict:
     """The parameter server's own hot path (SURVEY §8(a) BlockingStore rows):
     gradients arrive in host memory from comms/, the device store accumulates
@@ -821,6 +856,8 @@ def main(argv=None) -> int:
                     "check": run.verify(wire)}
             except Exception as e:  # recorded, never fatal for the main line
                 line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        if world > 1 and not args.no_host_fed:  # the PCIe-inclusive round at N > 1 (north star)
+            line["host_fed"] = host_fed_n(ono_amd, new_ring(args.wire, args.algo), elems, ctl, world)
         if args.sweep_mib:  # BASELINE config 4: the bandwidth-vs-bucket-size curve, main schedule
             def sweep_ring(e):
                 r = new_ring(args.wire, args.algo, e)
