@@ -866,6 +866,8 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const bool reg = is_registered(r, res_host, bytes) && is_registered(r, grad_host, bytes);
     const size_t CH = host_chunk_elems();
 
+    if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // sub-round pipeline (ono_xgmi.cpp)
+        return xgmi_pull_grads_host(r, res_host, grad_host, CH);
     if (r->n > 1 && resolved_algo(r) != ONO_ALGO_ALLREDUCE) {  // whole-bucket exact schedules
         ONO_HIP(hipMemcpyAsync(r->residual, res_host, bytes, hipMemcpyHostToDevice, r->cstream));
         int rc = pull_grads_impl(r, r->residual, r->grad, r->cstream);

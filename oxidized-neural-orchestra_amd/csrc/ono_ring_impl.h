@@ -168,6 +168,7 @@ int timed(ono_ring *r, hipStream_t s, int kind, F &&f) {
 
 // xGMI peer-access schedule (ono_xgmi.cpp)
 int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s);
+int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems);
 int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t C, float *gshard, float *wshard,
                  const OptLaunch &opt, float *v, float *s_, hipStream_t s);
 void xgmi_abort(ono_ring *r);

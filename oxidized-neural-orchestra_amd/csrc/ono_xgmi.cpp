@@ -60,6 +60,7 @@ struct XgmiState {
     uint32_t *err = nullptr;          // host-mapped: set by a barrier that timed out
     uint32_t *err_dev = nullptr;
     uint64_t timeout_ticks = 0;
+    std::vector<hipEvent_t> ev;       // host-fed sub-round pipeline: H2D / round / D2H per sub-round
 };
 
 }  // namespace ono
@@ -171,12 +172,15 @@ uint32_t head_of(const void *a, size_t esz_a, const void *b, size_t esz_b) {
     return pa == pb ? (4u - pa) & 3u : kScalarOnly;
 }
 
+// One round over a piece of every chunk: chunk q contributes elements
+// [off[q], off[q] + len[q]) of the buckets (a whole round: off = the chunk
+// starts, len = the chunk lengths).  Every rank passes the same pieces, whose
+// starts keep the chunks' 4-element phases (the slots are phase-matched).
 template <class W>
-int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s) {
+int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s, const size_t *off, const size_t *plen) {
     XgmiState *x = r->xgmi;
     const int n = r->n, pos = r->pos, c = (pos + 1) % n;
-    const auto &off = r->off;
-    auto len = [&](int q) { return off[q + 1] - off[q]; };
+    auto len = [&](int q) { return plen[q]; };
     constexpr bool f16 = sizeof(W) == 2;
     if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
         return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
@@ -323,7 +327,69 @@ int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t
 int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
     int rc = ensure_connected(r, s);
     if (rc) return rc;
-    return r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, res, grad, s) : xgmi_round<float>(r, res, grad, s);
+    std::vector<size_t> len(r->n);
+    for (int q = 0; q < r->n; q++) len[q] = r->off[q + 1] - r->off[q];
+    return r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, res, grad, s, r->off.data(), len.data())
+                                   : xgmi_round<float>(r, res, grad, s, r->off.data(), len.data());
+}
+
+// Host-fed round (the reference's buckets are host memory): the round is cut
+// into sub-rounds, sub-round j taking elements [j sub, (j+1) sub) of every
+// chunk, so the H2D of sub-round j+1 (hstream), the xGMI round of j (cstream)
+// and the D2H of j-1 (dstream) overlap, as the RCCL form's chunked pipeline
+// does.  Every element still goes through the same chain on the same owner,
+// so the result is the whole-bucket round's bit for bit.  The host residual
+// is zeroed once its sub-round has reached HBM.
+int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems) {
+    int rc = ensure_connected(r, r->cstream);
+    if (rc) return rc;
+    XgmiState *x = r->xgmi;
+    const int n = r->n;
+    const size_t sub = std::max<size_t>(64, sub_elems / (size_t)n / 64 * 64);  // keeps the 4-element phases
+    const size_t S = (r->maxc + sub - 1) / sub;
+    while (x->ev.size() < 3 * S) {
+        hipEvent_t ev;
+        ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        x->ev.push_back(ev);
+    }
+    std::vector<size_t> st(n), ln(n);
+    auto piece = [&](size_t j) {
+        for (int q = 0; q < n; q++) {
+            const size_t L = r->off[q + 1] - r->off[q], lo = std::min(L, j * sub);
+            st[q] = r->off[q] + lo;
+            ln[q] = std::min(L - lo, sub);
+        }
+    };
+    auto zero_host = [&](size_t j) -> int {  // sub-round j has reached HBM: zero its host residual
+        ONO_HIP(hipEventSynchronize(x->ev[3 * j]));
+        piece(j);
+        for (int q = 0; q < n; q++)
+            if (ln[q]) memset(res_host + st[q], 0, ln[q] * sizeof(float));
+        return ONO_OK;
+    };
+    for (size_t j = 0; j < S; j++) {
+        piece(j);
+        for (int q = 0; q < n; q++)
+            if (ln[q])
+                ONO_HIP(hipMemcpyAsync(r->residual + st[q], res_host + st[q], ln[q] * sizeof(float),
+                                       hipMemcpyHostToDevice, r->hstream));
+        ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
+        ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
+        rc = r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
+                                     : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
+        if (rc) return rc;
+        ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
+        ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
+        for (int q = 0; q < n; q++)
+            if (ln[q])
+                ONO_HIP(hipMemcpyAsync(grad_host + st[q], r->grad + st[q], ln[q] * sizeof(float),
+                                       hipMemcpyDeviceToHost, r->dstream));
+        ONO_HIP(hipEventRecord(x->ev[3 * j + 2], r->dstream));
+        if (j > 0 && (rc = zero_host(j - 1))) return rc;
+    }
+    if ((rc = zero_host(S - 1))) return rc;
+    ONO_HIP(hipStreamSynchronize(r->dstream));
+    return ONO_OK;
 }
 
 // ono_ring_abort: barriers still spinning on the device give up (they poll
@@ -346,6 +412,7 @@ void xgmi_free(ono_ring *r) {
     }
     for (int q = 0; q < (int)x->peer.size(); q++)
         if (q != r->pos && x->peer[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
+    for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
     (void)hipFree(x->xbuf);
     if (x->err) (void)hipHostFree(x->err);
     delete x;

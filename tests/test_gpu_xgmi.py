@@ -29,9 +29,9 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull") -> list:
+def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull", **env_extra) -> list:
     port = _port()
-    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather)
+    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather, **env_extra)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), str(port),
                                json.dumps(cases)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for r in range(n)]
@@ -92,6 +92,18 @@ def test_xgmi_sharded_ps_vs_store_oracle(n):
     cases = [{"kind": "ps", "length": 100003, "opt": k} for k in ("gd", "momentum", "adam")]
     cases += [{"kind": "ps", "length": n + 1, "opt": "gd", "steps": 2}]
     check(run_ranks(n, cases))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_xgmi_host_fed_sub_round_pipeline(n):
+    """pull_grads_host on an xGMI ring: sub-rounds of every chunk flow H2D ->
+    round -> D2H on three streams (ONO_HOST_CHUNK_MIB=1 here, so a 2^20 + 3
+    bucket takes several sub-rounds); pageable and page-locked host buckets,
+    both wires, bit-exact with the whole-bucket oracle, host residual zeroed."""
+    cases = [{"length": (1 << 20) + 3, "wire": w, "form": f, "rounds": 2}
+             for w in ("f32", "f16") for f in ("host", "host_registered")]
+    cases += [{"length": 4 * n + 1, "wire": "f16", "form": "host", "rounds": 1}]
+    check(run_ranks(n, cases, ONO_HOST_CHUNK_MIB="1"))
 
 
 def test_xgmi_timing_phases():

@@ -51,7 +51,18 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
             gen = O.synth_special if case.get("special") else O.synth
             ins = [gen(length, SEED + 100 * rd + case.get("seed", 0), r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, wire)
-            if form == "owned":
+            if form in ("host", "host_registered"):  # host-fed: sub-round pipeline (pageable / page-locked)
+                res_h = np.ascontiguousarray(ins[rank]).copy()
+                grad_h = np.full(length, 7.0, np.float32)
+                if form == "host_registered":
+                    ring.register_host(res_h)
+                    ring.register_host(grad_h)
+                ring.pull_grads_host(res_h, grad_h)
+                got, res_after = grad_h, res_h
+                if form == "host_registered":
+                    ring.unregister_host(res_h)
+                    ring.unregister_host(grad_h)
+            elif form == "owned":
                 ring.residual.copy_(torch.from_numpy(ins[rank]))
                 ring.pull_grads()
                 torch.cuda.synchronize()
