@@ -496,10 +496,14 @@ def host_fed_n(ono_amd, ring, elems: int, ctl, world: int, rounds: int = 5) -> d
         ring.unregister_host(res)
         ring.unregister_host(grad)
         t = sorted(ts)[len(ts) // 2]
-        piped = ring.wire == "f32" and ring.algo in ("auto", "allreduce")
+        if ring.wire == "f32" and ring.algo in ("auto", "allreduce"):
+            how = "H2D || all-reduce || D2H in 16 MiB chunks"
+        elif ring.algo == "xgmi":
+            how = "H2D || xGMI round || D2H in sub-rounds (a slice of every chunk each)"
+        else:
+            how = f"whole bucket: H2D, {ring.algo} round, D2H"
         return {"workload": f"pull_grads_host on {world} GPUs: registered host buckets of {elems * 4 >> 20} MiB per "
-                            "rank, " + ("H2D || all-reduce || D2H in 16 MiB chunks" if piped else
-                                        f"whole bucket: H2D, {ring.algo} round, D2H") + f" ({ring.wire} wire)",
+                            f"rank, {how} ({ring.wire} wire)",
                 "ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 2)}
     except Exception as e:  # noqa: BLE001 — informational
         return {"error": f"{type(e).__name__}: {e}"[:300]}
