@@ -153,6 +153,23 @@ def test_hop_kernels(n, off):
         assert_bitexact(host(dout), e / np.float32(d) if d != 1.0 else e)
 
 
+@pytest.mark.parametrize("n", [65, 71, 4099, (1 << 20) + 3])
+@pytest.mark.parametrize("hoff,foff", [(0, 0), (1, 0), (0, 2), (5, 1), (7, 3)])
+def test_f16_codec_operand_phases(n, hoff, foff):
+    """encode / decode_scale with the f16 and f32 operands at equal and at
+    different 4-element phases (vector body vs scalar fallback)."""
+    x = O.synth(n, SEED, 2)
+    h = O.f16_encode(x)
+    out = dev(np.zeros(n, np.uint16), hoff)
+    K.f16_encode(out, dev(x, foff))
+    assert np.array_equal(host(out), h)
+    for d in (1.0, 3.0):
+        dout = dev(np.zeros(n, np.float32), foff)
+        K.f16_decode_scale(dout, dev(h, hoff), d)
+        e = O.f16_decode(h)
+        assert_bitexact(host(dout), e / np.float32(d) if d != 1.0 else e)
+
+
 def test_nan_inf_propagation():
     x = np.array([np.nan, -np.inf, np.inf, 1.0, -0.0], np.float32)
     x = np.concatenate([x, np.array([0x7FC00001, 0xFF812345, 0x7F800001], np.uint32).view(np.float32)])
