@@ -114,6 +114,15 @@ int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g
                     float threshold, void *stream);
 int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
                     void *stream);
+/* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame
+ * received into device memory); same results and errors as ono_sparse_lift.
+ * Both parse on the device: speculative record starts per 256-B segment,
+ * verified walks, scan, expand; the reference's sequential host parse runs
+ * only when the speculation is refuted or the stream is malformed.          */
+int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
+                        void *stream);
+/* lifts so far (this process) that took the sequential host parse        */
+size_t ono_sparse_lift_fallbacks(void);
 int ono_sparse_mask(float *g_dev, size_t n, float threshold, int zero_kept, void *stream);
 
 /* synthetic gradient bucket (SURVEY.md §8(d) distribution), bit-identical to

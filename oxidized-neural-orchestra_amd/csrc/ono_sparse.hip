@@ -15,13 +15,16 @@
 // wave shuffles + LDS; values written, run starts record U and F) -> headers,
 // back to back on the stream (the totals stay on the device; the host reads
 // them once, at the end, for the wire length).
-// Decoding walks the run headers on the host (a sequential parse, as in the
-// reference, over R records) and expands all values on the device.
+// Decoding is a parallel parse on the device (the record stream is a linked
+// list: each header gives the next one's position), see "Lift" below; the
+// reference's sequential parse on the host remains as the exact fallback and
+// the source of the reference's error messages.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -265,6 +268,138 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
     }
 }
 
+// ---------------------------------------------------------------- lift ----
+// The record stream is cut into segments of kSeg bytes.  sl_starts picks, per
+// segment, the first 2-byte position whose next kLook records are all
+// structurally valid (a speculative record start; segment 0 starts at the
+// true head, byte 8).  sl_walk follows the records from each start until it
+// lands on a later segment's start (marking it reached) or the end of the
+// buffer.  The speculation is checked, not trusted: the walks are exactly the
+// sequential parse iff every speculative start was reached and no walk failed
+// (records are a deterministic successor chain, so a walk that lands on a
+// start has joined the true chain there).  Otherwise `bad` is raised and the
+// host parses sequentially — also how malformed input gets the reference's
+// error messages.  A scan of the per-segment record counts and offset sums
+// then places every record (sl_table: run start in g, first value index), and
+// sl_expand writes the values.
+constexpr int kSeg = 256, kLook = 4;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t *b, size_t p) {  // p even, b 2-B aligned
+    const uint16_t *h = (const uint16_t *)(b + p);
+    return (uint32_t)h[0] | (uint32_t)h[1] << 16;
+}
+
+__global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes, uint64_t total, size_t S,
+                                                 uint32_t *p0) {
+    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
+    if (t >= S) return;
+    if (t == 0) { p0[0] = 8; return; }
+    const size_t lo = 8 + t * kSeg, hi = lo + kSeg < nbytes ? lo + kSeg : nbytes;
+    for (size_t p = lo; p < hi; p += 2) {
+        size_t q = p;
+        uint64_t acc = 0;
+        bool ok = true;
+        for (int k = 0; k < kLook && q != nbytes; k++) {
+            if (nbytes - q < 8) { ok = false; break; }
+            const uint32_t off = ld32(b, q), len = ld32(b, q + 4);
+            // a start whose records run past the stream is no start; nor is
+            // one with a run of >= 2^16 values: a header read 2 B off its true
+            // position takes a half of the run length as the high half of its
+            // own (so >= 2^16), and such a jump lands on a true header about
+            // one time in five — after which every look-ahead record is valid.
+            // Long true runs only lose their segment a start (the walk from
+            // the previous start covers them).
+            // Runs are maximal in grad_drop's output, so a record after the
+            // first is >= 1 value past the previous run: offset 0 is no start
+            // either (zero-filled payload reads as offset 0).
+            if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
+            acc += (uint64_t)off + len;
+            if (acc > total) { ok = false; break; }
+            q += 8 + 2 * (size_t)len;
+        }
+        if (ok) { p0[t] = (uint32_t)p; return; }
+    }
+    p0[t] = kNone;
+}
+
+__global__ __launch_bounds__(kSB) void sl_walk(const uint8_t *b, size_t nbytes, uint64_t total, size_t S,
+                                               const uint32_t *p0, uint32_t *reached, uint32_t *nrec, uint32_t *gsum,
+                                               uint32_t *bad) {
+    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
+    if (t >= S) return;
+    uint32_t cnt = 0;
+    uint64_t sum = 0;
+    if (p0[t] != kNone) {
+        size_t pos = p0[t];
+        const size_t segend = 8 + (t + 1) * kSeg;
+        for (;;) {
+            if (pos == nbytes) break;  // the end of the stream
+            if (pos >= segend) {
+                const size_t u = (pos - 8) / kSeg;
+                const uint32_t pu = u < S ? p0[u] : kNone;
+                if (pu != kNone && pos == pu) { reached[u] = 1; break; }
+                if (pu != kNone && pos > pu) { *bad = 1; break; }  // stepped over a start: it was not a record
+            }
+            if (nbytes - pos < 8) { *bad = 1; break; }
+            const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
+            if ((nbytes - pos - 8) / 2 < len) { *bad = 1; break; }
+            sum += (uint64_t)off + len;
+            if (sum > total) { *bad = 1; break; }
+            cnt++;
+            pos += 8 + 2 * (size_t)len;
+        }
+    }
+    nrec[t] = cnt;
+    gsum[t] = (uint32_t)sum;
+}
+
+// record j: start[j] = its first element in g, cumF[j] = values before it
+// (the header sits at byte 8 + 8 j + 2 cumF[j]).  nrec / gsum: exclusive scans.
+__global__ __launch_bounds__(kSB) void sl_table(const uint8_t *b, uint64_t total, size_t S, const uint32_t *p0,
+                                                const uint32_t *reached, const uint32_t *nrec, const uint32_t *gsum,
+                                                const uint64_t *totals, uint32_t *start, uint32_t *cumF,
+                                                uint32_t *bad) {
+    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
+    if (t >= S || p0[t] == kNone) return;
+    if (t > 0 && !reached[t]) { *bad = 1; return; }  // a speculative start off the chain
+    size_t j = nrec[t];
+    const size_t jend = t + 1 < S ? nrec[t + 1] : (size_t)totals[0];
+    uint64_t gi = gsum[t];
+    size_t pos = p0[t];
+    for (; j < jend; j++) {
+        const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
+        gi += off;
+        if (gi > total || total - gi < len) { *bad = 1; return; }  // protocol.rs:127-129 (host reports it)
+        start[j] = (uint32_t)gi;
+        cumF[j] = (uint32_t)((pos - 8 - 8 * j) / 2);
+        gi += len;
+        pos += 8 + 2 * (size_t)len;
+    }
+}
+
+// value v belongs to record j with cumF[j] <= v < cumF[j+1]; it sits at byte
+// 16 + 8 j + 2 v.  F = (nbytes - 8 - 8 R) / 2 values in all.
+__global__ __launch_bounds__(kSB) void sl_expand(float *g, const uint8_t *b, size_t nbytes, const uint32_t *start,
+                                                 const uint32_t *cumF, const uint64_t *totals, const uint32_t *bad) {
+    if (*bad) return;
+    const size_t R = totals[0];
+    if (R == 0) return;
+    const size_t F = (nbytes - 8 - 8 * R) / 2;
+    const size_t stride = (size_t)gridDim.x * kSB;
+    for (size_t v = (size_t)blockIdx.x * kSB + threadIdx.x; v < F; v += stride) {
+        size_t lo = 0, hi = R;  // largest j with cumF[j] <= v
+        while (hi - lo > 1) {
+            const size_t mid = (lo + hi) / 2;
+            if (cumF[mid] <= v) lo = mid; else hi = mid;
+        }
+        const uint16_t h = *(const uint16_t *)(b + 16 + 8 * lo + 2 * v);
+        g[start[lo] + (v - cumF[lo])] = from_f16_sp(h);
+    }
+}
+
+__global__ void sl_flag_out(const uint32_t *bad, uint64_t *host_word) { host_word[0] = *bad; }
+
 // the totals into the host-mapped words (the exact-size path of a small buffer)
 __global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
     host_tot[0] = totals[0];
@@ -308,6 +443,136 @@ int scratch_for(size_t ntiles, size_t maxruns, Scratch **out) {
     }
     *out = &sc;
     return ONO_OK;
+}
+
+struct LiftScratch {
+    size_t seg_cap = 0, rec_cap = 0, buf_cap = 0;
+    uint32_t *seg = nullptr, *rec = nullptr, *bad = nullptr;
+    uint8_t *buf = nullptr;
+    uint64_t *totals = nullptr, *host_word = nullptr, *host_word_dev = nullptr;
+};
+LiftScratch g_lift[64];
+std::atomic<size_t> g_lift_fallbacks{0};
+
+template <class T> int grow(T **p, size_t &cap, size_t want) {
+    if (want <= cap) return ONO_OK;
+    (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    ONO_HIP(hipMalloc((void **)p, want * sizeof(T)));
+    cap = want;
+    return ONO_OK;
+}
+
+// The reference's sequential parse (protocol.rs:96-144) of a host copy of the
+// stream: the run table, or the reference's error.
+int lift_parse_host(const uint8_t *buf, size_t nbytes, uint64_t total, std::vector<uint64_t> &start,
+                    std::vector<uint64_t> &cumF) {
+    size_t gi = 0, bi = 8, F = 0;
+    while (bi < nbytes) {
+        if (nbytes - bi < 4) return set_error(ONO_E_PROTO, "Missing index bytes at grad lift");
+        uint32_t off = buf[bi] | buf[bi + 1] << 8 | buf[bi + 2] << 16 | (uint32_t)buf[bi + 3] << 24;
+        gi += off;
+        bi += 4;
+        if (nbytes - bi < 4) return set_error(ONO_E_PROTO, "Missing chunk length bytes at grad lift");
+        uint32_t len = buf[bi] | buf[bi + 1] << 8 | buf[bi + 2] << 16 | (uint32_t)buf[bi + 3] << 24;
+        bi += 4;
+        if (gi > total || total - gi < len) return set_error(ONO_E_PROTO, "Gradient chunk exceeds target vector bounds");
+        if ((nbytes - bi) / 2 < len) return set_error(ONO_E_PROTO, "Truncated float data");
+        start.push_back(gi);  // zero-length records stay in the table: the record
+        cumF.push_back(F);    // index must remain the header index (byte math in sp_expand)
+        F += len;
+        bi += 2 * (size_t)len;
+        gi += len;
+    }
+    return ONO_OK;
+}
+
+// Sequential fallback: host parse, tables up, expand (the original lift).
+int lift_host_path(float *g, const uint8_t *hbuf, const uint8_t *dbuf, size_t nbytes, uint64_t total,
+                   hipStream_t s) {
+    std::vector<uint64_t> start, cumF;
+    int rc = lift_parse_host(hbuf, nbytes, total, start, cumF);
+    if (rc) return rc;
+    const size_t R = start.size(), F = (nbytes - 8 - 8 * R) / 2;
+    if (F == 0) return ONO_OK;
+    uint64_t *dtab = nullptr;
+    ONO_HIP(hipMallocAsync((void **)&dtab, 2 * R * sizeof(uint64_t), s));
+    ONO_HIP(hipMemcpyAsync(dtab, start.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    ONO_HIP(hipMemcpyAsync(dtab + R, cumF.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(sp_expand, dim3((unsigned)((F + kSB - 1) / kSB)), dim3(kSB), 0, s, g, dbuf, dtab, dtab + R, R, F);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host vectors are released on return
+    (void)hipFreeAsync(dtab, s);
+    if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
+    return ONO_OK;
+}
+
+// Device lift of a device-resident stream.  hbuf: a host copy when the caller
+// has one (the fallback then needs no download), else nullptr.
+int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, const uint8_t *hbuf, size_t nbytes,
+                uint64_t total, hipStream_t s) {
+    if (total > cap) return set_error(ONO_E_SIZE, "sparse gradient of %llu values, buffer of %zu",
+                                      (unsigned long long)total, cap);
+    *out_len = total;
+    if (total) ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));  // grad.fill(0); resize(total, 0)
+    if (nbytes == 8) return ONO_OK;
+    std::vector<uint8_t> copy;
+    auto host_bytes = [&]() -> const uint8_t * {
+        if (hbuf) return hbuf;
+        copy.resize(nbytes);
+        if (hipMemcpyAsync(copy.data(), dbuf, nbytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return nullptr;
+        return copy.data();
+    };
+    // u32 record positions, starts and value counts: streams under 4 GiB,
+    // gradients under 2^32 values; anything larger parses on the host
+    if (nbytes >= 0xFFFFFFF0ull || total >= 0xFFFFFFFFull || ((uintptr_t)dbuf & 1)) {
+        const uint8_t *hb = host_bytes();
+        if (!hb) return set_error(ONO_E_HIP, "sparse lift: download of the stream failed");
+        return lift_host_path(g, hb, dbuf, nbytes, total, s);
+    }
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
+    LiftScratch &L = g_lift[dev];
+    const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, Rmax = (nbytes - 8) / 8;
+    if (!L.totals) {
+        ONO_HIP(hipMalloc((void **)&L.totals, 2 * sizeof(uint64_t)));
+        ONO_HIP(hipMalloc((void **)&L.bad, sizeof(uint32_t)));
+        ONO_HIP(hipHostMalloc((void **)&L.host_word, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostGetDevicePointer((void **)&L.host_word_dev, L.host_word, 0));
+    }
+    int rc = grow(&L.seg, L.seg_cap, 4 * S + 4);
+    if (!rc) rc = grow(&L.rec, L.rec_cap, 2 * Rmax + 2);
+    if (rc) return rc;
+    uint32_t *p0 = L.seg, *reached = L.seg + S, *nrec = L.seg + 2 * S, *gsum = L.seg + 3 * S;
+    uint32_t *start = L.rec, *cumF = L.rec + Rmax + 1;
+    volatile uint64_t *word = L.host_word;
+    *word = 1;
+    const unsigned sb = (unsigned)((S + kSB - 1) / kSB);
+    ONO_HIP(hipMemsetAsync(L.bad, 0, sizeof(uint32_t), s));
+    ONO_HIP(hipMemsetAsync(reached, 0, S * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(sl_starts, dim3(sb), dim3(kSB), 0, s, dbuf, nbytes, total, S, p0);
+    hipLaunchKernelGGL(sl_walk, dim3(sb), dim3(kSB), 0, s, dbuf, nbytes, total, S, p0, reached, nrec, gsum, L.bad);
+    hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, nrec, gsum, S, L.totals);
+    hipLaunchKernelGGL(sl_table, dim3(sb), dim3(kSB), 0, s, dbuf, total, S, p0, reached, nrec, gsum, L.totals, start,
+                       cumF, L.bad);
+    const size_t Fmax = (nbytes - 8) / 2;
+    const unsigned eb = (unsigned)std::min<size_t>(4096, (Fmax + kSB - 1) / kSB);
+    hipLaunchKernelGGL(sl_expand, dim3(eb), dim3(kSB), 0, s, g, dbuf, nbytes, start, cumF, L.totals, L.bad);
+    hipLaunchKernelGGL(sl_flag_out, dim3(1), dim3(1), 0, s, L.bad, L.host_word_dev);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
+    if (*word == 0) return ONO_OK;
+    // speculation missed or the stream is malformed: the sequential parse decides
+    g_lift_fallbacks.fetch_add(1);
+    ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));
+    const uint8_t *hb = host_bytes();
+    if (!hb) return set_error(ONO_E_HIP, "sparse lift: download of the stream failed");
+    return lift_host_path(g, hb, dbuf, nbytes, total, s);
 }
 
 }  // namespace
@@ -369,49 +634,36 @@ int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, si
 
 int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, size_t nbytes, void *stream) {
     if (!out_len || (!buf && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
-    // protocol.rs:96-144, the sequential parse of the record headers (host)
+    // protocol.rs:96-144: the total first, then the records
     if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
     uint64_t total = 0;
     for (int q = 0; q < 8; q++) total |= (uint64_t)buf[q] << (8 * q);
     if (total > cap) return set_error(ONO_E_SIZE, "sparse gradient of %llu values, buffer of %zu",
                                       (unsigned long long)total, cap);
-    std::vector<uint64_t> start, cumF;
-    size_t gi = 0, bi = 8, F = 0;
-    while (bi < nbytes) {
-        if (nbytes - bi < 4) return set_error(ONO_E_PROTO, "Missing index bytes at grad lift");
-        uint32_t off = buf[bi] | buf[bi + 1] << 8 | buf[bi + 2] << 16 | (uint32_t)buf[bi + 3] << 24;
-        gi += off;
-        bi += 4;
-        if (nbytes - bi < 4) return set_error(ONO_E_PROTO, "Missing chunk length bytes at grad lift");
-        uint32_t len = buf[bi] | buf[bi + 1] << 8 | buf[bi + 2] << 16 | (uint32_t)buf[bi + 3] << 24;
-        bi += 4;
-        if (gi > total || total - gi < len) return set_error(ONO_E_PROTO, "Gradient chunk exceeds target vector bounds");
-        if ((nbytes - bi) / 2 < len) return set_error(ONO_E_PROTO, "Truncated float data");
-        start.push_back(gi);  // zero-length records stay in the table: the record
-        cumF.push_back(F);    // index must remain the header index (byte math in sp_expand)
-        F += len;
-        bi += 2 * (size_t)len;
-        gi += len;
-    }
-    *out_len = total;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (total) ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));  // grad.fill(0); resize(total, 0)
-    if (F == 0) return ONO_OK;
-    const size_t R = start.size();
-    uint8_t *dbuf = nullptr;
-    uint64_t *dtab = nullptr;
-    ONO_HIP(hipMallocAsync((void **)&dbuf, nbytes, s));
-    ONO_HIP(hipMallocAsync((void **)&dtab, 2 * R * sizeof(uint64_t), s));
-    ONO_HIP(hipMemcpyAsync(dbuf, buf, nbytes, hipMemcpyHostToDevice, s));
-    ONO_HIP(hipMemcpyAsync(dtab, start.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    ONO_HIP(hipMemcpyAsync(dtab + R, cumF.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(sp_expand, dim3((unsigned)((F + kSB - 1) / kSB)), dim3(kSB), 0, s, g, dbuf, dtab, dtab + R, R, F);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host vectors and buffer are released on return
-    (void)hipFreeAsync(dbuf, s);
-    (void)hipFreeAsync(dtab, s);
-    if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
-    return ONO_OK;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
+    LiftScratch &L = g_lift[dev];
+    int rc = grow(&L.buf, L.buf_cap, nbytes);
+    if (rc) return rc;
+    ONO_HIP(hipMemcpyAsync(L.buf, buf, nbytes, hipMemcpyHostToDevice, s));
+    return lift_device(g, cap, out_len, L.buf, buf, nbytes, total, s);
+}
+
+size_t ono_sparse_lift_fallbacks(void) { return g_lift_fallbacks.load(); }
+
+int ono_sparse_lift_dev(float *g, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
+                        void *stream) {
+    if (!out_len || (!buf_dev && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
+    if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    uint64_t total = 0;
+    ONO_HIP(hipMemcpyAsync(&total, buf_dev, 8, hipMemcpyDeviceToHost, s));
+    ONO_HIP(hipStreamSynchronize(s));
+    return lift_device(g, cap, out_len, buf_dev, nullptr, nbytes, total, s);
 }
 
 int ono_sparse_mask(float *g, size_t n, float threshold, int zero_kept, void *stream) {

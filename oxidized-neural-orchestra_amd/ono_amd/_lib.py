@@ -95,6 +95,8 @@ _SIGS = {
     "ono_sparse_max_bytes": (_sz, [_sz]),
     "ono_sparse_drop": (_i, [_vp, _sz, C.POINTER(C.c_size_t), _fp, _sz, C.c_float, _vp]),
     "ono_sparse_lift": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
+    "ono_sparse_lift_dev": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
+    "ono_sparse_lift_fallbacks": (_sz, []),
     "ono_sparse_mask": (_i, [_fp, _sz, C.c_float, _i, _vp]),
     "ono_ring_unique_id": (_i, [C.c_char_p]),
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),

@@ -44,7 +44,10 @@ def grad_drop(g: torch.Tensor, threshold: float, stream=None) -> bytes:
     return bytes(buf[: nb.value].cpu().numpy())
 
 
-def grad_lift(buf: bytes, cap: int | None = None, device: str = "cuda", stream=None) -> torch.Tensor:
+def grad_lift(buf, cap: int | None = None, device: str = "cuda", stream=None) -> torch.Tensor:
+    """buf: the wire bytes (host) or a device uint8 tensor holding them."""
+    if isinstance(buf, torch.Tensor) and buf.is_cuda:
+        return grad_lift_dev(buf, cap, stream)
     b = np.frombuffer(bytes(buf), dtype=np.uint8)
     total = int.from_bytes(bytes(buf[:8]), "little") if len(buf) >= 8 else 0
     cap = total if cap is None else cap
@@ -53,6 +56,30 @@ def grad_lift(buf: bytes, cap: int | None = None, device: str = "cuda", stream=N
     call("ono_sparse_lift", kernels.f32_ptr(out), cap, C.byref(ln), b.ctypes.data if b.size else None, b.size,
          kernels.stream_handle(stream))
     torch.cuda.synchronize()
+    return out[: ln.value]
+
+
+def grad_drop_dev(g: torch.Tensor, threshold: float, stream=None) -> torch.Tensor:
+    """grad_drop leaving the wire bytes in HBM (a uint8 device tensor)."""
+    n = g.numel()
+    cap = lib().ono_sparse_max_bytes(n)
+    buf = torch.empty(cap + 8, dtype=torch.uint8, device=g.device)
+    nb = C.c_size_t(0)
+    call("ono_sparse_drop", buf.data_ptr(), cap, C.byref(nb), kernels.f32_ptr(g), n, float(threshold),
+         kernels.stream_handle(stream))
+    return buf[: nb.value]
+
+
+def grad_lift_dev(buf: torch.Tensor, cap: int | None = None, stream=None) -> torch.Tensor:
+    """grad_lift of wire bytes already in HBM (ono_sparse_lift_dev)."""
+    assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+    nb = buf.numel()
+    if cap is None:
+        cap = int.from_bytes(bytes(buf[:8].cpu().numpy()), "little") if nb >= 8 else 0
+    out = torch.empty(max(cap, 1), dtype=torch.float32, device=buf.device)
+    ln = C.c_size_t(0)
+    call("ono_sparse_lift_dev", kernels.f32_ptr(out), cap, C.byref(ln), buf.data_ptr() if nb else None, nb,
+         kernels.stream_handle(stream))
     return out[: ln.value]
 
 

@@ -120,3 +120,108 @@ def test_drop_exact_size_buffer_and_unaligned_input(offset):
             assert bytes(buf[: nb.value].cpu().numpy()) == want
         else:
             assert rc == 1  # ONO_E_SIZE
+
+
+# ----------------------------------------------------------- device lift ----
+def to_dev(b: bytes) -> torch.Tensor:
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda() if b else torch.empty(0, dtype=torch.uint8,
+                                                                                            device="cuda")
+
+
+def random_stream(rng, nrec: int, max_off: int, max_len: int, payload: str, min_off: int = 0) -> bytes:
+    """A valid sparse stream of nrec records built directly (not by grad_drop):
+    zero-length records, zero offsets and payloads chosen to look like record
+    headers ("zeros", "small": f16 bit patterns < 0x40) stress the speculative
+    record starts; "random": every f16 bit pattern."""
+    offs = rng.integers(min_off, max_off + 1, nrec)
+    lens = rng.integers(0, max_len + 1, nrec)
+    total = int(offs.sum() + lens.sum()) + int(rng.integers(0, 5))
+    parts = [np.uint64(total).tobytes()]
+    for o, ln in zip(offs, lens):
+        parts.append(np.array([o, ln], np.uint32).tobytes())
+        if payload == "zeros":
+            v = np.zeros(ln, np.uint16)
+        elif payload == "small":
+            v = rng.integers(0, 0x40, ln).astype(np.uint16)
+        else:
+            v = rng.integers(0, 1 << 16, ln).astype(np.uint16)
+        parts.append(v.tobytes())
+    return b"".join(parts)
+
+
+def test_lift_dev_kats():
+    assert SP.grad_lift(to_dev(KAT_BUF)).cpu().tolist() == [1.0, -1.0, 0.0, 2.0]
+    short = bytes([3, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 2, 0, 0, 0, 0, 60, 0, 188])
+    assert SP.grad_lift(to_dev(short)).cpu().tolist() == [0.0, 1.0, -1.0]
+    assert SP.grad_lift(to_dev(bytes(8))).numel() == 0
+
+
+@pytest.mark.parametrize("n", [2049, 65536 + 17, (1 << 20) + 5, 1 << 24])
+@pytest.mark.parametrize("r", [0.0, 0.5, 0.9, 0.999])
+def test_drop_lift_device_resident(n, r):
+    """drop -> lift with the stream never leaving HBM (ono_sparse_lift_dev), and
+    the host-stream lift over the same bytes: both equal the oracle's lift."""
+    g = O.synth(n, SEED + 23, 3)
+    t = float(np.quantile(np.abs(g), r)) if r > 0 else 0.0
+    t = max(t, 6.103515625e-05) if r > 0 else 0.0
+    wire = SP.grad_drop_dev(dev(g), t)
+    host_bytes = bytes(wire.cpu().numpy())
+    want = O.grad_lift(host_bytes, cap=n)
+    assert_bitexact(SP.grad_lift_dev(wire, n).cpu().numpy(), want)
+    assert_bitexact(SP.grad_lift(host_bytes, cap=n).cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("payload", ["random", "small", "zeros"])
+@pytest.mark.parametrize("nrec,max_off,max_len", [(1, 3, 5), (37, 2, 3), (5000, 4, 40), (200000, 1, 6),
+                                                  (3000, 0, 2000)])
+def test_lift_dev_random_streams(payload, nrec, max_off, max_len):
+    """Streams written directly (arbitrary offsets/lengths, zero-length records,
+    header-like payloads): the device parse equals the oracle whether its
+    speculative record starts hold or are refuted (sequential fallback)."""
+    rng = np.random.default_rng(nrec * 7 + max_len + len(payload))
+    b = random_stream(rng, nrec, max_off, max_len, payload)
+    total = int.from_bytes(b[:8], "little")
+    want = O.grad_lift(b, cap=max(total, 1))
+    assert_bitexact(SP.grad_lift_dev(to_dev(b), total).cpu().numpy(), want)
+    assert_bitexact(SP.grad_lift(b, cap=total).cpu().numpy(), want)
+
+
+def test_lift_dev_typical_stream_takes_the_parallel_parse():
+    """The bench's stream (90th-percentile threshold, 16 M values) must not fall
+    back to the sequential parse; neither must a drop-like stream (offsets >= 1)
+    with random f16 payload."""
+    L = ono_amd.lib()
+    g = ono_amd.kernels.synth(torch.empty(1 << 24, dtype=torch.float32, device="cuda"), SEED, 7)
+    t = float(torch.quantile(g[: 1 << 20].abs().float(), 0.9).item())
+    wire = SP.grad_drop_dev(g, t)
+    before = L.ono_sparse_lift_fallbacks()
+    back = SP.grad_lift_dev(wire, g.numel())
+    b2 = random_stream(np.random.default_rng(5), 100000, 3, 30, "random", min_off=1)  # drop-like: runs maximal
+    SP.grad_lift_dev(to_dev(b2), int.from_bytes(b2[:8], "little"))
+    assert L.ono_sparse_lift_fallbacks() == before
+    keep = g.abs() >= t
+    torch.cuda.synchronize()
+    ref = torch.where(keep, g.half().float(), torch.zeros_like(g))  # RNE f16 of the kept values
+    assert torch.equal(back.view(torch.int32), ref.view(torch.int32))
+
+
+@pytest.mark.parametrize("buf,msg", [
+    (bytes([4, 0, 0, 0, 0, 0, 0, 0, 0, 0]), "Missing index bytes"),
+    (bytes([4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0]), "Missing chunk length bytes"),
+    (bytes([4, 0, 0, 0, 0, 0, 0, 0, 3, 0, 0, 0, 2, 0, 0, 0, 0, 60, 0, 188]), "exceeds target vector bounds"),
+    (bytes([4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0, 0, 0, 0, 60]), "Truncated float data"),
+])
+def test_lift_dev_errors(buf, msg):
+    with pytest.raises(ono_amd.InvalidWorkerEvent, match=msg):
+        SP.grad_lift_dev(to_dev(buf), 16)
+
+
+def test_lift_dev_error_deep_in_a_long_stream():
+    """A bounds error in record 150000 of a valid-looking stream: the parallel
+    parse refutes itself and the sequential parse reports the reference's error."""
+    rng = np.random.default_rng(11)
+    b = bytearray(random_stream(rng, 200000, 2, 4, "random"))
+    total = int.from_bytes(b[:8], "little")
+    b[:8] = np.uint64(total // 2).tobytes()
+    with pytest.raises(ono_amd.InvalidWorkerEvent, match="exceeds target vector bounds"):
+        SP.grad_lift_dev(to_dev(bytes(b)), total)
