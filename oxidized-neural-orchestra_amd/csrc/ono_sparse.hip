@@ -239,7 +239,8 @@ __global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint
     }
 }
 
-// Lift: value v belongs to run j with cumF[j] <= v < cumF[j+1] (binary search);
+// Fallback lift (after a host parse): value v belongs to run j with
+// cumF[j] <= v < cumF[j+1] (binary search);
 // it sits at byte 16 + 8 j + 2 v and lands at start[j] + (v - cumF[j]).
 __global__ __launch_bounds__(kSB) void sp_expand(float *g, const uint8_t *buf, const uint64_t *start,
                                                  const uint64_t *cumF, size_t R, size_t F) {
@@ -271,29 +272,62 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 // ---------------------------------------------------------------- lift ----
 // The record stream is cut into segments of kSeg bytes.  sl_starts picks, per
 // segment, the first 2-byte position whose next kLook records are all
-// structurally valid (a speculative record start; segment 0 starts at the
-// true head, byte 8).  sl_walk follows the records from each start until it
-// lands on a later segment's start (marking it reached) or the end of the
-// buffer.  The speculation is checked, not trusted: the walks are exactly the
-// sequential parse iff every speculative start was reached and no walk failed
-// (records are a deterministic successor chain, so a walk that lands on a
-// start has joined the true chain there).  Otherwise `bad` is raised and the
-// host parses sequentially — also how malformed input gets the reference's
-// error messages.  A scan of the per-segment record counts and offset sums
-// then places every record (sl_table: run start in g, first value index), and
-// sl_expand writes the values.
-constexpr int kSeg = 256, kLook = 4;
+// plausible (a speculative record start; segment 0 starts at the true head,
+// byte 8).  sl_walk follows the records from each start until it lands on a
+// later segment's start (marking it reached) or the end of the stream.  The
+// speculation is checked, not trusted: the walks are exactly the sequential
+// parse iff every speculative start was reached and no walk failed (records
+// form a successor chain, so a walk that lands on a start has joined the true
+// chain there; the earliest start off the chain can only be reached from the
+// chain, so it stays unreached).  Otherwise `bad` is raised and the host
+// parses sequentially — also how malformed input gets the reference's error
+// messages.  Each walk's sum of (offset + length) is scanned (block-wide in
+// sl_walk, across blocks by sp_scan_tiles) to give the element index its
+// records start at; sl_place walks again and writes the values of short runs
+// itself, and queues runs longer than kShort for sl_long (one workgroup per
+// run).
+constexpr int kSeg = 128, kLook = 4, kShort = 16;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *b, size_t p) {  // p even, b 2-B aligned
     const uint16_t *h = (const uint16_t *)(b + p);
     return (uint32_t)h[0] | (uint32_t)h[1] << 16;
 }
+__device__ __forceinline__ uint16_t ld16(const uint8_t *b, size_t p) { return *(const uint16_t *)(b + p); }
 
-__global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes, uint64_t total, size_t S,
-                                                 uint32_t *p0) {
+// g[0, total) = 0 (grad.fill(0); resize(total, 0)) with total read from the
+// stream's first 8 bytes on the device, so the host need not wait for it.
+// tot[0] = total; flags: [0] bad, [1] queued long runs, [2] total > cap (then
+// nothing is written and every later kernel stands down through flags[0]).
+__global__ __launch_bounds__(kSB) void sl_zero(float *g, const uint8_t *b, size_t cap, int vec, uint64_t *tot,
+                                               uint32_t *flags, uint64_t *host_word) {
+    uint64_t total = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) total |= (uint64_t)ld16(b, 2 * q) << (16 * q);
+    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x, stride = (size_t)gridDim.x * kSB;
+    if (t == 0) {
+        tot[0] = total;
+        host_word[1] = total;
+        flags[0] = total > cap ? 1u : 0u;
+        flags[1] = 0;
+        flags[2] = total > cap ? 1u : 0u;
+    }
+    if (total > cap) return;
+    if (vec) {
+        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (size_t i = t; i < total / 4; i += stride) *(f4s *)(g + 4 * i) = z;
+        for (size_t i = 4 * (total / 4) + t; i < total; i += stride) g[i] = 0.0f;
+    } else {
+        for (size_t i = t; i < total; i += stride) g[i] = 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes, const uint64_t *tot, size_t S,
+                                                 uint32_t *p0, uint32_t *reached) {
     const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
     if (t >= S) return;
+    const uint64_t total = tot[0];
+    reached[t] = 0;
     if (t == 0) { p0[0] = 8; return; }
     const size_t lo = 8 + t * kSeg, hi = lo + kSeg < nbytes ? lo + kSeg : nbytes;
     for (size_t p = lo; p < hi; p += 2) {
@@ -303,16 +337,15 @@ __global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes
         for (int k = 0; k < kLook && q != nbytes; k++) {
             if (nbytes - q < 8) { ok = false; break; }
             const uint32_t off = ld32(b, q), len = ld32(b, q + 4);
-            // a start whose records run past the stream is no start; nor is
-            // one with a run of >= 2^16 values: a header read 2 B off its true
+            // A start whose records run past the stream is no start; nor is one
+            // with a run of >= 2^16 values: a header read 2 B off its true
             // position takes a half of the run length as the high half of its
-            // own (so >= 2^16), and such a jump lands on a true header about
-            // one time in five — after which every look-ahead record is valid.
-            // Long true runs only lose their segment a start (the walk from
-            // the previous start covers them).
-            // Runs are maximal in grad_drop's output, so a record after the
-            // first is >= 1 value past the previous run: offset 0 is no start
-            // either (zero-filled payload reads as offset 0).
+            // own (so >= 2^16), and such a jump lands on a true header about one
+            // time in five, after which every look-ahead record is valid.  Runs
+            // are maximal in grad_drop's output, so a record after the first is
+            // >= 1 value past the previous run: offset 0 is no start either
+            // (zero-filled payload reads as offset 0).  A true start refused
+            // here only leaves its segment to the previous walk.
             if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
             acc += (uint64_t)off + len;
             if (acc > total) { ok = false; break; }
@@ -323,14 +356,15 @@ __global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes
     p0[t] = kNone;
 }
 
-__global__ __launch_bounds__(kSB) void sl_walk(const uint8_t *b, size_t nbytes, uint64_t total, size_t S,
-                                               const uint32_t *p0, uint32_t *reached, uint32_t *nrec, uint32_t *gsum,
-                                               uint32_t *bad) {
+// per segment: gsum[t] = sum of (offset + length) over its records;
+// per block: bsum[block] = the block's total (scanned afterwards)
+__global__ __launch_bounds__(kSB) void sl_walk(const uint8_t *b, size_t nbytes, const uint64_t *tot, size_t S,
+                                               const uint32_t *p0, uint32_t *reached, uint32_t *gsum, uint32_t *bsum,
+                                               uint32_t *bscratch, uint32_t *flags) {
     const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
-    if (t >= S) return;
-    uint32_t cnt = 0;
+    const uint64_t total = tot[0];
     uint64_t sum = 0;
-    if (p0[t] != kNone) {
+    if (t < S && p0[t] != kNone) {
         size_t pos = p0[t];
         const size_t segend = 8 + (t + 1) * kSeg;
         for (;;) {
@@ -339,66 +373,84 @@ __global__ __launch_bounds__(kSB) void sl_walk(const uint8_t *b, size_t nbytes, 
                 const size_t u = (pos - 8) / kSeg;
                 const uint32_t pu = u < S ? p0[u] : kNone;
                 if (pu != kNone && pos == pu) { reached[u] = 1; break; }
-                if (pu != kNone && pos > pu) { *bad = 1; break; }  // stepped over a start: it was not a record
+                if (pu != kNone && pos > pu) { flags[0] = 1; break; }  // stepped over a start: not a record
             }
-            if (nbytes - pos < 8) { *bad = 1; break; }
+            if (nbytes - pos < 8) { flags[0] = 1; break; }
             const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
-            if ((nbytes - pos - 8) / 2 < len) { *bad = 1; break; }
+            if ((nbytes - pos - 8) / 2 < len) { flags[0] = 1; break; }
             sum += (uint64_t)off + len;
-            if (sum > total) { *bad = 1; break; }
-            cnt++;
+            if (sum > total) { flags[0] = 1; break; }
             pos += 8 + 2 * (size_t)len;
         }
     }
-    nrec[t] = cnt;
-    gsum[t] = (uint32_t)sum;
+    if (t < S) gsum[t] = (uint32_t)sum;
+    uint32_t ea, eb, ta, tb;
+    block_scan2((uint32_t)sum, 0u, ea, eb, ta, tb);
+    if (threadIdx.x == 0) { bsum[blockIdx.x] = ta; bscratch[blockIdx.x] = 0; }
 }
 
-// record j: start[j] = its first element in g, cumF[j] = values before it
-// (the header sits at byte 8 + 8 j + 2 cumF[j]).  nrec / gsum: exclusive scans.
-__global__ __launch_bounds__(kSB) void sl_table(const uint8_t *b, uint64_t total, size_t S, const uint32_t *p0,
-                                                const uint32_t *reached, const uint32_t *nrec, const uint32_t *gsum,
-                                                const uint64_t *totals, uint32_t *start, uint32_t *cumF,
-                                                uint32_t *bad) {
+__device__ __forceinline__ void put_run(float *g, const uint8_t *b, uint32_t gi, size_t vpos, uint32_t len,
+                                        uint32_t *longq, uint32_t qcap, uint32_t *flags) {
+    if (len <= (uint32_t)kShort) {
+        for (uint32_t i = 0; i < len; i++) g[gi + i] = from_f16_sp(ld16(b, vpos + 2 * i));
+    } else {
+        const uint32_t k = atomicAdd(&flags[1], 1u);
+        if (k >= qcap) { flags[0] = 1; return; }  // only off-chain walks can overfill it
+        longq[3 * k] = gi;
+        longq[3 * k + 1] = (uint32_t)vpos;
+        longq[3 * k + 2] = len;
+    }
+}
+
+// bsum: exclusive scan over blocks (sp_scan_tiles)
+__global__ __launch_bounds__(kSB) void sl_place(float *g, const uint8_t *b, size_t nbytes, const uint64_t *tot,
+                                                size_t S, const uint32_t *p0, const uint32_t *reached,
+                                                const uint32_t *gsum, const uint32_t *bsum, uint32_t *longq,
+                                                uint32_t qcap, uint32_t *flags) {
     const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
-    if (t >= S || p0[t] == kNone) return;
-    if (t > 0 && !reached[t]) { *bad = 1; return; }  // a speculative start off the chain
-    size_t j = nrec[t];
-    const size_t jend = t + 1 < S ? nrec[t + 1] : (size_t)totals[0];
-    uint64_t gi = gsum[t];
+    const uint64_t total = tot[0];
+    const uint32_t mine = t < S ? gsum[t] : 0u;
+    uint32_t ea, eb, ta, tb;
+    block_scan2(mine, 0u, ea, eb, ta, tb);
+    if (flags[0] || t >= S || p0[t] == kNone) return;  // a failed walk: nothing to place
+    if (t > 0 && !reached[t]) { flags[0] = 1; return; }  // a speculative start off the chain
+    // the same records sl_walk visited (it checked every one against the
+    // stream's bounds), stopping where it stopped
+    uint64_t gi = (uint64_t)bsum[blockIdx.x] + ea;
     size_t pos = p0[t];
-    for (; j < jend; j++) {
+    const size_t segend = 8 + (t + 1) * kSeg;
+    for (;;) {
+        if (pos == nbytes) break;
+        if (pos >= segend) {
+            const size_t u = (pos - 8) / kSeg;
+            const uint32_t pu = u < S ? p0[u] : kNone;
+            if (pu != kNone && pos >= pu) break;
+        }
         const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
         gi += off;
-        if (gi > total || total - gi < len) { *bad = 1; return; }  // protocol.rs:127-129 (host reports it)
-        start[j] = (uint32_t)gi;
-        cumF[j] = (uint32_t)((pos - 8 - 8 * j) / 2);
+        if (gi > total || total - gi < len) { flags[0] = 1; return; }  // protocol.rs:127-129 (host reports it)
+        put_run(g, b, (uint32_t)gi, pos + 8, len, longq, qcap, flags);
         gi += len;
         pos += 8 + 2 * (size_t)len;
     }
 }
 
-// value v belongs to record j with cumF[j] <= v < cumF[j+1]; it sits at byte
-// 16 + 8 j + 2 v.  F = (nbytes - 8 - 8 R) / 2 values in all.
-__global__ __launch_bounds__(kSB) void sl_expand(float *g, const uint8_t *b, size_t nbytes, const uint32_t *start,
-                                                 const uint32_t *cumF, const uint64_t *totals, const uint32_t *bad) {
-    if (*bad) return;
-    const size_t R = totals[0];
-    if (R == 0) return;
-    const size_t F = (nbytes - 8 - 8 * R) / 2;
-    const size_t stride = (size_t)gridDim.x * kSB;
-    for (size_t v = (size_t)blockIdx.x * kSB + threadIdx.x; v < F; v += stride) {
-        size_t lo = 0, hi = R;  // largest j with cumF[j] <= v
-        while (hi - lo > 1) {
-            const size_t mid = (lo + hi) / 2;
-            if (cumF[mid] <= v) lo = mid; else hi = mid;
-        }
-        const uint16_t h = *(const uint16_t *)(b + 16 + 8 * lo + 2 * v);
-        g[start[lo] + (v - cumF[lo])] = from_f16_sp(h);
+// runs longer than kShort: one workgroup per queued run
+__global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const uint32_t *longq,
+                                               const uint32_t *flags, uint64_t *host_word) {
+    const uint32_t bad = flags[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // every kernel that raises them has run
+        host_word[0] = bad;
+        host_word[2] = flags[2];
+    }
+    if (bad) return;
+    const uint32_t nq = flags[1];  // <= qcap when bad is clear
+    for (uint32_t k = blockIdx.x; k < nq; k += gridDim.x) {
+        const uint32_t gi = longq[3 * k], len = longq[3 * k + 2];
+        const size_t vpos = longq[3 * k + 1];
+        for (uint32_t i = threadIdx.x; i < len; i += kSB) g[gi + i] = from_f16_sp(ld16(b, vpos + 2 * i));
     }
 }
-
-__global__ void sl_flag_out(const uint32_t *bad, uint64_t *host_word) { host_word[0] = *bad; }
 
 // the totals into the host-mapped words (the exact-size path of a small buffer)
 __global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
@@ -447,7 +499,7 @@ int scratch_for(size_t ntiles, size_t maxruns, Scratch **out) {
 
 struct LiftScratch {
     size_t seg_cap = 0, rec_cap = 0, buf_cap = 0;
-    uint32_t *seg = nullptr, *rec = nullptr, *bad = nullptr;
+    uint32_t *seg = nullptr, *rec = nullptr, *flags = nullptr;
     uint8_t *buf = nullptr;
     uint64_t *totals = nullptr, *host_word = nullptr, *host_word_dev = nullptr;
 };
@@ -508,15 +560,10 @@ int lift_host_path(float *g, const uint8_t *hbuf, const uint8_t *dbuf, size_t nb
     return ONO_OK;
 }
 
-// Device lift of a device-resident stream.  hbuf: a host copy when the caller
-// has one (the fallback then needs no download), else nullptr.
+// Device lift of a device-resident stream, one host wait in all.  hbuf: a
+// host copy when the caller has one (the fallback then needs no download).
 int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, const uint8_t *hbuf, size_t nbytes,
-                uint64_t total, hipStream_t s) {
-    if (total > cap) return set_error(ONO_E_SIZE, "sparse gradient of %llu values, buffer of %zu",
-                                      (unsigned long long)total, cap);
-    *out_len = total;
-    if (total) ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));  // grad.fill(0); resize(total, 0)
-    if (nbytes == 8) return ONO_OK;
+                hipStream_t s) {
     std::vector<uint8_t> copy;
     auto host_bytes = [&]() -> const uint8_t * {
         if (hbuf) return hbuf;
@@ -526,47 +573,62 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
             return nullptr;
         return copy.data();
     };
-    // u32 record positions, starts and value counts: streams under 4 GiB,
-    // gradients under 2^32 values; anything larger parses on the host
-    if (nbytes >= 0xFFFFFFF0ull || total >= 0xFFFFFFFFull || ((uintptr_t)dbuf & 1)) {
+    auto size_error = [&](uint64_t total) {
+        return set_error(ONO_E_SIZE, "sparse gradient of %llu values, buffer of %zu", (unsigned long long)total, cap);
+    };
+    // u32 record positions, element indices and counts: streams under 4 GiB,
+    // gradients under 2^32 values; anything larger (or an odd stream address)
+    // parses on the host
+    if (nbytes >= 0xFFFFFFF0ull || cap >= 0xFFFFFFFFull || ((uintptr_t)dbuf & 1)) {
         const uint8_t *hb = host_bytes();
         if (!hb) return set_error(ONO_E_HIP, "sparse lift: download of the stream failed");
+        uint64_t total = 0;
+        for (int q = 0; q < 8; q++) total |= (uint64_t)hb[q] << (8 * q);
+        if (total > cap) return size_error(total);
+        *out_len = total;
+        if (total) ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));
         return lift_host_path(g, hb, dbuf, nbytes, total, s);
     }
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
     LiftScratch &L = g_lift[dev];
-    const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, Rmax = (nbytes - 8) / 8;
-    if (!L.totals) {
-        ONO_HIP(hipMalloc((void **)&L.totals, 2 * sizeof(uint64_t)));
-        ONO_HIP(hipMalloc((void **)&L.bad, sizeof(uint32_t)));
-        ONO_HIP(hipHostMalloc((void **)&L.host_word, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, nblk = S ? (S + kSB - 1) / kSB : 0;
+    const size_t qcap = (nbytes - 8) / (8 + 2 * (kShort + 1)) + 1;  // runs longer than kShort fit this many
+    if (!L.flags) {
+        ONO_HIP(hipMalloc((void **)&L.flags, 4 * sizeof(uint32_t)));
+        ONO_HIP(hipHostMalloc((void **)&L.host_word, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&L.host_word_dev, L.host_word, 0));
+        ONO_HIP(hipMalloc((void **)&L.totals, 4 * sizeof(uint64_t)));  // [0] total, [1..2] scan totals
     }
-    int rc = grow(&L.seg, L.seg_cap, 4 * S + 4);
-    if (!rc) rc = grow(&L.rec, L.rec_cap, 2 * Rmax + 2);
+    int rc = grow(&L.seg, L.seg_cap, 3 * S + 2 * nblk + 4);
+    if (!rc) rc = grow(&L.rec, L.rec_cap, 3 * qcap);
     if (rc) return rc;
-    uint32_t *p0 = L.seg, *reached = L.seg + S, *nrec = L.seg + 2 * S, *gsum = L.seg + 3 * S;
-    uint32_t *start = L.rec, *cumF = L.rec + Rmax + 1;
+    uint32_t *p0 = L.seg, *reached = L.seg + S, *gsum = L.seg + 2 * S, *bsum = L.seg + 3 * S,
+             *bscr = L.seg + 3 * S + nblk;
     volatile uint64_t *word = L.host_word;
-    *word = 1;
-    const unsigned sb = (unsigned)((S + kSB - 1) / kSB);
-    ONO_HIP(hipMemsetAsync(L.bad, 0, sizeof(uint32_t), s));
-    ONO_HIP(hipMemsetAsync(reached, 0, S * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(sl_starts, dim3(sb), dim3(kSB), 0, s, dbuf, nbytes, total, S, p0);
-    hipLaunchKernelGGL(sl_walk, dim3(sb), dim3(kSB), 0, s, dbuf, nbytes, total, S, p0, reached, nrec, gsum, L.bad);
-    hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, nrec, gsum, S, L.totals);
-    hipLaunchKernelGGL(sl_table, dim3(sb), dim3(kSB), 0, s, dbuf, total, S, p0, reached, nrec, gsum, L.totals, start,
-                       cumF, L.bad);
-    const size_t Fmax = (nbytes - 8) / 2;
-    const unsigned eb = (unsigned)std::min<size_t>(4096, (Fmax + kSB - 1) / kSB);
-    hipLaunchKernelGGL(sl_expand, dim3(eb), dim3(kSB), 0, s, g, dbuf, nbytes, start, cumF, L.totals, L.bad);
-    hipLaunchKernelGGL(sl_flag_out, dim3(1), dim3(1), 0, s, L.bad, L.host_word_dev);
+    word[0] = 1;
+    word[1] = word[2] = 0;
+    const int vec = ((uintptr_t)g & 15) == 0;
+    const unsigned zb = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (cap / 4 + kSB - 1) / kSB));
+    hipLaunchKernelGGL(sl_zero, dim3(zb), dim3(kSB), 0, s, g, dbuf, cap, vec, L.totals, L.flags, L.host_word_dev);
+    if (S) {
+        hipLaunchKernelGGL(sl_starts, dim3((unsigned)nblk), dim3(kSB), 0, s, dbuf, nbytes, L.totals, S, p0, reached);
+        hipLaunchKernelGGL(sl_walk, dim3((unsigned)nblk), dim3(kSB), 0, s, dbuf, nbytes, L.totals, S, p0, reached,
+                           gsum, bsum, bscr, L.flags);
+        hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, bsum, bscr, nblk, L.totals + 1);
+        hipLaunchKernelGGL(sl_place, dim3((unsigned)nblk), dim3(kSB), 0, s, g, dbuf, nbytes, L.totals, S, p0, reached,
+                           gsum, bsum, L.rec, (uint32_t)qcap, L.flags);
+    }
+    const unsigned lb = (unsigned)std::min<size_t>(1024, qcap);
+    hipLaunchKernelGGL(sl_long, dim3(lb), dim3(kSB), 0, s, g, dbuf, L.rec, L.flags, L.host_word_dev);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
-    if (*word == 0) return ONO_OK;
+    const uint64_t total = word[1];
+    if (word[2]) return size_error(total);
+    *out_len = total;
+    if (word[0] == 0) return ONO_OK;
     // speculation missed or the stream is malformed: the sequential parse decides
     g_lift_fallbacks.fetch_add(1);
     ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));
@@ -649,7 +711,7 @@ int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, s
     int rc = grow(&L.buf, L.buf_cap, nbytes);
     if (rc) return rc;
     ONO_HIP(hipMemcpyAsync(L.buf, buf, nbytes, hipMemcpyHostToDevice, s));
-    return lift_device(g, cap, out_len, L.buf, buf, nbytes, total, s);
+    return lift_device(g, cap, out_len, L.buf, buf, nbytes, s);
 }
 
 size_t ono_sparse_lift_fallbacks(void) { return g_lift_fallbacks.load(); }
@@ -660,10 +722,7 @@ int ono_sparse_lift_dev(float *g, size_t cap, size_t *out_len, const uint8_t *bu
     if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    uint64_t total = 0;
-    ONO_HIP(hipMemcpyAsync(&total, buf_dev, 8, hipMemcpyDeviceToHost, s));
-    ONO_HIP(hipStreamSynchronize(s));
-    return lift_device(g, cap, out_len, buf_dev, nullptr, nbytes, total, s);
+    return lift_device(g, cap, out_len, buf_dev, nullptr, nbytes, s);
 }
 
 int ono_sparse_mask(float *g, size_t n, float threshold, int zero_kept, void *stream) {

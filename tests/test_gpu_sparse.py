@@ -225,3 +225,39 @@ def test_lift_dev_error_deep_in_a_long_stream():
     b[:8] = np.uint64(total // 2).tobytes()
     with pytest.raises(ono_amd.InvalidWorkerEvent, match="exceeds target vector bounds"):
         SP.grad_lift_dev(to_dev(bytes(b)), total)
+
+
+def test_lift_dev_size_error_and_short_cap():
+    """total > cap: ONO_E_SIZE from the device-side check, nothing written."""
+    import ctypes as C
+
+    g = np.arange(64, dtype=np.float32)
+    wire = SP.grad_drop_dev(dev(g), 10.0)
+    out = torch.full((32,), 7.0, dtype=torch.float32, device="cuda")
+    ln = C.c_size_t(0)
+    rc = ono_amd.lib().ono_sparse_lift_dev(out.data_ptr(), 32, C.byref(ln), wire.data_ptr(), wire.numel(),
+                                           torch.cuda.current_stream().cuda_stream)
+    assert rc == 1  # ONO_E_SIZE
+    assert torch.all(out == 7.0)
+    back = SP.grad_lift_dev(wire, 100)  # larger cap: out_len is the stream's total
+    assert back.numel() == 64
+    assert_bitexact(back.cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=64))
+
+
+@pytest.mark.parametrize("offset", [0, 1, 2])
+def test_lift_dev_into_unaligned_gradient(offset):
+    """g at a 4-B (not 16-B) boundary: the device zero-fill's scalar form."""
+    import ctypes as C
+
+    n = 70001
+    g = O.synth(n, SEED + 29, 1)
+    t = float(np.quantile(np.abs(g), 0.7))
+    wire = SP.grad_drop_dev(dev(g), t)
+    base = torch.full((n + 8,), 5.0, dtype=torch.float32, device="cuda")
+    view = base[offset:offset + n]
+    ln = C.c_size_t(0)
+    rc = ono_amd.lib().ono_sparse_lift_dev(view.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(),
+                                           torch.cuda.current_stream().cuda_stream)
+    assert rc == 0 and ln.value == n
+    assert_bitexact(view.cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=n))
+    assert torch.all(base[:offset] == 5.0) and torch.all(base[offset + n:] == 5.0)
