@@ -395,7 +395,7 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     """the device top-k codec (comms/src/sparse/protocol.rs:57-144) on a 64 MiB
     gradient with the threshold at the 90th |g| percentile (~10 % of the values kept, the
     reference's r = 0.9).  Drop = count pass + scan + write pass + headers, a blocking call (the
-    wire length is needed on the host); bytes = 8 N read + the wire written.  Lift parses the
+    wire length is needed on the host); bytes = 4 N read + the wire written.  Lift parses the
     run headers on the host and expands on the device (host buffer in)."""
     import ctypes as C
 
@@ -453,7 +453,7 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     dlt, dlt_ev = sorted(tdl)[len(tdl) // 2], sorted(tdl_ev)[len(tdl_ev) // 2]
     lift_bytes = len(wire) + 4 * n
     kept = int(torch.count_nonzero(back).item())
-    drop_bytes = 8 * n + len(wire)
+    drop_bytes = 4 * n + len(wire)  # g read once + the stream written (the two-pass design reads g twice)
     return {"workload": "sparse grad_drop / grad_lift, 64 MiB f32 gradient, threshold = 90th |g| percentile",
             "kept_values": kept, "wire_bytes": len(wire),
             "drop": {"ms": round(td * 1e3, 3), "device_ms": round(tdev * 1e3, 3), "algorithmic_bytes": drop_bytes,

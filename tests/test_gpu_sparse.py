@@ -261,3 +261,23 @@ def test_lift_dev_into_unaligned_gradient(offset):
     assert rc == 0 and ln.value == n
     assert_bitexact(view.cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=n))
     assert torch.all(base[:offset] == 5.0) and torch.all(base[offset + n:] == 5.0)
+
+
+@pytest.mark.parametrize("pattern", ["far", "long_runs"])
+def test_drop_headers_across_tiles_and_scan_chunks(pattern):
+    """Run headers whose neighbour run is many tiles away, across the tile
+    scan's 8192-tile chunks (n > 2^24): the offset / length carries."""
+    n = 20_000_003
+    g = np.zeros(n, np.float32)
+    if pattern == "far":
+        for i in (0, 5, 2047, 2048, 4_000_000, 16_777_215, 16_777_216, 16_777_218, n - 1):
+            g[i] = 1.5
+    else:  # kept runs spanning tiles and the chunk boundary, gaps spanning many tiles
+        g[10_000:30_000] = -2.0
+        g[16_770_000:16_790_000] = 3.0
+        g[19_999_000:19_999_001] = 1.0
+        g[n - 3000:] = 0.75
+    got = SP.grad_drop_dev(dev(g), 0.5)
+    want = O.grad_drop(g, 0.5)
+    assert bytes(got.cpu().numpy()) == want
+    assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
