@@ -94,6 +94,26 @@ template <class T> __device__ __forceinline__ T ldn(const T *p) { return __built
 template <class T> __device__ __forceinline__ void st(T *p, T v) { *p = v; }
 // write-once outputs that nobody re-reads in this launch: non-temporal
 template <class T> __device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
+// Outputs of the ops that rewrite lines they read in the same launch (the
+// residual zeroed after it is read, acc += in): streaming stores at agent
+// scope, `global_store … nt sc1` (the builtin above gives `nt` alone).
+// Back-to-back 1R2W launches over fresh 256 MiB buffers
+// (tools/stream_variants.hip mode c): 125-129 us with `nt`, 120-121 us with
+// `nt sc1`; on the pure kR1W / 1R1W ops and the optimizer it measured worse,
+// so those keep st_nt.  Vector stores only (no scalar-cache writes).  The
+// compiler's hazard recognizer cannot see into the asm, so it carries the gfx9
+// store-data hazard itself: no VALU may overwrite the data VGPRs of a > 8-byte
+// store for 2 wait states on gfx940+ (`s_nop 1`).  vmcnt waits the compiler
+// emits for its own loads only grow stricter with these stores outstanding;
+// the "memory" clobber keeps them after every load of the op (ops load first).
+template <class T> __device__ __forceinline__ void st_sc1(T *p, T v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_sc1(f4 *p, f4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(h4 *p, h4 v) {
+    asm volatile("global_store_dwordx2 %0, %1, off nt sc1" : : "v"(p), "v"(__builtin_bit_cast(uint64_t, v))
+                 : "memory");
+}
 
 // --------------------------------------------------------- stream skeleton
 // Element range [0, n) split as [0, head) scalar | [head, head+4*nvec) 4-wide | tail scalar.
@@ -292,9 +312,9 @@ struct AccOp { // acc += in
     struct R { f4 a, b; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += in[i]; }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
+        return R{ldn((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + r.b); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_sc1((f4 *)(acc + i), r.a + r.b); }
 };
 
 template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
@@ -308,10 +328,10 @@ template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
         dst[i] = scl<M>(x, v);
         if (zero) zero[i] = 0.0f;
     }
-    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(src + i)); }
+    __device__ __forceinline__ R load(size_t i) const { return ldn((const f4 *)(src + i)); }
     __device__ __forceinline__ void store(size_t i, R x) const {
-        st_nt((f4 *)(dst + i), scl4<M>(x, v));
-        if (zero) st_nt((f4 *)(zero + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+        st_sc1((f4 *)(dst + i), scl4<M>(x, v));
+        if (zero) st_sc1((f4 *)(zero + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 };
 
@@ -347,10 +367,10 @@ template <class W> struct EncodeZeroOp {
         out[i] = Wire<W>::enc(chunk[i]);
         chunk[i] = 0.0f;
     }
-    __device__ __forceinline__ R load(size_t i) const { return ld((const f4 *)(chunk + i)); }
+    __device__ __forceinline__ R load(size_t i) const { return ldn((const f4 *)(chunk + i)); }
     __device__ __forceinline__ void store(size_t i, R x) const {
-        st_nt((WV *)(out + i), Wire<W>::enc4(x));
-        st_nt((f4 *)(chunk + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+        st_sc1((WV *)(out + i), Wire<W>::enc4(x));
+        st_sc1((f4 *)(chunk + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 };
 
@@ -361,9 +381,9 @@ template <class W> struct DecodeAddOp {
     struct R { f4 a; WV h; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += Wire<W>::dec(in[i]); }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
+        return R{ldn((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_sc1((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
 };
 
 template <class W> struct AddEncodeZeroOp {
@@ -378,12 +398,12 @@ template <class W> struct AddEncodeZeroOp {
         acc[i] = 0.0f;
     }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
+        return R{ldn((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
     __device__ __forceinline__ void store(size_t i, R r) const {
         f4 x = r.a + Wire<W>::dec4(r.h);
-        st_nt((WV *)(out + i), Wire<W>::enc4(x));
-        st_nt((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+        st_sc1((WV *)(out + i), Wire<W>::enc4(x));
+        st_sc1((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 };
 
@@ -402,13 +422,13 @@ template <class W, int M> struct AddFinishOp {
         acc[i] = 0.0f;
     }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
+        return R{ldn((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
     __device__ __forceinline__ void store(size_t i, R r) const {
         f4 x = r.a + Wire<W>::dec4(r.h);
-        st_nt((f4 *)(grad + i), scl4<M>(x, v));
-        st_nt((WV *)(out + i), Wire<W>::enc4(x));
-        st_nt((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
+        st_sc1((f4 *)(grad + i), scl4<M>(x, v));
+        st_sc1((WV *)(out + i), Wire<W>::enc4(x));
+        st_sc1((f4 *)(acc + i), f4{0.0f, 0.0f, 0.0f, 0.0f});
     }
 };
 

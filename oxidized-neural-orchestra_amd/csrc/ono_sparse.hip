@@ -550,12 +550,15 @@ int lift_host_path(float *g, const uint8_t *hbuf, const uint8_t *dbuf, size_t nb
     if (F == 0) return ONO_OK;
     uint64_t *dtab = nullptr;
     ONO_HIP(hipMallocAsync((void **)&dtab, 2 * R * sizeof(uint64_t), s));
-    ONO_HIP(hipMemcpyAsync(dtab, start.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    ONO_HIP(hipMemcpyAsync(dtab + R, cumF.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(sp_expand, dim3((unsigned)((F + kSB - 1) / kSB)), dim3(kSB), 0, s, g, dbuf, dtab, dtab + R, R, F);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipMemcpyAsync(dtab, start.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dtab + R, cumF.data(), R * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(sp_expand, dim3((unsigned)((F + kSB - 1) / kSB)), dim3(kSB), 0, s, g, dbuf, dtab, dtab + R,
+                           R, F);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(s);  // the host vectors are released on return
-    (void)hipFreeAsync(dtab, s);
+    (void)hipFreeAsync(dtab, s);  // on every path
     if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
     return ONO_OK;
 }

@@ -238,6 +238,179 @@ void pull_shape(Pool &P, hipStream_t s, bool fixed_out, bool per_launch_events, 
     for (int q = 0; q < 2 * L + 2; q++) CK(hipEventDestroy(ev[q]));
 }
 
+// The pull shape launched in isolation: a host wait before every launch (the
+// GPU idles ~10-20 us between kernels) vs the same launches back to back —
+// separates a kernel's burst rate from the sustained streaming rate.
+void pull_isolated(Pool &P, hipStream_t s, bool idle_between, int L) {
+    const int B = 64;
+    int blocks = (int)((P.nvec + B - 1) / B);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < ROT; r++) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)P.bufs[r * (MAXK + 2)], P.nvec, 9u + r);
+    CK(hipStreamSynchronize(s));
+    for (int i = 0; i < L; i++) {
+        int set = i % ROT;
+        Args a{};
+        a.in[0] = P.bufs[set * (MAXK + 2)];
+        a.out = P.bufs[set * (MAXK + 2) + MAXK];
+        a.zero = (f4 *)a.in[0];
+        if (idle_between) CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL((k_red2<1, true, 64, 1, false>), dim3(blocks), dim3(64), 0, s, a, P.nvec);
+        CK(hipEventRecord(e1, s));
+        if (idle_between) {
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            t.push_back(ms);
+        }
+        if (i % ROT == ROT - 1) {  // refill the residuals the lap zeroed (outside the timed launches)
+            if (!idle_between) CK(hipStreamSynchronize(s));
+            for (int r = 0; r < ROT; r++)
+                hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)P.bufs[r * (MAXK + 2)], P.nvec, 9u + r + i);
+            CK(hipStreamSynchronize(s));
+        }
+    }
+    CK(hipStreamSynchronize(s));
+    if (!idle_between) {  // back to back inside each lap: time one lap as a span
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < ROT; i++) {
+            Args a{};
+            a.in[0] = P.bufs[i * (MAXK + 2)];
+            a.out = P.bufs[i * (MAXK + 2) + MAXK];
+            a.zero = (f4 *)a.in[0];
+            hipLaunchKernelGGL((k_red2<1, true, 64, 1, false>), dim3(blocks), dim3(64), 0, s, a, P.nvec);
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms / ROT);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = 12.0 * 4 * P.nvec;
+    printf("pull n=1 B=64 %-26s %9.2f us %8.1f GB/s  %.3f of 8000\n", idle_between ? "isolated (host wait before)"
+           : "back-to-back lap of 6", ms * 1e3, bytes / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+__global__ void k_empty(int *p) {
+    if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 0;
+}
+
+// What precedes a timed pull-shape launch (host wait between pairs):
+//   0 nothing | 1 fill of another 256 MiB buffer | 2 empty kernel |
+//   3 fill of 16 MiB | 4 a pull-shape launch on another set | 5 fill 64 MiB
+void pull_after(Pool &P, hipStream_t s, int what, int L) {
+    const int B = 64;
+    int blocks = (int)((P.nvec + B - 1) / B);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int r = 0; r < ROT; r++) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)P.bufs[r * (MAXK + 2)], P.nvec, 3u + r);
+    CK(hipStreamSynchronize(s));
+    for (int i = 0; i < L; i++) {
+        const int set = i % ROT, other = (i + 3) % ROT;
+        Args a{};
+        a.in[0] = P.bufs[set * (MAXK + 2)];
+        a.out = P.bufs[set * (MAXK + 2) + MAXK];
+        a.zero = (f4 *)a.in[0];
+        f4 *scratch = P.bufs[other * (MAXK + 2) + 1];  // an input slot the pull shape never touches
+        if (what == 1) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, scratch, P.nvec, 1u + i);
+        if (what == 2) hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, (int *)nullptr);
+        if (what == 3) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, scratch, P.nvec / 16, 1u + i);
+        if (what == 5) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, scratch, P.nvec / 4, 1u + i);
+        if (what == 4) {
+            Args b{};
+            b.in[0] = P.bufs[other * (MAXK + 2) + 1];
+            b.out = P.bufs[other * (MAXK + 2) + 2];
+            b.zero = nullptr;
+            hipLaunchKernelGGL((k_red2<1, false, 64, 1, false>), dim3(blocks), dim3(64), 0, s, b, P.nvec);
+        }
+        CK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL((k_red2<1, true, 64, 1, false>), dim3(blocks), dim3(64), 0, s, a, P.nvec);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t.push_back(ms);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)a.in[0], P.nvec, 11u + i);  // refill what it zeroed
+        CK(hipStreamSynchronize(s));
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = 12.0 * 4 * P.nvec;
+    static const char *nm[] = {"nothing", "fill 256 MiB other", "empty kernel", "fill 16 MiB", "copy 256 MiB other",
+                               "fill 64 MiB"};
+    printf("pull after %-20s %9.2f us %8.1f GB/s  %.3f of 8000\n", nm[what], ms * 1e3,
+           bytes / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+// Cache-policy variants of the pull shape (buffer loads / stores with explicit
+// sc0 / sc1 / nt bits; aux: sc0 = 1, nt = 2, sc1 = 16), timed as the bench
+// runs them: back-to-back launches over freshly filled buffers.
+template <int LP, int SP>
+__global__ __launch_bounds__(64) void k_pol(const f4 *src, f4 *dst, f4 *zero, unsigned nvec) {
+    const unsigned v = blockIdx.x * 64 + threadIdx.x;
+    if (v >= nvec) return;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, 0x7FFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, 0x7FFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)zero, 0, 0x7FFFFFFF, 0x00020000);
+    f4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, LP);
+    __builtin_amdgcn_raw_buffer_store_b128(x, rd, v * 16, 0, SP);
+    __builtin_amdgcn_raw_buffer_store_b128(f4{0, 0, 0, 0}, rz, v * 16, 0, SP);
+}
+
+template <int LP, int SP>
+void pol_row(Pool &P, hipStream_t s, const char *name) {
+    const unsigned nvec = (unsigned)P.nvec;
+    const int blocks = (int)((P.nvec + 63) / 64);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int lap = 0; lap < 4; lap++) {
+        for (int r = 0; r < ROT; r++)
+            hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, (f4 *)P.bufs[r * (MAXK + 2)], P.nvec, 21u + r + lap);
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < ROT; i++) {
+            f4 *in = P.bufs[i * (MAXK + 2)], *out = P.bufs[i * (MAXK + 2) + MAXK];
+            if (LP < 0) {
+                Args a{};
+                a.in[0] = in;
+                a.out = out;
+                a.zero = in;
+                hipLaunchKernelGGL((k_red2<1, true, 64, 1, false>), dim3(blocks), dim3(64), 0, s, a, P.nvec);
+            } else {
+                hipLaunchKernelGGL((k_pol<LP < 0 ? 0 : LP, SP>), dim3(blocks), dim3(64), 0, s, in, out, in, nvec);
+            }
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (lap) t.push_back(ms / ROT);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = 12.0 * 4 * P.nvec;
+    printf("pull b2b %-32s %9.2f us %8.1f GB/s  %.3f of 8000\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+           bytes / (ms * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
 int main(int argc, char **argv) {
     size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (size_t)1 << 24;  // 64 MiB per buffer
     Pool P;
@@ -255,7 +428,32 @@ int main(int argc, char **argv) {
     CK(hipStreamSynchronize(s));
     printf("n=%zu (%.0f MiB per buffer), %d rotating sets, CUs=%d\n", n, n * 4.0 / (1 << 20), ROT, cus);
     const char *mode = argc > 2 ? argv[2] : "all";
-    if (mode[0] == 'p') {
+    if (mode[0] == 'c') {
+        for (int rep = 0; rep < 2; rep++) {
+            pol_row<-1, 0>(P, s, "global ld / nt st (product)");
+            pol_row<0, 2>(P, s, "ld - / st nt");
+            pol_row<0, 0>(P, s, "ld - / st -");
+            pol_row<2, 2>(P, s, "ld nt / st nt");
+            pol_row<0, 18>(P, s, "ld - / st nt sc1");
+            pol_row<0, 16>(P, s, "ld - / st sc1");
+            pol_row<0, 17>(P, s, "ld - / st sc0 sc1");
+            pol_row<0, 19>(P, s, "ld - / st sc0 nt sc1");
+            pol_row<0, 3>(P, s, "ld - / st sc0 nt");
+            pol_row<16, 2>(P, s, "ld sc1 / st nt");
+            pol_row<18, 18>(P, s, "ld nt sc1 / st nt sc1");
+            pol_row<17, 19>(P, s, "ld sc0 sc1 / st sc0 nt sc1");
+        }
+    } else if (mode[0] == 'x') {
+        for (int rep = 0; rep < 2; rep++)
+            for (int w : {0, 1, 2, 3, 5, 4}) pull_after(P, s, w, 14);
+    } else if (mode[0] == 'i') {
+        for (int rep = 0; rep < 2; rep++) {
+            pull_isolated(P, s, true, 24);
+            pull_isolated(P, s, false, 6);
+            row2<1, true, 64, 1, false>(P, s, "copy+zero 1R2W");
+            row2<1, true, 256, 1, false>(P, s, "copy+zero 1R2W");
+        }
+    } else if (mode[0] == 'p') {
         for (int rep = 0; rep < 2; rep++)
             for (int B : {256, 64})
                 for (bool fx : {true, false})
