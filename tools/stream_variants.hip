@@ -411,6 +411,63 @@ void pol_row(Pool &P, hipStream_t s, const char *name) {
     CK(hipEventDestroy(e1));
 }
 
+// kR1W (sum_scale shape) with explicit load / store cache policies
+template <int K, int LP, int SP>
+__global__ __launch_bounds__(64) void k_polk(Args a, unsigned nvec) {
+    const unsigned v = blockIdx.x * 64 + threadIdx.x;
+    if (v >= nvec) return;
+    f4 r = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)a.in[j], 0, 0x7FFFFFFF, 0x00020000);
+        r += __builtin_amdgcn_raw_buffer_load_b128(rs, v * 16, 0, LP);
+    }
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void *)a.out, 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(r * 0.5f, rd, v * 16, 0, SP);
+}
+
+template <int K, int LP, int SP>
+void polk_row(Pool &P, hipStream_t s, const char *name) {
+    const int blocks = (int)((P.nvec + 63) / 64);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int lap = 0; lap < 5; lap++) {
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < ROT; i++) {
+            Args a{};
+            for (int j = 0; j < K; j++) a.in[j] = P.bufs[i * (MAXK + 2) + j];
+            a.out = P.bufs[i * (MAXK + 2) + MAXK];
+            hipLaunchKernelGGL((k_polk<K, LP, SP>), dim3(blocks), dim3(64), 0, s, a, (unsigned)P.nvec);
+        }
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (lap) t.push_back(ms / ROT);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = (double)(K + 1) * 16 * P.nvec;
+    printf("sum%d b2b %-28s %9.2f us %8.1f GB/s  %.3f of 8000\n", K, name, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+           bytes / (ms * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+}
+
+template <int K> void polk_sweep(Pool &P, hipStream_t s) {
+    polk_row<K, 0, 2>(P, s, "ld - / st nt");
+    polk_row<K, 2, 2>(P, s, "ld nt / st nt (product)");
+    polk_row<K, 2, 18>(P, s, "ld nt / st nt sc1");
+    polk_row<K, 18, 2>(P, s, "ld nt sc1 / st nt");
+    polk_row<K, 18, 18>(P, s, "ld nt sc1 / st nt sc1");
+    polk_row<K, 16, 2>(P, s, "ld sc1 / st nt");
+    polk_row<K, 3, 2>(P, s, "ld sc0 nt / st nt");
+    polk_row<K, 2, 0>(P, s, "ld nt / st -");
+}
+
 int main(int argc, char **argv) {
     size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (size_t)1 << 24;  // 64 MiB per buffer
     Pool P;
@@ -428,7 +485,13 @@ int main(int argc, char **argv) {
     CK(hipStreamSynchronize(s));
     printf("n=%zu (%.0f MiB per buffer), %d rotating sets, CUs=%d\n", n, n * 4.0 / (1 << 20), ROT, cus);
     const char *mode = argc > 2 ? argv[2] : "all";
-    if (mode[0] == 'c') {
+    if (mode[0] == 'k' && mode[1] == 'c') {
+        for (int rep = 0; rep < 2; rep++) {
+            polk_sweep<2>(P, s);
+            polk_sweep<4>(P, s);
+            polk_sweep<8>(P, s);
+        }
+    } else if (mode[0] == 'c') {
         for (int rep = 0; rep < 2; rep++) {
             pol_row<-1, 0>(P, s, "global ld / nt st (product)");
             pol_row<0, 2>(P, s, "ld - / st nt");
