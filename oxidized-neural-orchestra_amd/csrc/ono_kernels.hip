@@ -94,13 +94,19 @@ template <class T> __device__ __forceinline__ T ldn(const T *p) { return __built
 template <class T> __device__ __forceinline__ void st(T *p, T v) { *p = v; }
 // write-once outputs that nobody re-reads in this launch: non-temporal
 template <class T> __device__ __forceinline__ void st_nt(T *p, T v) { __builtin_nontemporal_store(v, p); }
-// Outputs of the ops that rewrite lines they read in the same launch (the
-// residual zeroed after it is read, acc += in): streaming stores at agent
-// scope, `global_store … nt sc1` (the builtin above gives `nt` alone).
-// Back-to-back 1R2W launches over fresh 256 MiB buffers
-// (tools/stream_variants.hip mode c): 125-129 us with `nt`, 120-121 us with
-// `nt sc1`; on the pure kR1W / 1R1W ops and the optimizer it measured worse,
-// so those keep st_nt.  Vector stores only (no scalar-cache writes).  The
+// Outputs of the ops that consume the residual (read it, zero it, pass the
+// result on): streaming stores at agent scope, `global_store … nt sc1` (the
+// builtin above gives `nt` alone), after nt loads.  Producers that accumulate
+// into a buffer the next kernel reads (acc_residual, the store's f16
+// accumulate) keep plain loads + `nt` stores: those leave the residual in the
+// Infinity Cache for the pull, which the consumer policy would forfeit
+// (tools/stream_variants.hip mode t: acc + pull on one reused bucket, 224.8 us
+// per step with this split vs 253-257 us with the consumer policy everywhere).
+// The pull shape (1R2W) back to back over fresh 256 MiB buffers (mode c):
+// 125-129 us with plain loads + `nt` stores, 119-121 us with nt loads +
+// `nt sc1`; on one reused bucket after acc_residual (mode t) 103.7 -> 100 us.
+// On the kR1W / 1R1W ops and the optimizer it measured worse, so those keep
+// st_nt.  Vector stores only (no scalar-cache writes).  The
 // compiler's hazard recognizer cannot see into the asm, so it carries the gfx9
 // store-data hazard itself: no VALU may overwrite the data VGPRs of a > 8-byte
 // store for 2 wait states on gfx940+ (`s_nop 1`).  vmcnt waits the compiler
@@ -312,9 +318,9 @@ struct AccOp { // acc += in
     struct R { f4 a, b; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += in[i]; }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ldn((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st_sc1((f4 *)(acc + i), r.a + r.b); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + r.b); }
 };
 
 template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
@@ -381,9 +387,9 @@ template <class W> struct DecodeAddOp {
     struct R { f4 a; WV h; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += Wire<W>::dec(in[i]); }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ldn((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
+        return R{ld((const f4 *)(acc + i)), ldn((const WV *)(in + i))};
     }
-    __device__ __forceinline__ void store(size_t i, R r) const { st_sc1((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
+    __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + Wire<W>::dec4(r.h)); }
 };
 
 template <class W> struct AddEncodeZeroOp {

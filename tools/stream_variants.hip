@@ -468,6 +468,53 @@ template <int K> void polk_sweep(Pool &P, hipStream_t s) {
     polk_row<K, 2, 0>(P, s, "ld nt / st -");
 }
 
+// The training regime: ONE residual bucket reused every step — acc_residual
+// (res += g, 1 launch per local batch) then pull (grad = res, res = 0) —
+// with the pull's cache policy varied: is the bench's fresh-bucket gain real
+// when the same 256 MiB lines come back every step?
+template <int LP, int SP>
+__global__ __launch_bounds__(64) void k_acc(f4 *res, const f4 *g, unsigned nvec) {
+    const unsigned v = blockIdx.x * 64 + threadIdx.x;
+    if (v >= nvec) return;
+    __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)res, 0, 0x7FFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void *)g, 0, 0x7FFFFFFF, 0x00020000);
+    f4 a = __builtin_amdgcn_raw_buffer_load_b128(rr, v * 16, 0, LP);
+    f4 b = __builtin_amdgcn_raw_buffer_load_b128(rg, v * 16, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(a + b, rr, v * 16, 0, SP);
+}
+
+template <int LP, int SP, int PLP = LP, int PSP = SP>
+void train_row(Pool &P, hipStream_t s, const char *name, int acc_per_step) {
+    const int blocks = (int)((P.nvec + 63) / 64);
+    f4 *res = P.bufs[0], *grad = P.bufs[MAXK];
+    hipEvent_t e0, e1, p0, p1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventCreate(&p0));
+    CK(hipEventCreate(&p1));
+    std::vector<float> t, tp;
+    for (int it = 0; it < 12; it++) {
+        CK(hipEventRecord(e0, s));
+        for (int a = 0; a < acc_per_step; a++)
+            hipLaunchKernelGGL((k_acc<LP, SP>), dim3(blocks), dim3(64), 0, s, res, (const f4 *)P.bufs[1 + (a % 4)],
+                               (unsigned)P.nvec);
+        CK(hipEventRecord(p0, s));
+        hipLaunchKernelGGL((k_pol<PLP, PSP>), dim3(blocks), dim3(64), 0, s, (const f4 *)res, grad, res, (unsigned)P.nvec);
+        CK(hipEventRecord(p1, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms, mp;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipEventElapsedTime(&mp, p0, p1));
+        if (it >= 2) { t.push_back(ms); tp.push_back(mp); }
+    }
+    std::sort(t.begin(), t.end());
+    std::sort(tp.begin(), tp.end());
+    printf("train step (%d acc + pull) %-22s step %8.2f us   pull %8.2f us (%.3f of 8000)\n", acc_per_step, name,
+           t[t.size() / 2] * 1e3, tp[tp.size() / 2] * 1e3, 12.0 * 4 * P.nvec / (tp[tp.size() / 2] * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (size_t)1 << 24;  // 64 MiB per buffer
     Pool P;
@@ -485,7 +532,17 @@ int main(int argc, char **argv) {
     CK(hipStreamSynchronize(s));
     printf("n=%zu (%.0f MiB per buffer), %d rotating sets, CUs=%d\n", n, n * 4.0 / (1 << 20), ROT, cus);
     const char *mode = argc > 2 ? argv[2] : "all";
-    if (mode[0] == 'k' && mode[1] == 'c') {
+    if (mode[0] == 't') {
+        for (int rep = 0; rep < 2; rep++)
+            for (int A : {0, 1, 4}) {
+                train_row<0, 2>(P, s, "ld - / st nt", A);
+                train_row<2, 2>(P, s, "ld nt / st nt", A);
+                train_row<2, 18>(P, s, "ld nt / st nt sc1", A);
+                train_row<0, 2, 2, 18>(P, s, "acc -/nt, pull nt/nt sc1", A);
+                train_row<0, 2, 2, 2>(P, s, "acc -/nt, pull nt/nt", A);
+                train_row<0, 0, 0, 2>(P, s, "acc -/-, pull -/nt", A);
+            }
+    } else if (mode[0] == 'k' && mode[1] == 'c') {
         for (int rep = 0; rep < 2; rep++) {
             polk_sweep<2>(P, s);
             polk_sweep<4>(P, s);
