@@ -515,6 +515,49 @@ void train_row(Pool &P, hipStream_t s, const char *name, int acc_per_step) {
     fflush(stdout);
 }
 
+// f16 decode shape (8 B in, 16 B out per lane) with explicit policies
+template <int LP, int SP>
+__global__ __launch_bounds__(64) void k_dec(const unsigned short *in, f4 *out, unsigned nvec) {
+    const unsigned v = blockIdx.x * 64 + threadIdx.x;
+    if (v >= nvec) return;
+    __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)in, 0, 0x7FFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)out, 0, 0x7FFFFFFF, 0x00020000);
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    u2 h = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(ri, v * 8, 0, LP));
+    f4 r = {(float)__builtin_bit_cast(_Float16, (unsigned short)(h.x & 0xFFFF)),
+            (float)__builtin_bit_cast(_Float16, (unsigned short)(h.x >> 16)),
+            (float)__builtin_bit_cast(_Float16, (unsigned short)(h.y & 0xFFFF)),
+            (float)__builtin_bit_cast(_Float16, (unsigned short)(h.y >> 16))};
+    __builtin_amdgcn_raw_buffer_store_b128(r * 0.125f, ro, v * 16, 0, SP);
+}
+
+template <int LP, int SP>
+void dec_row(Pool &P, hipStream_t s, const char *name) {
+    const int blocks = (int)((P.nvec + 63) / 64);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> t;
+    for (int lap = 0; lap < 5; lap++) {
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < ROT; i++)
+            hipLaunchKernelGGL((k_dec<LP, SP>), dim3(blocks), dim3(64), 0, s,
+                               (const unsigned short *)P.bufs[i * (MAXK + 2)], P.bufs[i * (MAXK + 2) + MAXK],
+                               (unsigned)P.nvec);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (lap) t.push_back(ms / ROT);
+    }
+    std::sort(t.begin(), t.end());
+    double ms = t[t.size() / 2];
+    double bytes = 24.0 * P.nvec;
+    printf("decode b2b %-24s %9.2f us %8.1f GB/s  %.3f of 8000\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9,
+           bytes / (ms * 1e-3) / 1e9 / 8000.0);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (size_t)1 << 24;  // 64 MiB per buffer
     Pool P;
@@ -532,7 +575,17 @@ int main(int argc, char **argv) {
     CK(hipStreamSynchronize(s));
     printf("n=%zu (%.0f MiB per buffer), %d rotating sets, CUs=%d\n", n, n * 4.0 / (1 << 20), ROT, cus);
     const char *mode = argc > 2 ? argv[2] : "all";
-    if (mode[0] == 't') {
+    if (mode[0] == 'd') {
+        for (int rep = 0; rep < 2; rep++) {
+            dec_row<2, 2>(P, s, "ld nt / st nt (product)");
+            dec_row<0, 2>(P, s, "ld - / st nt");
+            dec_row<2, 0>(P, s, "ld nt / st -");
+            dec_row<2, 18>(P, s, "ld nt / st nt sc1");
+            dec_row<18, 18>(P, s, "ld nt sc1 / st nt sc1");
+            dec_row<2, 3>(P, s, "ld nt / st sc0 nt");
+            dec_row<2, 16>(P, s, "ld nt / st sc1");
+        }
+    } else if (mode[0] == 't') {
         for (int rep = 0; rep < 2; rep++)
             for (int A : {0, 1, 4}) {
                 train_row<0, 2>(P, s, "ld - / st nt", A);
