@@ -112,6 +112,7 @@ struct OptLaunch {
     bool plus_zero = true;
 };
 hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_,
-                             size_t n, bool zero_grad, hipStream_t st, float *w_copy = nullptr);
+                             size_t n, bool zero_grad, hipStream_t st, float *w_copy = nullptr,
+                             bool copy_for_peers = false);  // w_copy read by other ranks after a barrier
 
 }  // namespace ono

@@ -20,6 +20,9 @@
 // v_cvt_f16_f32 (round-to-nearest-even) with the `half` crate's NaN rule.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+#include <utility>
+
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -121,6 +124,17 @@ __device__ __forceinline__ void st_sc1(h4 *p, h4 v) {
                  : "memory");
 }
 
+// A later launch's flag store (the xGMI barrier) publishes what this launch
+// wrote for other ranks.  A wave may retire with stores still in flight and
+// the dispatch's end-of-kernel release is agent-scope, so it does not wait
+// for stores bound to memory another process or device reads: the wave
+// itself waits (system-scope release; the explicit vmcnt wait because the
+// fence's own can be dropped, guide §6 G16 P12).
+__device__ __forceinline__ void peer_stores_done() {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // --------------------------------------------------------- stream skeleton
 // Element range [0, n) split as [0, head) scalar | [head, head+4*nvec) 4-wide | tail scalar.
 // One 16-B vector per thread over a one-shot grid (ceil(nvec/64) one-wave workgroups):
@@ -129,6 +143,14 @@ __device__ __forceinline__ void st_sc1(h4 *p, h4 v) {
 // for every 1R2W / kR1W shape of this path; the hardware keeps enough bytes in
 // flight through wave count, not per-thread unrolling.  The grid-stride form
 // is kept for grids beyond the launch limit.
+// Ops whose stores other processes / devices read next (after a flag barrier
+// in a later launch) end every wave with op.finish(): see peer_stores_done().
+template <class Op, class = void> struct HasFinish : std::false_type {};
+template <class Op> struct HasFinish<Op, std::void_t<decltype(std::declval<const Op &>().finish())>> : std::true_type {};
+template <class Op> __device__ __forceinline__ void finish_wave(const Op &op) {
+    if constexpr (HasFinish<Op>::value) op.finish();
+}
+
 template <class Op>
 __global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t nvec, size_t n) {
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -137,6 +159,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t n
     if (tid < head) op.scalar(tid);
     if (tid < n - tail0) op.scalar(tail0 + tid);
     for (size_t v = tid; v < nvec; v += stride) op.store(head + 4 * v, op.load(head + 4 * v));
+    finish_wave(op);
 }
 
 // scalar-only fallback for operands whose 4-element phases differ
@@ -144,6 +167,7 @@ template <class Op>
 __global__ __launch_bounds__(kBlock) void ew_scalar_kernel(Op op, size_t n) {
     const size_t stride = (size_t)gridDim.x * kBlock;
     for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) op.scalar(i);
+    finish_wave(op);
 }
 
 // ---------------------------------------------------------------- grid ----
@@ -255,6 +279,11 @@ struct Outs {
 };
 template <int K, class W> struct DirectOp {
     typedef typename Wire<W>::V WV;
+    // outs read by other ranks after the next flag barrier: every wave waits
+    // for its stores to complete at system scope before it ends
+    __device__ __forceinline__ void finish() const {
+        if (sys_out) peer_stores_done();
+    }
     Ptrs in;
     float *grad;
     Outs out;  // nout copies of the result (f16 message / f32 grad value): local and/or peer HBM
@@ -484,7 +513,11 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
     float *g, *w, *v, *s;
     float *w2;  // optional copy of the updated parameters (all_reduce.rs:132), may be NULL
     float lr, mu, b1, omb1, b2, omb2, eps, step, nw;
+    int fence;  // w2 is read by other ranks after the next flag barrier (xGMI PS)
     struct R { f4 g, w, v, s; };
+    __device__ __forceinline__ void finish() const {
+        if (fence) peer_stores_done();
+    }
     __device__ __forceinline__ void one(float &gi, float &wi, float &vi, float &si) const {
         float gg = scl<M>(PZ ? gi + 0.0f : gi, nw);
         if constexpr (KIND == ONO_OPT_GD) {
@@ -572,13 +605,14 @@ hipError_t sum_scale_dispatch(int k, float *out, const Ptrs &p, size_t n, const 
 
 template <int KIND, bool ZERO>
 hipError_t opt_kind(const OptLaunch &o, float *g, float *w, float *v, float *s_, float *w2, size_t n,
-                    hipStream_t st) {
+                    hipStream_t st, bool fence) {
     Scale sc = make_scale(o.nworkers);
     float omb1 = 1.0f - o.beta1, omb2 = 1.0f - o.beta2;
     auto ph = {phase_of(g, 4), phase_of(w, 4), v ? phase_of(v, 4) : phase_of(g, 4),
                s_ ? phase_of(s_, 4) : phase_of(g, 4), w2 ? phase_of(w2, 4) : phase_of(g, 4)};
 #define ONO_OPT_OP(MODE, PZ) \
-    OptOp<KIND, MODE, ZERO, PZ>{g, w, v, s_, w2, o.lr, o.momentum, o.beta1, omb1, o.beta2, omb2, o.eps, o.step_size, sc.v}
+    OptOp<KIND, MODE, ZERO, PZ>{g,        w,       v,    s_,         w2,    o.lr, o.momentum, o.beta1, omb1, o.beta2, \
+                                omb2,     o.eps,   o.step_size, sc.v, fence ? 1 : 0}
     if (o.plus_zero) {
         switch (sc.mode) {
         case SCALE_NONE: return launch_ew(ONO_OPT_OP(SCALE_NONE, true), n, ph, st);
@@ -752,11 +786,11 @@ ONO_INST(float)
 #undef ONO_INST
 
 hipError_t launch_opt_update(const OptLaunch &o, float *g, float *w, float *v, float *s_, size_t n,
-                             bool zero_grad, hipStream_t st, float *w_copy) {
+                             bool zero_grad, hipStream_t st, float *w_copy, bool copy_for_peers) {
 #define ONO_OPT_CASE(KIND)                                                                     \
     case KIND:                                                                                 \
-        return zero_grad ? opt_kind<KIND, true>(o, g, w, v, s_, w_copy, n, st)                 \
-                         : opt_kind<KIND, false>(o, g, w, v, s_, w_copy, n, st);
+        return zero_grad ? opt_kind<KIND, true>(o, g, w, v, s_, w_copy, n, st, copy_for_peers) \
+                         : opt_kind<KIND, false>(o, g, w, v, s_, w_copy, n, st, copy_for_peers);
     switch (o.kind) {
         ONO_OPT_CASE(ONO_OPT_GD)
         ONO_OPT_CASE(ONO_OPT_MOMENTUM)

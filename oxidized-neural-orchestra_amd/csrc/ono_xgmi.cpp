@@ -227,8 +227,8 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s, const size_t
         ONO_K(r, s, launch_xgmi_pull(unpack, f16, f16 ? (float)n : 1.0f, s));
         return ONO_OK;
     }
-    W *out = reinterpret_cast<W *>(obuf_of(x, x->xbuf)) + ph(off[c]);
-    ONO_K(r, s, launch_direct<W>(grad + off[c], out, ins, n, len(c), (float)n, false, s));
+    W *out = reinterpret_cast<W *>(obuf_of(x, x->xbuf)) + ph(off[c]);  // peers pull it after the barrier:
+    ONO_K(r, s, launch_direct_multi<W>(grad + off[c], &out, 1, true, ins, n, len(c), (float)n, false, s));  // sys
     if ((rc = barrier(r, s))) return rc;  // 4.
 
     XSegs pull{};  // 5. every owner's result -> my grad
@@ -305,7 +305,7 @@ int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t
         for (int w = 0; w < n; w++)
             ins[w] = w == pos ? grad + lo(pos) : rbuf_of(x, x->xbuf, slot_of(w, pos)) + ph(lo(pos));
         ONO_K(r, s, launch_sum_scale(gshard, ins, n, len(pos), 1.0f, s));
-        ONO_K(r, s, launch_opt_update(opt, gshard, wshard, v, s_, len(pos), true, s, out));
+        ONO_K(r, s, launch_opt_update(opt, gshard, wshard, v, s_, len(pos), true, s, out, true));
     }
     if ((rc = barrier(r, s))) return rc;
 

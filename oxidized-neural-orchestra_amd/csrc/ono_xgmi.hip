@@ -64,9 +64,23 @@ template <class T> __device__ __forceinline__ void st_sys(T *p, T v) {
     *(volatile __attribute__((address_space(1))) T *)p = v;  // global_store ... sc0 sc1
 }
 
+// A later launch's flag store (the barrier) publishes what a push wrote into
+// peer memory.  A wave may retire with stores in flight and the dispatch's
+// end-of-kernel release is agent-scope, which does not wait for stores bound
+// to another process's / device's memory: each pushing wave waits for its
+// own stores at system scope before it ends (explicit vmcnt wait: the fence's
+// own can be dropped, guide §6 G16 P12).  Without it the owner's chain could
+// read a receive slot before the pushed slice landed (seen as a rare wrong
+// sum in the pipelined host-fed rounds, tests/test_gpu_xgmi.py).
+__device__ __forceinline__ void peer_stores_done() {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // f32 slice -> peer receive slot; ZERO: then zero the slice (the ring's
 // residual); without: a plain copy (the PS mode's gradient stays the caller's)
 template <bool ZERO> struct PushOp {
+    static constexpr bool kPeerStores = true;
     __device__ __forceinline__ static void scalar(const XSeg &s, size_t i) {
         float *src = (float *)s.src;
         st_sys((float *)s.dst + i, src[i]);
@@ -85,6 +99,7 @@ template <bool ZERO> struct PushOp {
 };
 
 template <int M> struct PullF32Op {  // owner's f32 result (already ÷n) -> grad
+    static constexpr bool kPeerStores = false;
     float v;
     __device__ __forceinline__ void scalar(const XSeg &s, size_t i) const {
         ((float *)s.dst)[i] = xs<M>(ld_sys((const float *)s.src + i), v);
@@ -98,6 +113,7 @@ template <int M> struct PullF32Op {  // owner's f32 result (already ÷n) -> grad
 };
 
 template <int M> struct PullF16Op {  // owner's f16 message -> grad = f32(h) / d
+    static constexpr bool kPeerStores = false;
     float v;
     __device__ __forceinline__ void scalar(const XSeg &s, size_t i) const {
         ((float *)s.dst)[i] = xs<M>(x_from_f16(ld_sys((const uint16_t *)s.src + i)), v);
@@ -123,6 +139,7 @@ __global__ __launch_bounds__(kXBlock) void xseg_kernel(Op op, XSegs g) {
             size_t i = (size_t)t * (4 * kXBlock) + (size_t)u * kXBlock + lane;
             if (i < s.n) op.scalar(s, i);
         }
+        if constexpr (Op::kPeerStores) peer_stores_done();
         return;
     }
     bool vec_ok;
@@ -134,6 +151,7 @@ __global__ __launch_bounds__(kXBlock) void xseg_kernel(Op op, XSegs g) {
         if ((size_t)lane < s.n - tail0) op.scalar(s, tail0 + lane);
     }
     if (vec_ok) op.vec(s, s.head + 4 * v);
+    if constexpr (Op::kPeerStores) peer_stores_done();
 }
 
 // One workgroup; lane q < n signals peer q and waits for q's signal.
