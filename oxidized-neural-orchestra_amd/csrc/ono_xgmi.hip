@@ -65,16 +65,17 @@ template <class T> __device__ __forceinline__ void st_sys(T *p, T v) {
 }
 
 // A later launch's flag store (the barrier) publishes what a push wrote into
-// peer memory.  A wave may retire with stores in flight and the dispatch's
-// end-of-kernel release is agent-scope, which does not wait for stores bound
-// to another process's / device's memory: each pushing wave waits for its
-// own stores at system scope before it ends (explicit vmcnt wait: the fence's
-// own can be dropped, guide §6 G16 P12).  Without it the owner's chain could
-// read a receive slot before the pushed slice landed (seen as a rare wrong
-// sum in the pipelined host-fed rounds, tests/test_gpu_xgmi.py).
+// peer memory.  A wave may retire with stores still in flight, and nothing at
+// the kernel boundary waits for stores bound to another process's / device's
+// memory: each pushing wave waits until its own stores are acknowledged
+// (`s_waitcnt vmcnt(0)`; they are sc0 sc1 stores, so acknowledged at system
+// scope) before it ends.  Without it the owner's chain could read a receive
+// slot before the pushed slice landed — seen as a wrong sum in about one run
+// in two of the pipelined host-fed test (tests/test_gpu_xgmi.py), none in 32
+// runs since.  A full system-scope release fence per wave (L2 writeback) was
+// tried first: correct, but 25x slower rounds.
 __device__ __forceinline__ void peer_stores_done() {
-    __atomic_thread_fence(__ATOMIC_RELEASE);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
 }
 
 // f32 slice -> peer receive slot; ZERO: then zero the slice (the ring's

@@ -31,7 +31,8 @@ def _port() -> int:
 
 def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull", **env_extra) -> list:
     port = _port()
-    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather, **env_extra)
+    env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather, ONO_XGMI_DIAG="1",
+               **env_extra)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), str(port),
                                json.dumps(cases)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for r in range(n)]

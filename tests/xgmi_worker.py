@@ -83,8 +83,25 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
             bad = np.flatnonzero(~O.same_or_both_nan(got, expect[rank]))
             if bad.size:
                 i = bad[0]
-                return (f"round {rd}: {bad.size}/{length} differ, first at {i}: "
-                        f"0x{bits(got)[i]:08x} vs 0x{bits(expect[rank])[i]:08x}")
+                msg = (f"round {rd}: {bad.size}/{length} differ, first at {i}: "
+                       f"0x{bits(got)[i]:08x} vs 0x{bits(expect[rank])[i]:08x}")
+                if os.environ.get("ONO_XGMI_DIAG"):  # where the wrong elements sit (chunk, sub-round) and what they hold
+                    off = [0]
+                    for q in range(n):
+                        off.append(off[-1] + length // n + (1 if q < length % n else 0))
+                    sub = max(64, (int(os.environ.get("ONO_HOST_CHUNK_MIB", "16")) << 18) // n // 64 * 64)
+                    where = {}
+                    for b in bad:
+                        q = int(np.searchsorted(off, b, side="right") - 1)
+                        key = (q, int((b - off[q]) // sub))
+                        where[key] = where.get(key, 0) + 1
+                    zeros = int((got[bad] == 0).sum())
+                    own = np.float32(ins[rank][bad]) / np.float32(n)
+                    msg += f" | by (chunk, subround): {sorted(where.items())[:8]} zeros={zeros}"
+                    msg += f" own/n={int((got[bad] == own).sum())}"
+                    lo, hi = int(bad.min()), int(bad.max())
+                    msg += f" span=[{lo},{hi}]"
+                return msg
             if bits(res_after).any():
                 return f"round {rd}: residual not zeroed ({np.count_nonzero(bits(res_after))} left)"
         return None
