@@ -110,6 +110,19 @@ int ono_f16_decode_scale(float *out, const uint16_t *in, size_t n, float divisor
  * bookkeeping — zero_kept=1: g = 0 where |g| >= t (worker_ring.rs:128-131),
  * zero_kept=0: g = 0 where |g| < t (:183-187).                               */
 size_t ono_sparse_max_bytes(size_t n);
+/* calculate_threshold (protocol.rs:33-49) on the device: the k-th smallest
+ * |g| of the sample in f32::total_cmp order, k = (m as f32 * (1 - r)) as
+ * usize (at most m - 1), then f32::max with f16::MIN_POSITIVE.  The sample is
+ * every value (idx_host NULL, m == n <= 16384) or the m <= 16384 indices the
+ * caller drew (idx_host: the reference draws them with rand 0.9.4's
+ * choose_multiple = rand::seq::index::sample(rng, n, 16384)).  Blocking.     */
+int ono_sparse_threshold(float *t_out, const float *g_dev, size_t n, const uint32_t *idx_host, size_t m, float r,
+                         void *stream);
+/* The deterministic stand-in sampler (Floyd's algorithm over a splitmix64
+ * stream at *state): `amount` distinct indices of [0, len) — all of them, with
+ * no draws, when amount == len.  NOT rand 0.9.4's StdRng; used when no
+ * sampler is installed, and restated by the CPU oracle.                     */
+int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t amount);
 int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
                     float threshold, void *stream);
 int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
@@ -146,12 +159,37 @@ int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device
 /* The TCP edge: the same manager over the worker's own sockets — fd_prev the
  * accepted connection from the previous worker, fd_next the connection to the
  * next (worker/src/builder.rs:272-311; the caller keeps ownership).  Frames
- * are the reference's byte for byte ([u64 BE len][u32 BE kind=1][f16 LE],
- * comms/src/protocol/msg.rs:120-191), so MI355X workers and reference Rust
- * workers can form one ring.  f16 wire, hop schedule; the hop arithmetic runs
- * in HBM (fused codec kernels), one D2H + H2D of the chunk per hop.          */
+ * are the reference's byte for byte ([u64 BE len][u32 BE kind][payload],
+ * comms/src/protocol/msg.rs:120-191): DenseGrad (kind 1/2, f16 LE) or, with
+ * ono_ring_set_sparse, SparseGrad (kind 3/4), so MI355X workers and reference
+ * Rust workers of either serializer form one ring.  Errors: a frame of
+ * another valid kind (0 control, 5 params, 6 data chunk) or of the wrong
+ * length -> ONO_E_PROTO ("Received an invalid worker event"); a kind byte
+ * >= 7 (msg.rs:187), a malformed sparse stream, a socket failure -> ONO_E_IO.
+ * f16 wire, hop schedule; the hop arithmetic runs in HBM (fused codec
+ * kernels), one D2H + H2D of the chunk per hop.                              */
 int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
                         int fd_next);
+/* The SparseCapable serializer of this worker (SerializerSpec sparse_capable{r};
+ * Compressor::compress, comms/src/handles/compressor.rs:71-98): every chunk it
+ * pushes is sent as a SparseGrad frame (kind 3) of its values with
+ * |g| >= t, t = calculate_threshold(chunk, r); the scatter then zeroes only the
+ * sent values of the residual (worker_ring.rs:126-133) and the gather keeps
+ * only the sent values in grad (:177-193).  ratio in (0, 1]; 0 = the Base
+ * (dense f16) serializer.  TCP rings only (n > 1): inside a node the dense
+ * schedules move fewer bytes than a sparse stream is worth.  Every worker
+ * accepts both gradient kinds whatever its own serializer
+ * (handles/worker.rs:102-108).  `seed` starts the default sampler's stream.   */
+int ono_ring_set_sparse(ono_ring *ring, float ratio, uint64_t seed);
+/* Draws the threshold sample of one push: `amount` = min(len, 16384) distinct
+ * indices of [0, len) into idx; return 0 on success.  Called for every sparse
+ * push (also when amount == len, so a caller-side RNG stays in step with the
+ * reference's, which draws from its StdRng on every calculate_threshold).
+ * A Rust integration installs rand::seq::index::sample over the Compressor's
+ * StdRng — the reference's choose_multiple draws exactly those indices.
+ * NULL restores the default (ono_sparse_sample_default).                     */
+typedef int (*ono_sample_fn)(void *ctx, size_t len, uint32_t *idx, size_t amount);
+int ono_ring_set_sampler(ono_ring *ring, ono_sample_fn fn, void *ctx);
 int ono_ring_destroy(ono_ring *ring);
 /* the owned buckets (device pointers): grad = WorkerRingManager.grad,
  * residual = WorkerRingManager.residual                                      */
@@ -343,6 +381,84 @@ int ono_ps_destroy(ono_ps *ps);
 /* grad_dev: this worker's gradient (nparams); params_dev: receives the
  * updated full parameter vector.  Stream-ordered.                           */
 int ono_ps_step(ono_ps *ps, const float *grad_dev, float *params_dev, void *stream);
+
+/* ===================================================================== */
+/* Exchange plans: the N > 1 schedules as data                             */
+/* ===================================================================== */
+/* Every collective schedule of pull_grads (ALLREDUCE incl. its segments,
+ * HOPS, DIRECT; either wire) and of ono_ps_step is built as a list of steps by
+ * a pure host function and executed by one interpreter (RCCL calls, HIP
+ * kernels, memsets, copies, side-stream forks / joins).  The same lists are
+ * exported here so a CPU test can check them for every rank count and bucket
+ * length — matched sends / receives per group, offsets in bounds, chunks
+ * tiling [0, N), no overlapping accesses across the two streams — and run
+ * them with host copies against the oracle, without an 8-GPU node.
+ * Operand i of a step is (buf[i], off[i]): an element offset into one of the
+ * rank's buffers (ono_plan_buf; sizes from ono_plan_buffers).               */
+typedef enum {
+    ONO_PLAN_GROUP_BEGIN = 0, /* ncclGroupStart                                        */
+    ONO_PLAN_SEND = 1,        /* ref0, count, dtype -> peer                              */
+    ONO_PLAN_RECV = 2,        /* ref0, count, dtype <- peer                              */
+    ONO_PLAN_GROUP_END = 3,   /* ncclGroupEnd                                          */
+    ONO_PLAN_ALLREDUCE = 4,   /* ref1[0, count) = sum over ranks of ref0[0, count) (f32) */
+    ONO_PLAN_REDUCE_SCATTER = 5, /* ref1[0, count) = sum over ranks of ref0[pos*count, +count) */
+    ONO_PLAN_ALL_GATHER = 6,  /* ref1[q*count, +count) = rank q's ref0[0, count)         */
+    ONO_PLAN_KERNEL = 7,      /* op over count elements                                  */
+    ONO_PLAN_MEMSET = 8,      /* ref0[0, count) = 0                                      */
+    ONO_PLAN_COPY = 9,        /* ref0[0, count) = ref1[0, count)                         */
+    ONO_PLAN_FORK = 10,       /* the side stream waits for the main stream's work so far */
+    ONO_PLAN_JOIN = 11        /* the main stream waits for the side stream's work so far */
+} ono_plan_kind;
+typedef enum {
+    ONO_POP_ENCODE_ZERO = 0,     /* [out wire, chunk]: out = enc(chunk); chunk = 0          */
+    ONO_POP_ADD_ENCODE_ZERO = 1, /* [out, acc, in]: x = acc + dec(in); out = enc(x); acc = 0 */
+    ONO_POP_ADD_FINISH = 2,      /* [grad, out, acc, in]: x = acc + dec(in); grad = x / d;
+                                    out = enc(x); acc = 0                                   */
+    ONO_POP_DECODE_SCALE = 3,    /* [out f32, in wire]: out = dec(in) / d                   */
+    ONO_POP_DIRECT = 4,          /* [grad, out | NONE, in_0 .. in_k-1]: p = in_0,
+                                    p = in_j + wire(p); grad = p / d; out = enc(p) (f16) or
+                                    grad (f32); zero in_k-1, or every in_j when flag      */
+    ONO_POP_SCALE_ZERO = 5,      /* [dst, src, zero | NONE]: dst = src / d; zero = 0        */
+    ONO_POP_OPT_UPDATE = 6       /* [g, w]: the store's fused (+0, / d, optimizer) update of
+                                    a shard; flag = zero g afterwards                       */
+} ono_plan_op;
+typedef enum {
+    ONO_PB_NONE = -1,
+    ONO_PB_RESIDUAL = 0, ONO_PB_GRAD = 1, /* the buckets (f32, size)                       */
+    ONO_PB_WIRE0 = 2, ONO_PB_WIRE1 = 3,   /* hop wire slots (wire dtype, maxchunk + 4)     */
+    ONO_PB_RBUF = 4,                      /* direct receive slots (f32, n x (maxchunk + 4)) */
+    ONO_PB_GSTAGE = 5,                    /* direct f16 all-gather staging (n x (maxchunk + 4)) */
+    ONO_PB_MSG = 6,                       /* the owner's f16 message (maxchunk + 4)          */
+    ONO_PB_GIN = 7, ONO_PB_GPAD = 8, ONO_PB_GSHARD = 9, /* PS: gradient in (nparams), padded
+                                             copy (n x shard), reduced shard (shard)        */
+    ONO_PB_PPAD = 10, ONO_PB_PARAMS = 11, /* PS: padded parameters, parameters out           */
+    ONO_PB_COUNT = 12
+} ono_plan_buf;
+#define ONO_PLAN_REFS (ONO_MAX_INPUTS + 2)
+typedef struct {
+    int32_t kind;   /* ono_plan_kind */
+    int32_t op;     /* ono_plan_op (KERNEL) */
+    int32_t peer;   /* SEND / RECV */
+    int32_t dtype;  /* ono_wire: element type of the step's data */
+    int32_t stream; /* 0 = the caller's stream, 1 = the side stream */
+    int32_t nref;
+    int32_t flag;
+    float divisor;
+    uint64_t count;
+    int32_t buf[ONO_PLAN_REFS];
+    uint64_t off[ONO_PLAN_REFS];
+} ono_plan_step;
+/* pull_grads of rank pos: algo ALLREDUCE (f32 wire; `segments` as
+ * ono_ring_set_pipeline resolves them, >= 1), HOPS or DIRECT.  Writes up to cap
+ * steps; *count = the plan's length (call with cap 0 to size it).           */
+int ono_plan_pull_grads(int algo, int wire, int pos, int nranks, size_t size, int segments, ono_plan_step *steps,
+                        size_t cap, size_t *count);
+/* ono_ps_step of rank pos over the RCCL communicator (reduce-scatter, fused
+ * update, all-gather; shards of ceil(nparams / nranks), zero-padded)        */
+int ono_plan_ps_step(int pos, int nranks, size_t nparams, ono_plan_step *steps, size_t cap, size_t *count);
+/* element counts of the plan buffers (ONO_PB_COUNT entries) for a ring of
+ * nranks over `size` elements and a PS of nparams                           */
+int ono_plan_buffers(int nranks, size_t size, size_t nparams, uint64_t *counts);
 
 #ifdef __cplusplus
 }

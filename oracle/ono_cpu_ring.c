@@ -14,6 +14,14 @@
  *   gather:  grad[own] = residual[own]; forward / copy f16 chunks; then /= n.
  * Timed region = the pull_grads() rounds only (residual refill is outside).
  *
+ * Serializer: Base (dense f16, default) or, with --sparse R, SparseCapable{R}
+ * (compressor.rs:71-98): every push is a SparseGrad frame (kind 3) of the
+ * values with |g| >= calculate_threshold(chunk, R) (protocol.rs:33-86; sample
+ * from ono_ref_sample_default at --sparse-seed above 16384 values); the scatter
+ * zeroes only the sent values (worker_ring.rs:126-133), the gather keeps only
+ * the sent values (:177-193).  Either serializer receives both kinds: a
+ * SparseGrad lifts into the zero-filled decode buffer (handles/worker.rs:102-108).
+ *
  * usage: ono_cpu_ring --ranks N --len L --rounds R [--seed S] [--check] [--no-pin]
  * prints one JSON line: {"ranks":..,"len":..,"rounds":..,"s_per_round":..,"gib_s":..,"check":..}
  *
@@ -41,12 +49,15 @@
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
+#include <math.h>
 
 typedef struct {
     int rank, n, rounds, pin;
     size_t len;
     uint64_t seed;
     int listen_fd, port_next, timer;
+    float ratio;        /* 0: Base serializer, else SparseCapable{ratio} */
+    uint64_t state;     /* the default sampler's stream */
     float *residual, *pristine, *grad;
     double elapsed;
 } worker_t;
@@ -116,6 +127,43 @@ static void set_nb(int fd) {
     fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
 }
 
+
+/* push_grad (handles/worker.rs:157-174): the frame of this worker's serializer
+ * for chunk ch; *t = the SparseCapable threshold (unused for Base). */
+static size_t push_frame(worker_t *w, const float *ch, size_t cl, uint16_t *comp, uint8_t *frame, uint32_t *sidx,
+                         float *t) {
+    if (w->ratio <= 0.0f) {
+        ono_ref_f16_encode(comp, ch, cl);
+        return ono_ref_frame_dense(frame, comp, cl, 0);
+    }
+    const size_t m = cl < 16384 ? cl : 16384;
+    if (cl > 16384) ono_ref_sample_default(&w->state, cl, sidx, m);
+    *t = ono_ref_sparse_threshold_sample(ch, cl, cl > 16384 ? sidx : NULL, m, w->ratio);
+    size_t nb = ono_ref_grad_drop(frame + 12, ch, cl, *t);
+    uint64_t len = 4 + (uint64_t)nb;
+    for (int q = 0; q < 8; q++) frame[q] = (uint8_t)(len >> (56 - 8 * q));
+    frame[8] = 0; frame[9] = 0; frame[10] = 0; frame[11] = 3; /* SparseGrad, is_last = false */
+    return 12 + nb;
+}
+
+/* recv_event (handles/worker.rs:82-108): a DenseGrad decodes, a SparseGrad
+ * lifts into the zero-filled buffer; returns the values it holds. */
+static size_t recv_grad(const uint8_t *b, size_t got, float *dec, size_t cap) {
+    const uint8_t kind = b[11];
+    if (kind == 1 || kind == 2) {
+        size_t m = (got - 12) / 2;
+        ono_ref_f16_decode(dec, (const uint16_t *)(b + 12), m);
+        return m;
+    }
+    if (kind == 3 || kind == 4) {
+        size_t m = 0;
+        if (ono_ref_grad_lift(dec, cap, &m, b + 12, got - 12)) { fprintf(stderr, "sparse lift failed\n"); exit(3); }
+        return m;
+    }
+    fprintf(stderr, "invalid worker event (kind %u)\n", kind);
+    exit(3);
+}
+
 static void *worker_main(void *arg) {
     worker_t *w = (worker_t *)arg;
     if (w->pin) {
@@ -137,10 +185,12 @@ static void *worker_main(void *arg) {
     size_t *off = (size_t *)malloc(sizeof(size_t) * (size_t)(n + 1));
     ono_ref_split_chunks(w->len, (size_t)n, off);
     size_t maxc = off[1] - off[0];
+    const size_t cap = 12 + 8 + 10 * ((maxc + 1) / 2) + 2 * maxc + 16;  /* a frame of either kind */
     uint16_t *comp = (uint16_t *)malloc(2 * maxc + 16);           /* compression_buf */
-    uint8_t *frame = (uint8_t *)malloc(12 + 2 * maxc + 16);
-    uint32_t *inbuf = (uint32_t *)malloc(12 + 2 * maxc + 16);      /* 4-B aligned, source.rs */
+    uint8_t *frame = (uint8_t *)malloc(cap);
+    uint32_t *inbuf = (uint32_t *)malloc(cap);                      /* 4-B aligned, source.rs */
     float *dec = (float *)malloc(sizeof(float) * (maxc + 4));      /* handle-owned Vec<f32> */
+    uint32_t *sidx = (uint32_t *)malloc(sizeof(uint32_t) * 16384);
 
     for (int round = 0; round < w->rounds; round++) {
         memcpy(w->residual, w->pristine, w->len * sizeof(float));
@@ -150,17 +200,16 @@ static void *worker_main(void *arg) {
         int i = w->rank;
         for (int s = 0; s < n - 1; s++) {
             size_t cl = off[i + 1] - off[i];
-            ono_ref_f16_encode(comp, w->residual + off[i], cl);
-            size_t fl = ono_ref_frame_dense(frame, comp, cl, 0);
+            float t = 0.0f;
+            size_t fl = push_frame(w, w->residual + off[i], cl, comp, frame, sidx, &t);
             size_t got = 0;
-            if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, 12 + 2 * maxc + 16, &got)) {
+            if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, cap, &got)) {
                 fprintf(stderr, "xchg failed\n"); exit(3);
             }
-            memset(w->residual + off[i], 0, cl * sizeof(float));
-            const uint8_t *b = (const uint8_t *)inbuf;
-            size_t m = (got - 12) / 2;
-            ono_ref_f16_decode(dec, (const uint16_t *)(b + 12), m);
+            if (w->ratio <= 0.0f) memset(w->residual + off[i], 0, cl * sizeof(float));
+            else for (size_t j = 0; j < cl; j++) if (fabsf(w->residual[off[i] + j]) >= t) w->residual[off[i] + j] = 0.0f;
             i = (i + n - 1) % n;
+            size_t m = recv_grad((const uint8_t *)inbuf, got, dec, off[i + 1] - off[i]);
             float *ch = w->residual + off[i];
             size_t k = off[i + 1] - off[i] < m ? off[i + 1] - off[i] : m;
             for (size_t j = 0; j < k; j++) ch[j] += dec[j];
@@ -173,18 +222,19 @@ static void *worker_main(void *arg) {
         } else {
             for (int j = 0; j < n - 1; j++) {
                 size_t cl = off[i + 1] - off[i];
-                ono_ref_f16_encode(comp, w->grad + off[i], cl);
-                size_t fl = ono_ref_frame_dense(frame, comp, cl, 0);
+                float t = 0.0f;
+                size_t fl = push_frame(w, w->grad + off[i], cl, comp, frame, sidx, &t);
                 size_t got = 0;
-                if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, 12 + 2 * maxc + 16, &got)) {
+                if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, cap, &got)) {
                     fprintf(stderr, "xchg failed\n"); exit(3);
                 }
+                if (w->ratio > 0.0f)
+                    for (size_t q = 0; q < cl; q++) if (fabsf(w->grad[off[i] + q]) < t) w->grad[off[i] + q] = 0.0f;
                 if (j == 0) memset(w->residual + off[i], 0, cl * sizeof(float));
-                const uint8_t *b = (const uint8_t *)inbuf;
-                size_t m = (got - 12) / 2;
-                ono_ref_f16_decode(dec, (const uint16_t *)(b + 12), m);
                 i = (i + n - 1) % n;
-                memcpy(w->grad + off[i], dec, (off[i + 1] - off[i]) * sizeof(float));
+                size_t m = recv_grad((const uint8_t *)inbuf, got, dec, off[i + 1] - off[i]);
+                if (m != off[i + 1] - off[i]) { fprintf(stderr, "gather: chunk length mismatch\n"); exit(3); }
+                memcpy(w->grad + off[i], dec, m * sizeof(float));
             }
             ono_ref_normalize(w->grad, w->len, (size_t)n);
         }
@@ -193,7 +243,7 @@ static void *worker_main(void *arg) {
     }
     if (fd_next >= 0) close(fd_next);
     if (fd_prev >= 0) close(fd_prev);
-    free(off); free(comp); free(frame); free(inbuf); free(dec);
+    free(off); free(comp); free(frame); free(inbuf); free(dec); free(sidx);
     return NULL;
 }
 
@@ -214,7 +264,7 @@ static int listen_on(int port, int *bound) {
 
 /* one worker of a ring whose other members are other processes */
 static int single_worker(int rank, int n, size_t len, int rounds, uint64_t seed, int listen_port,
-                         int next_port, const char *out) {
+                         int next_port, const char *out, float ratio, uint64_t sstate) {
     worker_t w = {0};
     int port = 0;
     w.listen_fd = listen_on(listen_port, &port);
@@ -222,7 +272,7 @@ static int single_worker(int rank, int n, size_t len, int rounds, uint64_t seed,
     printf("{\"port\": %d}\n", port);
     fflush(stdout);
     w.rank = rank; w.n = n; w.rounds = rounds; w.pin = 0; w.timer = 1;
-    w.len = len; w.seed = seed; w.port_next = next_port;
+    w.len = len; w.seed = seed; w.port_next = next_port; w.ratio = ratio; w.state = sstate;
     w.residual = (float *)malloc(len * sizeof(float));
     w.pristine = (float *)malloc(len * sizeof(float));
     w.grad = (float *)calloc(len, sizeof(float));
@@ -245,6 +295,8 @@ static int single_worker(int rank, int n, size_t len, int rounds, uint64_t seed,
 
 int main(int argc, char **argv) {
     int n = 2, rounds = 3, check = 0, pin = 1, rank = -1, listen_port = 0, next_port = -1;
+    float ratio = 0.0f;
+    uint64_t sstate = 0;
     size_t len = 109386;
     uint64_t seed = 0x0402026;
     const char *out = NULL;
@@ -258,13 +310,16 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--seed") && a + 1 < argc) seed = strtoull(argv[++a], 0, 0);
         else if (!strcmp(argv[a], "--check")) check = 1;
+        else if (!strcmp(argv[a], "--sparse") && a + 1 < argc) ratio = (float)atof(argv[++a]);
+        else if (!strcmp(argv[a], "--sparse-seed") && a + 1 < argc) sstate = strtoull(argv[++a], 0, 0);
         else if (!strcmp(argv[a], "--no-pin")) pin = 0;
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
+    if (ratio < 0.0f || ratio > 1.0f) { fprintf(stderr, "--sparse takes a ratio in (0, 1]\n"); return 1; }
     if (n < 1 || len < (size_t)n || rounds < 1) { fprintf(stderr, "need len >= ranks >= 1\n"); return 1; }
     if (rank >= 0) {
         if (rank >= n || (n > 1 && next_port <= 0)) { fprintf(stderr, "need rank < ranks, --next-port\n"); return 1; }
-        return single_worker(rank, n, len, rounds, seed, listen_port, next_port, out);
+        return single_worker(rank, n, len, rounds, seed, listen_port, next_port, out, ratio, sstate);
     }
     worker_t *w = (worker_t *)calloc((size_t)n, sizeof(worker_t));
     int *ports = (int *)calloc((size_t)n, sizeof(int));

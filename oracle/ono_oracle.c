@@ -12,6 +12,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
 static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
@@ -161,6 +166,89 @@ int ono_ref_ring_pull_grads(float *const *residual, float *const *grad, int n, s
         for (int r = 0; r < n; r++) ono_ref_normalize(grad[r], len, (size_t)n);
     }
     free(off); free(m16); free(m32); free(mlen); free(idx);
+    return 0;
+}
+
+/* One push of a chunk by a worker with serializer `ratio` (0 = Base): the
+ * values the receiver ends up with (its decode, or its lift into a zero-filled
+ * buffer) in msg; the threshold in *t (dense: +inf, nothing is "unsent").    */
+static void push_chunk(const float *ch, size_t cl, float ratio, uint64_t *state, float *msg, float *t) {
+    if (ratio <= 0.0f) {
+        for (size_t i = 0; i < cl; i++) msg[i] = ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i]));
+        *t = -1.0f;
+        return;
+    }
+    const size_t m = cl < 16384 ? cl : 16384;
+    uint32_t *idx = NULL;
+    if (cl > 16384) {
+        idx = (uint32_t *)malloc(m * sizeof(uint32_t));
+        ono_ref_sample_default(state, cl, idx, m);
+    }
+    *t = ono_ref_sparse_threshold_sample(ch, cl, idx, m, ratio);
+    free(idx);
+    for (size_t i = 0; i < cl; i++)
+        msg[i] = fabsf(ch[i]) >= *t ? ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i])) : 0.0f;
+}
+
+int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, int n, size_t len,
+                                   const float *ratio, uint64_t *state) {
+    if (n <= 0) return -1;
+    size_t *off = (size_t *)malloc(sizeof(size_t) * ((size_t)n + 1));
+    size_t nch = ono_ref_split_chunks(len, (size_t)n, off);
+    if (nch < (size_t)n) { free(off); return -1; }
+    size_t maxc = off[1] - off[0];
+    float *msg = (float *)malloc(sizeof(float) * (size_t)n * (maxc ? maxc : 1));
+    float *thr = (float *)malloc(sizeof(float) * (size_t)n);
+    int *idx = (int *)malloc(sizeof(int) * (size_t)n);
+    /* scatter (worker_ring.rs:112-147) */
+    for (int r = 0; r < n; r++) idx[r] = r;
+    for (int s = 0; s < n - 1; s++) {
+        for (int r = 0; r < n; r++) {
+            int c = idx[r];
+            float *ch = residual[r] + off[c];
+            size_t cl = off[c + 1] - off[c];
+            push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r]);
+            if (ratio[r] <= 0.0f) memset(ch, 0, cl * sizeof(float));               /* :133 */
+            else for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) >= thr[r]) ch[i] = 0.0f; /* :128-131 */
+        }
+        for (int r = 0; r < n; r++) {
+            int p = (r + n - 1) % n;
+            idx[r] = (idx[r] + n - 1) % n;
+            int c = idx[r];
+            float *ch = residual[r] + off[c];
+            size_t cl = off[c + 1] - off[c];
+            for (size_t i = 0; i < cl; i++) ch[i] += msg[(size_t)p * maxc + i]; /* :141-143 */
+        }
+    }
+    /* gather (worker_ring.rs:155-204) */
+    for (int r = 0; r < n; r++) {
+        idx[r] = (r + 1) % n;
+        int c = idx[r];
+        memcpy(grad[r] + off[c], residual[r] + off[c], (off[c + 1] - off[c]) * sizeof(float)); /* :166 */
+    }
+    if (n == 1) {
+        memset(residual[0] + off[idx[0]], 0, (off[idx[0] + 1] - off[idx[0]]) * sizeof(float));
+    } else {
+        for (int j = 0; j < n - 1; j++) {
+            for (int r = 0; r < n; r++) {
+                int c = idx[r];
+                float *ch = grad[r] + off[c];
+                size_t cl = off[c + 1] - off[c];
+                push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r]);
+                if (ratio[r] > 0.0f)
+                    for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) < thr[r]) ch[i] = 0.0f; /* :183-187 */
+                if (j == 0) memset(residual[r] + off[c], 0, cl * sizeof(float));            /* :191-193 */
+            }
+            for (int r = 0; r < n; r++) {
+                int p = (r + n - 1) % n;
+                idx[r] = (idx[r] + n - 1) % n;
+                int c = idx[r];
+                memcpy(grad[r] + off[c], msg + (size_t)p * maxc, (off[c + 1] - off[c]) * sizeof(float)); /* :200 */
+            }
+        }
+        for (int r = 0; r < n; r++) ono_ref_normalize(grad[r], len, (size_t)n);
+    }
+    free(off); free(msg); free(thr); free(idx);
     return 0;
 }
 
@@ -364,6 +452,51 @@ float ono_ref_sparse_threshold_full(const float *g, size_t n, float r) {
 static void put_le(uint8_t *b, uint64_t v, int bytes) {
     for (int i = 0; i < bytes; i++) b[i] = (uint8_t)(v >> (8 * i));
 }
+/* protocol.rs:33-49 over a sample: values |g[idx[i]]|, total_cmp order of the
+ * non-negative bit patterns (qsort; the rank statistic does not depend on how
+ * select_nth_unstable_by gets there), then the NaN-ignoring f32::max.        */
+float ono_ref_sparse_threshold_sample(const float *g, size_t n, const uint32_t *idx, size_t m, float r) {
+    if (n == 0 || m == 0) return 0.0f;
+    float *s = (float *)malloc(m * sizeof(float));
+    for (size_t i = 0; i < m; i++) s[i] = fabsf(g[idx ? idx[i] : i]);
+    qsort(s, m, sizeof(float), cmp_total);
+    float kf = (float)m * (1.0f - r);
+    size_t k = kf <= 0.0f ? 0 : (size_t)kf; /* `as usize` saturates */
+    if (k > m - 1) k = m - 1;
+    float t = s[k];
+    free(s);
+    const float min_pos_f16 = 6.103515625e-05f;
+    return t > min_pos_f16 ? t : min_pos_f16; /* f32::max ignores a NaN t */
+}
+
+static uint64_t sm_next(uint64_t *x) {
+    *x += 0x9E3779B97F4A7C15ULL;
+    return mix64(*x);
+}
+/* Floyd: for j in len-m .. len: t = draw % (j+1); take t, or j if t was taken */
+void ono_ref_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t m) {
+    if (m >= len) {
+        for (size_t i = 0; i < len; i++) idx[i] = (uint32_t)i;
+        return;
+    }
+    /* membership: open addressing over a power-of-two table */
+    size_t cap = 1;
+    while (cap < 4 * m) cap <<= 1;
+    uint32_t *tab = (uint32_t *)malloc(cap * sizeof(uint32_t));
+    memset(tab, 0xFF, cap * sizeof(uint32_t));
+    size_t c = 0;
+    for (size_t j = len - m; j < len; j++) {
+        uint32_t t = (uint32_t)(sm_next(state) % (uint64_t)(j + 1));
+        for (int pass = 0; pass < 2; pass++) {
+            size_t h = (size_t)(mix64(t) & (cap - 1));
+            while (tab[h] != 0xFFFFFFFFu && tab[h] != t) h = (h + 1) & (cap - 1);
+            if (tab[h] == 0xFFFFFFFFu) { tab[h] = t; idx[c++] = t; break; }
+            t = (uint32_t)j; /* taken: take j (never taken before) */
+        }
+    }
+    free(tab);
+}
+
 size_t ono_ref_grad_drop(uint8_t *buf, const float *g, size_t n, float threshold) {
     size_t o = 0, last_end = 0, i = 0;
     put_le(buf + o, (uint64_t)n, 8); o += 8;
@@ -421,11 +554,6 @@ size_t ono_ref_frame_dense(uint8_t *out, const uint16_t *h, size_t n, int is_las
 /* Synthetic gradients.  Classes by (h1>>32)%100:
  *   0 -> signed zero, 1 -> f16-subnormal magnitude, 2 -> exact f16 rounding
  *   tie, else ≈N(0, 0.0098^2) from a 4-term Irwin-Hall sum.                   */
-static inline uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    return z ^ (z >> 31);
-}
 void ono_ref_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset) {
     const uint64_t G = 0x9E3779B97F4A7C15ULL;
     uint64_t key = mix64(seed + G * (rank + 1));

@@ -48,6 +48,16 @@ size_t ono_ref_split_chunks(size_t len, size_t n, size_t *offsets);
  * Returns 0, or -1 when the reference would panic (len < nranks, len == 0).  */
 int ono_ref_ring_pull_grads(float *const *residual, float *const *grad, int nranks,
                             size_t len, int wire);
+/* The same round with each worker's serializer: ratio[r] == 0 -> Base (dense
+ * f16 DenseGrad), ratio[r] in (0, 1] -> SparseCapable{ratio[r]}: every push
+ * sends the values with |g| >= calculate_threshold(chunk, ratio) (sample drawn
+ * with ono_ref_sample_default at state[r] above 16384 values; state advanced),
+ * the scatter zeroes only the sent values (worker_ring.rs:126-133), the
+ * gather keeps only the sent values in grad (:177-193).  Receivers add
+ * (scatter) or copy (gather) the decoded / lifted chunk: a SparseGrad lifts
+ * into a zero-filled buffer (comms/src/handles/worker.rs:102-108).          */
+int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, int nranks, size_t len,
+                                   const float *ratio, uint64_t *state);
 
 /* ---- sum-and-scale: out[i] = (((in0+in1)+in2)+...)/divisor ------------------
  * The f32-wire ring's per-chunk arithmetic (worker_ring.rs:141-143 then
@@ -98,6 +108,15 @@ int ono_ref_wild_pull_params(ono_ref_wild *w, float *out, size_t n);
  * Threshold is only rng-independent when len <= 16384 (the sample is then the
  * whole gradient); returns NaN for longer inputs (rand 0.9.4 StdRng needed).  */
 float ono_ref_sparse_threshold_full(const float *g, size_t n, float r);
+/* calculate_threshold over a drawn sample (protocol.rs:33-49): idx = m sample
+ * indices (NULL: every value, m == n).  f32::abs, select_nth_unstable_by
+ * total_cmp at k = (m as f32 * (1 - r)) as usize (<= m - 1), f32::max with
+ * f16::MIN_POSITIVE.                                                          */
+float ono_ref_sparse_threshold_sample(const float *g, size_t n, const uint32_t *idx, size_t m, float r);
+/* The stand-in sampler (NOT rand 0.9.4): Floyd's algorithm over splitmix64 at
+ * *state; the identity with no draws when m == len.  Restated independently
+ * of the product's ono_sparse_sample_default, which must equal it.          */
+void ono_ref_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t m);
 size_t ono_ref_grad_drop(uint8_t *buf, const float *g, size_t n, float threshold);
 int ono_ref_grad_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, size_t nbytes);
 

@@ -80,6 +80,12 @@ def lib():
         L.ono_ref_frame_dense.restype = C.c_size_t
         L.ono_ref_frame_dense.argtypes = [_u8p, _u16p, C.c_size_t, C.c_int]
         L.ono_ref_synth.argtypes = [_fp, C.c_size_t, C.c_uint64, C.c_uint64, C.c_size_t]
+        L.ono_ref_sparse_threshold_sample.restype = C.c_float
+        L.ono_ref_sparse_threshold_sample.argtypes = [_fp, C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t, C.c_float]
+        L.ono_ref_sample_default.argtypes = [C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t]
+        L.ono_ref_ring_pull_grads_sparse.restype = C.c_int
+        L.ono_ref_ring_pull_grads_sparse.argtypes = [C.POINTER(_fp), C.POINTER(_fp), C.c_int, C.c_size_t,
+                                                     C.POINTER(C.c_float), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -127,6 +133,41 @@ def ring_pull_grads(residuals: list[np.ndarray], wire: str = "f16"):
     if rc != 0:
         raise ValueError("reference panics: fewer chunks than ranks")
     return grads, res
+
+
+def ring_pull_grads_sparse(residuals: list[np.ndarray], ratios, states):
+    """The round with per-worker serializers (ratio 0 = Base dense f16, else
+    SparseCapable{ratio}; states = the default samplers' streams).  Returns
+    (grads, residuals_after, states_after)."""
+    n = len(residuals)
+    res = [np.array(r, dtype=np.float32, copy=True) for r in residuals]
+    length = res[0].size
+    grads = [np.zeros(length, np.float32) for _ in range(n)]
+    rp = (_fp * n)(*[_f(r) for r in res])
+    gp = (_fp * n)(*[_f(g) for g in grads])
+    rat = (C.c_float * n)(*[float(x) for x in ratios])
+    st = (C.c_uint64 * n)(*[int(x) & (2 ** 64 - 1) for x in states])
+    if lib().ono_ref_ring_pull_grads_sparse(rp, gp, n, length, rat, st) != 0:
+        raise ValueError("reference panics: fewer chunks than ranks")
+    return grads, res, [st[i] for i in range(n)]
+
+
+def sample_default(state: int, length: int, amount: int):
+    """The stand-in threshold sampler: (indices, next state)."""
+    st = C.c_uint64(state & (2 ** 64 - 1))
+    out = np.empty(max(amount, 1), np.uint32)
+    lib().ono_ref_sample_default(C.byref(st), length, out.ctypes.data_as(C.POINTER(C.c_uint32)), amount)
+    return out[:amount].copy(), st.value
+
+
+def sparse_threshold_sample(g: np.ndarray, r: float, idx=None) -> float:
+    """calculate_threshold over the sample idx (None: every value)."""
+    g = np.ascontiguousarray(g, dtype=np.float32)
+    if idx is None:
+        return float(lib().ono_ref_sparse_threshold_sample(_f(g), g.size, None, g.size, r))
+    ix = np.ascontiguousarray(idx, dtype=np.uint32)
+    return float(lib().ono_ref_sparse_threshold_sample(_f(g), g.size, ix.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                       ix.size, r))
 
 
 def sum_scale(ins: list[np.ndarray], divisor: float) -> np.ndarray:
@@ -322,7 +363,7 @@ class CpuRingWorker:
     worker and a reference worker can share one ring."""
 
     def __init__(self, rank: int, ranks: int, length: int, next_port: int, rounds: int = 1,
-                 seed: int = 0x0402026, listen_port: int = 0):
+                 seed: int = 0x0402026, listen_port: int = 0, sparse: float = 0.0, sparse_seed: int = 0):
         import json
         import tempfile
 
@@ -334,7 +375,10 @@ class CpuRingWorker:
         self.proc = subprocess.Popen(
             [CPU_RING, "--rank", str(rank), "--ranks", str(ranks), "--len", str(length),
              "--next-port", str(next_port), "--listen-port", str(listen_port), "--rounds", str(rounds),
-             "--seed", str(seed), "--out", self.out], stdout=subprocess.PIPE, text=True)
+             "--seed", str(seed), "--out", self.out,
+             # the ratio as the exact decimal of its f32 value (no double rounding in atof)
+             "--sparse", repr(float(np.float32(sparse))), "--sparse-seed", str(sparse_seed)],
+            stdout=subprocess.PIPE, text=True)
         self.port = json.loads(self.proc.stdout.readline())["port"]
 
     def result(self, timeout: float = 120):

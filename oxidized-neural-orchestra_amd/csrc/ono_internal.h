@@ -34,11 +34,13 @@ Scale make_scale(float divisor);
 
 // split_chunks (worker/src/middlewares/mod.rs:15-59): offsets of min(len, n) chunks
 std::vector<size_t> split_chunks(size_t len, size_t n);
+inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to chunk starts
 
 // ---- kernel launchers (ono_kernels.hip); return hipSuccess or the launch error
 hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n, float divisor,
                             hipStream_t s);
-hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s);
+// keep: the accumulator is re-read soon (the ring's residual): cacheable loads
+hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s, bool keep = false);
 hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divisor, float *zero,
                              hipStream_t s);
 hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,

@@ -339,13 +339,20 @@ template <int K, class W> struct DirectOp {
     }
 };
 
-struct AccOp { // acc += in
+// acc += in.  KEEP: the accumulator is read again soon (the ring's residual:
+// acc_residual per batch, then pull_grads) — plain loads leave it in the
+// Infinity Cache (acc + pull on one reused 64 MiB bucket: 55.8 us per step vs
+// 62.2 with nt loads, tools/kernel_variants.hip "train").  Otherwise (a
+// one-off accumulate over fresh buffers) both operands stream with nt loads
+// (64 MiB: 72 -> 79 % of 8 TB/s, "acc ... ntacc").
+template <bool KEEP> struct AccOp {
     float *acc;
     const float *in;
     struct R { f4 a, b; };
     __device__ __forceinline__ void scalar(size_t i) const { acc[i] += in[i]; }
     __device__ __forceinline__ R load(size_t i) const {
-        return R{ld((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
+        if constexpr (KEEP) return R{ld((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
+        else return R{ldn((const f4 *)(acc + i)), ldn((const f4 *)(in + i))};
     }
     __device__ __forceinline__ void store(size_t i, R r) const { st_nt((f4 *)(acc + i), r.a + r.b); }
 };
@@ -711,8 +718,9 @@ template hipError_t launch_direct_multi<uint16_t>(float *, uint16_t *const *, in
 template hipError_t launch_direct_multi<float>(float *, float *const *, int, bool, const float *const *, int, size_t,
                                                float, bool, hipStream_t);
 
-hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s) {
-    return launch_ew(AccOp{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);
+hipError_t launch_acc(float *acc, const float *in, size_t n, hipStream_t s, bool keep) {
+    if (keep) return launch_ew(AccOp<true>{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);
+    return launch_ew(AccOp<false>{acc, in}, n, {phase_of(acc, 4), phase_of(in, 4)}, s);
 }
 
 hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divisor, float *zero,

@@ -16,9 +16,6 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <poll.h>
-#include <sys/socket.h>
-
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
@@ -33,6 +30,7 @@
 #include <vector>
 
 #include "ono_internal.h"
+#include "ono_plan.h"
 #include "ono_ring_impl.h"
 
 
@@ -136,374 +134,178 @@ int host_threads() {
 
 namespace {
 
-template <class W> ncclDataType_t nccl_type();
-template <> ncclDataType_t nccl_type<uint16_t>() { return ncclFloat16; }
-template <> ncclDataType_t nccl_type<float>() { return ncclFloat32; }
-
-// One hop over the reference's TCP wire (the TCP edge).
-// The f16 payload comes down from HBM into a pinned frame
-//   [u64 BE len = 4 + payload][u32 BE kind = 1: DenseGrad, is_last = false][f16 LE ...]
-// (msg.rs:120-151, sink.rs:37-58, worker.rs:157-174) and is sent to `next`
-// while the previous worker's frame is read (try_join!, worker_ring.rs:122-123;
-// source.rs:34-57), validated as a DenseGrad of the expected length, and goes
-// up to HBM for the next fused kernel.  Frames are byte-identical to the
-// reference's, so MI355X workers and reference Rust workers can share a ring.
-//
-// Pipelined in r->tcp_block pieces: the D2H of piece b+1 overlaps the send of
-// piece b (a sender thread waits on per-piece events), and each received
-// piece goes up to HBM while the next one is still on the socket.  Sending and
-// receiving run on two threads, so the two kernel-side socket copies overlap.
-size_t tcp_block_bytes() {  // env ONO_TCP_BLOCK_KIB (default 4 MiB), read once per ring
-    const char *v = getenv("ONO_TCP_BLOCK_KIB");
-    long k = v ? atol(v) : 0;
-    return k > 0 ? (size_t)k << 10 : size_t(4) << 20;
-}
-constexpr int kTcpPollMs = 100;  // abort / peer-failure latency
-constexpr size_t kTcpInline = size_t(256) << 10;  // frames up to this go through one poll loop
-
-struct TcpErr {
-    int code = ONO_OK;
-    char msg[160] = {0};
+// ---- the plan interpreter ----------------------------------------------
+// Every RCCL schedule (ALLREDUCE and its segments, HOPS, DIRECT, the PS step)
+// is a list of steps built by ono_plan.cpp and executed here; the same lists
+// are checked and run on the CPU by tests/test_plans.py.  Schedules:
+//   HOPS    worker_ring.rs:112-204 as ncclSend/ncclRecv pairs, with the fused
+//           codec kernels between hops:
+//             scatter hop 0      encode_zero        (:122, :133)
+//             scatter hops 1..   add_encode_zero    (:141-143 then :122, :133)
+//             last scatter hop   add_finish         (:141-143, :166, :191-193, ÷n)
+//             gather hops        decode_scale       (:200, ÷n) + forward the
+//                                received bytes (f16(f32(h)) == h)
+//   DIRECT  built for the fully connected xGMI of one node (every GPU pair has
+//           its own link): instead of n-1 dependent hops over one link,
+//           1. all-to-all (grouped ncclSend/ncclRecv to every peer): rank q
+//              receives every rank's slice of the chunk it owns, c = q+1
+//              (worker_ring.rs:162-166);
+//           2. one fused kernel on the owner replays the reference chain for
+//              chunk c in the reference order c, c+1, ..., c+n-1 (DirectOp):
+//              bit-exact with the hop ring for both wires at every n;
+//              grad[c] = chain / n; own slice zeroed;
+//           3. the rest of the residual is zeroed on the side stream, beside
+//           4. the all-gather of the owned chunk (f32 values, or the f16
+//              message the reference forwards hop by hop), decoded and divided
+//              on arrival.  Bytes per rank on the wire: (n-1)/n (4 + 4) N for
+//              f32, (n-1)/n (4 + 2) N for f16 — all links busy at once.
+//   ALLREDUCE  ncclAllReduce(sum) + the fused finaliser (÷n, residual = 0);
+//           with k segments the finaliser of segment j runs on the side stream
+//           while segment j+1 is on the wire.
+struct PlanCtx {
+    void *base[ONO_PB_COUNT] = {};
+    int wire = ONO_WIRE_F32;
+    const OptLaunch *opt = nullptr;  // OPT_UPDATE: the PS optimizer and its shard state
+    float *v = nullptr, *s = nullptr;
 };
 
-// Wait until `fd` is ready for `ev`; false (with e set) on abort, stop or poll error.
-bool tcp_wait(ono_ring *r, int fd, short ev, const std::atomic<bool> &stop, TcpErr &e) {
-    for (;;) {
-        if (r->aborted.load()) { e.code = ONO_E_ABORTED; snprintf(e.msg, sizeof e.msg, "ring aborted"); return false; }
-        if (stop.load()) { e.code = ONO_E_OTHER; return false; }  // the other side already failed
-        struct pollfd p = {fd, ev, 0};
-        int pr = poll(&p, 1, kTcpPollMs);
-        if (pr < 0 && errno != EINTR) {
-            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "poll: %s", strerror(errno)); return false;
-        }
-        if (pr > 0) return true;
+size_t plan_esize(const PlanCtx &c, int buf) {
+    switch (buf) {
+    case ONO_PB_WIRE0:
+    case ONO_PB_WIRE1: return c.wire == ONO_WIRE_F16 ? 2 : 4;
+    case ONO_PB_GSTAGE:
+    case ONO_PB_MSG: return 2;
+    default: return 4;
     }
 }
-
-// One send(2) of the frame's ready bytes; false (e set) on a socket error.
-bool tcp_send_some(ono_ring *r, const uint8_t *tx, size_t &sent, size_t ready, TcpErr &e) {
-    ssize_t k = send(r->fd_next, tx + sent, ready - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
-    if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
-        e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "send to next worker: %s", strerror(errno));
-        return false;
-    }
-    if (k > 0) sent += (size_t)k;
-    return true;
+void *plan_ptr(const PlanCtx &c, const ono_plan_step &st, int i) {
+    const int b = st.buf[i];
+    if (b < 0 || b >= ONO_PB_COUNT || !c.base[b]) return nullptr;
+    return static_cast<char *>(c.base[b]) + st.off[i] * plan_esize(c, b);
 }
 
-// Receive side of one hop: header validation, then each complete piece of the
-// payload goes up to HBM while the next one is still on the socket.
-struct TcpRecv {
-    uint8_t *rx;  // where the frame lands (header, then payload)
-    size_t got = 0, need = 12, issued = 0;
-    bool have_hdr = false;
-    explicit TcpRecv(uint8_t *frame) : rx(frame) {}
-    bool done() const { return got >= need && have_hdr; }
-    // one recv(2); false (e set) on a socket or protocol error.  recv_dev ==
-    // nullptr: the payload stays where it landed (zero-copy frames).
-    bool step(ono_ring *r, uint8_t *recv_dev, size_t payload, hipStream_t s, TcpErr &e) {
-        ssize_t k = recv(r->fd_prev, rx + got, need - got, MSG_DONTWAIT);
-        if (k == 0) { e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "previous worker closed the connection"); return false; }
-        if (k < 0) {
-            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) return true;
-            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "recv from previous worker: %s", strerror(errno));
-            return false;
-        }
-        got += (size_t)k;
-        if (!have_hdr && got >= 12) {
-            uint64_t l = 0;
-            for (int i = 0; i < 8; i++) l = (l << 8) | rx[i];
-            const uint32_t kind = (uint32_t)rx[8] << 24 | (uint32_t)rx[9] << 16 | (uint32_t)rx[10] << 8 | rx[11];
-            // only a DenseGrad of this hop's chunk is a valid event (worker_ring.rs:136-138)
-            if ((kind & 0xFF) != 1 && (kind & 0xFF) != 2) {  // Header::from_be_bytes(..) as u8 (msg.rs:168)
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind & 0xFF);
-                return false;
-            }
-            if (l != 4 + (uint64_t)payload) {
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
-                         (unsigned long long)(l < 4 ? 0 : l - 4), payload);
-                return false;
-            }
-            need = 12 + payload;
-            have_hdr = true;
-        }
-        if (have_hdr && recv_dev) {
-            const size_t blk = r->tcp_block, avail = got - 12;
-            while (issued < avail && (avail - issued >= blk || avail == payload)) {
-                const size_t c = std::min(blk, payload - issued);
-                hipError_t he = hipMemcpyAsync(recv_dev + issued, rx + 12 + issued, c, hipMemcpyHostToDevice, s);
-                if (he != hipSuccess) {
-                    e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "H2D of a frame: %s", hipGetErrorString(he));
-                    return false;
-                }
-                issued += c;
-            }
-        }
-        return true;
-    }
-};
-
-void tcp_send_frame(ono_ring *r, size_t payload, const std::atomic<bool> &stop, TcpErr &e) {
-    const size_t blk = r->tcp_block;
-    const size_t out = 12 + payload;
-    size_t sent = 0;
-    for (size_t b = 0; sent < out; b++) {
-        const size_t ready = std::min(out, 12 + (b + 1) * blk);
-        if (payload) {
-            hipError_t he = hipEventSynchronize(r->tx_ev[b]);
-            if (he != hipSuccess) {
-                e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "D2H of a frame: %s", hipGetErrorString(he));
-                return;
-            }
-        }
-        while (sent < ready)
-            if (!tcp_wait(r, r->fd_next, POLLOUT, stop, e) || !tcp_send_some(r, r->tx, sent, ready, e)) return;
-    }
-}
-
-void tcp_recv_frame(ono_ring *r, uint8_t *recv_dev, size_t payload, hipStream_t s,
-                    const std::atomic<bool> &stop, TcpErr &e) {
-    TcpRecv rv(r->rx);
-    while (!rv.done())
-        if (!tcp_wait(r, r->fd_prev, POLLIN, stop, e) || !rv.step(r, recv_dev, payload, s, e)) return;
-}
-
-// Small frames: one thread drives both directions from one poll loop (a
-// thread hand-off costs more than the transfer); the whole frame is already
-// down in tx.
-int tcp_xchg_inline(ono_ring *r, const uint8_t *tx, size_t send_bytes, uint8_t *rx, uint8_t *recv_dev,
-                    size_t recv_bytes, hipStream_t s) {
-    const size_t out = 12 + send_bytes;
-    size_t sent = 0;
-    TcpRecv rv(rx);
-    TcpErr e;
-    while (sent < out || !rv.done()) {
-        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-        struct pollfd p[2];
-        int np = 0, is = -1, ir = -1;
-        if (sent < out) { p[np] = {r->fd_next, POLLOUT, 0}; is = np++; }
-        if (!rv.done()) { p[np] = {r->fd_prev, POLLIN, 0}; ir = np++; }
-        int pr = poll(p, (nfds_t)np, kTcpPollMs);
-        if (pr < 0 && errno != EINTR) return set_error(ONO_E_IO, "poll: %s", strerror(errno));
-        if (pr <= 0) continue;
-        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP)) && !tcp_send_some(r, tx, sent, out, e))
-            return set_error(e.code, "%s", e.msg);
-        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP)) && !rv.step(r, recv_dev, recv_bytes, s, e))
-            return set_error(e.code, "%s", e.msg);
+int side_stream(ono_ring *r) {
+    if (!r->astream) {
+        ONO_HIP(hipStreamCreateWithFlags(&r->astream, hipStreamNonBlocking));
+        ONO_HIP(hipEventCreateWithFlags(&r->ev_ajoin, hipEventDisableTiming));
     }
     return ONO_OK;
 }
 
-int tcp_xchg(ono_ring *r, const void *send_dev, size_t send_bytes, void *recv_dev, size_t recv_bytes,
-             hipStream_t s) {
-    uint8_t *tx = r->tx;
-    const size_t blk = r->tcp_block;
-    const uint64_t flen = 4 + (uint64_t)send_bytes;
-    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
-    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
-    const size_t nblk = (send_bytes + blk - 1) / blk;
-    if (nblk > r->tx_ev.size()) return set_error(ONO_E_ARG, "frame of %zu bytes exceeds the ring's chunk", send_bytes);
-    for (size_t b = 0; b < nblk; b++) {
-        const size_t o = b * blk, c = std::min(blk, send_bytes - o);
-        ONO_HIP(hipMemcpyAsync(tx + 12 + o, static_cast<const uint8_t *>(send_dev) + o, c, hipMemcpyDeviceToHost, s));
-        ONO_HIP(hipEventRecord(r->tx_ev[b], s));
+template <class W>
+hipError_t plan_kernel(const PlanCtx &c, const ono_plan_step &st, hipStream_t q) {
+    auto p = [&](int i) { return plan_ptr(c, st, i); };
+    const size_t n = st.count;
+    switch (st.op) {
+    case ONO_POP_ENCODE_ZERO:
+        return launch_encode_zero<W>(static_cast<W *>(p(0)), static_cast<float *>(p(1)), n, q);
+    case ONO_POP_ADD_ENCODE_ZERO:
+        return launch_add_encode_zero<W>(static_cast<W *>(p(0)), static_cast<float *>(p(1)),
+                                         static_cast<const W *>(p(2)), n, q);
+    case ONO_POP_ADD_FINISH:
+        return launch_add_finish<W>(static_cast<float *>(p(0)), static_cast<W *>(p(1)), static_cast<float *>(p(2)),
+                                    static_cast<const W *>(p(3)), n, st.divisor, q);
+    case ONO_POP_DECODE_SCALE:
+        return launch_decode_scale<W>(static_cast<float *>(p(0)), static_cast<const W *>(p(1)), n, st.divisor, q);
+    case ONO_POP_DIRECT: {
+        const float *ins[ONO_MAX_INPUTS];
+        const int k = st.nref - 2;
+        if (k < 1 || k > ONO_MAX_INPUTS) return hipErrorInvalidValue;
+        for (int j = 0; j < k; j++) ins[j] = static_cast<const float *>(p(2 + j));
+        return launch_direct<W>(static_cast<float *>(p(0)), static_cast<W *>(p(1)), ins, k, n, st.divisor,
+                                st.flag != 0, q);
     }
-    // rx is free once the previous hop's H2D pieces ran: they precede piece 0's D2H on s
-    if (nblk) ONO_HIP(hipEventSynchronize(r->tx_ev[0]));
-    else ONO_HIP(hipStreamSynchronize(s));
-    if (send_bytes <= kTcpInline && recv_bytes <= kTcpInline)  // small: no thread hand-off
-        return tcp_xchg_inline(r, r->tx, send_bytes, r->rx, static_cast<uint8_t *>(recv_dev), recv_bytes, s);
-    std::atomic<bool> stop_send{false}, stop_recv{false};
-    TcpErr es, er;
-    std::thread sender([&] {
-        tcp_send_frame(r, send_bytes, stop_send, es);
-        if (es.code) stop_recv.store(true);
-    });
-    tcp_recv_frame(r, static_cast<uint8_t *>(recv_dev), recv_bytes, s, stop_recv, er);
-    if (er.code) stop_send.store(true);
-    sender.join();
-    // report the root cause, not the "other side failed" stop
-    const TcpErr &e = (er.code && er.code != ONO_E_OTHER) ? er : (es.code && es.code != ONO_E_OTHER) ? es : er;
-    if (e.code) return set_error(e.code, "%s", e.msg);
-    return ONO_OK;
+    case ONO_POP_SCALE_ZERO:
+        return launch_scale_zero(static_cast<float *>(p(0)), static_cast<const float *>(p(1)), n, st.divisor,
+                                 static_cast<float *>(p(2)), q);
+    case ONO_POP_OPT_UPDATE:
+        if (!c.opt) return hipErrorInvalidValue;
+        return launch_opt_update(*c.opt, static_cast<float *>(p(0)), static_cast<float *>(p(1)), c.v, c.s, n,
+                                 st.flag != 0, q);
+    default:
+        return hipErrorInvalidValue;
+    }
 }
 
-// Zero-copy hop (small frames): the payload to send was written by the codec
-// kernel straight into pinned host memory at send_pay, the frame arrives in
-// place at recv_pay - 12 and the next kernel reads it there.
-int tcp_xchg_zc(ono_ring *r, void *send_pay, size_t send_bytes, void *recv_pay, size_t recv_bytes, hipStream_t s) {
-    uint8_t *tx = static_cast<uint8_t *>(send_pay) - 12;
-    const uint64_t flen = 4 + (uint64_t)send_bytes;
-    for (int i = 0; i < 8; i++) tx[i] = (uint8_t)(flen >> (56 - 8 * i));
-    tx[8] = 0; tx[9] = 0; tx[10] = 0; tx[11] = 1;
-    // the producing kernel has written the payload, and the kernel that read
-    // the receive buffer in the previous hop has finished with it
-    ONO_HIP(hipStreamSynchronize(s));
-    uint8_t *rx = static_cast<uint8_t *>(recv_pay) - 12;
-    if (send_bytes <= kTcpInline && recv_bytes <= kTcpInline)
-        return tcp_xchg_inline(r, tx, send_bytes, rx, nullptr, recv_bytes, s);
-    // larger frames: send and receive on two threads (two kernel socket copies at once)
-    std::atomic<bool> stop_send{false}, stop_recv{false};
-    TcpErr es, er;
-    std::thread sender([&] {
-        size_t sent = 0;
-        while (sent < 12 + send_bytes)
-            if (!tcp_wait(r, r->fd_next, POLLOUT, stop_send, es) || !tcp_send_some(r, tx, sent, 12 + send_bytes, es)) {
-                stop_recv.store(true);
-                return;
-            }
-    });
-    TcpRecv rv(rx);
-    while (!rv.done())
-        if (!tcp_wait(r, r->fd_prev, POLLIN, stop_recv, er) || !rv.step(r, nullptr, recv_bytes, s, er)) {
-            stop_send.store(true);
+ncclDataType_t plan_nccl_type(int dtype) { return dtype == ONO_WIRE_F16 ? ncclFloat16 : ncclFloat32; }
+
+int run_plan(ono_ring *r, const std::vector<ono_plan_step> &plan, const PlanCtx &c, hipStream_t s) {
+    size_t forks = 0;
+    for (const auto &st : plan) forks += st.kind == ONO_PLAN_FORK;
+    if (forks) {
+        int rc = side_stream(r);
+        if (rc) return rc;
+        while (r->ev_seg.size() < forks) {
+            hipEvent_t ev;
+            ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            r->ev_seg.push_back(ev);
+        }
+    }
+    size_t fork = 0;
+    EventPair grp;
+    for (size_t i = 0; i < plan.size(); i++) {
+        const ono_plan_step &st = plan[i];
+        hipStream_t q = st.stream ? r->astream : s;
+        switch (st.kind) {
+        case ONO_PLAN_GROUP_BEGIN:
+            if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+            if (r->timer.on) ONO_HIP(r->timer.begin(s, grp, ONO_PHASE_RCCL));
+            ONO_NCCL(ncclGroupStart());
+            break;
+        case ONO_PLAN_SEND:
+            ONO_NCCL(ncclSend(plan_ptr(c, st, 0), st.count, plan_nccl_type(st.dtype), st.peer, r->comm, s));
+            break;
+        case ONO_PLAN_RECV:
+            ONO_NCCL(ncclRecv(plan_ptr(c, st, 0), st.count, plan_nccl_type(st.dtype), st.peer, r->comm, s));
+            break;
+        case ONO_PLAN_GROUP_END:
+            ONO_NCCL(ncclGroupEnd());
+            if (r->timer.on) ONO_HIP(r->timer.end(s, grp));
+            break;
+        case ONO_PLAN_ALLREDUCE:
+        case ONO_PLAN_REDUCE_SCATTER:
+        case ONO_PLAN_ALL_GATHER: {
+            if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+            int rc = timed(r, s, ONO_PHASE_RCCL, [&]() -> int {
+                const void *src = plan_ptr(c, st, 0);
+                void *dst = plan_ptr(c, st, 1);
+                if (st.kind == ONO_PLAN_ALLREDUCE)
+                    ONO_NCCL(ncclAllReduce(src, dst, st.count, ncclFloat32, ncclSum, r->comm, s));
+                else if (st.kind == ONO_PLAN_REDUCE_SCATTER)
+                    ONO_NCCL(ncclReduceScatter(src, dst, st.count, ncclFloat32, ncclSum, r->comm, s));
+                else
+                    ONO_NCCL(ncclAllGather(src, dst, st.count, ncclFloat32, r->comm, s));
+                return ONO_OK;
+            });
+            if (rc) return rc;
             break;
         }
-    sender.join();
-    const TcpErr &e = (er.code && er.code != ONO_E_OTHER) ? er : (es.code && es.code != ONO_E_OTHER) ? es : er;
-    if (e.code) return set_error(e.code, "%s", e.msg);
-    return ONO_OK;
-}
-
-// One pull_grads round of rank `pos`, exact reference hop order, wire W.
-template <class W>
-int ring_hops(ono_ring *r, float *res, float *grad, hipStream_t s) {
-    const int n = r->n, pos = r->pos;
-    const auto &off = r->off;
-    auto len = [&](int c) { return off[c + 1] - off[c]; };
-    auto slot = [&](int b, int c) {
-        return (r->zc[0] ? reinterpret_cast<W *>(r->zc[b] + 16) : static_cast<W *>(r->wbuf[b])) + ph(off[c]);
-    };
-    const int next = (pos + 1) % n, prev = (pos + n - 1) % n;
-    const float fn = (float)n;
-    auto xchg = [&](int bs, int cs, int br, int cr) -> int {
-        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-        if (r->zc[0])
-            return timed(r, s, 1, [&]() -> int {
-                return tcp_xchg_zc(r, slot(bs, cs), len(cs) * sizeof(W), slot(br, cr), len(cr) * sizeof(W), s);
-            });
-        if (r->fd_next >= 0)
-            return timed(r, s, 1, [&]() -> int {
-                return tcp_xchg(r, slot(bs, cs), len(cs) * sizeof(W), slot(br, cr), len(cr) * sizeof(W), s);
-            });
-        return timed(r, s, 1, [&]() -> int {
-            ONO_NCCL(ncclGroupStart());
-            ONO_NCCL(ncclSend(slot(bs, cs), len(cs), nccl_type<W>(), next, r->comm, s));
-            ONO_NCCL(ncclRecv(slot(br, cr), len(cr), nccl_type<W>(), prev, r->comm, s));
-            ONO_NCCL(ncclGroupEnd());
-            return ONO_OK;
-        });
-    };
-    // ---- scatter: out buffer 0, in buffer 1 ----
-    ONO_K(r, s, launch_encode_zero<W>(slot(0, pos), res + off[pos], len(pos), s));
-    for (int st = 0; st < n - 1; st++) {
-        int cs = ((pos - st) % n + n) % n, cr = ((pos - st - 1) % n + n) % n;
-        int rc = xchg(0, cs, 1, cr);
-        if (rc) return rc;
-        if (st < n - 2)
-            ONO_K(r, s, launch_add_encode_zero<W>(slot(0, cr), res + off[cr], slot(1, cr), len(cr), s));
-        else
-            ONO_K(r, s, launch_add_finish<W>(grad + off[cr], slot(0, cr), res + off[cr], slot(1, cr),
-                                             len(cr), fn, s));
+        case ONO_PLAN_KERNEL:
+            if (c.wire == ONO_WIRE_F16 && st.dtype == ONO_WIRE_F16)
+                ONO_K(r, q, plan_kernel<uint16_t>(c, st, q));
+            else
+                ONO_K(r, q, plan_kernel<float>(c, st, q));
+            break;
+        case ONO_PLAN_MEMSET:
+            ONO_HIP(hipMemsetAsync(plan_ptr(c, st, 0), 0, st.count * plan_esize(c, st.buf[0]), q));
+            break;
+        case ONO_PLAN_COPY:
+            ONO_HIP(hipMemcpyAsync(plan_ptr(c, st, 0), plan_ptr(c, st, 1), st.count * plan_esize(c, st.buf[0]),
+                                   hipMemcpyDeviceToDevice, q));
+            break;
+        case ONO_PLAN_FORK:
+            ONO_HIP(hipEventRecord(r->ev_seg[fork], s));
+            ONO_HIP(hipStreamWaitEvent(r->astream, r->ev_seg[fork], 0));
+            fork++;
+            break;
+        case ONO_PLAN_JOIN:
+            ONO_HIP(hipEventRecord(r->ev_ajoin, r->astream));
+            ONO_HIP(hipStreamWaitEvent(s, r->ev_ajoin, 0));
+            break;
+        default:
+            return set_error(ONO_E_ARG, "plan step %zu: kind %d", i, st.kind);
+        }
     }
-    // ---- gather: forward what arrived, alternate the two buffers ----
-    int bo = 0, bi = 1;
-    for (int j = 0; j < n - 1; j++) {
-        int cs = ((pos + 1 - j) % n + n) % n, cr = ((pos - j) % n + n) % n;
-        int rc = xchg(bo, cs, bi, cr);
-        if (rc) return rc;
-        ONO_K(r, s, launch_decode_scale<W>(grad + off[cr], slot(bi, cr), len(cr), fn, s));
-        std::swap(bo, bi);
-    }
-    return ONO_OK;
-}
-
-// The direct schedule, built for the fully connected xGMI of one node (every
-// GPU pair has its own link): instead of n-1 dependent hops over one link,
-//   1. all-to-all (grouped ncclSend/ncclRecv to every peer): rank q receives
-//      every rank's slice of the chunk it owns, c = q+1 (worker_ring.rs:162-166);
-//   2. one fused kernel on the owner replays the reference chain for chunk c in
-//      the reference order c, c+1, ..., c+n-1 (DirectOp): bit-exact with the
-//      hop ring for both wires at every n; grad[c] = chain / n; own slice zeroed;
-//   3. the rest of the residual is zeroed on a side stream, beside
-//   4. the all-gather of the owned chunk (f32 values, or the f16 message that
-//      the reference forwards hop by hop), decoded and divided on arrival.
-// Bytes per rank on the wire: (n-1)/n (4 + 4) N for f32, (n-1)/n (4 + 2) N for
-// f16 — all links busy at once.
-int alloc_direct(ono_ring *r) {
-    if (r->rbuf) return ONO_OK;
-    const size_t slot = r->maxc + 4;
-    ONO_HIP(hipMalloc((void **)&r->rbuf, (size_t)r->n * slot * sizeof(float)));
-    ONO_HIP(hipMalloc((void **)&r->gstage, (size_t)r->n * slot * sizeof(uint16_t)));
-    ONO_HIP(hipMalloc((void **)&r->msg, slot * sizeof(uint16_t)));
-    ONO_HIP(hipStreamCreateWithFlags(&r->zstream, hipStreamNonBlocking));
-    ONO_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming));
-    ONO_HIP(hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming));
-    return ONO_OK;
-}
-
-template <class W>
-int direct_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
-    const int n = r->n, pos = r->pos, c = (pos + 1) % n;
-    if (n > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "direct schedule supports up to %d ranks", ONO_MAX_INPUTS);
-    int rc = alloc_direct(r);
-    if (rc) return rc;
-    const auto &off = r->off;
-    auto len = [&](int q) { return off[q + 1] - off[q]; };
-    const size_t slot = r->maxc + 4;
-    constexpr bool f16 = sizeof(W) == 2;
-    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-    rc = timed(r, s, 1, [&]() -> int {  // 1. all-to-all of chunk slices
-        ONO_NCCL(ncclGroupStart());
-        for (int q = 0; q < n; q++) {
-            if (q == pos) continue;
-            const int cq = (q + 1) % n, k = (q - c + n) % n;
-            ONO_NCCL(ncclSend(res + off[cq], len(cq), ncclFloat32, q, r->comm, s));
-            ONO_NCCL(ncclRecv(r->rbuf + (size_t)k * slot + ph(off[c]), len(c), ncclFloat32, q, r->comm, s));
-        }
-        ONO_NCCL(ncclGroupEnd());
-        return ONO_OK;
-    });
-    if (rc) return rc;
-    const float *ins[ONO_MAX_INPUTS];  // 2. the chain, in the reference order
-    for (int k = 0; k < n - 1; k++) ins[k] = r->rbuf + (size_t)k * slot + ph(off[c]);
-    ins[n - 1] = res + off[c];
-    W *out = f16 ? reinterpret_cast<W *>(r->msg + ph(off[c])) : nullptr;
-    ONO_K(r, s, launch_direct<W>(grad + off[c], out, ins, n, len(c), (float)n, false, s));
-    ONO_HIP(hipEventRecord(r->ev_fork, s));  // 3. zero the sent slices beside the all-gather
-    ONO_HIP(hipStreamWaitEvent(r->zstream, r->ev_fork, 0));
-    if (off[c] > 0) ONO_HIP(hipMemsetAsync(res, 0, off[c] * sizeof(float), r->zstream));
-    if (off[c + 1] < r->size)
-        ONO_HIP(hipMemsetAsync(res + off[c + 1], 0, (r->size - off[c + 1]) * sizeof(float), r->zstream));
-    ONO_HIP(hipEventRecord(r->ev_join, r->zstream));
-    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-    rc = timed(r, s, 1, [&]() -> int {  // 4. all-gather of the owned chunk
-        ONO_NCCL(ncclGroupStart());
-        for (int q = 0; q < n; q++) {
-            if (q == pos) continue;
-            const int cq = (q + 1) % n;
-            if (f16) {
-                ONO_NCCL(ncclSend(r->msg + ph(off[c]), len(c), ncclFloat16, q, r->comm, s));
-                ONO_NCCL(ncclRecv(r->gstage + (size_t)q * slot + ph(off[cq]), len(cq), ncclFloat16, q, r->comm, s));
-            } else {
-                ONO_NCCL(ncclSend(grad + off[c], len(c), ncclFloat32, q, r->comm, s));
-                ONO_NCCL(ncclRecv(grad + off[cq], len(cq), ncclFloat32, q, r->comm, s));
-            }
-        }
-        ONO_NCCL(ncclGroupEnd());
-        return ONO_OK;
-    });
-    if (rc) return rc;
-    if (f16)
-        for (int q = 0; q < n; q++) {
-            if (q == pos) continue;
-            const int cq = (q + 1) % n;
-            ONO_K(r, s, launch_decode_scale<uint16_t>(grad + off[cq], r->gstage + (size_t)q * slot + ph(off[cq]),
-                                                      len(cq), (float)n, s));
-        }
-    ONO_HIP(hipStreamWaitEvent(s, r->ev_join, 0));
     return ONO_OK;
 }
 
@@ -536,48 +338,40 @@ int ensure_comm(ono_ring *r) {
     return ONO_OK;
 }
 
-// grad = (sum over ranks of res) / n, res = 0: RCCL all-reduce + fused finaliser.
-// With k > 1 segments the finaliser of segment j (on astream) overlaps the
-// all-reduce of segment j+1 (on s); every element still sees one all-reduce and
-// one finaliser, so the result is the unsegmented one.
-int allreduce_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
-    int rc = ensure_comm(r);
-    if (rc) return rc;
-    const float fn = (float)r->n;
-    const int nseg = ar_segments(r);
-    if (nseg <= 1) {
-        rc = timed(r, s, 1, [&]() -> int {
-            ONO_NCCL(ncclAllReduce(res, grad, r->size, ncclFloat32, ncclSum, r->comm, s));
-            return ONO_OK;
-        });
-        if (rc) return rc;
-        ONO_K(r, s, launch_scale_zero(grad, grad, r->size, fn, res, s));
-        return ONO_OK;
-    }
-    if (!r->astream) {
-        ONO_HIP(hipStreamCreateWithFlags(&r->astream, hipStreamNonBlocking));
-        ONO_HIP(hipEventCreateWithFlags(&r->ev_ajoin, hipEventDisableTiming));
-    }
-    while (r->ev_seg.size() < (size_t)nseg) {
-        hipEvent_t ev;
-        ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        r->ev_seg.push_back(ev);
-    }
-    const size_t seg = ((r->size + nseg - 1) / nseg + 63) & ~size_t(63);  // 256-B aligned segments
-    for (int k = 0; k < nseg && (size_t)k * seg < r->size; k++) {
-        const size_t lo = (size_t)k * seg, len = std::min(seg, r->size - lo);
-        rc = timed(r, s, 1, [&]() -> int {
-            ONO_NCCL(ncclAllReduce(res + lo, grad + lo, len, ncclFloat32, ncclSum, r->comm, s));
-            return ONO_OK;
-        });
-        if (rc) return rc;
-        ONO_HIP(hipEventRecord(r->ev_seg[k], s));
-        ONO_HIP(hipStreamWaitEvent(r->astream, r->ev_seg[k], 0));
-        ONO_K(r, r->astream, launch_scale_zero(grad + lo, grad + lo, len, fn, res + lo, r->astream));
-    }
-    ONO_HIP(hipEventRecord(r->ev_ajoin, r->astream));
-    ONO_HIP(hipStreamWaitEvent(s, r->ev_ajoin, 0));
+// the direct schedule's buffers: all-to-all receive slots, f16 all-gather
+// staging, the owner's f16 message
+int alloc_direct(ono_ring *r) {
+    if (r->rbuf) return ONO_OK;
+    const size_t slot = r->maxc + 4;
+    ONO_HIP(hipMalloc((void **)&r->rbuf, (size_t)r->n * slot * sizeof(float)));
+    ONO_HIP(hipMalloc((void **)&r->gstage, (size_t)r->n * slot * sizeof(uint16_t)));
+    ONO_HIP(hipMalloc((void **)&r->msg, slot * sizeof(uint16_t)));
     return ONO_OK;
+}
+
+// pull_grads over RCCL: the rank's plan for (algo, wire, segments), cached
+int plan_pull_grads_impl(ono_ring *r, int algo, float *res, float *grad, hipStream_t s) {
+    int rc = ONO_OK;
+    if (algo == ONO_ALGO_ALLREDUCE && (rc = ensure_comm(r))) return rc;
+    if (algo == ONO_ALGO_DIRECT && (rc = alloc_direct(r))) return rc;
+    const int segs = algo == ONO_ALGO_ALLREDUCE ? ar_segments(r) : 0;
+    if (r->plan.empty() || r->plan_algo != algo || r->plan_segments != segs) {
+        std::vector<ono_plan_step> p;
+        if ((rc = plan_pull_grads(p, algo, r->wire, r->pos, r->n, r->size, segs))) return rc;
+        r->plan.swap(p);
+        r->plan_algo = algo;
+        r->plan_segments = segs;
+    }
+    PlanCtx c;
+    c.wire = r->wire;
+    c.base[ONO_PB_RESIDUAL] = res;
+    c.base[ONO_PB_GRAD] = grad;
+    c.base[ONO_PB_WIRE0] = r->wbuf[0];
+    c.base[ONO_PB_WIRE1] = r->wbuf[1];
+    c.base[ONO_PB_RBUF] = r->rbuf;
+    c.base[ONO_PB_GSTAGE] = r->gstage;
+    c.base[ONO_PB_MSG] = r->msg;
+    return run_plan(r, r->plan, c, s);
 }
 
 int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
@@ -586,13 +380,14 @@ int pull_grads_impl(ono_ring *r, float *res, float *grad, hipStream_t s) {
         ONO_K(r, s, launch_scale_zero(grad, res, r->size, 1.0f, res, s));
         return ONO_OK;
     }
-    switch (resolved_algo(r)) {
-    case ONO_ALGO_ALLREDUCE:
-        return allreduce_impl(r, res, grad, s);
+    const int algo = resolved_algo(r);
+    switch (algo) {
     case ONO_ALGO_HOPS:
-        return r->wire == ONO_WIRE_F16 ? ring_hops<uint16_t>(r, res, grad, s) : ring_hops<float>(r, res, grad, s);
+        if (r->fd_next >= 0) return tcp_pull_grads(r, res, grad, s);
+        return plan_pull_grads_impl(r, algo, res, grad, s);
+    case ONO_ALGO_ALLREDUCE:
     case ONO_ALGO_DIRECT:
-        return r->wire == ONO_WIRE_F16 ? direct_impl<uint16_t>(r, res, grad, s) : direct_impl<float>(r, res, grad, s);
+        return plan_pull_grads_impl(r, algo, res, grad, s);
     case ONO_ALGO_XGMI:
         return xgmi_pull_grads(r, res, grad, s);
     default:
@@ -619,61 +414,6 @@ static int ring_validate(ono_ring **out, int pos, int nranks, size_t size, int w
     if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
     if (size < (size_t)nranks)  // reference: chunks[pos] out of bounds (worker_ring.rs:120-122)
         return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, nranks);
-    return ONO_OK;
-}
-
-// The reference's ring over its own TCP connections (builder.rs:272-311 hands
-// the worker an accepted `prev` and a connected `next` stream): f16 wire, hop
-// schedule, the arithmetic in HBM, the frames on the caller's sockets.
-int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
-                        int fd_next) {
-    int rc = ring_validate(out, pos, nranks, size, ONO_WIRE_F16);
-    if (rc) return rc;
-    if (nranks > 1 && (fd_prev < 0 || fd_next < 0)) return set_error(ONO_E_ARG, "sockets required for nranks > 1");
-    // reuse the common allocation path (nranks == 1 needs neither sockets nor an id)
-    static const uint8_t no_uid[ONO_UID_BYTES] = {0};
-    rc = ono_ring_create(out, 0, 1, size, device, no_uid, ONO_WIRE_F16);
-    if (rc) return rc;
-    ono_ring *r = *out;
-    if (nranks == 1) return ONO_OK;
-    *out = nullptr;
-    r->n = nranks;
-    r->pos = pos;
-    r->off = split_chunks(size, (size_t)nranks);
-    r->maxc = r->off[1] - r->off[0];
-    r->algo = ONO_ALGO_HOPS;
-    r->fd_prev = fd_prev;
-    r->fd_next = fd_next;
-    r->frame_cap = 12 + 2 * (r->maxc + 4);
-    DeviceGuard g(device);
-    hipError_t e;
-    for (int b = 0; b < 2; b++)
-        if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(float))) != hipSuccess) {
-            ono_ring_destroy(r);
-            return hip_error(e, "wire buffer allocation", __FILE__, __LINE__);
-        }
-    if ((e = hipHostMalloc((void **)&r->tx, r->frame_cap, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc((void **)&r->rx, r->frame_cap, hipHostMallocDefault)) != hipSuccess) {
-        ono_ring_destroy(r);
-        return hip_error(e, "frame buffer allocation", __FILE__, __LINE__);
-    }
-    // zero-copy frames up to ONO_TCP_ZEROCOPY KiB of payload (default 256; 0 = off)
-    const char *zc_env = getenv("ONO_TCP_ZEROCOPY");
-    const size_t zc_max = zc_env ? (size_t)atol(zc_env) << 10 : kTcpInline;
-    if (2 * (r->maxc + 4) <= zc_max)
-        for (int b = 0; b < 2; b++)
-            if ((e = hipHostMalloc((void **)&r->zc[b], 16 + 2 * (r->maxc + 4), hipHostMallocCoherent)) != hipSuccess) {
-                ono_ring_destroy(r);
-                return hip_error(e, "zero-copy frame allocation", __FILE__, __LINE__);
-            }
-    r->tcp_block = tcp_block_bytes();
-    r->tx_ev.assign((2 * (r->maxc + 4) + r->tcp_block - 1) / r->tcp_block, nullptr);
-    for (auto &ev : r->tx_ev)
-        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
-            ono_ring_destroy(r);
-            return hip_error(e, "frame event creation", __FILE__, __LINE__);
-        }
-    *out = r;
     return ONO_OK;
 }
 
@@ -737,21 +477,21 @@ int ono_ring_destroy(ono_ring *r) {
         for (hipEvent_t ev : r->tx_ev) (void)hipEventDestroy(ev);
         for (uint8_t *z : r->zc)
             if (z) (void)hipHostFree(z);
-        if (r->tx) (void)hipHostFree(r->tx);
-        if (r->rx) (void)hipHostFree(r->rx);
+        for (uint8_t *h : {r->tx, r->rx, r->sp_rx})
+            if (h) (void)hipHostFree(h);
+        (void)hipFree(r->sp_dev);
+        (void)hipFree(r->sp_tmp);
+        delete[] r->sample_idx;
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);
-        if (r->zstream) (void)hipStreamSynchronize(r->zstream);
         if (r->astream) (void)hipStreamSynchronize(r->astream);
         for (hipEvent_t ev : r->ev_seg) (void)hipEventDestroy(ev);
         if (r->ev_ajoin) (void)hipEventDestroy(r->ev_ajoin);
         (void)hipFree(r->rbuf);
         (void)hipFree(r->gstage);
         (void)hipFree(r->msg);
-        for (hipEvent_t ev : {r->ev_fork, r->ev_join})
-            if (ev) (void)hipEventDestroy(ev);
-        for (hipStream_t st : {r->hstream, r->cstream, r->dstream, r->zstream, r->astream})
+        for (hipStream_t st : {r->hstream, r->cstream, r->dstream, r->astream})
             if (st) (void)hipStreamDestroy(st);
     }
     delete r;
@@ -766,7 +506,7 @@ int ono_ring_acc_residual(ono_ring *r, const float *grad_dev, void *stream) {
     if (!r || !grad_dev) return set_error(ONO_E_ARG, "NULL argument");
     DeviceGuard g(r->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    ONO_K(r, s, launch_acc(r->residual, grad_dev, r->size, s));
+    ONO_K(r, s, launch_acc(r->residual, grad_dev, r->size, s, true));
     return ONO_OK;
 }
 
@@ -873,8 +613,10 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
         int rc = pull_grads_impl(r, r->residual, r->grad, r->cstream);
         if (rc) return rc;
         ONO_HIP(hipMemcpyAsync(grad_host, r->grad, bytes, hipMemcpyDeviceToHost, r->cstream));
+        if (r->sparse_r > 0.0f)  // SparseCapable: the residual keeps what was not sent (worker_ring.rs:126-133)
+            ONO_HIP(hipMemcpyAsync(res_host, r->residual, bytes, hipMemcpyDeviceToHost, r->cstream));
         ONO_HIP(hipStreamSynchronize(r->cstream));
-        memset(res_host, 0, bytes);
+        if (r->sparse_r <= 0.0f) memset(res_host, 0, bytes);
         return ONO_OK;
     }
 
@@ -1162,6 +904,7 @@ struct ono_ps {
     float *gpad = nullptr, *ppad = nullptr, *gshard = nullptr, *v = nullptr, *s = nullptr;
     OptLaunch opt{};
     float beta1_t = 1.0f, beta2_t = 1.0f;
+    std::vector<ono_plan_step> plan;  // the RCCL step of this rank (n > 1)
 };
 
 int ono_ps_create(ono_ps **out, ono_ring *ring, const float *init, size_t nparams,
@@ -1218,33 +961,26 @@ int ono_ps_step(ono_ps *p, const float *grad, float *params, void *stream) {
     }
     if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // peer-access form, no padding needed
         return xgmi_ps_step(r, grad, params, N, C, p->gshard, p->ppad + (size_t)r->pos * C, p->opt, p->v, p->s, s);
-    const float *gsrc = grad;
-    if (p->padded != N) {
-        ONO_HIP(hipMemcpyAsync(p->gpad, grad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-        gsrc = p->gpad;
+    if (r->n > 1) {  // reduce-scatter -> fused update -> all-gather, as a plan (ono_plan.cpp)
+        if (p->plan.empty()) {
+            int rc = plan_ps_step(p->plan, r->pos, r->n, N);
+            if (rc) return rc;
+        }
+        PlanCtx c;
+        c.base[ONO_PB_GIN] = const_cast<float *>(grad);
+        c.base[ONO_PB_GPAD] = p->gpad;
+        c.base[ONO_PB_GSHARD] = p->gshard;
+        c.base[ONO_PB_PPAD] = p->ppad;
+        c.base[ONO_PB_PARAMS] = params;
+        c.opt = &p->opt;
+        c.v = p->v;
+        c.s = p->s;
+        return run_plan(r, p->plan, c, s);
     }
-    if (r->n > 1) {
-        int rc = timed(r, s, 1, [&]() -> int {
-            ONO_NCCL(ncclReduceScatter(gsrc, p->gshard, C, ncclFloat32, ncclSum, r->comm, s));
-            return ONO_OK;
-        });
-        if (rc) return rc;
-    } else {
-        ONO_HIP(hipMemcpyAsync(p->gshard, gsrc, C * sizeof(float), hipMemcpyDeviceToDevice, s));
-    }
-    float *wshard = p->ppad + (size_t)r->pos * C;
-    if (hi > lo) ONO_K(r, s, launch_opt_update(p->opt, p->gshard, wshard, p->v, p->s, hi - lo, true, s));
-    if (r->n > 1) {
-        float *dst = p->padded != N ? p->ppad : params;
-        int rc = timed(r, s, 1, [&]() -> int {
-            ONO_NCCL(ncclAllGather(wshard, dst, C, ncclFloat32, r->comm, s));
-            return ONO_OK;
-        });
-        if (rc) return rc;
-        if (dst != params) ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-    } else {
-        ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-    }
+    // one worker: the store's update on the whole vector
+    ONO_HIP(hipMemcpyAsync(p->gshard, grad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (hi > lo) ONO_K(r, s, launch_opt_update(p->opt, p->gshard, p->ppad, p->v, p->s, hi - lo, true, s));
+    ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
     return ONO_OK;
 }
 

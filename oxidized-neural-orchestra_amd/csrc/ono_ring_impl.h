@@ -101,7 +101,6 @@ struct DeviceGuard {
     }
 };
 
-inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to chunk starts
 
 }  // namespace ono
 
@@ -114,25 +113,42 @@ struct ono_ring {
     void *wbuf[2] = {nullptr, nullptr};  // hop-ring wire buffers, (maxc + 4) x 4 B each
     int algo = ONO_ALGO_AUTO;
     // direct schedule: all-to-all receive slots, all-gather staging (f16),
-    // the owner's f16 message; zstream zeroes the residual beside the all-gather
+    // the owner's f16 message
     float *rbuf = nullptr;
     uint16_t *gstage = nullptr, *msg = nullptr;
-    hipStream_t zstream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // the rank's exchange plan (ono_plan.cpp) for plan_algo / plan_segments
+    std::vector<ono_plan_step> plan;
+    int plan_algo = -1, plan_segments = -1;
     ncclComm_t comm = nullptr;
-    // TCP transport (ono_ring_create_tcp): the caller's connected sockets to the
-    // previous and next worker, pinned frame buffers (rx 4-B aligned, source.rs:43-50)
+    // TCP transport (ono_ring_create_tcp, ono_tcp.cpp): the caller's connected
+    // sockets to the previous and next worker, pinned frame buffers (grown on
+    // demand; payloads 4-B aligned like the reference's Vec<u32>, source.rs:43-50)
     int fd_prev = -1, fd_next = -1;
-    uint8_t *tx = nullptr, *rx = nullptr;
-    size_t frame_cap = 0;
+    uint8_t *tx = nullptr, *rx = nullptr, *sp_rx = nullptr;
+    size_t tx_cap = 0, rx_cap = 0, sp_rx_cap = 0;
     size_t tcp_block = 0;           // pipelining piece of a frame (tcp_block_bytes())
+    // SparseCapable serializer (ono_ring_set_sparse): keep ratio r of each
+    // pushed chunk (0 = the Base dense serializer); the sampler draws the
+    // threshold sample above 16384 values (default: ono_sparse_sample_default
+    // over sample_state); sp_dev holds this worker's encoded frame in HBM,
+    // sp_tmp a lifted incoming chunk
+    float sparse_r = 0.0f;
+    uint64_t sample_state = 0;
+    ono_sample_fn sampler = nullptr;
+    void *sampler_ctx = nullptr;
+    uint32_t *sample_idx = nullptr;
+    uint8_t *sp_dev = nullptr;
+    size_t sp_dev_cap = 0;
+    float *sp_tmp = nullptr;
     // small-frame TCP rings: the wire buffers are pinned host frames the codec
     // kernels read and write in place (no D2H / H2D per hop); zc[b] + 16 is the
     // payload base, so a frame's 12-byte header sits just before its payload
     uint8_t *zc[2] = {nullptr, nullptr};
     std::vector<hipEvent_t> tx_ev;  // one per piece of a frame's D2H
     // segmented f32 all-reduce (ono_ring_set_pipeline): the finaliser of
-    // segment k runs on astream while segment k+1 is still on the wire
+    // segment k runs on astream while segment k+1 is still on the wire; the
+    // plans' side stream (astream) is also where the direct schedule zeroes
+    // the residual beside its all-gather (ev_seg: one event per fork)
     int segments = 0;  // 0 = unresolved: env ONO_AR_SEGMENTS, default 4
     hipStream_t astream = nullptr;
     std::vector<hipEvent_t> ev_seg;
@@ -165,6 +181,9 @@ int timed(ono_ring *r, hipStream_t s, int kind, F &&f) {
 
 #define ONO_K(ring, s, expr) \
     do { int rc_ = timed(ring, s, 0, [&]() -> int { ONO_HIP(expr); return ONO_OK; }); if (rc_) return rc_; } while (0)
+
+// the TCP edge's pull_grads (ono_tcp.cpp)
+int tcp_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s);
 
 // xGMI peer-access schedule (ono_xgmi.cpp)
 int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s);

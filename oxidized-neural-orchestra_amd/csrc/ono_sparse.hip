@@ -649,6 +649,63 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     return lift_host_path(g, hb, dbuf, nbytes, total, s);
 }
 
+
+// ---------------------------------------------------------- threshold ----
+// calculate_threshold (comms/src/sparse/protocol.rs:33-49): the sample's
+// |g| values (f32::abs clears the sign bit), the k-th in f32::total_cmp order
+// (select_nth_unstable_by), then f32::max with f16::MIN_POSITIVE (NaN-ignoring).
+// total_cmp on sign-clear floats is the order of their bit patterns (NaN above
+// +inf), so this is an exact radix select over u32 keys: one workgroup, the
+// sample (<= 16384 keys) staged in LDS, four 8-bit digit passes, each a
+// histogram with LDS atomics and a scan for the digit that holds rank k.
+constexpr int kThrT = 1024;
+constexpr uint32_t kSampleMax = 16384;  // SAMPLE_SIZE, protocol.rs:13-19
+__global__ __launch_bounds__(kThrT) void sp_threshold(const float *g, const uint32_t *idx, uint32_t m, uint32_t k,
+                                                      float *t_out) {
+    __shared__ uint32_t keys[kSampleMax];
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sel[2];
+    for (uint32_t i = threadIdx.x; i < m; i += kThrT) {
+        const size_t j = idx ? idx[i] : i;
+        keys[i] = __builtin_bit_cast(uint32_t, g[j]) & 0x7FFFFFFFu;
+    }
+    uint32_t prefix = 0, mask = 0, kk = k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (uint32_t b = threadIdx.x; b < 256; b += kThrT) hist[b] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += kThrT) {
+            const uint32_t key = keys[i];
+            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t c = 0, d = 0;
+            for (; d < 255; d++) {
+                if (c + hist[d] > kk) break;
+                c += hist[d];
+            }
+            sel[0] = prefix | (d << shift);
+            sel[1] = kk - c;
+        }
+        __syncthreads();
+        prefix = sel[0];
+        kk = sel[1];
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float mp = 6.103515625e-05f;  // f16::MIN_POSITIVE
+        const float t = __builtin_bit_cast(float, prefix);
+        t_out[0] = prefix > 0x7F800000u ? mp : (t > mp ? t : mp);
+    }
+}
+
+struct ThrScratch {
+    uint32_t *idx = nullptr;
+    float *t_host = nullptr, *t_dev = nullptr;
+};
+ThrScratch g_thr[64];
+
 }  // namespace
 
 extern "C" {
@@ -724,6 +781,42 @@ int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, s
     if (rc) return rc;
     ONO_HIP(hipMemcpyAsync(L.buf, buf, nbytes, hipMemcpyHostToDevice, s));
     return lift_device(g, cap, out_len, L.buf, buf, nbytes, s);
+}
+
+
+int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t *idx_host, size_t m, float r,
+                         void *stream) {
+    if (!t_out || (n && !g)) return set_error(ONO_E_ARG, "NULL argument");
+    if (!(r > 0.0f && r <= 1.0f)) return set_error(ONO_E_ARG, "ratio %g outside (0, 1]", (double)r);
+    if (idx_host ? (m == 0 || m > kSampleMax) : (n > kSampleMax || m != n))
+        return set_error(ONO_E_ARG, "sample of %zu values from %zu: at most %u, and indices above %u values", m, n,
+                         kSampleMax, kSampleMax);
+    if (n == 0) { *t_out = 0.0f; return ONO_OK; }  // an empty gradient: nothing is kept
+    if (idx_host)
+        for (size_t i = 0; i < m; i++)
+            if (idx_host[i] >= n) return set_error(ONO_E_ARG, "sample index %u out of %zu", idx_host[i], n);
+    // (sample.len() as f32 * (1.0 - r)) as usize, clamped to the last index
+    const float kf = (float)m * (1.0f - r);
+    size_t k = kf <= 0.0f ? 0 : (size_t)kf;
+    if (k > m - 1) k = m - 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
+    ThrScratch &T = g_thr[dev];
+    if (!T.idx) {
+        ONO_HIP(hipMalloc((void **)&T.idx, kSampleMax * sizeof(uint32_t)));
+        ONO_HIP(hipHostMalloc((void **)&T.t_host, sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostGetDevicePointer((void **)&T.t_dev, T.t_host, 0));
+    }
+    if (idx_host) ONO_HIP(hipMemcpyAsync(T.idx, idx_host, m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(sp_threshold, dim3(1), dim3(kThrT), 0, s, g, idx_host ? T.idx : nullptr, (uint32_t)m,
+                       (uint32_t)k, T.t_dev);
+    ONO_HIP(hipGetLastError());
+    ONO_HIP(hipStreamSynchronize(s));
+    *t_out = *(volatile float *)T.t_host;
+    return ONO_OK;
 }
 
 size_t ono_sparse_lift_fallbacks(void) { return g_lift_fallbacks.load(); }

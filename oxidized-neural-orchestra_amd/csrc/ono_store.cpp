@@ -120,7 +120,7 @@ static int accumulate(ono_store *st, const float *grad, size_t n, hipMemcpyKind 
     } else {
         // store.rs:84-91: the active index is read once per accumulate
         int active = st->active_idx.load(std::memory_order_acquire);
-        ONO_HIP(launch_acc(st->grads[active], st->scratch, n, s));
+        ONO_HIP(launch_acc(st->grads[active], st->scratch, n, s, true));
     }
     ONO_HIP(hipStreamSynchronize(s));
     return ONO_OK;

@@ -1,0 +1,667 @@
+// ono_tcp.cpp — the TCP edge: WorkerRingManager over the
+// worker's own sockets, speaking the reference's frames byte for byte, with
+// the hop arithmetic in HBM.
+//
+// Frames (comms/src/protocol/msg.rs:120-191, codec/sink.rs:37-58,
+// codec/source.rs:34-57):
+//   [u64 BE len = 4 + payload][u32 BE kind][payload]
+// The kind byte is the header's u32 cast to u8 (msg.rs:168):
+//   1 / 2  DenseGrad  (is_last false / true): f16 LE values
+//   3 / 4  SparseGrad (is_last false / true): the grad_drop stream
+//          [u64 LE total][{u32 LE offset, u32 LE run, f16 LE x run}*]
+//          (comms/src/sparse/protocol.rs:57-86)
+//   0 control (JSON), 5 params, 6 data chunk: valid messages but not a
+//          gradient — the ring's "Received an invalid worker event"
+//          (worker_ring.rs:136-138, :195-197) -> ONO_E_PROTO
+//   >= 7   Msg::deserialize's invalid_kind_byte io::Error (msg.rs:187) -> ONO_E_IO
+// A worker receives either gradient kind whatever its own serializer is
+// (WorkerHandle::recv_event lifts SparseGrad into the handle's zero-filled
+// buffer, comms/src/handles/worker.rs:102-108), so MI355X workers share a
+// ring with reference workers of either serializer.
+//
+// Serializers of this worker (its push_grad, handles/worker.rs:157-174):
+//   Base (default)       DenseGrad of f16(chunk) (compressor.rs:106-118)
+//   SparseCapable{r}     (ono_ring_set_sparse) SparseGrad of the chunk's
+//                        values with |g| >= t, t = calculate_threshold(chunk, r)
+//                        (protocol.rs:33-49), and the ring's sparse branches:
+//                        scatter zeroes only the sent values (worker_ring.rs:126-133),
+//                        gather keeps only the sent values in grad (:177-193).
+//
+// One hop = the fused kernel (or the sparse encoder) writes the payload, it
+// comes down to a pinned frame in pieces (D2H + one event per piece) and a
+// sender thread ships each piece as soon as it lands, while this thread reads
+// the previous worker's frame, validates the header and sends each complete
+// piece of a dense payload up to HBM while the rest is still on the socket.
+// Small dense frames (<= 256 KiB, ONO_TCP_ZEROCOPY) skip HBM: the codec
+// kernels read and write them in pinned host memory.
+#include <hip/hip_runtime.h>
+
+#include <poll.h>
+#include <sys/socket.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <unordered_set>
+#include <vector>
+
+#include "ono_internal.h"
+#include "ono_ring_impl.h"
+
+using namespace ono;
+
+namespace {
+
+constexpr int kTcpPollMs = 100;                   // abort / peer-failure latency
+constexpr size_t kTcpInline = size_t(256) << 10;  // frames up to this go through one poll loop
+constexpr size_t kSampleMax = 16384;              // SAMPLE_SIZE (protocol.rs:13-19)
+
+enum : uint32_t {
+    KIND_CONTROL = 0,
+    KIND_DENSE = 1,
+    KIND_DENSE_LAST = 2,
+    KIND_SPARSE = 3,
+    KIND_SPARSE_LAST = 4,
+    KIND_MAX_VALID = 6,
+};
+
+size_t tcp_block_bytes() {  // env ONO_TCP_BLOCK_KIB (default 4 MiB), read once per ring
+    const char *v = getenv("ONO_TCP_BLOCK_KIB");
+    long k = v ? atol(v) : 0;
+    return k > 0 ? (size_t)k << 10 : size_t(4) << 20;
+}
+
+struct TcpErr {
+    int code = ONO_OK;
+    char msg[192] = {0};
+};
+
+// pinned host buffer grown on demand (never while a transfer into it is pending)
+int grow_pinned(uint8_t **p, size_t *cap, size_t need) {
+    if (*cap >= need) return ONO_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    ONO_HIP(hipHostMalloc((void **)p, need, hipHostMallocDefault));
+    *cap = need;
+    return ONO_OK;
+}
+
+int ensure_tx_events(ono_ring *r, size_t pieces) {
+    while (r->tx_ev.size() < pieces) {
+        hipEvent_t ev;
+        ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        r->tx_ev.push_back(ev);
+    }
+    return ONO_OK;
+}
+
+void put_header(uint8_t *h, size_t payload, uint32_t kind) {
+    const uint64_t flen = 4 + (uint64_t)payload;
+    for (int i = 0; i < 8; i++) h[i] = (uint8_t)(flen >> (56 - 8 * i));
+    for (int i = 0; i < 4; i++) h[8 + i] = (uint8_t)(kind >> (24 - 8 * i));
+}
+
+// What this worker sends in one hop: a contiguous frame in pinned memory whose
+// payload is complete (zero-copy) or arrives by D2H pieces gated on r->tx_ev.
+struct Outgoing {
+    const uint8_t *frame = nullptr;
+    size_t payload = 0;
+    size_t pieces = 0;  // 0: complete
+};
+
+// Where the previous worker's frame goes.  A DenseGrad must carry exactly
+// dense_bytes (this hop's chunk); it lands at dense_host and, when dense_dev is
+// set, goes up to HBM piece by piece.  A SparseGrad lands in r->sp_rx (host).
+struct Incoming {
+    size_t dense_bytes = 0;
+    uint8_t *dense_host = nullptr;
+    uint8_t *dense_dev = nullptr;
+    size_t sparse_cap = 0;
+    uint32_t kind = 0;  // result: KIND_DENSE or KIND_SPARSE
+    size_t bytes = 0;   // result: payload bytes
+};
+
+// Wait until `fd` is ready for `ev`; false (with e set) on abort, stop or poll error.
+bool tcp_wait(ono_ring *r, int fd, short ev, const std::atomic<bool> &stop, TcpErr &e) {
+    for (;;) {
+        if (r->aborted.load()) { e.code = ONO_E_ABORTED; snprintf(e.msg, sizeof e.msg, "ring aborted"); return false; }
+        if (stop.load()) { e.code = ONO_E_OTHER; return false; }  // the other side already failed
+        struct pollfd p = {fd, ev, 0};
+        int pr = poll(&p, 1, kTcpPollMs);
+        if (pr < 0 && errno != EINTR) {
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "poll: %s", strerror(errno)); return false;
+        }
+        if (pr > 0) return true;
+    }
+}
+
+// One send(2) of the frame's ready bytes; false (e set) on a socket error.
+bool tcp_send_some(ono_ring *r, const uint8_t *tx, size_t &sent, size_t ready, TcpErr &e) {
+    ssize_t k = send(r->fd_next, tx + sent, ready - sent, MSG_DONTWAIT | MSG_NOSIGNAL);
+    if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+        e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "send to next worker: %s", strerror(errno));
+        return false;
+    }
+    if (k > 0) sent += (size_t)k;
+    return true;
+}
+
+// Receive side of one hop: the 12-byte header first, then the payload into
+// the destination its kind selects.
+struct TcpRecv {
+    Incoming &in;
+    uint8_t hdr[12];
+    size_t got = 0, need = 12, issued = 0;  // got/need count header + payload bytes
+    bool have_hdr = false;
+    uint8_t *dst = nullptr, *dev = nullptr;
+    explicit TcpRecv(Incoming &i) : in(i) {}
+    bool done() const { return have_hdr && got >= need; }
+
+    bool header(ono_ring *r, TcpErr &e) {
+        uint64_t l = 0;
+        for (int i = 0; i < 8; i++) l = (l << 8) | hdr[i];
+        const uint32_t kind = hdr[11];  // Header::from_be_bytes(..) as u8 (msg.rs:168)
+        if (kind > KIND_MAX_VALID) {     // msg.rs:187: invalid_kind_byte
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "invalid kind byte %u", kind); return false;
+        }
+        if (l < 4) {
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "frame of %llu bytes has no header", (unsigned long long)l);
+            return false;
+        }
+        const uint64_t pay = l - 4;
+        if (kind == KIND_DENSE || kind == KIND_DENSE_LAST) {
+            if (pay != in.dense_bytes) {  // the hop's chunk (worker_ring.rs:141-143, :200)
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
+                         (unsigned long long)pay, in.dense_bytes);
+                return false;
+            }
+            dst = in.dense_host;
+            dev = in.dense_dev;
+            in.kind = KIND_DENSE;
+        } else if (kind == KIND_SPARSE || kind == KIND_SPARSE_LAST) {
+            if (pay > in.sparse_cap) {  // longer than any grad_drop of this hop's chunk
+                e.code = ONO_E_PROTO;
+                snprintf(e.msg, sizeof e.msg,
+                         "Received an invalid worker event (sparse payload of %llu bytes, at most %zu)",
+                         (unsigned long long)pay, in.sparse_cap);
+                return false;
+            }
+            if (int rc = grow_pinned(&r->sp_rx, &r->sp_rx_cap, std::max<size_t>(pay, 8))) {
+                e.code = rc; snprintf(e.msg, sizeof e.msg, "%s", ono_last_error()); return false;
+            }
+            dst = r->sp_rx;
+            dev = nullptr;
+            in.kind = KIND_SPARSE;
+        } else {  // a control message, params or a data chunk where a gradient is required
+            e.code = ONO_E_PROTO;
+            snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind);
+            return false;
+        }
+        in.bytes = (size_t)pay;
+        need = 12 + (size_t)pay;
+        have_hdr = true;
+        return true;
+    }
+
+    // one recv(2); false (e set) on a socket or protocol error
+    bool step(ono_ring *r, hipStream_t s, TcpErr &e) {
+        uint8_t *p = have_hdr ? dst + (got - 12) : hdr + got;
+        const size_t want = have_hdr ? need - got : 12 - got;
+        ssize_t k = recv(r->fd_prev, p, want, MSG_DONTWAIT);
+        if (k == 0) { e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "previous worker closed the connection"); return false; }
+        if (k < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) return true;
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "recv from previous worker: %s", strerror(errno));
+            return false;
+        }
+        got += (size_t)k;
+        if (!have_hdr && got == 12 && !header(r, e)) return false;
+        if (have_hdr && dev) {  // complete pieces go up to HBM while the rest is on the socket
+            const size_t blk = r->tcp_block, avail = got - 12, payload = need - 12;
+            while (issued < avail && (avail - issued >= blk || avail == payload)) {
+                const size_t c = std::min(blk, payload - issued);
+                hipError_t he = hipMemcpyAsync(dev + issued, dst + issued, c, hipMemcpyHostToDevice, s);
+                if (he != hipSuccess) {
+                    e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "H2D of a frame: %s", hipGetErrorString(he));
+                    return false;
+                }
+                issued += c;
+            }
+        }
+        return true;
+    }
+};
+
+// Ships `out`, waiting for each D2H piece before sending the bytes it covers.
+void tcp_send_frame(ono_ring *r, const Outgoing &out, const std::atomic<bool> &stop, TcpErr &e) {
+    const size_t blk = r->tcp_block, total = 12 + out.payload;
+    size_t sent = 0;
+    for (size_t b = 0; sent < total; b++) {
+        const size_t ready = out.pieces ? std::min(total, 12 + (b + 1) * blk) : total;
+        if (out.pieces && b < out.pieces) {
+            hipError_t he = hipEventSynchronize(r->tx_ev[b]);
+            if (he != hipSuccess) {
+                e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "D2H of a frame: %s", hipGetErrorString(he));
+                return;
+            }
+        }
+        while (sent < ready)
+            if (!tcp_wait(r, r->fd_next, POLLOUT, stop, e) || !tcp_send_some(r, out.frame, sent, ready, e)) return;
+    }
+}
+
+// Small frames: one thread drives both directions from one poll loop (a
+// thread hand-off costs more than the transfer).
+int tcp_exchange_inline(ono_ring *r, const Outgoing &out, Incoming &in, hipStream_t s) {
+    if (out.pieces) ONO_HIP(hipEventSynchronize(r->tx_ev[out.pieces - 1]));  // the whole payload is down
+    const size_t total = 12 + out.payload;
+    size_t sent = 0;
+    TcpRecv rv(in);
+    TcpErr e;
+    while (sent < total || !rv.done()) {
+        if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+        struct pollfd p[2];
+        int np = 0, is = -1, ir = -1;
+        if (sent < total) { p[np] = {r->fd_next, POLLOUT, 0}; is = np++; }
+        if (!rv.done()) { p[np] = {r->fd_prev, POLLIN, 0}; ir = np++; }
+        int pr = poll(p, (nfds_t)np, kTcpPollMs);
+        if (pr < 0 && errno != EINTR) return set_error(ONO_E_IO, "poll: %s", strerror(errno));
+        if (pr <= 0) continue;
+        if (is >= 0 && (p[is].revents & (POLLOUT | POLLERR | POLLHUP)) && !tcp_send_some(r, out.frame, sent, total, e))
+            return set_error(e.code, "%s", e.msg);
+        if (ir >= 0 && (p[ir].revents & (POLLIN | POLLERR | POLLHUP)) && !rv.step(r, s, e))
+            return set_error(e.code, "%s", e.msg);
+    }
+    return ONO_OK;
+}
+
+// One hop: send `out` to next while receiving prev's frame (try_join!,
+// worker_ring.rs:122-123).  The receive buffers are free: the caller
+// synchronized the stream work that read them.
+int tcp_exchange(ono_ring *r, const Outgoing &out, Incoming &in, hipStream_t s) {
+    if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+    if (out.payload <= kTcpInline && in.dense_bytes <= kTcpInline) return tcp_exchange_inline(r, out, in, s);
+    std::atomic<bool> stop_send{false}, stop_recv{false};
+    TcpErr es, er;
+    std::thread sender([&] {
+        tcp_send_frame(r, out, stop_send, es);
+        if (es.code) stop_recv.store(true);
+    });
+    TcpRecv rv(in);
+    while (!rv.done())
+        if (!tcp_wait(r, r->fd_prev, POLLIN, stop_recv, er) || !rv.step(r, s, er)) {
+            stop_send.store(true);
+            break;
+        }
+    sender.join();
+    // report the root cause, not the "other side failed" stop
+    const TcpErr &e = (er.code && er.code != ONO_E_OTHER) ? er : (es.code && es.code != ONO_E_OTHER) ? es : er;
+    if (e.code) return set_error(e.code, "%s", e.msg);
+    return ONO_OK;
+}
+
+// splitmix64 (the default sampler's generator)
+uint64_t sm_next(uint64_t &x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+class TcpRing {
+public:
+    TcpRing(ono_ring *r, hipStream_t s) : r_(r), s_(s), n_(r->n), pos_(r->pos), zc_(r->zc[0] != nullptr) {}
+
+    int pull_grads(float *res, float *grad) {
+        return r_->sparse_r > 0.0f ? pull_sparse(res, grad) : pull_dense(res, grad);
+    }
+
+private:
+    size_t off(int c) const { return r_->off[c]; }
+    size_t len(int c) const { return r_->off[c + 1] - r_->off[c]; }
+    int mod(int x) const { return ((x % n_) + n_) % n_; }
+    // the f16 wire slot b holding chunk c (phase-matched to the chunk start)
+    uint16_t *slot(int b, int c) const {
+        return (zc_ ? reinterpret_cast<uint16_t *>(r_->zc[b] + 16) : static_cast<uint16_t *>(r_->wbuf[b])) +
+               ph(off(c));
+    }
+
+    // D2H of `bytes` from device `src` into r->tx + 12, in pieces with events
+    int stage_down(const void *src, size_t bytes, size_t &pieces) {
+        const size_t blk = r_->tcp_block;
+        pieces = (bytes + blk - 1) / blk;
+        int rc = ensure_tx_events(r_, pieces);
+        if (rc) return rc;
+        for (size_t b = 0; b < pieces; b++) {
+            const size_t o = b * blk, c = std::min(blk, bytes - o);
+            ONO_HIP(hipMemcpyAsync(r_->tx + 12 + o, static_cast<const uint8_t *>(src) + o, c, hipMemcpyDeviceToHost,
+                                   s_));
+            ONO_HIP(hipEventRecord(r_->tx_ev[b], s_));
+        }
+        return ONO_OK;
+    }
+    // the receive buffers are free once the stream work before this hop ran
+    int settle(const Outgoing &o) {
+        if (o.pieces) ONO_HIP(hipEventSynchronize(r_->tx_ev[0]));  // everything enqueued before the D2H
+        else ONO_HIP(hipStreamSynchronize(s_));
+        return ONO_OK;
+    }
+
+    // Base serializer: DenseGrad of the f16 payload already in slot(b, c)
+    int out_dense(int b, int c, Outgoing &o) {
+        const size_t bytes = 2 * len(c);
+        o = Outgoing{};
+        o.payload = bytes;
+        if (zc_) {  // the codec kernel wrote the payload in place; the header goes just before it
+            uint8_t *f = reinterpret_cast<uint8_t *>(slot(b, c)) - 12;
+            put_header(f, bytes, KIND_DENSE);
+            o.frame = f;
+            ONO_HIP(hipStreamSynchronize(s_));
+            return ONO_OK;
+        }
+        int rc = grow_pinned(&r_->tx, &r_->tx_cap, 12 + bytes);
+        if (rc) return rc;
+        put_header(r_->tx, bytes, KIND_DENSE);
+        o.frame = r_->tx;
+        if ((rc = stage_down(slot(b, c), bytes, o.pieces))) return rc;
+        return settle(o);
+    }
+
+    // SparseCapable serializer: t = calculate_threshold(chunk, r), then the
+    // SparseGrad of grad_drop(chunk, t) (compressor.rs:71-98)
+    int out_sparse(const float *chunk, size_t L, float &t, Outgoing &o) {
+        int rc = threshold(chunk, L, t);
+        if (rc) return rc;
+        const size_t cap = ono_sparse_max_bytes(L);
+        if (r_->sp_dev_cap < cap) {
+            (void)hipFree(r_->sp_dev);
+            r_->sp_dev = nullptr;
+            r_->sp_dev_cap = 0;
+            ONO_HIP(hipMalloc((void **)&r_->sp_dev, cap + 8));
+            r_->sp_dev_cap = cap;
+        }
+        size_t nb = 0;
+        if ((rc = ono_sparse_drop(r_->sp_dev, cap, &nb, chunk, L, t, s_))) return rc;
+        if ((rc = grow_pinned(&r_->tx, &r_->tx_cap, 12 + nb))) return rc;
+        o = Outgoing{};
+        put_header(r_->tx, nb, KIND_SPARSE);
+        o.frame = r_->tx;
+        o.payload = nb;
+        if ((rc = stage_down(r_->sp_dev, nb, o.pieces))) return rc;
+        return settle(o);
+    }
+
+    // calculate_threshold over the sample the sampler draws (all values up to
+    // SAMPLE_SIZE; above, the caller's sampler or the default one)
+    int threshold(const float *chunk, size_t L, float &t) {
+        const size_t m = std::min(L, kSampleMax);
+        bool sampled = false;
+        if (r_->sampler) {
+            if (r_->sampler(r_->sampler_ctx, L, r_->sample_idx, m) != 0)
+                return set_error(ONO_E_OTHER, "the sampler failed for a chunk of %zu values", L);
+            sampled = L > kSampleMax;
+        } else if (L > kSampleMax) {
+            int rc = ono_sparse_sample_default(&r_->sample_state, L, r_->sample_idx, m);
+            if (rc) return rc;
+            sampled = true;
+        }
+        return ono_sparse_threshold(&t, chunk, L, sampled ? r_->sample_idx : nullptr, m, r_->sparse_r, s_);
+    }
+
+    Incoming in_for(int c, int b) const {
+        Incoming in;
+        in.dense_bytes = 2 * len(c);
+        if (zc_) {
+            in.dense_host = reinterpret_cast<uint8_t *>(slot(b, c));
+        } else {
+            in.dense_host = r_->rx + 12;
+            in.dense_dev = reinterpret_cast<uint8_t *>(slot(b, c));
+        }
+        in.sparse_cap = ono_sparse_max_bytes(len(c));
+        return in;
+    }
+    int ensure_rx() {
+        return grow_pinned(&r_->rx, &r_->rx_cap, 12 + 2 * (r_->maxc + 4));
+    }
+
+    // A received SparseGrad lifted into dst (zero-filled + the runs), which
+    // must be this hop's chunk length (the reference's zip / copy_from_slice)
+    int lift(const Incoming &in, float *dst, int c) {
+        uint64_t total = 0;
+        for (int q = 0; q < 8 && q < (int)in.bytes; q++) total |= (uint64_t)r_->sp_rx[q] << (8 * q);
+        if (in.bytes >= 8 && total != len(c))
+            return set_error(ONO_E_PROTO, "Received an invalid worker event (sparse gradient of %llu values, expected %zu)",
+                             (unsigned long long)total, len(c));
+        size_t got = 0;
+        int rc = ono_sparse_lift(dst, len(c), &got, r_->sp_rx, in.bytes, s_);
+        // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
+        if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
+        return rc;
+    }
+    int tmp() {
+        if (!r_->sp_tmp) ONO_HIP(hipMalloc((void **)&r_->sp_tmp, (r_->maxc + 4) * sizeof(float)));
+        return ONO_OK;
+    }
+    // phase-matched scratch for chunk c
+    float *tmp_for(int c) const { return r_->sp_tmp + ph(off(c)); }
+
+    // ---- Base serializer: the fused codec kernels (ono_ring.cpp's hop ring)
+    // with a lift in between when the previous worker sent a SparseGrad.
+    int pull_dense(float *res, float *grad) {
+        int rc = ensure_rx();
+        if (rc) return rc;
+        const float fn = (float)n_;
+        // scatter: out slot 0, in slot 1
+        ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, pos_), res + off(pos_), len(pos_), s_));
+        for (int st = 0; st < n_ - 1; st++) {
+            const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
+            Outgoing o;
+            Incoming in = in_for(cr, 1);
+            if ((rc = out_dense(0, cs, o)) || (rc = xchg(o, in))) return rc;
+            const bool last = st == n_ - 2;
+            if (in.kind == KIND_DENSE) {
+                if (!last)
+                    ONO_K(r_, s_, launch_add_encode_zero<uint16_t>(slot(0, cr), res + off(cr), slot(1, cr), len(cr), s_));
+                else
+                    ONO_K(r_, s_, launch_add_finish<uint16_t>(grad + off(cr), slot(0, cr), res + off(cr), slot(1, cr),
+                                                              len(cr), fn, s_));
+                continue;
+            }
+            if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
+            ONO_K(r_, s_, launch_acc(res + off(cr), tmp_for(cr), len(cr), s_, true));  // :141-143
+            if (!last) {
+                ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, cr), res + off(cr), len(cr), s_));
+            } else {  // grad = x / n, the f16 message, residual = 0 (add_finish without the add)
+                const float *ins[1] = {res + off(cr)};
+                ONO_K(r_, s_, launch_direct<uint16_t>(grad + off(cr), slot(0, cr), ins, 1, len(cr), fn, true, s_));
+            }
+        }
+        // gather: forward what arrived, alternate the two slots
+        int bo = 0, bi = 1;
+        for (int j = 0; j < n_ - 1; j++) {
+            const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
+            Outgoing o;
+            Incoming in = in_for(cr, bi);
+            if ((rc = out_dense(bo, cs, o)) || (rc = xchg(o, in))) return rc;
+            if (in.kind == KIND_DENSE) {
+                ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(bi, cr), len(cr), fn, s_));
+            } else {  // :200 copies the lifted chunk; the next hop forwards its f16 image
+                if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
+                ONO_K(r_, s_, launch_scale_zero(grad + off(cr), tmp_for(cr), len(cr), fn, nullptr, s_));
+                ONO_K(r_, s_, launch_encode<uint16_t>(slot(bi, cr), tmp_for(cr), len(cr), s_));
+            }
+            std::swap(bo, bi);
+        }
+        return ONO_OK;
+    }
+
+    // ---- SparseCapable serializer (worker_ring.rs:112-204 with the sparse
+    // branches): unfused — each hop's threshold is taken over the chunk as the
+    // reference holds it, so the division by n waits for the end (:101-105).
+    int pull_sparse(float *res, float *grad) {
+        int rc = ensure_rx();
+        if (rc) return rc;
+        float t = 0.0f;
+        for (int st = 0; st < n_ - 1; st++) {  // scatter (:112-147)
+            const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
+            Outgoing o;
+            Incoming in = in_for(cr, 1);
+            if ((rc = out_sparse(res + off(cs), len(cs), t, o)) || (rc = xchg(o, in))) return rc;
+            if ((rc = ono_sparse_mask(res + off(cs), len(cs), t, 1, s_))) return rc;  // :128-131: sent values leave
+            if (in.kind == KIND_DENSE) {
+                ONO_K(r_, s_, launch_decode_add<uint16_t>(res + off(cr), slot(1, cr), len(cr), s_));
+            } else {
+                if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
+                ONO_K(r_, s_, launch_acc(res + off(cr), tmp_for(cr), len(cr), s_, true));
+            }
+        }
+        const int own = mod(pos_ + 1);  // gather (:155-204)
+        ONO_HIP(hipMemcpyAsync(grad + off(own), res + off(own), len(own) * sizeof(float), hipMemcpyDeviceToDevice,
+                               s_));  // :166
+        for (int j = 0; j < n_ - 1; j++) {
+            const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
+            Outgoing o;
+            Incoming in = in_for(cr, 1);
+            if ((rc = out_sparse(grad + off(cs), len(cs), t, o)) || (rc = xchg(o, in))) return rc;
+            if ((rc = ono_sparse_mask(grad + off(cs), len(cs), t, 0, s_))) return rc;  // :183-187: keep the sent
+            if (j == 0) ONO_HIP(hipMemsetAsync(res + off(own), 0, len(own) * sizeof(float), s_));  // :191-193
+            if (in.kind == KIND_DENSE) {
+                ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(1, cr), len(cr), 1.0f, s_));
+            } else if ((rc = lift(in, grad + off(cr), cr))) {
+                return rc;
+            }
+        }
+        ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105
+        return ONO_OK;
+    }
+
+    int xchg(const Outgoing &o, Incoming &in) {
+        return timed(r_, s_, ONO_PHASE_RCCL, [&]() -> int { return tcp_exchange(r_, o, in, s_); });
+    }
+
+    ono_ring *r_;
+    hipStream_t s_;
+    int n_, pos_;
+    bool zc_;
+};
+
+}  // namespace
+
+namespace ono {
+int tcp_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
+    TcpRing t(r, s);
+    return t.pull_grads(res, grad);
+}
+}  // namespace ono
+
+extern "C" {
+
+// The reference's ring over its own TCP connections (builder.rs:272-311 hands
+// the worker an accepted `prev` and a connected `next` stream): f16 wire, hop
+// schedule, the arithmetic in HBM, the frames on the caller's sockets.
+int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
+                        int fd_next) {
+    if (!out) return set_error(ONO_E_ARG, "out is NULL");
+    *out = nullptr;
+    if (nranks < 1 || pos < 0 || pos >= nranks) return set_error(ONO_E_ARG, "pos=%d nranks=%d", pos, nranks);
+    if (size < (size_t)nranks)
+        return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, nranks);
+    if (nranks > 1 && (fd_prev < 0 || fd_next < 0)) return set_error(ONO_E_ARG, "sockets required for nranks > 1");
+    // reuse the common allocation path (nranks == 1 needs neither sockets nor an id)
+    static const uint8_t no_uid[ONO_UID_BYTES] = {0};
+    int rc = ono_ring_create(out, 0, 1, size, device, no_uid, ONO_WIRE_F16);
+    if (rc) return rc;
+    ono_ring *r = *out;
+    r->sample_idx = new uint32_t[kSampleMax];
+    if (nranks == 1) return ONO_OK;
+    *out = nullptr;
+    r->n = nranks;
+    r->pos = pos;
+    r->off = split_chunks(size, (size_t)nranks);
+    r->maxc = r->off[1] - r->off[0];
+    r->algo = ONO_ALGO_HOPS;
+    r->fd_prev = fd_prev;
+    r->fd_next = fd_next;
+    DeviceGuard g(device);
+    hipError_t e;
+    for (int b = 0; b < 2; b++)
+        if ((e = hipMalloc(&r->wbuf[b], (r->maxc + 4) * sizeof(float))) != hipSuccess) {
+            ono_ring_destroy(r);
+            return hip_error(e, "wire buffer allocation", __FILE__, __LINE__);
+        }
+    // zero-copy frames up to ONO_TCP_ZEROCOPY KiB of payload (default 256; 0 = off)
+    const char *zc_env = getenv("ONO_TCP_ZEROCOPY");
+    const size_t zc_max = zc_env ? (size_t)atol(zc_env) << 10 : kTcpInline;
+    if (2 * (r->maxc + 4) <= zc_max)
+        for (int b = 0; b < 2; b++)
+            if ((e = hipHostMalloc((void **)&r->zc[b], 16 + 2 * (r->maxc + 4), hipHostMallocCoherent)) != hipSuccess) {
+                ono_ring_destroy(r);
+                return hip_error(e, "zero-copy frame allocation", __FILE__, __LINE__);
+            }
+    r->tcp_block = tcp_block_bytes();
+    if ((rc = grow_pinned(&r->tx, &r->tx_cap, 12 + 2 * (r->maxc + 4))) ||
+        (rc = grow_pinned(&r->rx, &r->rx_cap, 12 + 2 * (r->maxc + 4))) ||
+        (rc = ensure_tx_events(r, (2 * (r->maxc + 4) + r->tcp_block - 1) / r->tcp_block))) {
+        ono_ring_destroy(r);
+        return rc;
+    }
+    *out = r;
+    return ONO_OK;
+}
+
+int ono_ring_set_sparse(ono_ring *r, float ratio, uint64_t seed) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    if (!(ratio == 0.0f || (ratio > 0.0f && ratio <= 1.0f)))
+        return set_error(ONO_E_ARG, "ratio %g: SparseCapable keeps a fraction in (0, 1], 0 = the Base serializer",
+                         (double)ratio);
+    if (ratio > 0.0f && r->n > 1 && r->fd_next < 0)
+        return set_error(ONO_E_ARG, "the SparseCapable serializer is a TCP-wire format: TCP rings only");
+    std::lock_guard<std::mutex> lk(r->mu);
+    if (!r->sample_idx) r->sample_idx = new uint32_t[kSampleMax];
+    r->sparse_r = ratio;
+    r->sample_state = seed;
+    return ONO_OK;
+}
+
+int ono_ring_set_sampler(ono_ring *r, ono_sample_fn fn, void *ctx) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->sampler = fn;
+    r->sampler_ctx = ctx;
+    return ONO_OK;
+}
+
+// Floyd's algorithm over a splitmix64 stream: `amount` distinct indices of
+// [0, len), in draw order.  Not rand 0.9.4's index::sample (StdRng is ChaCha12
+// and is not restated here): it is the deterministic stand-in both this
+// library and the CPU oracle use when no sampler is installed.
+int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t amount) {
+    if (!state || (amount && !idx)) return set_error(ONO_E_ARG, "NULL argument");
+    if (len > 0xFFFFFFFFull) return set_error(ONO_E_ARG, "sample indices are u32");
+    if (amount > len) return set_error(ONO_E_ARG, "sample of %zu from %zu values", amount, len);
+    if (amount == len) {  // the whole chunk: no draws
+        for (size_t i = 0; i < len; i++) idx[i] = (uint32_t)i;
+        return ONO_OK;
+    }
+    std::unordered_set<uint32_t> seen;
+    seen.reserve(2 * amount);
+    size_t c = 0;
+    for (size_t j = len - amount; j < len; j++) {
+        const uint32_t t = (uint32_t)(sm_next(*state) % (uint64_t)(j + 1));
+        if (seen.insert(t).second) {
+            idx[c++] = t;
+        } else {
+            seen.insert((uint32_t)j);
+            idx[c++] = (uint32_t)j;
+        }
+    }
+    return ONO_OK;
+}
+
+}  // extern "C"

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the library load; see above)
 
 from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, IoError, OnoError,
                    RcclError, SizeMismatch, header_functions, lib)
-from . import kernels, sparse
+from . import kernels, plan, sparse
 from .ring import DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id
 from .store import (Adam, AddOptimizer, BarrierSync, BlockingStore, DynBarrier, GradientDescent,
                     GradientDescentWithMomentum, NoBlockingSync, WildStore, shard_size_for)

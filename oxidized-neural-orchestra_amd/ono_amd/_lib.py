@@ -68,12 +68,24 @@ _ERR = {ONO_E_SIZE: SizeMismatch, ONO_E_PROTO: InvalidWorkerEvent, ONO_E_HIP: Hi
         ONO_E_IO: IoError}
 
 
+PLAN_REFS = MAX_INPUTS + 2
+
+
+class PlanStep(C.Structure):
+    """ono_plan_step (include/ono_reduce.h): one step of an exchange plan."""
+    _fields_ = [("kind", C.c_int32), ("op", C.c_int32), ("peer", C.c_int32), ("dtype", C.c_int32),
+                ("stream", C.c_int32), ("nref", C.c_int32), ("flag", C.c_int32), ("divisor", C.c_float),
+                ("count", C.c_uint64), ("buf", C.c_int32 * PLAN_REFS), ("off", C.c_uint64 * PLAN_REFS)]
+
+
 class OptSpec(C.Structure):
     _fields_ = [("kind", C.c_int), ("lr", C.c_float), ("momentum", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float)]
 
 
 LEADER_FN = C.CFUNCTYPE(None, C.c_void_p)
+# ono_sample_fn: int (*)(void *ctx, size_t len, uint32_t *idx, size_t amount)
+SAMPLE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t)
 
 _vp, _fp, _sz, _i, _u64 = C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_uint64
 
@@ -98,6 +110,10 @@ _SIGS = {
     "ono_sparse_lift_dev": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_fallbacks": (_sz, []),
     "ono_sparse_mask": (_i, [_fp, _sz, C.c_float, _i, _vp]),
+    "ono_sparse_threshold": (_i, [C.POINTER(C.c_float), _fp, _sz, _vp, _sz, C.c_float, _vp]),
+    "ono_sparse_sample_default": (_i, [C.POINTER(C.c_uint64), _sz, _vp, _sz]),
+    "ono_ring_set_sparse": (_i, [_vp, C.c_float, _u64]),
+    "ono_ring_set_sampler": (_i, [_vp, _vp, _vp]),
     "ono_ring_unique_id": (_i, [C.c_char_p]),
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
     "ono_ring_create_tcp": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i, _i]),
@@ -152,6 +168,9 @@ _SIGS = {
     "ono_ps_create": (_i, [C.POINTER(C.c_void_p), _vp, _fp, _sz, C.POINTER(OptSpec)]),
     "ono_ps_destroy": (_i, [_vp]),
     "ono_ps_step": (_i, [_vp, _fp, _fp, _vp]),
+    "ono_plan_pull_grads": (_i, [_i, _i, _i, _i, _sz, _i, _vp, _sz, C.POINTER(C.c_size_t)]),
+    "ono_plan_ps_step": (_i, [_i, _i, _sz, _vp, _sz, C.POINTER(C.c_size_t)]),
+    "ono_plan_buffers": (_i, [_i, _sz, _sz, C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

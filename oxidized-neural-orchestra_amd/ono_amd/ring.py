@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import kernels
-from ._lib import ALGO, PHASES, UID_BYTES, WIRE, XGMI_HANDLE_BYTES, call, lib
+from ._lib import ALGO, PHASES, SAMPLE_FN, UID_BYTES, WIRE, XGMI_HANDLE_BYTES, call, lib
 
 
 class _DevArray:
@@ -196,6 +196,36 @@ class WorkerRingManager:
         """n > 1 exchange schedule: "allreduce" | "hops" | "direct" | "xgmi" | "auto"."""
         call("ono_ring_set_algo", self._h, ALGO[algo])
         self.algo = algo
+
+    def set_sparse(self, r: float, seed: int = 0) -> None:
+        """The SparseCapable{r} serializer (compressor.rs:71-98): SparseGrad
+        frames of the values with |g| >= calculate_threshold(chunk, r), the
+        ring's sparse branches (worker_ring.rs:126-133, :177-193).  r = 0
+        returns to the Base (dense f16) serializer.  TCP rings only.  `seed`
+        starts the default threshold sampler (used above 16384 values)."""
+        call("ono_ring_set_sparse", self._h, float(r), int(seed) & (2 ** 64 - 1))
+
+    def set_sampler(self, fn) -> None:
+        """fn(length, amount) -> `amount` distinct indices of [0, length): the
+        threshold sample of every sparse push (the reference draws it with
+        rand::seq::index::sample on the Compressor's StdRng).  None restores
+        the default sampler."""
+        if fn is None:
+            self._sampler = None
+            call("ono_ring_set_sampler", self._h, None, None)
+            return
+
+        def tramp(_ctx, length, idx, amount):
+            try:
+                got = np.asarray(fn(int(length), int(amount)), dtype=np.uint32)
+                if got.shape != (amount,):
+                    return 1
+                C.memmove(idx, got.ctypes.data, 4 * amount)
+                return 0
+            except Exception:  # reported to the ring as a sampler failure
+                return 1
+        self._sampler = SAMPLE_FN(tramp)  # kept alive as long as the ring
+        call("ono_ring_set_sampler", self._h, C.cast(self._sampler, C.c_void_p), None)
 
     def set_pipeline(self, segments: int) -> None:
         """Segments of the f32 all-reduce schedule (finaliser of segment j

@@ -34,6 +34,29 @@ def threshold_full(g: np.ndarray, r: float) -> float:
     return float(max(a[k], MIN_POSITIVE_F16))
 
 
+def threshold(g: torch.Tensor, r: float, idx=None, stream=None) -> float:
+    """calculate_threshold on the device (ono_sparse_threshold): over every
+    value (len <= 16384, idx None) or the sample indices `idx` (<= 16384)."""
+    n = g.numel()
+    t = C.c_float()
+    if idx is None:
+        call("ono_sparse_threshold", C.byref(t), kernels.f32_ptr(g), n, None, n, float(r), kernels.stream_handle(stream))
+    else:
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        call("ono_sparse_threshold", C.byref(t), kernels.f32_ptr(g), n, ix.ctypes.data, ix.size, float(r),
+             kernels.stream_handle(stream))
+    return t.value
+
+
+def sample_default(state: int, length: int, amount: int) -> tuple[np.ndarray, int]:
+    """The default threshold sampler (ono_sparse_sample_default): (indices,
+    next state).  Host code — no device needed."""
+    st = C.c_uint64(state & (2 ** 64 - 1))
+    out = np.empty(amount, dtype=np.uint32)
+    call("ono_sparse_sample_default", C.byref(st), length, out.ctypes.data if amount else None, amount)
+    return out, st.value
+
+
 def grad_drop(g: torch.Tensor, threshold: float, stream=None) -> bytes:
     n = g.numel()
     cap = lib().ono_sparse_max_bytes(n)

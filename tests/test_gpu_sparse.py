@@ -281,3 +281,49 @@ def test_drop_headers_across_tiles_and_scan_chunks(pattern):
     want = O.grad_drop(g, 0.5)
     assert bytes(got.cpu().numpy()) == want
     assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
+
+
+# ------------------------------------------------ calculate_threshold on the device
+def _threshold_inputs(n, seed):
+    x = O.synth(n, seed, 0)
+    rng = np.random.default_rng(seed)
+    k = max(1, n // 50)
+    x[rng.integers(0, n, k)] = 0.0
+    x[rng.integers(0, n, k)] = -0.0
+    x[rng.integers(0, n, k)] = np.float32(6.103515625e-05)          # the floor itself
+    x[rng.integers(0, n, k)] = x[rng.integers(0, n, k)]           # ties
+    x[rng.integers(0, n, max(1, k // 4))] = np.inf
+    x.view(np.uint32)[rng.integers(0, n, max(1, k // 4))] = 0xFFC01234  # -NaN with a payload
+    return x
+
+
+@pytest.mark.parametrize("n", [1, 2, 17, 1000, 16384])
+@pytest.mark.parametrize("r", [0.05, 0.4, 0.9, 1.0])
+def test_threshold_full_sample_vs_oracle(n, r):
+    """sp_threshold (radix select over the |g| bit patterns in LDS) equals the
+    restated calculate_threshold (sort in total_cmp order, k-th, max with
+    f16::MIN_POSITIVE) — NaN, inf, signed zeros and ties included."""
+    x = _threshold_inputs(n, SEED + n)
+    got = SP.threshold(torch.from_numpy(x).cuda(), r)
+    want = O.sparse_threshold_sample(x, r)
+    assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32), (got, want)
+
+
+@pytest.mark.parametrize("n,r", [(16385, 0.4), (100000, 0.1), (1 << 22, 0.9)])
+def test_threshold_drawn_sample_vs_oracle(n, r):
+    """Above 16384 values the sample is the caller's indices (a duplicate-free
+    draw); the device gathers them from HBM."""
+    x = _threshold_inputs(n, SEED + 7)
+    idx, _ = O.sample_default(99, n, 16384)
+    got = SP.threshold(torch.from_numpy(x).cuda(), r, idx)
+    assert np.float32(got).view(np.uint32) == np.float32(O.sparse_threshold_sample(x, r, idx)).view(np.uint32)
+
+
+def test_threshold_argument_errors():
+    g = torch.zeros(20000, device="cuda")
+    with pytest.raises(ono_amd.InvalidArgument):
+        SP.threshold(g, 0.4)  # above 16384 values a sample is required
+    with pytest.raises(ono_amd.InvalidArgument):
+        SP.threshold(g[:10], 1.5)
+    with pytest.raises(ono_amd.InvalidArgument):
+        SP.threshold(g[:10], 0.4, np.array([3, 10], np.uint32))  # index out of range

@@ -14,7 +14,13 @@ sockets):
 * the bytes an MI355X worker puts on the wire equal the reference framing of
   the reference's f16 encoding of its chunk;
 * the reference's failure behaviour: an invalid event is InvalidWorkerEvent
-  (worker_ring.rs:136-138), a closed peer is an io error, abort() unblocks.
+  (worker_ring.rs:136-138), a closed peer is an io error, abort() unblocks;
+* the SparseCapable serializer (ono_ring_set_sparse): SparseGrad frames
+  (kind 3, comms/src/protocol/msg.rs:175-178) on the wire, the ring's sparse
+  branches (worker_ring.rs:126-133, 177-193), and every worker accepting
+  both gradient kinds (handles/worker.rs:102-108) — all-GPU and mixed rings
+  with reference-style CPU workers of either serializer, bit-exact with the
+  restatement (oracle ono_ref_ring_pull_grads_sparse).
 """
 import socket
 import threading
@@ -48,8 +54,9 @@ class GpuWorker(threading.Thread):
     pull_grads (device or host-fed form); keeps the last round's results."""
 
     def __init__(self, rank, n, length, inputs, prev=None, nxt=None, connect=None, listener=None,
-                 host_fed=False):
+                 host_fed=False, sparse=None, sampler=None):
         super().__init__(daemon=True)
+        self.sparse, self.sampler = sparse, sampler  # (ratio, seed) of SparseCapable; a sampler callback
         self.rank, self.n, self.length, self.inputs = rank, n, length, inputs
         self.prev, self.nxt, self.connect, self.listener = prev, nxt, connect, listener
         self.host_fed = host_fed
@@ -69,6 +76,10 @@ class GpuWorker(threading.Thread):
             with torch.cuda.stream(s):
                 self.ring = ono_amd.WorkerRingManager.over_tcp(self.rank, self.n, self.length,
                                                                self.prev, self.nxt)
+                if self.sparse is not None:
+                    self.ring.set_sparse(*self.sparse)
+                if self.sampler is not None:
+                    self.ring.set_sampler(self.sampler)
                 self.ready.set()
                 for x in self.inputs:
                     if self.host_fed:
@@ -230,7 +241,7 @@ def start_two_rank(length, x):
     return w, links[1], pairs
 
 
-def test_tcp_ring_wire_bytes_and_invalid_kind():
+def test_tcp_ring_wire_bytes():
     length = 10001
     x = O.synth(length, SEED + 1, 0)
     w, (from_gpu, to_gpu), pairs = start_two_rank(length, x)
@@ -238,11 +249,29 @@ def test_tcp_ring_wire_bytes_and_invalid_kind():
         frame = recv_frame(from_gpu)
         (a, b) = O.split_chunks(length, 2)[0]
         assert frame == O.frame_dense(O.f16_encode(x[a:b]))  # byte for byte the reference's
-        bad = bytearray(O.frame_dense(O.f16_encode(np.zeros(length - b, np.float32))))
-        bad[11] = 3  # a Control frame where a DenseGrad is required
+        to_gpu.close()
+        w.join(60)
+    finally:
+        close_all(s for p in pairs for s in p)
+
+
+@pytest.mark.parametrize("kind,err", [(0, "proto"), (5, "proto"), (6, "proto"), (7, "io"), (200, "io")])
+def test_tcp_ring_frame_kinds(kind, err):
+    """A control message (0), params (5) or a data chunk (6) where a gradient
+    is required is the ring's InvalidWorkerEvent (worker_ring.rs:136-138);
+    kind bytes >= 7 fail Msg::deserialize with invalid_kind_byte (msg.rs:187),
+    an io::Error.  (Kinds 3/4 are SparseGrad — accepted, see the sparse tests.)"""
+    length = 10001
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED + 1, 0))
+    try:
+        recv_frame(from_gpu)
+        (a, b) = O.split_chunks(length, 2)[1]
+        bad = bytearray(O.frame_dense(O.f16_encode(np.zeros(b - a, np.float32))))
+        bad[11] = kind
         to_gpu.sendall(bytes(bad))
         w.join(60)
-        assert isinstance(w.err, ono_amd.InvalidWorkerEvent), w.err
+        want = ono_amd.InvalidWorkerEvent if err == "proto" else ono_amd.IoError
+        assert isinstance(w.err, want), w.err
     finally:
         close_all(s for p in pairs for s in p)
 
@@ -282,5 +311,174 @@ def test_tcp_ring_abort_unblocks():
         w.join(30)
         assert not w.is_alive()
         assert isinstance(w.err, ono_amd.Aborted), w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+
+
+# ------------------------------------------------------------ sparse mode
+def frame_sparse(payload: bytes, kind: int = 3) -> bytes:
+    return (4 + len(payload)).to_bytes(8, "big") + kind.to_bytes(4, "big") + payload
+
+
+def oracle_rounds(x_rounds, ratios, seeds):
+    """The restated rounds, the samplers' streams carried from round to round."""
+    st = list(seeds)
+    for x in x_rounds:
+        g, res, st = O.ring_pull_grads_sparse(x, ratios, st)
+    return g, res
+
+
+@pytest.mark.parametrize("n,length,ratios", [(2, 10001, [0.4, 0.4]), (2, 70001, [0.1, 0.9]),
+                                             (3, 40000, [0.25, 0.0, 0.6]), (4, 109386, [0.3, 0.3, 0.0, 1.0]),
+                                             (5, 4099, [0.5, 0.0, 0.0, 0.2, 0.7])])
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_tcp_ring_sparse_socketpairs_vs_oracle(n, length, ratios, zero_copy, monkeypatch):
+    """All-GPU rings of SparseCapable and Base workers (chunks below and above
+    the 16384-value sample), two rounds: bit-exact with the restatement."""
+    if not zero_copy:
+        monkeypatch.setenv("ONO_TCP_ZEROCOPY", "0")
+    seeds = [77 + r for r in range(n)]
+    ins = inputs_for(n, length, 2, SEED + 41)
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(2)], *links[r],
+                    sparse=(ratios[r], seeds[r]) if ratios[r] else None) for r in range(n)]
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        close_all(s for p in pairs for s in p)
+    eg, er = oracle_rounds(ins, ratios, seeds)
+    for r in range(n):
+        assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
+
+
+def test_tcp_ring_sparse_host_fed_and_sampler_callback():
+    """The host-fed form, and a caller-installed sampler (the boundary a Rust
+    integration uses to draw rand's index::sample): here a Python sampler that
+    draws the stand-in stream, so the restatement still applies."""
+    n, length, ratios = 3, 60000, [0.3, 0.3, 0.3]
+    seeds = [5, 6, 7]
+    ins = inputs_for(n, length, 2, SEED + 43)
+
+    def sampler_for(seed):
+        state = [seed]
+
+        def draw(ln, amount):
+            idx, state[0] = O.sample_default(state[0], ln, amount)
+            return idx
+        return draw
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(2)], *links[r], host_fed=(r == 1),
+                    sparse=(ratios[r], 0), sampler=sampler_for(seeds[r])) for r in range(n)]
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        close_all(s for p in pairs for s in p)
+    eg, er = oracle_rounds(ins, ratios, seeds)
+    for r in range(n):
+        assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
+
+
+@pytest.mark.parametrize("n,cpu_ranks,length,ratios", [(2, (1,), 109386, [0.4, 0.4]),
+                                                       (3, (1,), 40000, [0.0, 0.25, 0.5]),
+                                                       (4, (1, 3), 65539, [0.3, 0.0, 0.6, 0.1]),
+                                                       (5, (2, 3), 4099, [0.0, 0.9, 0.2, 0.0, 0.5])])
+def test_tcp_ring_sparse_mixed_with_reference_workers(n, cpu_ranks, length, ratios):
+    """MI355X workers and reference-style CPU workers, each with its own
+    serializer (SparseCapable or Base), in one loopback ring: bit-exact."""
+    rounds, seed = 2, SEED + 47
+    seeds = [300 + r for r in range(n)]
+    listeners, ports = {}, {}
+    for r in range(n):
+        if r not in cpu_ranks:
+            listeners[r] = socket.create_server(("127.0.0.1", 0))
+            ports[r] = listeners[r].getsockname()[1]
+    cpu, gpu = {}, []
+    try:
+        for r in sorted(cpu_ranks, reverse=True):
+            cpu[r] = O.CpuRingWorker(r, n, length, ports[(r + 1) % n], rounds=rounds, seed=seed, sparse=ratios[r],
+                                     sparse_seed=seeds[r])
+            ports[r] = cpu[r].port
+        x = [O.synth(length, seed, r) for r in range(n)]
+        gpu = [GpuWorker(r, n, length, [x[r]] * rounds, connect=lambda r=r: ports[(r + 1) % n],
+                         listener=listeners[r], sparse=(ratios[r], seeds[r]) if ratios[r] else None)
+               for r in range(n) if r not in cpu_ranks]
+        for w in gpu:
+            w.start()
+        join_all(gpu)
+        got = {w.rank: (w.grad, w.residual) for w in gpu}
+        for r, c in cpu.items():
+            g, res, _ = c.result()
+            got[r] = (g, res)
+    finally:
+        for c in cpu.values():
+            c.close()
+        close_all(listeners.values())
+        for w in gpu:
+            for s in (w.prev, w.nxt):
+                if s is not None:
+                    s.close()
+    eg, er = oracle_rounds([x] * rounds, ratios, seeds)
+    for r in range(n):
+        assert_bitexact(got[r][0], eg[r], f"grad rank {r}")
+        assert_bitexact(got[r][1], er[r], f"residual rank {r}")
+
+
+def test_tcp_ring_sparse_wire_bytes_and_lift_of_peer_frame():
+    """The first frame of a SparseCapable MI355X worker is the reference's
+    SparseGrad of grad_drop(chunk, calculate_threshold(chunk, r)); a SparseGrad
+    the peer sends back is lifted and added (scatter) like the reference's."""
+    length, r = 20000, 0.4
+    x = O.synth(length, SEED + 3, 0)
+    links, pairs = socketpair_links(2)
+    w = GpuWorker(0, 2, length, [x], *links[0], sparse=(r, 0))
+    w.start()
+    from_gpu, to_gpu = links[1]
+    try:
+        frame = recv_frame(from_gpu)
+        (a, b) = O.split_chunks(length, 2)[0]
+        t = O.sparse_threshold(x[a:b], r)
+        assert frame == frame_sparse(O.grad_drop(x[a:b], t))
+        # the peer (rank 1) answers with its own sparse chunk 1, then takes the gather frame
+        (c, d) = O.split_chunks(length, 2)[1]
+        y = O.synth(length, SEED + 3, 1)
+        ty = O.sparse_threshold(y[c:d], 0.6)
+        to_gpu.sendall(frame_sparse(O.grad_drop(y[c:d], ty)))
+        g_frame = recv_frame(from_gpu)  # rank 0's gather push of its owned chunk 1
+        assert g_frame[8:12] == (3).to_bytes(4, "big")
+        to_gpu.close()
+        w.join(60)
+    finally:
+        close_all(s for p in pairs for s in p)
+    # rank 0's chunk 1 = x + lift(peer); the gather push carries grad_drop of it
+    owned = x[c:d] + O.grad_lift(O.grad_drop(y[c:d], ty), d - c)
+    t1 = O.sparse_threshold(owned, r)
+    assert g_frame == frame_sparse(O.grad_drop(owned, t1))
+
+
+@pytest.mark.parametrize("payload,err", [("total", "proto"), ("short", "io"), ("overrun", "io"), ("huge", "proto")])
+def test_tcp_ring_sparse_bad_frames(payload, err):
+    """A SparseGrad whose total is not the hop's chunk, or whose stream is
+    malformed (the lift's errors, protocol.rs:96-144) or longer than any
+    encoding of the chunk."""
+    length = 10001
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
+    (a, b) = O.split_chunks(length, 2)[1]
+    m = b - a
+    body = {"total": (m + 1).to_bytes(8, "little"),
+            "short": m.to_bytes(8, "little") + b"\x00\x00\x00",
+            "overrun": m.to_bytes(8, "little") + (m - 1).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"\0" * 10,
+            "huge": m.to_bytes(8, "little") + b"\0" * (8 * m)}[payload]  # > any grad_drop of m values
+    try:
+        recv_frame(from_gpu)
+        to_gpu.sendall(frame_sparse(body))
+        w.join(60)
+        want = ono_amd.InvalidWorkerEvent if err == "proto" else ono_amd.IoError
+        assert isinstance(w.err, want), w.err
     finally:
         close_all(s for p in pairs for s in p)
