@@ -231,8 +231,8 @@ typedef enum {
  *              the data path: each rank maps its peers' exchange regions (IPC,
  *              uncached HBM) and the kernels push slices into the owners'
  *              receive slots and pull the owners' results over xGMI, with
- *              device-side flag barriers (timeout: env ONO_XGMI_TIMEOUT_S,
- *              default 30 s -> ONO_E_IO).  Bit-exact for both wires; ranks of
+ *              device-side flag barriers (timeout: ono_ring_set_xgmi_timeout,
+ *              default 600 s -> ONO_E_IO).  Bit-exact for both wires; ranks of
  *              one node; n <= ONO_MAX_INPUTS.  On an RCCL ring the exchange
  *              regions are connected over the communicator on first use.    */
 int ono_ring_set_algo(ono_ring *ring, int algo);
@@ -245,6 +245,12 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
 int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
+/* How long an xGMI barrier waits for a peer (seconds, > 0) before the round
+ * fails with ONO_E_IO; 0 = env ONO_XGMI_TIMEOUT_S, else 600 s.  The reference
+ * ring blocks while a peer is slow: set this above the longest time ranks may
+ * drift apart between rounds (evaluation, checkpointing on one rank).
+ * ono_ring_abort ends a waiting barrier at once.                            */
+int ono_ring_set_xgmi_timeout(ono_ring *ring, double seconds);
 /* Health of the rounds already enqueued: call after synchronizing the stream.
  * ONO_E_IO when an xGMI barrier timed out (that round's results are invalid,
  * and every later call fails the same way), ONO_E_ABORTED after

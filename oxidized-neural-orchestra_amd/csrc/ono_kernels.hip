@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "ono_device.h"
 #include "ono_internal.h"
 
 namespace ono {
@@ -122,15 +123,6 @@ __device__ __forceinline__ void st_sc1(f4 *p, f4 v) {
 __device__ __forceinline__ void st_sc1(h4 *p, h4 v) {
     asm volatile("global_store_dwordx2 %0, %1, off nt sc1" : : "v"(p), "v"(__builtin_bit_cast(uint64_t, v))
                  : "memory");
-}
-
-// A later launch's flag store (the xGMI barrier) publishes what this launch
-// wrote for other ranks.  A wave may retire with stores still in flight and
-// nothing at the kernel boundary waits for stores bound to memory another
-// process or device reads: the wave itself waits until its stores are
-// acknowledged (see ono_xgmi.hip, peer_stores_done).
-__device__ __forceinline__ void peer_stores_done() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
 }
 
 // --------------------------------------------------------- stream skeleton
@@ -286,7 +278,7 @@ template <int K, class W> struct DirectOp {
     float *grad;
     Outs out;  // nout copies of the result (f16 message / f32 grad value): local and/or peer HBM
     int nout;
-    int sys_out;  // outs are peer HBM: system-coherent (sc0 sc1) stores, see ono_xgmi.hip
+    int sys_out;  // outs are peer HBM: system-coherent (sc0 sc1) stores, see ono_device.h
     float v;
     int mode;  // SCALE_RECIP or SCALE_DIV
     int zall;
@@ -301,7 +293,7 @@ template <int K, class W> struct DirectOp {
         grad[i] = gv;
         const W m = sizeof(W) == 2 ? Wire<W>::enc(p) : Wire<W>::enc(gv);
         for (int j = 0; j < nout; j++) {
-            if (sys_out) *(volatile __attribute__((address_space(1))) W *)(static_cast<W *>(out.p[j]) + i) = m;
+            if (sys_out) st_sys(static_cast<W *>(out.p[j]) + i, m);
             else static_cast<W *>(out.p[j])[i] = m;
         }
         if (zall) {
@@ -326,7 +318,7 @@ template <int K, class W> struct DirectOp {
         st_nt((f4 *)(grad + i), gv);
         const WV m = sizeof(W) == 2 ? Wire<W>::enc4(p) : Wire<W>::enc4(gv);
         for (int j = 0; j < nout; j++) {
-            if (sys_out) *(volatile __attribute__((address_space(1))) WV *)(static_cast<W *>(out.p[j]) + i) = m;
+            if (sys_out) st_sys((WV *)(static_cast<W *>(out.p[j]) + i), m);
             else st_nt((WV *)(static_cast<W *>(out.p[j]) + i), m);
         }
         const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -546,7 +538,10 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         one(gi, wi, vi, si);
         g[i] = gi;
         w[i] = wi;
-        if (w2) w2[i] = wi;
+        if (w2) {
+            if (fence) st_sys(w2 + i, wi);
+            else w2[i] = wi;
+        }
         if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) v[i] = vi;
         if constexpr (KIND == ONO_OPT_ADAM) s[i] = si;
     }
@@ -565,7 +560,10 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         for (int j = 0; j < 4; j++) one(gg[j], ww[j], vv[j], ss[j]);
         st_nt((f4 *)(g + i), f4{gg[0], gg[1], gg[2], gg[3]});
         st_nt((f4 *)(w + i), f4{ww[0], ww[1], ww[2], ww[3]});
-        if (w2) st_nt((f4 *)(w2 + i), f4{ww[0], ww[1], ww[2], ww[3]});
+        if (w2) {  // fence: peers read the copy after the next flag barrier (system-coherent stores)
+            if (fence) st_sys((f4 *)(w2 + i), f4{ww[0], ww[1], ww[2], ww[3]});
+            else st_nt((f4 *)(w2 + i), f4{ww[0], ww[1], ww[2], ww[3]});
+        }
         if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) st_nt((f4 *)(v + i), f4{vv[0], vv[1], vv[2], vv[3]});
         if constexpr (KIND == ONO_OPT_ADAM) st_nt((f4 *)(s + i), f4{ss[0], ss[1], ss[2], ss[3]});
     }

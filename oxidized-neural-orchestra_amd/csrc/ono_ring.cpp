@@ -953,14 +953,26 @@ int ono_ps_step(ono_ps *p, const float *grad, float *params, void *stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t N = p->nparams, C = p->shard;
     const size_t lo = std::min(N, (size_t)r->pos * C), hi = std::min(N, lo + C);
-    if (p->opt.kind == ONO_OPT_ADAM) {  // adam.rs:76-80 in f32 on the host
-        p->beta1_t *= p->opt.beta1;
-        p->beta2_t *= p->opt.beta2;
-        float bc1 = 1.0f - p->beta1_t, bc2 = 1.0f - p->beta2_t;
-        p->opt.step_size = p->opt.lr * (std::sqrt(bc2) / bc1);
+    // adam.rs:76-80 in f32 on the host.  The powers advance only when an update
+    // is actually enqueued (a step refused before launching anything leaves
+    // the bias correction where it was, as a reference update that never ran).
+    OptLaunch o = p->opt;
+    float b1t = p->beta1_t, b2t = p->beta2_t;
+    if (o.kind == ONO_OPT_ADAM) {
+        b1t *= o.beta1;
+        b2t *= o.beta2;
+        float bc1 = 1.0f - b1t, bc2 = 1.0f - b2t;
+        o.step_size = o.lr * (std::sqrt(bc2) / bc1);
     }
+    auto commit = [&](int rc) {
+        if (rc == ONO_OK) {
+            p->beta1_t = b1t;
+            p->beta2_t = b2t;
+        }
+        return rc;
+    };
     if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // peer-access form, no padding needed
-        return xgmi_ps_step(r, grad, params, N, C, p->gshard, p->ppad + (size_t)r->pos * C, p->opt, p->v, p->s, s);
+        return commit(xgmi_ps_step(r, grad, params, N, C, p->gshard, p->ppad + (size_t)r->pos * C, o, p->v, p->s, s));
     if (r->n > 1) {  // reduce-scatter -> fused update -> all-gather, as a plan (ono_plan.cpp)
         if (p->plan.empty()) {
             int rc = plan_ps_step(p->plan, r->pos, r->n, N);
@@ -972,16 +984,16 @@ int ono_ps_step(ono_ps *p, const float *grad, float *params, void *stream) {
         c.base[ONO_PB_GSHARD] = p->gshard;
         c.base[ONO_PB_PPAD] = p->ppad;
         c.base[ONO_PB_PARAMS] = params;
-        c.opt = &p->opt;
+        c.opt = &o;
         c.v = p->v;
         c.s = p->s;
-        return run_plan(r, p->plan, c, s);
+        return commit(run_plan(r, p->plan, c, s));
     }
     // one worker: the store's update on the whole vector
     ONO_HIP(hipMemcpyAsync(p->gshard, grad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-    if (hi > lo) ONO_K(r, s, launch_opt_update(p->opt, p->gshard, p->ppad, p->v, p->s, hi - lo, true, s));
+    if (hi > lo) ONO_K(r, s, launch_opt_update(o, p->gshard, p->ppad, p->v, p->s, hi - lo, true, s));
     ONO_HIP(hipMemcpyAsync(params, p->ppad, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-    return ONO_OK;
+    return commit(ONO_OK);
 }
 
 }  // extern "C"

@@ -165,6 +165,7 @@ struct ono_ring {
     ono::Timer timer;
     // xGMI peer-access schedule (ONO_ALGO_XGMI, ono_xgmi.cpp); owned, freed by ono_xgmi_free
     ono::XgmiState *xgmi = nullptr;
+    double xgmi_timeout_s = 0;  // ono_ring_set_xgmi_timeout (0 = env ONO_XGMI_TIMEOUT_S, else the default)
 };
 
 namespace ono {
@@ -191,6 +192,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
 int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t C, float *gshard, float *wshard,
                  const OptLaunch &opt, float *v, float *s_, hipStream_t s);
 void xgmi_abort(ono_ring *r);
+void xgmi_set_timeout(ono_ring *r);  // re-reads r->xgmi_timeout_s into an allocated region
 void xgmi_free(ono_ring *r);  // collective: a final barrier before unmapping
 
 }  // namespace ono

@@ -92,14 +92,36 @@ int xgmi_alloc(ono_ring *r) {
     ONO_HIP(hipHostMalloc((void **)&x->err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
     *x->err = 0;
     ONO_HIP(hipHostGetDevicePointer((void **)&x->err_dev, x->err, 0));
+    xgmi_set_timeout(r);
+    return ONO_OK;
+}
+
+}  // namespace
+
+namespace ono {
+
+// How long a device barrier waits for a peer before it gives up (ONO_E_IO).
+// The reference's TCP ring blocks for as long as a peer is merely slow, so the
+// default is long (kDefaultTimeoutS): ranks may drift apart by up to that much
+// between rounds (rank-0 evaluation, checkpointing).  The bound exists so that
+// a peer that died cannot pin a spinning workgroup forever; ono_ring_abort
+// ends a waiting barrier at once.  Per ring: ono_ring_set_xgmi_timeout; else
+// env ONO_XGMI_TIMEOUT_S.
+constexpr double kDefaultTimeoutS = 600.0;
+void xgmi_set_timeout(ono_ring *r) {
+    XgmiState *x = r->xgmi;
+    if (!x) return;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, r->device) != hipSuccess || khz <= 0)
         khz = 100000;  // MI300-class constant 100 MHz wall clock
     const char *e = getenv("ONO_XGMI_TIMEOUT_S");
-    const double secs = e && atof(e) > 0 ? atof(e) : 30.0;
+    const double secs = r->xgmi_timeout_s > 0 ? r->xgmi_timeout_s : e && atof(e) > 0 ? atof(e) : kDefaultTimeoutS;
     x->timeout_ticks = (uint64_t)(secs * khz * 1000.0);
-    return ONO_OK;
 }
+
+}  // namespace ono
+
+namespace {
 
 uint64_t *flags_of(uint8_t *region) { return reinterpret_cast<uint64_t *>(region); }
 float *rbuf_of(const XgmiState *x, uint8_t *region, int k) {
@@ -367,28 +389,43 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
             if (ln[q]) memset(res_host + st[q], 0, ln[q] * sizeof(float));
         return ONO_OK;
     };
-    for (size_t j = 0; j < S; j++) {
-        piece(j);
-        for (int q = 0; q < n; q++)
-            if (ln[q])
-                ONO_HIP(hipMemcpyAsync(r->residual + st[q], res_host + st[q], ln[q] * sizeof(float),
-                                       hipMemcpyHostToDevice, r->hstream));
-        ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
-        ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
-        rc = r->wire == ONO_WIRE_F16 ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
-                                     : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
-        if (rc) return rc;
-        ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
-        ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
-        for (int q = 0; q < n; q++)
-            if (ln[q])
-                ONO_HIP(hipMemcpyAsync(grad_host + st[q], r->grad + st[q], ln[q] * sizeof(float),
-                                       hipMemcpyDeviceToHost, r->dstream));
-        ONO_HIP(hipEventRecord(x->ev[3 * j + 2], r->dstream));
-        if (j > 0 && (rc = zero_host(j - 1))) return rc;
-    }
-    if ((rc = zero_host(S - 1))) return rc;
-    ONO_HIP(hipStreamSynchronize(r->dstream));
+    auto rounds = [&]() -> int {
+        for (size_t j = 0; j < S; j++) {
+            piece(j);
+            for (int q = 0; q < n; q++)
+                if (ln[q])
+                    ONO_HIP(hipMemcpyAsync(r->residual + st[q], res_host + st[q], ln[q] * sizeof(float),
+                                           hipMemcpyHostToDevice, r->hstream));
+            ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
+            ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
+            int rc2 = r->wire == ONO_WIRE_F16
+                          ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
+                          : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
+            if (rc2) return rc2;
+            ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
+            ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
+            for (int q = 0; q < n; q++)
+                if (ln[q])
+                    ONO_HIP(hipMemcpyAsync(grad_host + st[q], r->grad + st[q], ln[q] * sizeof(float),
+                                           hipMemcpyDeviceToHost, r->dstream));
+            ONO_HIP(hipEventRecord(x->ev[3 * j + 2], r->dstream));
+            if (j > 0 && (rc2 = zero_host(j - 1))) return rc2;
+        }
+        return zero_host(S - 1);
+    };
+    rc = rounds();
+    // Every copy into or out of the caller's buffers is done before we return,
+    // whether or not the round failed (the buffers are the caller's again).
+    const hipError_t e1 = hipStreamSynchronize(r->hstream), e2 = hipStreamSynchronize(r->cstream),
+                     e3 = hipStreamSynchronize(r->dstream);
+    if (rc) return rc;
+    for (hipError_t e : {e1, e2, e3})
+        if (e != hipSuccess) return hip_error(e, "host-fed xGMI round", __FILE__, __LINE__);
+    // A barrier that gave up let the later kernels run on partly landed slots:
+    // the round's output is invalid and the host residual has already been
+    // zeroed, so it must not report success (ono_ring_check's condition).
+    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
+        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
     return ONO_OK;
 }
 
@@ -465,6 +502,14 @@ int ono_ring_check(const ono_ring *r) {
     if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
     if (r->xgmi && r->xgmi->err && __atomic_load_n(r->xgmi->err, __ATOMIC_ACQUIRE) == 1u)
         return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    return ONO_OK;
+}
+
+int ono_ring_set_xgmi_timeout(ono_ring *r, double seconds) {
+    if (!r) return set_error(ONO_E_ARG, "ring is NULL");
+    if (!(seconds >= 0) || seconds > 1e7) return set_error(ONO_E_ARG, "timeout %g s", seconds);
+    r->xgmi_timeout_s = seconds;
+    xgmi_set_timeout(r);  // later barriers use it (an allocated region keeps its flags)
     return ONO_OK;
 }
 

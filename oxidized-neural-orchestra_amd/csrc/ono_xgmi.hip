@@ -19,6 +19,7 @@
 // reference arithmetic; these kernels only move bytes, HBM- and link-bound.
 #include <hip/hip_runtime.h>
 
+#include "ono_device.h"
 #include "ono_internal.h"
 
 namespace ono {
@@ -51,31 +52,6 @@ __device__ __forceinline__ void seg_geometry(const XSeg &s, uint32_t t, int lane
     nvec = (s.n - s.head) / 4;
     v = (size_t)t * kXBlock + lane;
     vec_ok = v < nvec;
-}
-
-// Peer HBM (and the exchange slots peers write) is accessed system-coherent:
-// volatile accesses compile to sc0 sc1 loads/stores on gfx950, which no cache
-// on either GPU keeps, whatever cache policy the IPC import maps the peer's
-// region with.  Streaming data gains nothing from caching anyway.
-template <class T> __device__ __forceinline__ T ld_sys(const T *p) {
-    return *(const volatile __attribute__((address_space(1))) T *)p;  // global_load ... sc0 sc1
-}
-template <class T> __device__ __forceinline__ void st_sys(T *p, T v) {
-    *(volatile __attribute__((address_space(1))) T *)p = v;  // global_store ... sc0 sc1
-}
-
-// A later launch's flag store (the barrier) publishes what a push wrote into
-// peer memory.  A wave may retire with stores still in flight, and nothing at
-// the kernel boundary waits for stores bound to another process's / device's
-// memory: each pushing wave waits until its own stores are acknowledged
-// (`s_waitcnt vmcnt(0)`; they are sc0 sc1 stores, so acknowledged at system
-// scope) before it ends.  Without it the owner's chain could read a receive
-// slot before the pushed slice landed — seen as a wrong sum in about one run
-// in two of the pipelined host-fed test (tests/test_gpu_xgmi.py), none in 32
-// runs since.  A full system-scope release fence per wave (L2 writeback) was
-// tried first: correct, but 25x slower rounds.
-__device__ __forceinline__ void peer_stores_done() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
 }
 
 // f32 slice -> peer receive slot; ZERO: then zero the slice (the ring's

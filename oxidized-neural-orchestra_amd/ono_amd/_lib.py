@@ -120,6 +120,7 @@ _SIGS = {
     "ono_ring_create_xgmi": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, _i]),
     "ono_ring_xgmi_handle": (_i, [_vp, C.c_char_p]),
     "ono_ring_xgmi_connect": (_i, [_vp, C.c_char_p]),
+    "ono_ring_set_xgmi_timeout": (_i, [_vp, C.c_double]),
     "ono_ring_check": (_i, [_vp]),
     "ono_ring_destroy": (_i, [_vp]),
     "ono_ring_set_pipeline": (_i, [_vp, _i]),

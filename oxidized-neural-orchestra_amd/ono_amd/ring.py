@@ -232,6 +232,11 @@ class WorkerRingManager:
         overlaps the all-reduce of segment j+1); 1 = unsegmented, 0 = default."""
         call("ono_ring_set_pipeline", self._h, segments)
 
+    def set_xgmi_timeout(self, seconds: float) -> None:
+        """How long an xGMI barrier waits for a slow peer before the round
+        fails with IoError (0 = env ONO_XGMI_TIMEOUT_S, else 600 s)."""
+        call("ono_ring_set_xgmi_timeout", self._h, float(seconds))
+
     def check(self) -> None:
         """Raise if the rounds enqueued so far are invalid (synchronize first):
         IoError after an xGMI barrier timeout, Aborted after abort()."""

@@ -1,0 +1,123 @@
+"""Code-object checks of the memory ordering the xGMI schedule relies on
+(csrc/ono_device.h): a deterministic test, no GPU needed.
+
+Stores that another rank reads after a flag barrier — the push into a peer's
+receive slot, the owner chain's result slot / peer gather slots, the PS shard
+copy — must be system-coherent (`global_store… sc0 sc1`) and must be
+acknowledged before the wave that issued them ends: nothing at a kernel
+boundary waits for stores bound to another device's memory, and the barrier's
+release fence runs in a later launch.  The race this prevents (an owner chain
+reading a receive slot before the pushed slice landed) showed up about one run
+in two before the waits existed, and can only be provoked by timing, so the
+property is checked where it is decided: in the gfx950 code object shipped in
+libono_reduce.so.  The check fails if the stores lose their system scope, or
+if a wave can reach `s_endpgm` (or leave its block) with such a store not yet
+waited for by `s_waitcnt vmcnt(0)`.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oxidized-neural-orchestra_amd", "ono_amd", "libono_reduce.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+pytestmark = pytest.mark.skipif(not (os.path.exists(LIB) and os.access(OBJDUMP, os.X_OK)),
+                                reason="library or llvm-objdump missing")
+
+_FUNC = re.compile(r"^[0-9a-f]+ <([^>]+)>:")
+
+
+def _kernels(tmp_path) -> dict:
+    """kernel symbol -> list of instruction strings (layout order), every
+    gfx950 bundle of the library."""
+    lib = tmp_path / "lib.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, cwd=tmp_path, capture_output=True)
+    out: dict = {}
+    for f in sorted(os.listdir(tmp_path)):
+        if "amdgcn" not in f or "gfx950" not in f:
+            continue
+        asm = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", str(tmp_path / f)], check=True,
+                             capture_output=True, text=True).stdout
+        cur = None
+        for line in asm.splitlines():
+            m = _FUNC.match(line)
+            if m:
+                cur = out.setdefault(m.group(1), [])
+                continue
+            ins = line.split("//")[0].strip()
+            if cur is not None and ins:
+                cur.append(ins)
+    assert out, "no gfx950 code object found in libono_reduce.so"
+    return out
+
+
+def _is_sys_store(ins: str) -> bool:
+    return ins.startswith(("global_store", "buffer_store", "flat_store")) and " sc0" in ins and " sc1" in ins
+
+
+def _waits_vm0(ins: str) -> bool:
+    return ins.startswith("s_waitcnt") and "vmcnt(0)" in ins
+
+
+def _unwaited(instrs: list) -> list:
+    """sys stores not followed by vmcnt(0) before the next s_endpgm / branch in layout order"""
+    bad = []
+    for i, ins in enumerate(instrs):
+        if not _is_sys_store(ins):
+            continue
+        for nxt in instrs[i + 1:]:
+            if _waits_vm0(nxt):
+                break
+            if nxt.startswith(("s_endpgm", "s_branch", "s_cbranch", "s_setpc")):
+                bad.append(f"{ins!r} reaches {nxt!r} without s_waitcnt vmcnt(0)")
+                break
+        else:
+            bad.append(f"{ins!r} is never waited for")
+    return bad
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    return _kernels(tmp_path_factory.mktemp("isa"))
+
+
+@pytest.mark.parametrize("op", ["PushOp", "DirectOp", "OptOp"])
+def test_peer_visible_stores_are_system_scope(kernels, op):
+    """every kernel that writes memory peers read has sc0 sc1 stores (push
+    always; DirectOp with sys_out and OptOp with the PS fence, run-time flags
+    compiled into the same kernel)"""
+    ks = {k: v for k, v in kernels.items() if op in k}
+    assert ks, f"no {op} kernel in the code object"
+    missing = [k for k, v in ks.items() if not any(_is_sys_store(i) for i in v)]
+    assert not missing, f"{op} kernels without system-scope stores: {missing[:3]}"
+
+
+def test_system_scope_stores_are_waited_for_before_the_wave_ends(kernels):
+    """data stores only: the barrier's own flag store is a release atomic that
+    peers poll for (its wave then spins, and ends behind a seq_cst fence)"""
+    bad = {k: b for k, v in kernels.items() if "xbarrier" not in k and (b := _unwaited(v))}
+    assert not bad, "\n".join(f"{k}: {b[0]}" for k, b in list(bad.items())[:5])
+
+
+def test_barrier_uses_system_scope_flags(kernels):
+    """the flag barrier: system-scope release before the flag store (a
+    write-back of this GPU's L2, `buffer_wbl2 sc0 sc1`) and acquire loads
+    that bypass every cache level (sc0 sc1)"""
+    ks = [v for k, v in kernels.items() if "xbarrier" in k]
+    assert len(ks) == 1
+    code = ks[0]
+    assert any(i.startswith("buffer_wbl2") and "sc1" in i for i in code), "no system-scope release"
+    assert any(i.startswith("global_load_dwordx2") and " sc0" in i and " sc1" in i for i in code), \
+        "flag loads are not system coherent"
+
+
+def test_checker_sees_a_missing_wait():
+    """the checker itself: a sys store followed by s_endpgm with no wait fails"""
+    assert _unwaited(["global_store_dwordx4 v[0:1], v[2:5], off sc0 sc1", "s_endpgm"])
+    assert not _unwaited(["global_store_dwordx4 v[0:1], v[2:5], off sc0 sc1", "s_waitcnt vmcnt(0)", "s_endpgm"])
+    assert _unwaited(["global_store_dword v0, v1, s[0:1] sc0 sc1", "s_cbranch_execz 3", "s_waitcnt vmcnt(0)"])
