@@ -338,7 +338,7 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
     u16 = lambda: torch.empty(n, dtype=torch.int16, device="cuda")  # noqa: E731
     out = {}
 
-    def timed(name, kernel, per_elem, make_set, launch, nsets):
+    def timed(name, kernel, per_elem, make_set, launch, nsets, elems=n, note=None):
         sets = [make_set(i) for i in range(nsets)]
         torch.cuda.synchronize()
         for i in range(warmup):
@@ -351,19 +351,29 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
         b.record(stream)
         torch.cuda.synchronize()
         us = a.elapsed_time(b) / steps * 1e3
-        gbs = per_elem * n / (us * 1e-6) / 1e9
-        pmc = pmc_traffic(kernel, n)
-        out[name] = {"bytes_per_launch": per_elem * n, "us_per_launch": round(us, 2), "achieved_gbs": round(gbs, 1),
-                     "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
-                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
+        gbs = per_elem * elems / (us * 1e-6) / 1e9
+        pmc = pmc_traffic(kernel, elems)
+        out[name] = {"bytes_per_launch": per_elem * elems, "us_per_launch": round(us, 2),
+                     "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                     "rotating_sets": nsets, "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
+        if elems != n:
+            out[name]["elems"] = elems
+        if note:
+            out[name]["note"] = note
+        for st in sets:  # optimizer sets own device state
+            for o in st:
+                if hasattr(o, "close"):
+                    o.close()
         del sets
         torch.cuda.empty_cache()
 
-    def filled(i, r):
-        return ono_amd.kernels.synth(f32(), SEED + i, r)
+    def filled(i, r, m=n):
+        return ono_amd.kernels.synth(torch.empty(m, dtype=torch.float32, device="cuda"), SEED + i, r)
 
     timed("acc_residual", "AccOp", 12, lambda i: (filled(i, 0), filled(i, 1)),
-          lambda st: ono_amd.kernels.acc(st[0], st[1]), 6)
+          lambda st: ono_amd.kernels.acc(st[0], st[1]), 6,
+          note="ono_acc_f32 over fresh buffers (nt loads); the ring's acc_residual keeps its residual cacheable for "
+               "the pull that follows (DESIGN §3)")
 
     def hop_set(i):
         h = u16()
@@ -379,13 +389,31 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
     timed("f16_decode_scale", "DecodeScaleOp<unsigned short", 6, dec_set,
           lambda st: ono_amd.kernels.f16_decode_scale(st[0], st[1], 8.0), 12)
 
+    # The owner kernel of the DIRECT / XGMI schedules at the 8-GPU shape of the
+    # headline bucket: 256 MiB / 8 ranks = 8 M-element chunks; 7 received
+    # slices + the owner's own slice in, grad + the result message out, the
+    # own slice zeroed (worker_ring.rs:122-143, :166, :133; zero_all = 0 as on
+    # the xGMI ring).  f32: 8*4 + 4 + 4 + 4 = 44 B/elem; f16 message: 42.
+    c8 = 8 << 20
+    for wire, per in (("f32", 44), ("f16", 42)):
+        def chain_set(i, wire=wire):
+            ins = [filled(i, r, c8) for r in range(8)]
+            msg = torch.empty(c8, dtype=torch.int16 if wire == "f16" else torch.float32, device="cuda")
+            return (torch.empty(c8, dtype=torch.float32, device="cuda"), msg, ins)
+        timed(f"owner_chain_{wire}_n8", "DirectOp<8, float" if wire == "f32" else "DirectOp<8, unsigned short", per,
+              chain_set, lambda st, wire=wire: ono_amd.kernels.direct_chain(st[0], st[1], st[2], 8.0, wire), 5,
+              elems=c8)
+
+    # Consumer optimizers: every set has its own optimizer state, so the
+    # momentum / Adam moments rotate with the gradients and parameters and no
+    # launch can be served from the 256 MiB Infinity Cache (a training loop
+    # reuses one state set; that regime is cache-assisted and is not an HBM figure).
     for name, kind, opt, per in (("gd", 0, ono_amd.GradientDescent(0.1), 20),
                                  ("momentum", 1, ono_amd.GradientDescentWithMomentum(0.1, 0.9), 28),
                                  ("adam", 2, ono_amd.Adam(1e-3, 0.9, 0.999, 1e-8), 36)):
-        dev_opt = ono_amd.DeviceOptimizer(opt, n)
-        timed(f"consumer_{name}", f"OptOp<{kind},", per, lambda i: (filled(i, 4), filled(i, 5), f32()),
-              lambda st, o=dev_opt: o.step(st[0], st[1], st[2]), 4)
-        dev_opt.close()
+        timed(f"consumer_{name}", f"OptOp<{kind},", per,
+              lambda i, opt=opt: (filled(i, 4), filled(i, 5), f32(), ono_amd.DeviceOptimizer(opt, n)),
+              lambda st: st[3].step(st[0], st[1], st[2]), 4)
     return {"workload": "the path's other kernels on 64 MiB f32 buckets (16 M elements), device-resident",
             "hbm_peak_gbs": HBM_PEAK_GBS,
             "timing": "one HIP event pair around K back-to-back launches over rotating sets", **out}
@@ -810,6 +838,17 @@ def main(argv=None) -> int:
             if extra["roofline"]["achieved"] and link.get("gbs"):
                 extra["roofline"]["frac_of_measured_links"] = round(
                     extra["roofline"]["achieved"] / (link["gbs"] * (world - 1)), 4)
+        # The north_star's bar (>= 70 % of xGMI algorithmic bandwidth) is per GPU:
+        # `value` is N x algBW, so it grows with N even if every link slows
+        # down.  An all-reduce moves 2(N-1)/N x bucket per rank; over N-1 links
+        # of B GB/s per direction that takes >= 2 bucket / (N B), i.e. algBW <=
+        # N B / 2 (307 GB/s at N = 8).  Whole-step time, local kernels included.
+        algbw = bucket_bytes * args.steps / elapsed / 1e9
+        peak_alg = world * XGMI_LINK_GBS / 2
+        extra["roofline"].update({
+            "per_gpu_algbw_gbs": round(algbw, 2), "xgmi_algbw_peak_gbs": round(peak_alg, 1),
+            "frac_of_xgmi_algbw": round(algbw / peak_alg, 4), "north_star_target_frac_of_xgmi_algbw": 0.70,
+            "value_note": "value = N x per-GPU algBW (GiB/s, weak scaling); compare frac_of_xgmi_algbw across N"})
 
     def leg(name, fn):  # informational legs: a failure is recorded in the line, never fatal to it
         try:

@@ -98,6 +98,18 @@ int ono_f16_add_encode_zero(uint16_t *out, float *acc, const uint16_t *in, size_
 /* gather receive: out = f32(in) / divisor         (worker_ring.rs:200 + :101-105) */
 int ono_f16_decode_scale(float *out, const uint16_t *in, size_t n, float divisor, void *stream);
 
+/* The chunk owner's reduction of the DIRECT / XGMI schedules (one fused
+ * kernel per round): ins[j] = the slice of chunk c from rank c+j (HOST array
+ * of k device pointers, the owner's own residual slice last).
+ *   p = ins[0];  p = ins[j] + wire(p) for j = 1..k-1   (wire = f16 round trip
+ *   or identity) — the reference hop chain worker_ring.rs:122-143;
+ *   grad = p / divisor (:166 + param_manager.rs:183-188);
+ *   out = f16(p) (f16 wire: the message the gather forwards, :177-193) or
+ *   grad (f32 wire); out may be NULL;
+ *   ins[k-1] = 0, or every ins[j] = 0 when zero_all (:133, :191-193).        */
+int ono_direct_chain(float *grad, void *out, const float *const *ins, int k, size_t n, float divisor, int wire,
+                     int zero_all, void *stream);
+
 /* Sparse top-(1-r) gradient codec (comms/src/sparse/protocol.rs:33-144), the
  * SparseCapable serializer's wire format, byte-exact:
  *   [u64 LE total_len] { [u32 LE offset][u32 LE run_len][f16 LE x run_len] }*
@@ -129,7 +141,7 @@ int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *bu
                     void *stream);
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame
  * received into device memory); same results and errors as ono_sparse_lift.
- * Both parse on the device: speculative record starts per 256-B segment,
+ * Both parse on the device: speculative record starts per 128-B segment,
  * verified walks, scan, expand; the reference's sequential host parse runs
  * only when the speculation is refuted or the stream is malformed.          */
 int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,

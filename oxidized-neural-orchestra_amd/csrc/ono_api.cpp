@@ -101,6 +101,19 @@ int ono_f16_decode_scale(float *out, const uint16_t *in, size_t n, float divisor
     ONO_LAUNCH(launch_decode_scale<uint16_t>(out, in, n, divisor, S(stream)));
 }
 
+int ono_direct_chain(float *grad, void *out, const float *const *ins, int k, size_t n, float divisor, int wire,
+                     int zero_all, void *stream) {
+    if (k < 1 || k > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "k=%d outside [1, %d]", k, ONO_MAX_INPUTS);
+    if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
+    if (n && (!grad || !ins)) return set_error(ONO_E_ARG, "NULL pointer");
+    for (int j = 0; n && j < k; j++)
+        if (!ins[j]) return set_error(ONO_E_ARG, "ins[%d] is NULL", j);
+    if (wire == ONO_WIRE_F16)
+        ONO_LAUNCH(launch_direct<uint16_t>(grad, static_cast<uint16_t *>(out), ins, k, n, divisor, zero_all != 0,
+                                           S(stream)));
+    ONO_LAUNCH(launch_direct<float>(grad, static_cast<float *>(out), ins, k, n, divisor, zero_all != 0, S(stream)));
+}
+
 int ono_synth_f32(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset, void *stream) {
     if (n && !out) return set_error(ONO_E_ARG, "NULL pointer");
     ONO_LAUNCH(launch_synth(out, n, seed, rank, offset, S(stream)));

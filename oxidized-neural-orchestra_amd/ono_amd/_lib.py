@@ -104,6 +104,7 @@ _SIGS = {
     "ono_f16_add_encode_zero": (_i, [_vp, _fp, _vp, _sz, _vp]),
     "ono_f16_decode_scale": (_i, [_fp, _vp, _sz, C.c_float, _vp]),
     "ono_synth_f32": (_i, [_fp, _sz, _u64, _u64, _sz, _vp]),
+    "ono_direct_chain": (_i, [_fp, _vp, C.POINTER(C.c_void_p), _i, _sz, C.c_float, _i, _i, _vp]),
     "ono_sparse_max_bytes": (_sz, [_sz]),
     "ono_sparse_drop": (_i, [_vp, _sz, C.POINTER(C.c_size_t), _fp, _sz, C.c_float, _vp]),
     "ono_sparse_lift": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),

@@ -44,6 +44,27 @@ def sum_scale(out: torch.Tensor, ins: list[torch.Tensor], divisor: float = 1.0, 
     return out
 
 
+def direct_chain(grad: torch.Tensor, out, ins: list[torch.Tensor], divisor: float, wire: str = "f32",
+                 zero_all: bool = False, stream=None) -> torch.Tensor:
+    """The DIRECT / XGMI owner's fused chain (worker_ring.rs:122-143, :166,
+    :101-105): p = ins[0]; p = ins[j] + wire(p); grad = p / divisor; out =
+    f16(p) (f16 wire) or grad (f32 wire) when given; the last input (or all,
+    zero_all) zeroed."""
+    k = len(ins)
+    if not 1 <= k <= MAX_INPUTS:
+        raise ValueError(f"1 <= k <= {MAX_INPUTS}")
+    n = grad.numel()
+    if any(x.numel() != n for x in ins) or (out is not None and out.numel() != n):
+        raise ValueError("all operands must have the same length")
+    if out is not None and out.element_size() != (2 if wire == "f16" else 4):
+        raise ValueError("out element size does not match the wire")
+    arr = (C.c_void_p * k)(*[f32_ptr(x) for x in ins])
+    optr = None if out is None else (u16_ptr(out) if wire == "f16" else f32_ptr(out))
+    call("ono_direct_chain", f32_ptr(grad), optr, arr, k, n, float(divisor),
+         1 if wire == "f16" else 0, int(zero_all), stream_handle(stream))
+    return grad
+
+
 def acc(acc: torch.Tensor, x: torch.Tensor, stream=None) -> torch.Tensor:
     """acc += x — ParamManager::acc_residual (param_manager.rs:191-197)."""
     if acc.numel() != x.numel():

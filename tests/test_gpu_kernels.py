@@ -206,3 +206,48 @@ def test_full_size_sum_scale_property():
     assert_bitexact(got, O.sum_scale(hs, 4.0))
     full = [host(t) for t in ins]
     assert_bitexact(host(out), O.sum_scale(full, 4.0), "all 16M elements")
+
+
+@pytest.mark.parametrize("wire", ["f32", "f16"])
+@pytest.mark.parametrize("n,length", [(2, 4099), (3, 1000003), (8, (1 << 20) + 5), (16, 65541)])
+def test_direct_chain_is_the_owner_of_the_ring(wire, n, length):
+    """ono_direct_chain over the slices of chunk c (rank c, c+1, ..., owner
+    c-1 last) gives the owner's grad of the oracle ring, and its message is
+    what every replica ends up with (f16: decode / n) — the DIRECT / XGMI owner
+    kernel against worker_ring.rs:112-204 as restated by the oracle."""
+    res = [O.synth(length, SEED + 11, r) for r in range(n)]
+    grads, _ = O.ring_pull_grads(res, wire)
+    for ci, (lo, hi) in enumerate(O.split_chunks(length, n)):
+        if ci % max(1, n // 3):  # a few chunks per case
+            continue
+        owner = (ci - 1) % n
+        off = (lo + ci) % 4
+        ins = [dev(res[(ci + j) % n][lo:hi], off) for j in range(n)]
+        g = dev(np.zeros(hi - lo, np.float32), off)
+        out = (dev(np.zeros(hi - lo, np.uint16), off) if wire == "f16" else dev(np.zeros(hi - lo, np.float32), off))
+        K.direct_chain(g, out, ins, float(n), wire)
+        assert_bitexact(host(g), grads[owner][lo:hi], f"owner grad, chunk {ci}")
+        other = (owner + 1) % n
+        if wire == "f16":
+            dec = O.f16_decode(host(out))
+            assert_bitexact((dec / np.float32(n)).astype(np.float32), grads[other][lo:hi],
+                            f"replica from the message, chunk {ci}")
+        else:
+            assert_bitexact(host(out), grads[owner][lo:hi], f"f32 message, chunk {ci}")
+        assert not host(ins[-1]).any(), "own slice not zeroed"
+        for j in range(n - 1):
+            assert_bitexact(host(ins[j]), res[(ci + j) % n][lo:hi], "received slices must stay untouched")
+
+
+def test_direct_chain_zero_all_and_no_out():
+    n, length = 5, 4099
+    ins_h = [O.synth(length, SEED + 12, r) for r in range(n)]
+    ins = [dev(x) for x in ins_h]
+    g = dev(np.zeros(length, np.float32))
+    K.direct_chain(g, None, ins, 5.0, "f16", zero_all=True)
+    p = ins_h[0].copy()
+    for j in range(1, n):
+        p = (ins_h[j] + O.f16_decode(O.f16_encode(p))).astype(np.float32)
+    assert_bitexact(host(g), (p / np.float32(5.0)).astype(np.float32))
+    for t in ins:
+        assert not host(t).any()
