@@ -38,18 +38,9 @@ constexpr int kSB = 256;             // threads per block (4 waves)
 constexpr int kEPT = 8;              // elements per thread
 constexpr int kTile = kSB * kEPT;    // 2048 elements per tile
 
-__device__ __forceinline__ uint16_t to_f16_sp(float x) {  // half 2.7.1 f32 -> f16
-    uint16_t b = __builtin_bit_cast(uint16_t, (_Float16)x);
-    uint32_t u = __builtin_bit_cast(uint32_t, x);
-    uint16_t nb = (uint16_t)(((u >> 16) & 0x8000u) | 0x7E00u | ((u & 0x7FFFFFu) >> 13));
-    return __builtin_isnan(x) ? nb : b;
-}
-__device__ __forceinline__ float from_f16_sp(uint16_t b) {
-    float f = (float)__builtin_bit_cast(_Float16, b);
-    uint32_t nb = ((uint32_t)(b & 0x8000u) << 16) | 0x7FC00000u | ((uint32_t)(b & 0x3FFu) << 13);
-    bool nan = ((b & 0x7C00u) == 0x7C00u) && (b & 0x3FFu);
-    return nan ? __builtin_bit_cast(float, nb) : f;
-}
+// half 2.7.1 conversions = the gfx950 cvt instructions, NaN rules included (ono_kernels.hip to_f16)
+__device__ __forceinline__ uint16_t to_f16_sp(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
+__device__ __forceinline__ float from_f16_sp(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 
 // g.abs() >= threshold (NaN never kept, as in Rust)
 __device__ __forceinline__ bool kept(float x, float t) { return fabsf(x) >= t; }

@@ -30,13 +30,8 @@ typedef uint16_t h4 __attribute__((ext_vector_type(4)));
 
 constexpr int kXBlock = 64;  // one wave per workgroup, one 16-B vector per lane (as ew_kernel)
 
-// half 2.7.1 f16_to_f32 (same rule as ono_kernels.hip from_f16)
-__device__ __forceinline__ float x_from_f16(uint16_t b) {
-    float f = (float)__builtin_bit_cast(_Float16, b);
-    uint32_t nb = ((uint32_t)(b & 0x8000u) << 16) | 0x7FC00000u | ((uint32_t)(b & 0x3FFu) << 13);
-    bool nan = ((b & 0x7C00u) == 0x7C00u) && (b & 0x3FFu);
-    return nan ? __builtin_bit_cast(float, nb) : f;
-}
+// half 2.7.1 f16_to_f32 = v_cvt_f32_f16, NaN payloads included (ono_kernels.hip from_f16)
+__device__ __forceinline__ float x_from_f16(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 
 template <int M> __device__ __forceinline__ float xs(float x, float v) {
     if constexpr (M == SCALE_NONE) return x;

@@ -44,7 +44,7 @@ def main() -> int:
     ap.add_argument("--elems", type=int, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp", "AccOp", "AddEncodeZeroOp",
-                                                  "DecodeScaleOp", "OptOp"])
+                                                  "DecodeScaleOp", "OptOp", "DirectOp<8,"])
     ap.add_argument("--algo-bytes-per-elem", type=float, default=12.0)
     ap.add_argument("--local-elems", type=int, default=16 << 20,
                     help="bucket length of bench.py's local_reduce (SumScaleOp<k> kernels: (k+1) x 4 B/elem)")
@@ -66,6 +66,9 @@ def main() -> int:
             elems, algo = a.local_elems, 12.0 * a.local_elems
         elif "DecodeScaleOp" in name:  # path_kernels: f16 in, f32 out
             elems, algo = a.local_elems, 6.0 * a.local_elems
+        elif "DirectOp<8," in name:  # path_kernels owner chain, 8 M-element chunks: 44 B (f32) / 42 B (f16)
+            elems = 8 << 20
+            algo = (42.0 if "unsigned short" in name else 44.0) * elems
         else:
             elems, algo = a.elems, a.algo_bytes_per_elem * a.elems
         if not algo:

@@ -73,6 +73,21 @@ struct DecShape {
     }
     __device__ __forceinline__ static void store(const Args &a, size_t v, f4 r) { stn((f4 *)a.out + v, r * 0.125f); }
 };
+// the product's decode: half 2.7.1 f16_to_f32 with its NaN rule spelled out
+__device__ __forceinline__ float dec1_nan(uint16_t b) {
+    float f = (float)__builtin_bit_cast(_Float16, b);
+    uint32_t nb = ((uint32_t)(b & 0x8000u) << 16) | 0x7FC00000u | ((uint32_t)(b & 0x3FFu) << 13);
+    bool nan = ((b & 0x7C00u) == 0x7C00u) && (b & 0x3FFu);
+    return nan ? __builtin_bit_cast(float, nb) : f;
+}
+struct DecNanShape {
+    static constexpr double bytes_per_elem = 6.0;
+    __device__ __forceinline__ static void load(const Args &a, size_t v, f4 &r) {
+        h4 h = ldn((const h4 *)a.in[0] + v);
+        r = f4{dec1_nan(h.x), dec1_nan(h.y), dec1_nan(h.z), dec1_nan(h.w)};
+    }
+    __device__ __forceinline__ static void store(const Args &a, size_t v, f4 r) { stn((f4 *)a.out + v, r * 0.125f); }
+};
 struct AccShape {
     static constexpr double bytes_per_elem = 12.0;
     __device__ __forceinline__ static void load(const Args &a, size_t v, f4 &r) {
@@ -170,6 +185,28 @@ template <class Sh> void add_rows(std::vector<Row> &rows, const char *shape, int
     rows.push_back({std::string(shape) + " b256", b, per_set, L_b256<Sh>, {}});
 }
 
+// Does the hardware conversion already follow the half crate's NaN rules?
+//   f16 -> f32: sign | 0x7FC00000 | mant << 13     (every one of the 2^16 patterns)
+//   f32 -> f16: sign | 0x7E00 | mant >> 13 for NaN (every NaN f32 pattern, 2^24 of them x sign)
+__global__ void k_nan_check(unsigned long long *bad) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t < 65536u) {
+        const uint16_t b = (uint16_t)t;
+        const uint32_t hw = __builtin_bit_cast(uint32_t, (float)__builtin_bit_cast(_Float16, b));
+        const uint32_t sw = __builtin_bit_cast(uint32_t, dec1_nan(b));
+        if (hw != sw) atomicAdd(bad, 1ull);
+    }
+    // f32 NaNs: exponent all ones, mantissa != 0; t enumerates sign and mantissa
+    const uint32_t mant = t & 0x7FFFFFu, sign = (t >> 23) & 1u;
+    if (mant) {
+        const uint32_t u = (sign << 31) | 0x7F800000u | mant;
+        const float x = __builtin_bit_cast(float, u);
+        const uint16_t hw = __builtin_bit_cast(uint16_t, (_Float16)x);
+        const uint16_t sw = (uint16_t)(((u >> 16) & 0x8000u) | 0x7E00u | ((u & 0x7FFFFFu) >> 13));
+        if (hw != sw) atomicAdd(bad + 1, 1ull);
+    }
+}
+
 int main(int argc, char **argv) {
     if (argc > 1) N = (size_t)atol(argv[1]) << 18;
     const int passes = argc > 2 ? atoi(argv[2]) : 5;
@@ -179,7 +216,17 @@ int main(int argc, char **argv) {
     printf("# %s, %d CUs, %zu f32 elements per buffer (%zu MiB), %d passes, median of per-pass means\n",
            p.gcnArchName, p.multiProcessorCount, N, N >> 18, passes);
     std::vector<Row> rows;
-    if (argc > 3 && !strcmp(argv[3], "skew")) {
+    if (argc > 3 && !strcmp(argv[3], "nan")) {
+        unsigned long long *bad, hb[2];
+        CK(hipMalloc(&bad, 16));
+        CK(hipMemset(bad, 0, 16));
+        hipLaunchKernelGGL(k_nan_check, dim3((1u << 24) / 256), dim3(256), 0, g_s, bad);
+        CK(hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost));
+        printf("hardware vs half-crate NaN rule: f16->f32 mismatches %llu of 65536, f32->f16 NaN mismatches %llu of "
+               "%u\n", hb[0], hb[1], (1u << 24) - 2);
+        add_rows<DecShape>(rows, "dec", 2);
+        add_rows<DecNanShape>(rows, "decnan", 2);
+    } else if (argc > 3 && !strcmp(argv[3], "skew")) {
         for (size_t sk : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)8192, (size_t)65536 + 512}) {
             char nm[64];
             auto add = [&](const char *shape, double bpe, int per, void (*f)(const Args &, size_t)) {
