@@ -239,6 +239,199 @@ __global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint
     }
 }
 
+// ------------------------------------------------------- one-pass drop ----
+// The encoder as ONE launch with one read of g from HBM (the four-launch
+// pipeline above reads it twice and keeps a run table in global memory).
+// A grid of G co-resident workgroups (a cooperative launch: the runtime
+// guarantees every workgroup is resident, or refuses the launch), workgroup
+// w owning the tiles [w tpw, (w+1) tpw):
+//   1. count   per tile: flags, block scan -> kept / runs, the tile's first
+//              run start (kept values before it) in LDS; the workgroup's
+//              totals, first run start and last run start into its record
+//              (plain loads: the workgroup's slice of g stays in L2 / the
+//              Infinity Cache for step 3)
+//   2. barrier one grid-wide arrival counter; then every workgroup scans all
+//              G records (L2-resident, read through agent-scope loads): its
+//              own prefix (F0, S0), the nearest earlier workgroup with a run
+//              (U of its last run start: the first header's offset) and the
+//              nearest later one (F at its first run start: the last header's
+//              length), and the totals (wire length; the cap check)
+//   3. write   per tile again (nt loads, g's last use): values AND headers are
+//              placed in an LDS image of the tile's byte range, which goes
+//              out with coalesced 4-byte stores — no run table in HBM, no
+//              header pass.  The offsets / lengths that cross a tile come
+//              from the carry (previous run start) and the LDS tile records
+//              or the step-2 neighbour (next run start).
+// HBM traffic: 4N + wire.  A barrier that does not complete within the
+// timeout (a workgroup was not resident after all) raises the error word and
+// the host re-runs the four-launch encoder.
+constexpr int kMaxTPW = 32;  // tiles per workgroup (LDS tile records)
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+struct WgRec {
+    uint32_t F, S;       // kept values / runs started in the workgroup
+    uint32_t firstF;     // kept values in the workgroup before its first run start (kNone: no run)
+    uint32_t lastIdx;    // element index of its last run start
+    uint32_t lastF;      // kept values in the workgroup before that start
+};
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kSB) void sp_drop1(const float *g, size_t n, float t, uint32_t ntiles, uint32_t tpw,
+                                                WgRec *recs, unsigned long long *ctr, unsigned long long target,
+                                                uint8_t *buf, size_t cap, uint64_t *host_tot, uint32_t *err,
+                                                uint64_t timeout_ticks, bool vec) {
+    __shared__ uint16_t stage[kStageU16];
+    __shared__ uint32_t su[kTile / 2 + 1], sf[kTile / 2 + 1];
+    __shared__ uint32_t tF[kMaxTPW], tS[kMaxTPW], tFirst[kMaxTPW];
+    __shared__ uint32_t lastIdx, lastF;
+    __shared__ unsigned long long prevKey, nextKey;
+    __shared__ uint32_t base0[2];
+    const uint32_t w = blockIdx.x, G = gridDim.x;
+    const uint32_t t0 = w * tpw, t1 = min(ntiles, t0 + tpw);
+    const int tid = threadIdx.x;
+    if (tid == 0) { lastIdx = kNone; lastF = 0; prevKey = 0; nextKey = ~0ull; }
+
+    // 1. count
+    uint32_t Fw = 0, Sw = 0;  // running workgroup totals (every thread)
+    for (uint32_t tt = t0; tt < t1; tt++) {
+        const size_t base = (size_t)tt * kTile + (size_t)tid * kEPT;
+        float x[kEPT];
+        Bits b = thread_bits<false>(g, n, t, base, vec, x);
+        uint32_t ea, eb, ta, tb;
+        block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
+        const uint32_t i = tt - t0;
+        if (tid == 0) { tF[i] = ta; tS[i] = tb; if (!tb) tFirst[i] = kNone; }
+        if (b.start) {
+            if (eb == 0) {  // this thread holds the tile's first run start
+                const int e = __builtin_ctz(b.start);
+                tFirst[i] = ea + __popc(b.keep & ((1u << e) - 1u));
+            }
+            if (eb + __popc(b.start) == tb) {  // ... and / or its last one
+                const int e = 31 - __builtin_clz(b.start);
+                lastIdx = (uint32_t)(base + e);
+                lastF = Fw + ea + __popc(b.keep & ((1u << e) - 1u));
+            }
+        }
+        Fw += ta;
+        Sw += tb;
+        __syncthreads();  // block_scan2's LDS and the records are reused
+    }
+    if (tid == 0) {
+        uint32_t firstF = kNone, f = 0;
+        for (uint32_t i = 0; i < t1 - t0; i++) {
+            if (tS[i]) { firstF = f + tFirst[i]; break; }
+            f += tF[i];
+        }
+        WgRec r{Fw, Sw, firstF, lastIdx, lastF};
+        uint32_t *d = reinterpret_cast<uint32_t *>(recs + w);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(&r);
+        for (int q = 0; q < 5; q++) __hip_atomic_store(d + q, src[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // 2. grid barrier: release the record, arrive, wait for all G arrivals
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t c0 = wall_clock64();
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (wall_clock64() - c0 > timeout_ticks) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+
+    // 2b. every record: own prefix, neighbours with runs, totals
+    uint32_t cF = 0, cS = 0;  // carry over record chunks
+    for (uint32_t c = 0; c < G; c += kSB) {
+        const uint32_t r = c + tid;
+        uint32_t rf = 0, rs = 0, rfirst = kNone, rlidx = 0, rlf = 0;
+        if (r < G) {
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(recs + r);
+            rf = ld_agent(q); rs = ld_agent(q + 1); rfirst = ld_agent(q + 2); rlidx = ld_agent(q + 3); rlf = ld_agent(q + 4);
+        }
+        uint32_t ea, eb, ta, tb;
+        block_scan2(rf, rs, ea, eb, ta, tb);
+        const uint32_t pf = cF + ea, ps = cS + eb;  // record r's exclusive prefix
+        if (r == w) { base0[0] = pf; base0[1] = ps; }
+        if (r < G && rs) {
+            if (r < w)  // U = index - F at the start: the offset of the next header
+                atomicMax(&prevKey, ((unsigned long long)(r + 1) << 32) | (uint32_t)(rlidx - (pf + rlf)));
+            if (r > w) atomicMin(&nextKey, ((unsigned long long)r << 32) | (uint32_t)(pf + rfirst));
+        }
+        cF += ta;
+        cS += tb;
+        __syncthreads();
+    }
+    const uint32_t Ftot = cF, R = cS;
+    const size_t wire = 8 + 8 * (size_t)R + 2 * (size_t)Ftot;
+    if (w == 0 && tid == 0) {
+        host_tot[0] = Ftot;
+        host_tot[1] = R;
+        if (wire <= cap)
+            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
+    }
+    if (wire > cap) return;  // the host reports ONO_E_SIZE
+    uint32_t Fcur = base0[0], Scur = base0[1];
+    uint32_t carryU = prevKey ? (uint32_t)prevKey : 0u;  // U of the previous run start (0 before the first)
+    const uint32_t nextWgF = nextKey != ~0ull ? (uint32_t)nextKey : Ftot;
+
+    // 3. write
+    for (uint32_t tt = t0; tt < t1; tt++) {
+        const uint32_t i = tt - t0;
+        const size_t base = (size_t)tt * kTile + (size_t)tid * kEPT;
+        float x[kEPT];
+        Bits b = thread_bits<true>(g, n, t, base, vec, x);
+        uint32_t ea, eb, ta, tb;
+        block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
+        uint32_t f = ea, sl = eb;
+        if (b.keep) {
+#pragma unroll
+            for (int e = 0; e < kEPT; e++) {
+                if (!(b.keep >> e & 1u)) continue;
+                if (b.start >> e & 1u) {
+                    su[sl] = (uint32_t)(base + e) - (Fcur + f);  // U(s_j)
+                    sf[sl] = f;                                    // kept before s_j within the tile
+                    sl++;
+                }
+                stage[4 * sl + f] = to_f16_sp(x[e]);
+                f++;
+            }
+        }
+        // F (global) at the first run start after this tile
+        uint32_t nextF = nextWgF, fp = Fcur + ta;
+        for (uint32_t j = i + 1; j < t1 - t0; j++) {
+            if (tS[j]) { nextF = fp + tFirst[j]; break; }
+            fp += tF[j];
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < tb; k += kSB) {  // headers into the image
+            const uint32_t off = su[k] - (k ? su[k - 1] : carryU);
+            const uint32_t len = (k + 1 < tb ? Fcur + sf[k + 1] : nextF) - (Fcur + sf[k]);
+            uint16_t *h = stage + 4 * k + sf[k];
+            h[0] = (uint16_t)off;
+            h[1] = (uint16_t)(off >> 16);
+            h[2] = (uint16_t)len;
+            h[3] = (uint16_t)(len >> 16);
+        }
+        __syncthreads();
+        const uint32_t nu16 = 4 * tb + ta;
+        uint16_t *dst = (uint16_t *)(buf + 8 + 8 * (size_t)Scur + 2 * (size_t)Fcur);
+        const uint32_t h = (uint32_t)(((uintptr_t)dst >> 1) & 1u) < nu16 ? (uint32_t)(((uintptr_t)dst >> 1) & 1u) : nu16;
+        if (tid == 0 && h) dst[0] = stage[0];
+        const uint32_t npair = (nu16 - h) / 2;
+        uint32_t *d32 = (uint32_t *)(dst + h);
+        for (uint32_t k = tid; k < npair; k += kSB)
+            d32[k] = (uint32_t)stage[h + 2 * k] | (uint32_t)stage[h + 2 * k + 1] << 16;
+        if (tid == 0 && h + 2 * npair < nu16) dst[nu16 - 1] = stage[nu16 - 1];
+        if (tb) carryU = su[tb - 1];
+        Fcur += ta;
+        Scur += tb;
+        __syncthreads();  // stage / su / sf reused by the next tile
+    }
+}
+
 // Fallback lift (after a host parse): value v belongs to run j with
 // cumF[j] <= v < cumF[j+1] (binary search);
 // it sits at byte 16 + 8 j + 2 v and lands at start[j] + (v - cumF[j]).
@@ -287,7 +480,6 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 // itself, and queues runs longer than kShort for sl_long (one workgroup per
 // run).
 constexpr int kSeg = 128, kLook = 4, kShort = 16;
-constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *b, size_t p) {  // p even, b 2-B aligned
     const uint16_t *h = (const uint16_t *)(b + p);
@@ -465,6 +657,15 @@ struct Scratch {
     size_t tiles_cap = 0, runs_cap = 0;
     uint32_t *tiles = nullptr, *runs = nullptr;
     uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
+    // one-pass encoder (sp_drop1): workgroup records, the grid barrier's
+    // arrival counter (never reset: launch k waits for base + G arrivals),
+    // and a host-mapped error word for a barrier that timed out
+    size_t recs_cap = 0;
+    WgRec *recs = nullptr;
+    unsigned long long *ctr = nullptr;
+    unsigned long long ctr_base = 0;
+    uint32_t *err = nullptr, *err_dev = nullptr;
+    int max_grid = -1;  // co-resident workgroups of sp_drop1 (0: cooperative launch unavailable)
 };
 std::mutex g_scratch_mu;
 Scratch g_scratch[64];
@@ -701,7 +902,90 @@ ThrScratch g_thr[64];
 
 extern "C" {
 
+size_t ono_sparse_drop_fallbacks(void) { return g_drop_fallbacks.load(); }
+
 size_t ono_sparse_max_bytes(size_t n) { return 8 + 10 * ((n + 1) / 2) + 2 * n; }
+
+}  // extern "C"
+
+namespace {
+
+std::atomic<size_t> g_drop_fallbacks{0};
+
+bool onepass_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("ONO_SPARSE_ONEPASS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The one-pass encoder; *done = false when it does not apply (too many tiles
+// for one co-resident grid, cooperative launch unavailable, or its barrier
+// timed out), and the caller runs the four-launch encoder instead.
+int drop_onepass(Scratch *sc, uint8_t *buf, size_t cap, const float *g, size_t n, float threshold, bool vec,
+                 hipStream_t s, bool *done) {
+    *done = false;
+    const size_t ntiles = (n + kTile - 1) / kTile;
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (sc->max_grid < 0) {
+        int coop = 0, cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) coop = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sp_drop1, kSB, 0) != hipSuccess) per = 0;
+        sc->max_grid = coop ? cus * per : 0;
+        ONO_HIP(hipMalloc((void **)&sc->ctr, sizeof(unsigned long long)));
+        ONO_HIP(hipMemset(sc->ctr, 0, sizeof(unsigned long long)));
+        ONO_HIP(hipHostMalloc((void **)&sc->err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostGetDevicePointer((void **)&sc->err_dev, sc->err, 0));
+        *sc->err = 0;
+    }
+    if (sc->max_grid <= 0) return ONO_OK;
+    const size_t tpw = (ntiles + (size_t)sc->max_grid - 1) / (size_t)sc->max_grid;
+    if (tpw > (size_t)kMaxTPW) return ONO_OK;
+    const uint32_t G = (uint32_t)((ntiles + tpw - 1) / tpw);
+    if (G > sc->recs_cap) {
+        (void)hipFree(sc->recs);
+        sc->recs = nullptr;
+        sc->recs_cap = 0;
+        ONO_HIP(hipMalloc((void **)&sc->recs, (size_t)G * sizeof(WgRec)));
+        sc->recs_cap = G;
+    }
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    const uint64_t ticks = (uint64_t)khz * 2000;  // 2 s: co-resident workgroups arrive within microseconds
+    uint32_t nt = (uint32_t)ntiles, tp = (uint32_t)tpw;
+    unsigned long long target = sc->ctr_base + G;
+    WgRec *recs = sc->recs;
+    unsigned long long *ctr = sc->ctr;
+    uint64_t *ht = sc->host_tot_dev;
+    uint32_t *err = sc->err_dev;
+    uint64_t tk = ticks;
+    void *args[] = {(void *)&g, (void *)&n, (void *)&threshold, (void *)&nt, (void *)&tp, (void *)&recs, (void *)&ctr,
+                    (void *)&target, (void *)&buf, (void *)&cap, (void *)&ht, (void *)&err, (void *)&tk, (void *)&vec};
+    *sc->err = 0;
+    hipError_t e = hipLaunchCooperativeKernel((const void *)sp_drop1, dim3(G), dim3(kSB), args, 0, s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        sc->max_grid = 0;  // not available here: the four-launch encoder from now on
+        return ONO_OK;
+    }
+    ONO_HIP(hipStreamSynchronize(s));
+    if (__atomic_load_n(sc->err, __ATOMIC_ACQUIRE)) {  // some workgroup gave up waiting: start the counter afresh
+        ONO_HIP(hipMemset(sc->ctr, 0, sizeof(unsigned long long)));
+        sc->ctr_base = 0;
+        *sc->err = 0;
+        return ONO_OK;
+    }
+    sc->ctr_base = target;
+    *done = true;
+    return ONO_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, float threshold,
                     void *stream) {
@@ -723,6 +1007,20 @@ int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, si
     uint32_t *tileF = sc->tiles, *tileS = sc->tiles + ntiles + 1, *RU = sc->runs, *RF = sc->runs + maxruns;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     tot[0] = tot[1] = 0;
+    if (ntiles && onepass_enabled()) {
+        bool done = false;
+        rc = drop_onepass(sc, buf, cap, g, n, threshold, vec, s, &done);
+        if (rc) return rc;
+        if (done) {
+            const size_t need = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
+            if (need > cap)
+                return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu", need, cap);
+            *nbytes = need;
+            return ONO_OK;
+        }
+        g_drop_fallbacks++;
+        tot[0] = tot[1] = 0;
+    }
     uint64_t *totals = sc->totals_dev;
     hipError_t e = hipSuccess;
     if (ntiles) {
