@@ -902,8 +902,6 @@ ThrScratch g_thr[64];
 
 extern "C" {
 
-size_t ono_sparse_drop_fallbacks(void) { return g_drop_fallbacks.load(); }
-
 size_t ono_sparse_max_bytes(size_t n) { return 8 + 10 * ((n + 1) / 2) + 2 * n; }
 
 }  // extern "C"
@@ -986,6 +984,8 @@ int drop_onepass(Scratch *sc, uint8_t *buf, size_t cap, const float *g, size_t n
 }  // namespace
 
 extern "C" {
+
+size_t ono_sparse_drop_fallbacks(void) { return g_drop_fallbacks.load(); }
 
 int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, float threshold,
                     void *stream) {
