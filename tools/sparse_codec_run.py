@@ -1,4 +1,4 @@
-"""Drop + device lift of the bench's sparse workload (64 MiB gradient, 90th
+"""K drops + K device lifts of the bench's sparse workload (64 MiB gradient, 90th
 percentile threshold), K times — a short program for rocprofv3 kernel stats."""
 import ctypes as C
 import os
@@ -14,11 +14,27 @@ n = 16 << 20
 g = ono_amd.kernels.synth(torch.empty(n, dtype=torch.float32, device="cuda"), 1234, 7)
 t = float(torch.quantile(g[: 1 << 20].abs().float(), 0.9).item())
 L = ono_amd.lib()
+import time  # noqa: E402
 wire = ono_amd.sparse.grad_drop_dev(g, t)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(K):
+    wire = ono_amd.sparse.grad_drop_dev(g, t)
+print(f"drop {(time.perf_counter() - t0) / K * 1e6:.1f} us per blocking call (grid cap "
+      f"{os.environ.get('ONO_SPARSE_GRID', 'none')}, one-pass {os.environ.get('ONO_SPARSE_ONEPASS', '1')}, "
+      f"cooperative {os.environ.get('ONO_SPARSE_COOP', '1')})")
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+for _ in range(K):
+    wire = ono_amd.sparse.grad_drop_dev(g, t)
+ev1.record()
+torch.cuda.synchronize()
+print(f"drop {ev0.elapsed_time(ev1) / K * 1e3:.1f} us per call between events on the stream")
 out = torch.empty(n, dtype=torch.float32, device="cuda")
 ln = C.c_size_t(0)
 s = torch.cuda.current_stream().cuda_stream
 for _ in range(K):
     ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
 torch.cuda.synchronize()
-print("fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
+print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "drop fallbacks", L.ono_sparse_drop_fallbacks(),
+      "wire", wire.numel())
