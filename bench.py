@@ -487,10 +487,8 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
             "drop": {"ms": round(td * 1e3, 3), "device_ms": round(tdev * 1e3, 3), "algorithmic_bytes": drop_bytes,
                      "achieved_gbs": round(drop_bytes / tdev / 1e9, 1),
                      "frac_of_hbm_peak": round(drop_bytes / tdev / 1e9 / HBM_PEAK_GBS, 4),
-                     "encoder": "four-launch" if L.ono_sparse_drop_fallbacks() else "one-pass (cooperative launch)",
                      "note": "ms = wall time of the blocking C call; device_ms = HIP events around it on its "
-                             "stream (one cooperative launch: count, grid barrier, write of values + headers; "
-                             "then the host read of the totals)"},
+                             "stream (count + tile scan + write + headers, then the host read of the totals)"},
             "lift": {"ms": round(lt * 1e3, 3), "note": "host wire buffer in (Python bytes): H2D + device parse + "
                                                         "expand, wall time through the Python wrapper"},
             "lift_dev": {"ms": round(dlt * 1e3, 3), "device_ms": round(dlt_ev * 1e3, 3),

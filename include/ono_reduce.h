@@ -137,14 +137,6 @@ int ono_sparse_threshold(float *t_out, const float *g_dev, size_t n, const uint3
 int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t amount);
 int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
                     float threshold, void *stream);
-/* drop is ONE cooperative launch (one read of g: count, grid barrier, values
- * and headers written from an LDS image of each tile's byte range) while the
- * gradient fits one co-resident grid (<= 32 tiles of 2048 values per
- * workgroup); otherwise — or if the launch is refused — four launches (count,
- * tile scan, write, headers).  Drops so far (this process) that took the
- * four-launch encoder although the one-pass one was enabled
- * (env ONO_SPARSE_ONEPASS=0 disables it):                                    */
-size_t ono_sparse_drop_fallbacks(void);
 int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
                     void *stream);
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame

@@ -57,7 +57,9 @@ struct Bits {
 };
 typedef float f4s __attribute__((ext_vector_type(4)));
 template <bool NTL>
-__device__ __forceinline__ void load_thread(const float *g, size_t n, size_t base, bool vec, float (&x)[kEPT]) {
+__device__ __forceinline__ Bits thread_bits(const float *g, size_t n, float t, size_t base, bool vec,
+                                            float (&x)[kEPT]) {
+    Bits b;
     if (vec && base + kEPT <= n) {
         f4s a, c;
         if constexpr (NTL) {
@@ -72,9 +74,6 @@ __device__ __forceinline__ void load_thread(const float *g, size_t n, size_t bas
 #pragma unroll
         for (int e = 0; e < kEPT; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
     }
-}
-__device__ __forceinline__ Bits bits_of(const float *g, size_t n, float t, size_t base, const float (&x)[kEPT]) {
-    Bits b;
 #pragma unroll
     for (int e = 0; e < kEPT; e++)
         if (base + e < n && kept(x[e], t)) b.keep |= 1u << e;
@@ -85,12 +84,6 @@ __device__ __forceinline__ Bits bits_of(const float *g, size_t n, float t, size_
     if (lane == 0) prev = base > 0 && base - 1 < n ? (kept(g[base - 1], t) ? 1u : 0u) : 0u;
     b.start = b.keep & ~((b.keep << 1) | prev);
     return b;
-}
-template <bool NTL>
-__device__ __forceinline__ Bits thread_bits(const float *g, size_t n, float t, size_t base, bool vec,
-                                            float (&x)[kEPT]) {
-    load_thread<NTL>(g, n, base, vec, x);
-    return bits_of(g, n, t, base, x);
 }
 
 // Exclusive block-wide scan of (a, b) pairs: wave-level shuffles (64 lanes),
@@ -246,330 +239,6 @@ __global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint
     }
 }
 
-// ------------------------------------------------------- one-pass drop ----
-// The encoder as ONE launch with one read of g from HBM (the four-launch
-// pipeline above reads it twice and keeps a run table in global memory).
-// A grid of G co-resident workgroups (a cooperative launch: the runtime
-// guarantees every workgroup is resident, or refuses the launch), workgroup
-// w owning the tiles [w tpw, (w+1) tpw):
-//   1. count   per tile: flags, block scan -> kept / runs, the tile's first
-//              run start (kept values before it) in LDS; the workgroup's
-//              totals, first run start and last run start into its record
-//              (plain loads: the workgroup's slice of g stays in L2 / the
-//              Infinity Cache for step 3)
-//   2. barrier one grid-wide arrival counter; then every workgroup scans all
-//              G records (L2-resident, read through agent-scope loads): its
-//              own prefix (F0, S0), the nearest earlier workgroup with a run
-//              (U of its last run start: the first header's offset) and the
-//              nearest later one (F at its first run start: the last header's
-//              length), and the totals (wire length; the cap check)
-//   3. write   per tile again (nt loads, g's last use): values AND headers are
-//              placed in an LDS image of the tile's byte range, which goes
-//              out with coalesced 4-byte stores — no run table in HBM, no
-//              header pass.  The offsets / lengths that cross a tile come
-//              from the carry (previous run start) and the LDS tile records
-//              or the step-2 neighbour (next run start).
-// HBM traffic: 4N + wire.  A barrier that does not complete within the
-// timeout (a workgroup was not resident after all) raises the error word and
-// the host re-runs the four-launch encoder.
-constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kMaxGrid = 1024;  // workgroups of the one-pass grid at most (every one scans all records)
-// A workgroup's record: two words, each carrying the launch's 16-bit epoch
-// in its top quarter so it validates itself (no flag, no store ordering):
-//   word 0: F | S << 16 | firstF << 32     kept values / runs started in the
-//           workgroup; kept values before its first run start (kNone16: none)
-//   word 1: lastRel | lastF << 16          its last run start (element offset
-//           in the workgroup) and the kept values before it
-// Every field is < 2^16: a workgroup holds at most 8 tiles = 16384 elements.
-struct WgRec {
-    uint64_t word[2];
-};
-constexpr uint32_t kNone16 = 0xFFFFu;
-
-
-// Exclusive block-wide scan of N u32 values per thread at once (wave
-// shuffles, one LDS exchange of the wave totals, one barrier for all N).
-template <int N>
-__device__ __forceinline__ void block_scan_vec(const uint32_t (&v)[N], uint32_t (&ex)[N], uint32_t (&tot)[N]) {
-    __shared__ uint32_t wt[kSB / 64][N];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t in[N];
-#pragma unroll
-    for (int i = 0; i < N; i++) in[i] = v[i];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-        for (int i = 0; i < N; i++) {
-            const uint32_t y = __shfl_up(in[i], d, 64);
-            if (lane >= d) in[i] += y;
-        }
-    }
-    if (lane == 63) {
-#pragma unroll
-        for (int i = 0; i < N; i++) wt[wave][i] = in[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        uint32_t p = 0, tt = 0;
-#pragma unroll
-        for (int q = 0; q < kSB / 64; q++) {
-            if (q < wave) p += wt[q][i];
-            tt += wt[q][i];
-        }
-        ex[i] = p + in[i] - v[i];
-        tot[i] = tt;
-    }
-}
-
-__device__ __forceinline__ uint64_t rec_get(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int TPW>
-__global__ __launch_bounds__(kSB, 4) void sp_drop1(const float *g, size_t n, float t, uint32_t ntiles, uint32_t tpw,
-                                                WgRec *recs, uint32_t epoch,
-                                                uint8_t *buf, size_t cap, uint64_t *host_tot, uint32_t *err,
-                                                uint64_t timeout_ticks, bool vec, uint64_t *dbg) {
-    __shared__ uint16_t stage[kStageU16];
-    __shared__ uint32_t su[kTile / 2 + 1], sf[kTile / 2 + 1];
-    __shared__ uint32_t scanE[TPW][kSB];  // per tile and thread: kept | runs << 16 before it in the tile
-    __shared__ uint8_t lk[TPW][kSB];      // per tile and thread: its last element kept
-    __shared__ uint32_t tF[TPW], tS[TPW], tFirst[TPW], tLastIdx[TPW], tLastF[TPW];
-    __shared__ unsigned long long prevKey, nextKey;
-    __shared__ uint32_t base0[2], gprev;
-    __shared__ int gone;
-    const uint32_t w = blockIdx.x, G = gridDim.x;
-    const uint32_t t0 = w * tpw, t1 = min(ntiles, t0 + tpw), nt = t1 - t0;
-    const int tid = threadIdx.x;
-    if (dbg && tid == 0) dbg[5 * w] = wall_clock64();
-
-    // 1. count.  Every tile of the workgroup is loaded up front (all in
-    // flight at once; g is read from HBM exactly once) and stays in
-    // registers until step 3.  Run starts need "element before kept": from
-    // the neighbouring thread through LDS, across tiles too; only the
-    // workgroup's first element looks at memory (loaded with the tiles).
-    if (tid == 0) {
-        const size_t b0 = (size_t)t0 * kTile;
-        gprev = b0 > 0 && b0 - 1 < n && kept(g[b0 - 1], t) ? 1u : 0u;
-        prevKey = 0;
-        nextKey = ~0ull;
-        gone = 0;
-    }
-    // Loaded in halves of the workgroup's tiles (each half's loads in flight
-    // together: 32 KiB per workgroup) and reduced at once to keep flags; only
-    // the flags cross the barrier.  Plain loads: the workgroup's 64 KiB slice
-    // stays in the Infinity Cache for step 3's second look (its only HBM read
-    // is this one), and the registers stay few enough for 4 workgroups / CU.
-    constexpr int H = TPW > 1 ? TPW / 2 : 1;
-    uint32_t keep[TPW];
-#pragma unroll
-    for (int h0 = 0; h0 < TPW; h0 += H) {
-        float x[H][kEPT];
-#pragma unroll
-        for (int j = 0; j < H; j++)
-            if ((uint32_t)(h0 + j) < nt)
-                load_thread<false>(g, n, (size_t)(t0 + h0 + j) * kTile + (size_t)tid * kEPT, vec, x[j]);
-#pragma unroll
-        for (int j = 0; j < H; j++) {
-            const int i = h0 + j;
-            keep[i] = 0;
-            const size_t base = (size_t)(t0 + i) * kTile + (size_t)tid * kEPT;
-#pragma unroll
-            for (int e = 0; e < kEPT; e++)
-                if ((uint32_t)i < nt && base + e < n && kept(x[j][e], t)) keep[i] |= 1u << e;
-            lk[i][tid] = (uint8_t)((keep[i] >> (kEPT - 1)) & 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t start[TPW], ex[TPW], tot[TPW];
-    {
-    uint32_t cnt[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; i++) {
-        const uint32_t prev = tid ? lk[i][tid - 1] : (i ? lk[i - 1][kSB - 1] : gprev);
-        start[i] = keep[i] & ~((keep[i] << 1) | prev);
-        cnt[i] = (uint32_t)__popc(keep[i]) | (uint32_t)__popc(start[i]) << 16;  // <= 2048 / 1024: no carry
-    }
-    block_scan_vec<TPW>(cnt, ex, tot);
-    }
-    if (dbg && tid == 0) dbg[5 * w + 1] = wall_clock64();
-#pragma unroll
-    for (int i = 0; i < TPW; i++) {
-        scanE[i][tid] = ex[i];
-        const uint32_t ea = ex[i] & 0xFFFFu, eb = ex[i] >> 16, ta = tot[i] & 0xFFFFu, tb = tot[i] >> 16;
-        const size_t base = (size_t)(t0 + i) * kTile + (size_t)tid * kEPT;
-        if (tid == 0) {  // (tFirst of a tile with runs: its owner below, any wave — never overwritten here)
-            tF[i] = ta;
-            tS[i] = tb;
-            if (!tb) tFirst[i] = kNone;
-        }
-        if (start[i]) {
-            if (eb == 0) {  // the tile's first run start is this thread's
-                const int e = __builtin_ctz(start[i]);
-                tFirst[i] = ea + __popc(keep[i] & ((1u << e) - 1u));
-            }
-            if (eb + __popc(start[i]) == tb) {  // ... and / or its last one
-                const int e = 31 - __builtin_clz(start[i]);
-                tLastIdx[i] = (uint32_t)(base + e);
-                tLastF[i] = ea + __popc(keep[i] & ((1u << e) - 1u));
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t Fw = 0, Sw = 0, firstF = kNone, lastIdx = kNone, lastF = 0;
-        for (uint32_t i = 0; i < nt; i++) {
-            if (tS[i]) {
-                if (firstF == kNone) firstF = Fw + tFirst[i];
-                lastIdx = tLastIdx[i];
-                lastF = Fw + tLastF[i];
-            }
-            Fw += tF[i];
-            Sw += tS[i];
-        }
-        // 2. publish (self-validating words)
-        const uint64_t ep = (uint64_t)epoch << 48;
-        const uint32_t wstart = t0 * kTile;
-        const uint64_t w0 = (uint64_t)Fw | (uint64_t)Sw << 16 | (uint64_t)(firstF == kNone ? kNone16 : firstF) << 32 | ep;
-        const uint64_t w1 = (uint64_t)(lastIdx == kNone ? 0u : lastIdx - wstart) | (uint64_t)lastF << 16 | ep;
-        __hip_atomic_store(recs[w].word, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(recs[w].word + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (dbg) dbg[5 * w + 2] = wall_clock64();
-    }
-
-    // 2b. every record (<= kRecPer per thread, all loads in flight at once;
-    // each thread waits for its own records — no shared counter, so no hot
-    // address: G arrivals at one agent-scope atomic serialise at the memory
-    // side): own prefix, neighbours with runs, totals
-    constexpr int kRecPer = kMaxGrid / kSB;
-    uint64_t v[kRecPer][2];
-    const uint64_t c0 = wall_clock64();
-    const uint64_t epk = (uint64_t)epoch << 48, emask = 0xFFFFull << 48;
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        const uint32_t r = (uint32_t)tid * kRecPer + k;
-        v[k][0] = r < G ? rec_get(recs[r].word) : epk;
-        v[k][1] = r < G ? rec_get(recs[r].word + 1) : epk;
-    }
-    for (;;) {  // until every record of this thread carries this launch's epoch
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < kRecPer; k++) ok &= (v[k][0] & emask) == epk && (v[k][1] & emask) == epk;
-        if (ok) break;
-        if (wall_clock64() - c0 > timeout_ticks) {  // not co-resident after all: write nothing
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            gone = 1;
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-        for (int k = 0; k < kRecPer; k++) {
-            const uint32_t r = (uint32_t)tid * kRecPer + k;
-            if (r < G && (v[k][0] & emask) != epk) v[k][0] = rec_get(recs[r].word);
-            if (r < G && (v[k][1] & emask) != epk) v[k][1] = rec_get(recs[r].word + 1);
-        }
-    }
-    uint32_t sF = 0, sS = 0;
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        const uint32_t r = (uint32_t)tid * kRecPer + k;
-        if (r < G) { sF += (uint32_t)(v[k][0] & 0xFFFFu); sS += (uint32_t)(v[k][0] >> 16) & 0xFFFFu; }
-    }
-    uint32_t pF, pS, Ftot, R;
-    block_scan2(sF, sS, pF, pS, Ftot, R);
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        const uint32_t r = (uint32_t)tid * kRecPer + k;
-        if (r >= G) break;
-        const uint32_t rf = (uint32_t)(v[k][0] & 0xFFFFu), rs = (uint32_t)(v[k][0] >> 16) & 0xFFFFu;
-        const uint32_t rfirst = (uint32_t)(v[k][0] >> 32) & 0xFFFFu;
-        const uint32_t rlidx = r * tpw * kTile + ((uint32_t)v[k][1] & 0xFFFFu), rlf = (uint32_t)(v[k][1] >> 16) & 0xFFFFu;
-        if (r == w) { base0[0] = pF; base0[1] = pS; }
-        if (rs) {
-            if (r < w)  // U = index - F at the start: the offset of the next header
-                atomicMax(&prevKey, ((unsigned long long)(r + 1) << 32) | (uint32_t)(rlidx - (pF + rlf)));
-            if (r > w) atomicMin(&nextKey, ((unsigned long long)r << 32) | (uint32_t)(pF + rfirst));
-        }
-        pF += rf;
-        pS += rs;
-    }
-    __syncthreads();
-    if (gone) return;
-    if (dbg && tid == 0) dbg[5 * w + 3] = wall_clock64();
-    const size_t wire = 8 + 8 * (size_t)R + 2 * (size_t)Ftot;
-    if (w == 0 && tid == 0) {
-        host_tot[0] = Ftot;
-        host_tot[1] = R;
-        if (wire <= cap)
-            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
-    }
-    if (wire > cap) return;  // the host reports ONO_E_SIZE
-    uint32_t Fcur = base0[0], Scur = base0[1];
-    uint32_t carryU = prevKey ? (uint32_t)prevKey : 0u;  // U of the previous run start (0 before the first)
-    const uint32_t nextWgF = nextKey != ~0ull ? (uint32_t)nextKey : Ftot;
-
-    // 3. write: values and headers into an LDS image of each tile's byte
-    // range, then the range out with coalesced stores (flags and scans from
-    // step 1; the values read again, from the Infinity Cache, one tile ahead)
-    float xc[kEPT], xn[kEPT];
-    load_thread<true>(g, n, (size_t)t0 * kTile + (size_t)tid * kEPT, vec, xn);
-#pragma unroll
-    for (int i = 0; i < TPW; i++) {
-        if ((uint32_t)i >= nt) break;
-        const size_t base = (size_t)(t0 + i) * kTile + (size_t)tid * kEPT;
-#pragma unroll
-        for (int e = 0; e < kEPT; e++) xc[e] = xn[e];
-        if ((uint32_t)(i + 1) < nt) load_thread<true>(g, n, base + kTile, vec, xn);
-        const uint32_t ta = tF[i], tb = tS[i];
-        uint32_t f = scanE[i][tid] & 0xFFFFu, sl = scanE[i][tid] >> 16;
-        if (keep[i]) {
-#pragma unroll
-            for (int e = 0; e < kEPT; e++) {
-                if (!(keep[i] >> e & 1u)) continue;
-                if (start[i] >> e & 1u) {
-                    su[sl] = (uint32_t)(base + e) - (Fcur + f);  // U(s_j)
-                    sf[sl] = f;                                    // kept before s_j within the tile
-                    sl++;
-                }
-                stage[4 * sl + f] = to_f16_sp(xc[e]);
-                f++;
-            }
-        }
-        // F (global) at the first run start after this tile
-        uint32_t nextF = nextWgF, fp = Fcur + ta;
-        for (uint32_t j = i + 1; j < nt; j++) {
-            if (tS[j]) { nextF = fp + tFirst[j]; break; }
-            fp += tF[j];
-        }
-        __syncthreads();
-        for (uint32_t k = tid; k < tb; k += kSB) {  // headers into the image
-            const uint32_t off = su[k] - (k ? su[k - 1] : carryU);
-            const uint32_t len = (k + 1 < tb ? Fcur + sf[k + 1] : nextF) - (Fcur + sf[k]);
-            uint16_t *h = stage + 4 * k + sf[k];
-            h[0] = (uint16_t)off;
-            h[1] = (uint16_t)(off >> 16);
-            h[2] = (uint16_t)len;
-            h[3] = (uint16_t)(len >> 16);
-        }
-        __syncthreads();
-        const uint32_t nu16 = 4 * tb + ta;
-        uint16_t *dst = (uint16_t *)(buf + 8 + 8 * (size_t)Scur + 2 * (size_t)Fcur);
-        const uint32_t h = (uint32_t)(((uintptr_t)dst >> 1) & 1u) < nu16 ? (uint32_t)(((uintptr_t)dst >> 1) & 1u) : nu16;
-        if (tid == 0 && h) dst[0] = stage[0];
-        const uint32_t npair = (nu16 - h) / 2;
-        uint32_t *d32 = (uint32_t *)(dst + h);
-        for (uint32_t k = tid; k < npair; k += kSB)
-            d32[k] = (uint32_t)stage[h + 2 * k] | (uint32_t)stage[h + 2 * k + 1] << 16;
-        if (tid == 0 && h + 2 * npair < nu16) dst[nu16 - 1] = stage[nu16 - 1];
-        if (tb) carryU = su[tb - 1];
-        Fcur += ta;
-        Scur += tb;
-        __syncthreads();  // stage / su / sf reused by the next tile
-    }
-    if (dbg && tid == 0) dbg[5 * w + 4] = wall_clock64();
-}
-
 // Fallback lift (after a host parse): value v belongs to run j with
 // cumF[j] <= v < cumF[j+1] (binary search);
 // it sits at byte 16 + 8 j + 2 v and lands at start[j] + (v - cumF[j]).
@@ -618,6 +287,7 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 // itself, and queues runs longer than kShort for sl_long (one workgroup per
 // run).
 constexpr int kSeg = 128, kLook = 4, kShort = 16;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *b, size_t p) {  // p even, b 2-B aligned
     const uint16_t *h = (const uint16_t *)(b + p);
@@ -795,14 +465,6 @@ struct Scratch {
     size_t tiles_cap = 0, runs_cap = 0;
     uint32_t *tiles = nullptr, *runs = nullptr;
     uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
-    // one-pass encoder (sp_drop1): workgroup records, the grid barrier's
-    // (tagged with the launch's epoch, so no reset between launches), and a
-    // host-mapped error word for a record that never arrived
-    size_t recs_cap = 0;
-    WgRec *recs = nullptr;
-    uint32_t epoch = 0;
-    uint32_t *err = nullptr, *err_dev = nullptr;
-    int max_grid[4] = {-1, -1, -1, -1};  // co-resident workgroups of sp_drop1<1, 2, 4, 8> (0: unavailable)
 };
 std::mutex g_scratch_mu;
 Scratch g_scratch[64];
@@ -1041,122 +703,6 @@ extern "C" {
 
 size_t ono_sparse_max_bytes(size_t n) { return 8 + 10 * ((n + 1) / 2) + 2 * n; }
 
-}  // extern "C"
-
-namespace {
-
-std::atomic<size_t> g_drop_fallbacks{0};
-uint64_t *g_drop_dbg = nullptr;
-
-bool onepass_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("ONO_SPARSE_ONEPASS");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-// The one-pass encoder; *done = false when it does not apply (too many tiles
-// for one co-resident grid, cooperative launch unavailable, or its barrier
-// timed out), and the caller runs the four-launch encoder instead.
-int drop_onepass(Scratch *sc, uint8_t *buf, size_t cap, const float *g, size_t n, float threshold, bool vec,
-                 hipStream_t s, bool *done) {
-    *done = false;
-    const size_t ntiles = (n + kTile - 1) / kTile;
-    int dev = 0;
-    ONO_HIP(hipGetDevice(&dev));
-    static const void *const kKernels[4] = {(const void *)sp_drop1<1>, (const void *)sp_drop1<2>,
-                                            (const void *)sp_drop1<4>, (const void *)sp_drop1<8>};
-    if (!sc->err) {
-        ONO_HIP(hipHostMalloc((void **)&sc->err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
-        ONO_HIP(hipHostGetDevicePointer((void **)&sc->err_dev, sc->err, 0));
-        *sc->err = 0;
-    }
-    // Tiles per workgroup: the smallest of 1, 2, 4, 8 that keeps the grid
-    // co-resident and at most 1024 workgroups (every workgroup scans all
-    // G records after the barrier, and G workgroups poll one counter line).
-    const char *cap_env = getenv("ONO_SPARSE_GRID");  // measurement knob
-    const int gcap = cap_env && atoi(cap_env) > 0 ? std::min(atoi(cap_env), kMaxGrid) : kMaxGrid;
-    int pick = -1, tpw = 0;
-    for (int k = 0; k < 4 && pick < 0; k++) {
-        if (sc->max_grid[k] < 0) {
-            int coop = 0, cus = 0, per = 0;
-            if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess) coop = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kKernels[k], kSB, 0) != hipSuccess) per = 0;
-            sc->max_grid[k] = coop ? cus * per : 0;
-        }
-        const size_t G = (ntiles + (1u << k) - 1) >> k;
-        if (sc->max_grid[k] > 0 && G <= (size_t)std::min(sc->max_grid[k], gcap)) {
-            pick = k;
-            tpw = 1 << k;
-        }
-    }
-    if (pick < 0) return ONO_OK;  // too many tiles for one co-resident grid
-    const uint32_t G = (uint32_t)((ntiles + tpw - 1) / tpw);
-    if (G > sc->recs_cap) {
-        (void)hipFree(sc->recs);
-        sc->recs = nullptr;
-        sc->recs_cap = 0;
-        ONO_HIP(hipMalloc((void **)&sc->recs, (size_t)G * sizeof(WgRec)));
-        ONO_HIP(hipMemset(sc->recs, 0, (size_t)G * sizeof(WgRec)));  // tag 0 = no launch yet
-        sc->recs_cap = G;
-    }
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-    const uint64_t ticks = (uint64_t)khz * 2000;  // 2 s: co-resident workgroups arrive within microseconds
-    uint32_t nt = (uint32_t)ntiles, tp = (uint32_t)tpw;
-    uint32_t epoch = (sc->epoch + 1) & 0xFFFFu;  // 16-bit epochs, never 0 (a zeroed record)
-    if (epoch == 0) {  // wrapped: no record may still carry an old epoch that comes round again
-        ONO_HIP(hipMemsetAsync(sc->recs, 0, sc->recs_cap * sizeof(WgRec), s));
-        epoch = 1;
-    }
-    WgRec *recs = sc->recs;
-    uint64_t *ht = sc->host_tot_dev;
-    uint32_t *err = sc->err_dev;
-    uint64_t tk = ticks;
-    uint64_t *dbg = g_drop_dbg;  // ono_sparse_drop_debug: per-workgroup phase timestamps
-    void *args[] = {(void *)&g, (void *)&n, (void *)&threshold, (void *)&nt, (void *)&tp, (void *)&recs, (void *)&epoch,
-                    (void *)&buf, (void *)&cap, (void *)&ht, (void *)&err, (void *)&tk, (void *)&vec,
-                    (void *)&dbg};
-    *sc->err = 0;
-    // A cooperative launch guarantees the grid is co-resident (or refuses);
-    // ONO_SPARSE_COOP=0 launches it plainly, relying on the occupancy bound
-    // (and on the wait's timeout + fallback when another kernel holds CUs).
-    static const bool coop = [] {
-        const char *e = getenv("ONO_SPARSE_COOP");
-        return !(e && e[0] == '0');
-    }();
-    hipError_t e = coop ? hipLaunchCooperativeKernel(kKernels[pick], dim3(G), dim3(kSB), args, 0, s)
-                        : hipLaunchKernel(kKernels[pick], dim3(G), dim3(kSB), args, 0, s);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        sc->max_grid[pick] = 0;  // refused for this shape: the four-launch encoder from now on
-        return ONO_OK;
-    }
-    ONO_HIP(hipStreamSynchronize(s));
-    sc->epoch = epoch;
-    if (__atomic_load_n(sc->err, __ATOMIC_ACQUIRE)) {  // some workgroup gave up waiting
-        *sc->err = 0;
-        return ONO_OK;
-    }
-    *done = true;
-    return ONO_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-size_t ono_sparse_drop_fallbacks(void) { return g_drop_fallbacks.load(); }
-
-// measurement hook (not in the header): per-workgroup wall-clock stamps of the
-// one-pass encoder's phases, 5 per workgroup, into a device buffer (NULL: off)
-int ono_sparse_drop_debug(uint64_t *dbg_dev) {
-    g_drop_dbg = dbg_dev;
-    return ONO_OK;
-}
-
 int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, float threshold,
                     void *stream) {
     if (!nbytes || (n && !g) || !buf) return set_error(ONO_E_ARG, "NULL argument");
@@ -1177,20 +723,6 @@ int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, si
     uint32_t *tileF = sc->tiles, *tileS = sc->tiles + ntiles + 1, *RU = sc->runs, *RF = sc->runs + maxruns;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     tot[0] = tot[1] = 0;
-    if (ntiles && onepass_enabled()) {
-        bool done = false;
-        rc = drop_onepass(sc, buf, cap, g, n, threshold, vec, s, &done);
-        if (rc) return rc;
-        if (done) {
-            const size_t need = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
-            if (need > cap)
-                return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu", need, cap);
-            *nbytes = need;
-            return ONO_OK;
-        }
-        g_drop_fallbacks++;
-        tot[0] = tot[1] = 0;
-    }
     uint64_t *totals = sc->totals_dev;
     hipError_t e = hipSuccess;
     if (ntiles) {

@@ -283,33 +283,6 @@ def test_drop_headers_across_tiles_and_scan_chunks(pattern):
     assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
 
 
-@pytest.mark.parametrize("n,r", [(2049, 0.5), ((1 << 20) + 5, 0.9), (10_000_003, 0.99), (1 << 24, 0.0)])
-def test_drop_takes_the_one_pass_encoder(n, r):
-    """the one-pass cooperative encoder serves every drop that fits one
-    co-resident grid (up to 1024 workgroups x 8 tiles of 2048 values: the
-    64 MiB gradient of the bench), byte-exact; larger ones take the four
-    launches (test_drop_headers_across_tiles_and_scan_chunks)"""
-    L = ono_amd.lib()
-    g = O.synth(n, SEED + 21, 0)
-    t = O.sparse_threshold(g, r) if n <= 16384 else float(np.quantile(np.abs(g), r)) if r else 0.0
-    before = L.ono_sparse_drop_fallbacks()
-    got = SP.grad_drop_dev(dev(g), t)
-    assert L.ono_sparse_drop_fallbacks() == before, "the drop fell back to the four-launch encoder"
-    assert bytes(got.cpu().numpy()) == O.grad_drop(g, t)
-
-
-def test_drop_one_pass_repeated_launches_keep_the_barrier_in_step():
-    """the grid barrier's arrival counter is never reset between launches:
-    many drops of different grid sizes back to back stay exact"""
-    L = ono_amd.lib()
-    before = L.ono_sparse_drop_fallbacks()
-    for i, n in enumerate([5000, 300_000, 4099, 3_000_001, 2048 * 7, 1 << 20] * 3):
-        g = O.synth(n, SEED + 30 + i, 0)
-        t = float(np.quantile(np.abs(g), 0.8))
-        assert bytes(SP.grad_drop_dev(dev(g), t).cpu().numpy()) == O.grad_drop(g, t), f"drop {i} (n={n})"
-    assert L.ono_sparse_drop_fallbacks() == before
-
-
 # ------------------------------------------------ calculate_threshold on the device
 def _threshold_inputs(n, seed):
     x = O.synth(n, seed, 0)

@@ -20,9 +20,7 @@ torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(K):
     wire = ono_amd.sparse.grad_drop_dev(g, t)
-print(f"drop {(time.perf_counter() - t0) / K * 1e6:.1f} us per blocking call (grid cap "
-      f"{os.environ.get('ONO_SPARSE_GRID', 'none')}, one-pass {os.environ.get('ONO_SPARSE_ONEPASS', '1')}, "
-      f"cooperative {os.environ.get('ONO_SPARSE_COOP', '1')})")
+print(f"drop {(time.perf_counter() - t0) / K * 1e6:.1f} us per blocking call")
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
 for _ in range(K):
@@ -36,5 +34,4 @@ s = torch.cuda.current_stream().cuda_stream
 for _ in range(K):
     ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
 torch.cuda.synchronize()
-print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "drop fallbacks", L.ono_sparse_drop_fallbacks(),
-      "wire", wire.numel())
+print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
