@@ -207,6 +207,62 @@ __global__ void k_nan_check(unsigned long long *bad) {
     }
 }
 
+// ---- optimizer consumer / owner-chain shapes (mode "opt"): load policy L
+// (0 plain, 1 nt) and store policy S (0 nt, 1 nt sc1) for the all-reduce
+// consumer (GD: params, grad in; params, grad = 0, params copy out) with
+// momentum / Adam state, and the 8-input owner chain (8 in; grad, message,
+// own slice = 0 out)
+template <int L> __device__ __forceinline__ f4 ldp(const void *p, size_t v) {
+    if constexpr (L) return ldn((const f4 *)p + v);
+    else return ((const f4 *)p)[v];
+}
+template <int S> __device__ __forceinline__ void stp(void *p, size_t v, f4 x) {
+    if constexpr (S) st_sc1((f4 *)p + v, x);
+    else stn((f4 *)p + v, x);
+}
+template <int KIND, int L, int S> struct OptShape {  // KIND 0 GD, 1 momentum, 2 Adam
+    static constexpr double bytes_per_elem = KIND == 0 ? 20.0 : KIND == 1 ? 28.0 : 36.0;
+    __device__ __forceinline__ static void run(const Args &a, size_t v) {
+        f4 w = ldp<L>(a.in[0], v), g = ldp<L>(a.in[1], v) * 0.5f;
+        if constexpr (KIND == 0) {
+            w -= 0.1f * g;
+        } else if constexpr (KIND == 1) {
+            f4 m = ldp<L>(a.in[2], v) * 0.9f + g;
+            stp<S>((void *)a.in[2], v, m);
+            w -= 0.1f * m;
+        } else {
+            f4 m = ldp<L>(a.in[2], v) * 0.9f + 0.1f * g, q = ldp<L>(a.in[3], v) * 0.999f + 0.001f * g * g;
+            stp<S>((void *)a.in[2], v, m);
+            stp<S>((void *)a.in[3], v, q);
+            w -= 0.001f * m / (f4{__builtin_sqrtf(q.x), __builtin_sqrtf(q.y), __builtin_sqrtf(q.z), __builtin_sqrtf(q.w)} + 1e-8f);
+        }
+        stp<S>((void *)a.in[0], v, w);
+        stp<S>((void *)a.in[1], v, f4{0, 0, 0, 0});
+        stp<S>(a.out, v, w);
+    }
+};
+template <int L, int LO, int S> struct ChainShape {  // 7 received (policy L) + own (policy LO) -> grad, msg, own = 0
+    static constexpr double bytes_per_elem = 44.0;
+    __device__ __forceinline__ static void run(const Args &a, size_t v) {
+        f4 p = ldp<L>(a.in[0], v);
+#pragma unroll
+        for (int k = 1; k < 7; k++) p = ldp<L>(a.in[k], v) + p;
+        p = ldp<LO>(a.in[7], v) + p;
+        const f4 gv = p * 0.125f;
+        stp<S>(a.out, v, gv);
+        stp<S>(a.out2, v, gv);
+        stp<S>((void *)a.in[7], v, f4{0, 0, 0, 0});
+    }
+};
+template <class Sh>
+__global__ __launch_bounds__(64) void k_run(Args a, size_t nvec) {
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < nvec) Sh::run(a, v);
+}
+template <class Sh> void L_run(const Args &a, size_t nvec) {
+    hipLaunchKernelGGL(k_run<Sh>, dim3((unsigned)((nvec + 63) / 64)), dim3(64), 0, g_s, a, nvec);
+}
+
 int main(int argc, char **argv) {
     if (argc > 1) N = (size_t)atol(argv[1]) << 18;
     const int passes = argc > 2 ? atoi(argv[2]) : 5;
@@ -226,6 +282,23 @@ int main(int argc, char **argv) {
                "%u\n", hb[0], hb[1], (1u << 24) - 2);
         add_rows<DecShape>(rows, "dec", 2);
         add_rows<DecNanShape>(rows, "decnan", 2);
+    } else if (argc > 3 && !strcmp(argv[3], "opt")) {
+        auto add = [&](const char *nm, double bpe, int per, void (*f)(const Args &, size_t)) {
+            rows.push_back(Row{nm, bpe * (double)N, per, f, {}});
+        };
+        add("gd L0 S0", 20, 3, L_run<OptShape<0, 0, 0>>);
+        add("gd L1 S0", 20, 3, L_run<OptShape<0, 1, 0>>);
+        add("gd L1 S1", 20, 3, L_run<OptShape<0, 1, 1>>);
+        add("mom L0 S0", 28, 4, L_run<OptShape<1, 0, 0>>);
+        add("mom L1 S0", 28, 4, L_run<OptShape<1, 1, 0>>);
+        add("mom L1 S1", 28, 4, L_run<OptShape<1, 1, 1>>);
+        add("adam L0 S0", 36, 5, L_run<OptShape<2, 0, 0>>);
+        add("adam L1 S0", 36, 5, L_run<OptShape<2, 1, 0>>);
+        add("adam L1 S1", 36, 5, L_run<OptShape<2, 1, 1>>);
+        add("chain8 L1 LO0 S0", 44, 10, L_run<ChainShape<1, 0, 0>>);
+        add("chain8 L1 LO1 S0", 44, 10, L_run<ChainShape<1, 1, 0>>);
+        add("chain8 L1 LO1 S1", 44, 10, L_run<ChainShape<1, 1, 1>>);
+        add("chain8 L0 LO0 S0", 44, 10, L_run<ChainShape<0, 0, 0>>);
     } else if (argc > 3 && !strcmp(argv[3], "skew")) {
         for (size_t sk : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)8192, (size_t)65536 + 512}) {
             char nm[64];
@@ -265,6 +338,7 @@ int main(int argc, char **argv) {
                 a.out = op(r.per_set - 1);
                 a.out2 = op(r.per_set > 2 ? 1 : 0);
                 if (r.name.rfind("sz", 0) == 0) a.out2 = op(1);
+                if (r.per_set == 10) a.out2 = op(8);  // chain8: 8 inputs, grad, message
                 r.launch(a, nvec);
             };
             for (int i = 0; i < W; i++) go(i);
