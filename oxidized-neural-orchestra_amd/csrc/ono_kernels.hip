@@ -274,7 +274,10 @@ template <int K, int M, bool NTL> struct SumScaleOp {
 struct Outs {
     void *p[ONO_MAX_INPUTS];
 };
-template <int K, class W> struct DirectOp {
+// ZALL is a template parameter (the load policy of every slice is decided at
+// compile time; a plain load where an nt load belongs cost the owner chain at
+// n = 8 about 20 %: profiles/r02_opt_variants.txt, "chain8 L0" vs "L1").
+template <int K, class W, bool ZALL> struct DirectOp {
     typedef typename Wire<W>::V WV;
     // outs read by other ranks after the next flag barrier: every wave waits
     // for its stores to complete at system scope before it ends
@@ -288,7 +291,6 @@ template <int K, class W> struct DirectOp {
     int sys_out;  // outs are peer HBM: system-coherent (sc0 sc1) stores, see ono_device.h
     float v;
     int mode;  // SCALE_RECIP or SCALE_DIV
-    int zall;
     typedef f4 R;
     __device__ __forceinline__ float wq(float p) const { return Wire<W>::dec(Wire<W>::enc(p)); }
     __device__ __forceinline__ f4 wq4(f4 p) const { return Wire<W>::dec4(Wire<W>::enc4(p)); }
@@ -303,21 +305,30 @@ template <int K, class W> struct DirectOp {
             if (sys_out) st_sys(static_cast<W *>(out.p[j]) + i, m);
             else static_cast<W *>(out.p[j])[i] = m;
         }
-        if (zall) {
+        if constexpr (ZALL) {
 #pragma unroll
             for (int k = 0; k < K; k++) const_cast<float *>(in.p[k])[i] = 0.0f;
         } else {
             const_cast<float *>(in.p[K - 1])[i] = 0.0f;
         }
     }
-    __device__ __forceinline__ f4 get(int k, size_t i) const {
-        if (!zall && k < K - 1) return ldn((const f4 *)(in.p[k] + i));  // received slices: read once
-        return ld((const f4 *)(in.p[k] + i));                          // rewritten (zeroed) below
-    }
+    // Received slices are read once (nt loads); slices zeroed in this pass
+    // (the own one, or all with ZALL) take plain loads.  The two forms are
+    // separate straight-line loops: a `k < K - 1 ? ldn : ld` inside one loop
+    // was merged by the compiler into a single plain load before unrolling.
     __device__ __forceinline__ R load(size_t i) const {
-        f4 p = get(0, i);
+        f4 x[K];
+        if constexpr (ZALL) {
 #pragma unroll
-        for (int k = 1; k < K; k++) p = get(k, i) + wq4(p);
+            for (int k = 0; k < K; k++) x[k] = ld((const f4 *)(in.p[k] + i));
+        } else {
+#pragma unroll
+            for (int k = 0; k < K - 1; k++) x[k] = ldn((const f4 *)(in.p[k] + i));
+            x[K - 1] = ld((const f4 *)(in.p[K - 1] + i));
+        }
+        f4 p = x[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) p = x[k] + wq4(p);
         return p;
     }
     __device__ __forceinline__ void store(size_t i, R p) const {
@@ -329,7 +340,7 @@ template <int K, class W> struct DirectOp {
             else st_nt((WV *)(static_cast<W *>(out.p[j]) + i), m);
         }
         const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (zall) {
+        if constexpr (ZALL) {
 #pragma unroll
             for (int k = 0; k < K; k++) st_nt((f4 *)const_cast<float *>(in.p[k] + i), z);
         } else {
@@ -552,12 +563,14 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
         if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) v[i] = vi;
         if constexpr (KIND == ONO_OPT_ADAM) s[i] = si;
     }
+    // every operand is read once and rewritten: nt loads (+3-5 % over plain
+    // loads on fresh buffers for GD / momentum / Adam, profiles/r02_opt_variants.txt)
     __device__ __forceinline__ R load(size_t i) const {
         R r{};
-        r.g = ld((const f4 *)(g + i));
-        r.w = ld((const f4 *)(w + i));
-        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) r.v = ld((const f4 *)(v + i));
-        if constexpr (KIND == ONO_OPT_ADAM) r.s = ld((const f4 *)(s + i));
+        r.g = ldn((const f4 *)(g + i));
+        r.w = ldn((const f4 *)(w + i));
+        if constexpr (KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM) r.v = ldn((const f4 *)(v + i));
+        if constexpr (KIND == ONO_OPT_ADAM) r.s = ldn((const f4 *)(s + i));
         return r;
     }
     __device__ __forceinline__ void store(size_t i, R r) const {
@@ -650,8 +663,9 @@ hipError_t direct_k(float *grad, const Outs &out, int nout, bool sys_out, const 
     for (int k = 0; k < K; k++) ph[c++] = phase_of(p.p[k], 4);
     // SCALE_NONE (d == 1) runs as a multiply by 1: the identity, -0 and NaN payloads included
     const int mode = sc.mode == SCALE_DIV ? SCALE_DIV : SCALE_RECIP;
-    DirectOp<K, W> op{p, grad, out, nout, sys_out ? 1 : 0, sc.mode == SCALE_NONE ? 1.0f : sc.v, mode, zall ? 1 : 0};
-    return launch_ew_arr(op, n, ph, c, s);
+    const float v = sc.mode == SCALE_NONE ? 1.0f : sc.v;
+    if (zall) return launch_ew_arr(DirectOp<K, W, true>{p, grad, out, nout, sys_out ? 1 : 0, v, mode}, n, ph, c, s);
+    return launch_ew_arr(DirectOp<K, W, false>{p, grad, out, nout, sys_out ? 1 : 0, v, mode}, n, ph, c, s);
 }
 
 template <int K, class W>

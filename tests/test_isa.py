@@ -126,3 +126,36 @@ def test_checker_sees_a_missing_wait():
     assert _unwaited(["global_store_dwordx4 v[0:1], v[2:5], off sc0 sc1", "s_endpgm"])
     assert not _unwaited(["global_store_dwordx4 v[0:1], v[2:5], off sc0 sc1", "s_waitcnt vmcnt(0)", "s_endpgm"])
     assert _unwaited(["global_store_dword v0, v1, s[0:1] sc0 sc1", "s_cbranch_execz 3", "s_waitcnt vmcnt(0)"])
+
+
+# ---- cache policy of the stream kernels (round 2: a run-time flag once let the
+# compiler merge DirectOp's two load forms and drop the non-temporal hint)
+def _vec_loads(code):
+    return [i for i in code if i.startswith("global_load_dwordx")]
+
+
+def _one_shot(kernels, op):
+    """the one-shot (loop-free) instances of ew_kernel<op...>"""
+    return {k: v for k, v in kernels.items() if "ew_kernel" in k and op in k and k.endswith("Lb0EEEvT_mmm")}
+
+
+def test_direct_chain_reads_received_slices_non_temporal(kernels):
+    """DirectOp<K, W, ZALL = false>: the K-1 received slices with nt loads, the
+    owner's own slice (zeroed in the same pass) with a plain load"""
+    ks = {k: v for k, v in _one_shot(kernels, "DirectOp").items() if re.search(r"DirectOpILi\d+E[tf]Lb0E", k)}
+    assert ks
+    for k, code in ks.items():
+        m = re.search(r"DirectOpILi(\d+)E", k)
+        K = int(m.group(1))
+        loads = _vec_loads(code)
+        nt = [i for i in loads if " nt" in i]
+        assert len(loads) == K and len(nt) == K - 1, f"{k}: {len(nt)} nt of {len(loads)} vector loads"
+
+
+def test_optimizer_and_sum_scale_stream_non_temporal(kernels):
+    for op in ("OptOp", "SumScaleOp"):
+        for k, code in _one_shot(kernels, op).items():
+            if op == "SumScaleOp" and not re.search(r"SumScaleOpILi\d+ELi\dELb1E", k):
+                continue  # the in-place form (out aliases an input) keeps plain loads
+            loads = _vec_loads(code)
+            assert loads and all(" nt" in i for i in loads), f"{k}: {loads}"
