@@ -111,5 +111,6 @@ def test_xgmi_timing_phases():
     check(run_ranks(3, [{"kind": "timing"}]))
 
 
-def test_xgmi_barrier_timeout_is_an_error_not_a_hang():
-    check(run_ranks(2, [{"kind": "timeout"}], 120.0))
+@pytest.mark.parametrize("how", ["env", "api", "host"])
+def test_xgmi_barrier_timeout_is_an_error_not_a_hang(how):
+    check(run_ranks(2, [{"kind": "timeout", "how": how}], 120.0))

@@ -168,20 +168,35 @@ def run_timing(rank: int, n: int) -> str | None:
         ring.close()
 
 
-def run_timeout(rank: int, n: int) -> str | None:
+def run_timeout(rank: int, n: int, how: str = "env") -> str | None:
     """Rank 0 starts a round alone: its barrier gives up after the timeout and
     the next call fails with IoError instead of hanging; the late rank's
-    teardown is bounded too."""
-    os.environ["ONO_XGMI_TIMEOUT_S"] = "2"  # read when the ring's region is allocated
+    teardown is bounded too.  how: "env" (ONO_XGMI_TIMEOUT_S when the region
+    is made), "api" (ono_ring_set_xgmi_timeout on a live ring), "host" (the
+    host-fed round must itself report the timed-out barrier: its output is
+    invalid and the host residual already zeroed)."""
+    os.environ["ONO_XGMI_TIMEOUT_S"] = "2" if how == "env" else "10"  # read when the region is allocated
     try:
         ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, 4096, allgather, wire="f32")
     finally:
         os.environ["ONO_XGMI_TIMEOUT_S"] = "10"
     try:
+        if how != "env":
+            ring.set_xgmi_timeout(2.0)
         if rank == 0:
             t0 = time.time()
-            ring.pull_grads()
-            torch.cuda.synchronize()
+            if how == "host":
+                res = np.ones(4096, np.float32)
+                grad = np.zeros(4096, np.float32)
+                try:
+                    ring.pull_grads_host(res, grad)
+                except ono_amd.IoError:
+                    pass
+                else:
+                    return "a host-fed round over a timed-out barrier reported success"
+            else:
+                ring.pull_grads()
+                torch.cuda.synchronize()
             waited = time.time() - t0
             try:
                 ring.check()
@@ -212,7 +227,7 @@ def main() -> int:
     for case in cases:
         try:
             kind = case.get("kind", "ring")
-            msg = run_timeout(rank, n) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
+            msg = run_timeout(rank, n, case.get("how", "env")) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
                 run_timing(rank, n) if kind == "timing" else run_case(rank, n, case)
         except Exception as e:  # reported, the parent asserts
             msg = f"{type(e).__name__}: {e}"
