@@ -113,12 +113,54 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
     eb = pb + ib - b;
 }
 
+// The same scan for the per-thread counts of the count / write passes, which
+// are small (kept <= 8, run starts <= 4 of a thread's 8 elements): each bit
+// plane of the count is one wave ballot, and mbcnt counts the set bits below
+// the lane — an exact exclusive wave scan with no cross-lane data movement
+// (7 ballots instead of 12 ds_bpermute round trips of the shuffle ladder).
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+template <int BITS>
+__device__ __forceinline__ void wave_scan_small(uint32_t v, uint32_t &ex, uint32_t &tot) {
+    ex = 0;
+    tot = 0;
+#pragma unroll
+    for (int b = 0; b < BITS; b++) {
+        const uint64_t m = __ballot((v >> b) & 1u);
+        ex += mbcnt64(m) << b;
+        tot += (uint32_t)__popcll(m) << b;
+    }
+}
+__device__ __forceinline__ void block_scan_counts(uint32_t a, uint32_t b, uint32_t &ea, uint32_t &eb, uint32_t &ta,
+                                                  uint32_t &tb) {
+    __shared__ uint32_t wa[kSB / 64], wb[kSB / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t xa, xb, sa, sb;
+    wave_scan_small<4>(a, xa, sa);  // a <= kEPT = 8
+    wave_scan_small<3>(b, xb, sb);  // b <= kEPT / 2 = 4
+    if (lane == 0) { wa[wave] = sa; wb[wave] = sb; }
+    __syncthreads();
+    uint32_t pa = 0, pb = 0;
+    ta = 0;
+    tb = 0;
+#pragma unroll
+    for (int w = 0; w < kSB / 64; w++) {
+        if (w < wave) { pa += wa[w]; pb += wb[w]; }
+        ta += wa[w];
+        tb += wb[w];
+    }
+    ea = pa + xa;
+    eb = pb + xb;
+}
+static_assert(kEPT == 8, "block_scan_counts sizes its bit planes for 8 elements per thread");
+
 __global__ __launch_bounds__(kSB) void sp_count(const float *g, size_t n, float t, uint32_t *tileF, uint32_t *tileS,
                                                 bool vec) {
     float x[kEPT];
     Bits b = thread_bits<false>(g, n, t, (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT, vec, x);
     uint32_t ea, eb, ta, tb;
-    block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
+    block_scan_counts(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
     if (threadIdx.x == 0) { tileF[blockIdx.x] = ta; tileS[blockIdx.x] = tb; }
 }
 
@@ -183,7 +225,7 @@ __global__ __launch_bounds__(kSB) void sp_write(const float *g, size_t n, float 
     float x[kEPT];  // the values stay in registers from the flag pass (g is read once here)
     Bits b = thread_bits<true>(g, n, t, base, vec, x);
     uint32_t ea, eb, ta, tb;
-    block_scan2(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
+    block_scan_counts(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
     const uint32_t F0 = tileF[blockIdx.x], S0 = tileS[blockIdx.x];
     uint32_t f = ea, sl = eb;  // this thread's kept values / runs before it, within the tile
     if (b.keep) {
