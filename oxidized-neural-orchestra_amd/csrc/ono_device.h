@@ -17,6 +17,18 @@ template <class T> __device__ __forceinline__ void st_sys(T *p, T v) {
     *(volatile __attribute__((address_space(1))) T *)p = v;  // global_store ... sc0 sc1
 }
 
+// The same system-coherent 16-byte store without the volatile semantics: the
+// compiler waits for every volatile store to complete before the next memory
+// operation (`s_waitcnt vmcnt(0)` after each), which keeps a remote round
+// trip per store on the wave's critical path; this one is waited for once, by
+// peer_stores_done() at the end of the wave.  Vector store (no scalar-cache
+// write); `s_nop 1` covers the gfx940+ store-data hazard the compiler cannot
+// see through the asm (as st_sc1 in ono_kernels.hip).
+typedef float f4_dev __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sys_async(f4_dev *p, f4_dev v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+
 // Publication of stores other ranks read after a flag barrier.
 //
 // The barrier is a later launch on the same stream: its first lane runs a

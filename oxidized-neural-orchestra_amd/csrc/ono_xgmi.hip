@@ -62,10 +62,10 @@ template <bool ZERO> struct PushOp {
         f4 *src = (f4 *)((float *)s.src + i);
         if constexpr (ZERO) {
             f4 x = *src;  // plain load: the same lines are rewritten (zeroed) below
-            st_sys((f4 *)((float *)s.dst + i), x);
+            st_sys_async((f4 *)((float *)s.dst + i), x);
             __builtin_nontemporal_store(f4{0.0f, 0.0f, 0.0f, 0.0f}, src);
         } else {
-            st_sys((f4 *)((float *)s.dst + i), __builtin_nontemporal_load(src));
+            st_sys_async((f4 *)((float *)s.dst + i), __builtin_nontemporal_load(src));
         }
     }
 };
