@@ -477,6 +477,22 @@ int ono_plan_ps_step(int pos, int nranks, size_t nparams, ono_plan_step *steps, 
 /* element counts of the plan buffers (ONO_PB_COUNT entries) for a ring of
  * nranks over `size` elements and a PS of nparams                           */
 int ono_plan_buffers(int nranks, size_t size, size_t nparams, uint64_t *counts);
+/* Every rank's plan executed by nranks co-resident ranks on ONE device, in
+ * lockstep: local steps through the same kernel launcher the RCCL interpreter
+ * uses; a group's sends matched with the peers' receives and carried out as
+ * device copies; all-reduce / reduce-scatter as the sum over ranks in rank
+ * order, all-gather as copies.  Runs the N > 1 schedules' device work on a
+ * one-GPU box (RCCL refuses two ranks per device).  Blocking.
+ * pull_grads: residuals[r], grads[r] are rank r's buckets of `size`.        */
+int ono_plan_run_local(int algo, int wire, int nranks, size_t size, int segments, float *const *residuals,
+                       float *const *grads, void *stream);
+/* ono_ps_step's plan: grads[r] (nparams) in, params[r] (nparams) out; shards[r]
+ * is rank r's shard of the parameters (split at ceil(nparams / nranks)) and
+ * its optimizer state v[r], s[r] (may be NULL for GD), updated in place;
+ * step_size is Adam's lr sqrt(1 - b2^t) / (1 - b1^t) for this step.         */
+int ono_plan_run_local_ps(int nranks, size_t nparams, const float *const *grads, float *const *params,
+                          float *const *shards, float *const *v, float *const *s, const ono_opt_spec *opt,
+                          float step_size, void *stream);
 
 #ifdef __cplusplus
 }

@@ -856,7 +856,221 @@ static int local_direct(float *const *res, float *const *grad, int R, size_t n, 
     return rc;
 }
 
+// ---------------------------------------------- plans on one device ------
+// Every rank's exchange plan executed by co-resident ranks on ONE device, in
+// lockstep: each rank runs its local steps (kernels, memsets, copies) up to
+// its next communication step; when every rank is there, the group's sends
+// are matched with the peers' receives (k-th send r -> q with q's k-th
+// receive from r) and carried out as device copies, and a collective is
+// carried out by the library's kernels (all-reduce / reduce-scatter: the sum
+// over ranks in rank order; all-gather: copies).  One stream, so forks and
+// joins are moot.  The kernel steps go through plan_kernel — the very code the
+// RCCL interpreter (run_plan) launches — so this runs the N > 1 schedules'
+// device work on a one-GPU box, where RCCL refuses two ranks per device.
+namespace {
+
+struct LocalRank {
+    std::vector<ono_plan_step> plan;
+    size_t pc = 0;
+    PlanCtx ctx;
+    std::vector<void *> owned;
+};
+
+bool is_comm(int kind) {
+    return kind == ONO_PLAN_GROUP_BEGIN || kind == ONO_PLAN_ALLREDUCE || kind == ONO_PLAN_REDUCE_SCATTER ||
+           kind == ONO_PLAN_ALL_GATHER;
+}
+
+size_t dtype_size(int dtype) { return dtype == ONO_WIRE_F16 ? 2 : 4; }
+
+int run_local_step(LocalRank &R, const ono_plan_step &st, hipStream_t s) {
+    const PlanCtx &c = R.ctx;
+    switch (st.kind) {
+    case ONO_PLAN_KERNEL:
+        ONO_HIP(c.wire == ONO_WIRE_F16 && st.dtype == ONO_WIRE_F16 ? plan_kernel<uint16_t>(c, st, s)
+                                                                   : plan_kernel<float>(c, st, s));
+        return ONO_OK;
+    case ONO_PLAN_MEMSET:
+        ONO_HIP(hipMemsetAsync(plan_ptr(c, st, 0), 0, st.count * plan_esize(c, st.buf[0]), s));
+        return ONO_OK;
+    case ONO_PLAN_COPY:
+        ONO_HIP(hipMemcpyAsync(plan_ptr(c, st, 0), plan_ptr(c, st, 1), st.count * plan_esize(c, st.buf[0]),
+                               hipMemcpyDeviceToDevice, s));
+        return ONO_OK;
+    case ONO_PLAN_FORK:
+    case ONO_PLAN_JOIN:
+        return ONO_OK;
+    default:
+        return set_error(ONO_E_ARG, "plan step kind %d outside a group", st.kind);
+    }
+}
+
+int run_plans_local(std::vector<LocalRank> &ranks, hipStream_t s) {
+    const int n = (int)ranks.size();
+    for (;;) {
+        int done = 0;
+        for (LocalRank &R : ranks) {  // local work up to the next communication step
+            while (R.pc < R.plan.size() && !is_comm(R.plan[R.pc].kind)) {
+                int rc = run_local_step(R, R.plan[R.pc], s);
+                if (rc) return rc;
+                R.pc++;
+            }
+            if (R.pc == R.plan.size()) done++;
+        }
+        if (done == n) return ONO_OK;
+        if (done) return set_error(ONO_E_ARG, "plans end at different communication steps");
+        const int kind = ranks[0].plan[ranks[0].pc].kind;
+        for (LocalRank &R : ranks)
+            if (R.plan[R.pc].kind != kind) return set_error(ONO_E_ARG, "plans disagree on a communication step");
+        if (kind == ONO_PLAN_GROUP_BEGIN) {
+            struct P2P { int self, peer, k; const ono_plan_step *st; };
+            std::vector<P2P> sends, recvs;
+            for (int r = 0; r < n; r++) {
+                LocalRank &R = ranks[r];
+                std::vector<int> ns(n, 0), nr(n, 0);
+                for (R.pc++; R.pc < R.plan.size() && R.plan[R.pc].kind != ONO_PLAN_GROUP_END; R.pc++) {
+                    const ono_plan_step &st = R.plan[R.pc];
+                    if (st.peer < 0 || st.peer >= n) return set_error(ONO_E_ARG, "peer %d", st.peer);
+                    if (st.kind == ONO_PLAN_SEND) sends.push_back({r, st.peer, ns[st.peer]++, &st});
+                    else if (st.kind == ONO_PLAN_RECV) recvs.push_back({r, st.peer, nr[st.peer]++, &st});
+                    else return set_error(ONO_E_ARG, "step kind %d inside a group", st.kind);
+                }
+                if (R.pc == R.plan.size()) return set_error(ONO_E_ARG, "group without its end");
+                R.pc++;  // past GROUP_END
+            }
+            if (sends.size() != recvs.size()) return set_error(ONO_E_ARG, "unmatched sends / receives");
+            for (const P2P &rv : recvs) {
+                const P2P *sd = nullptr;
+                for (const P2P &x : sends)
+                    if (x.self == rv.peer && x.peer == rv.self && x.k == rv.k) { sd = &x; break; }
+                if (!sd || sd->st->count != rv.st->count || sd->st->dtype != rv.st->dtype)
+                    return set_error(ONO_E_ARG, "receive of rank %d from %d has no matching send", rv.self, rv.peer);
+                void *dst = plan_ptr(ranks[rv.self].ctx, *rv.st, 0);
+                const void *src = plan_ptr(ranks[sd->self].ctx, *sd->st, 0);
+                if (rv.st->count) ONO_HIP(hipMemcpyAsync(dst, src, rv.st->count * dtype_size(rv.st->dtype),
+                                                         hipMemcpyDeviceToDevice, s));
+            }
+            continue;
+        }
+        // collectives: f32, the sum over ranks in rank order
+        const size_t count = ranks[0].plan[ranks[0].pc].count;
+        std::vector<const float *> src(n);
+        for (int q = 0; q < n; q++) src[q] = static_cast<const float *>(plan_ptr(ranks[q].ctx, ranks[q].plan[ranks[q].pc], 0));
+        for (int r = 0; r < n; r++) {
+            const ono_plan_step &st = ranks[r].plan[ranks[r].pc];
+            float *dst = static_cast<float *>(plan_ptr(ranks[r].ctx, st, 1));
+            if (st.count != count) return set_error(ONO_E_ARG, "collective counts differ");
+            if (kind == ONO_PLAN_ALL_GATHER) {
+                for (int q = 0; q < n; q++)
+                    if (count) ONO_HIP(hipMemcpyAsync(dst + (size_t)q * count, src[q], count * 4, hipMemcpyDeviceToDevice, s));
+                continue;
+            }
+            std::vector<const float *> ins(n);
+            for (int q = 0; q < n; q++) ins[q] = src[q] + (kind == ONO_PLAN_REDUCE_SCATTER ? (size_t)r * count : 0);
+            if (n > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "%d ranks", n);
+            if (count) ONO_HIP(launch_sum_scale(dst, ins.data(), n, count, 1.0f, s));
+        }
+        for (LocalRank &R : ranks) R.pc++;
+    }
+}
+
+int alloc_plan_buffers(std::vector<LocalRank> &ranks, int n, size_t size, size_t nparams, int wire) {
+    uint64_t cnt[ONO_PB_COUNT];
+    plan_buffers(n, size, nparams, cnt);
+    for (LocalRank &R : ranks) {
+        R.ctx.wire = wire;
+        for (int b : {ONO_PB_WIRE0, ONO_PB_WIRE1, ONO_PB_RBUF, ONO_PB_GSTAGE, ONO_PB_MSG}) {
+            if (R.ctx.base[b]) continue;
+            void *p = nullptr;
+            const size_t bytes = std::max<size_t>(cnt[b] * plan_esize(R.ctx, b), 16);
+            ONO_HIP(hipMalloc(&p, bytes));
+            R.owned.push_back(p);
+            R.ctx.base[b] = p;
+        }
+    }
+    return ONO_OK;
+}
+
+void free_plan_buffers(std::vector<LocalRank> &ranks) {
+    for (LocalRank &R : ranks)
+        for (void *p : R.owned) (void)hipFree(p);
+}
+
+}  // namespace
+
 extern "C" {
+
+int ono_plan_run_local(int algo, int wire, int nranks, size_t size, int segments, float *const *residuals,
+                       float *const *grads, void *stream) {
+    if (!residuals || !grads || nranks < 1 || nranks > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "nranks must be in [1, %d]", ONO_MAX_INPUTS);
+    for (int r = 0; r < nranks; r++)
+        if (!residuals[r] || !grads[r]) return set_error(ONO_E_ARG, "NULL bucket for rank %d", r);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::vector<LocalRank> ranks(nranks);
+    for (int r = 0; r < nranks; r++) {
+        int rc = plan_pull_grads(ranks[r].plan, algo, wire, r, nranks, size, std::max(segments, 1));
+        if (rc) return rc;
+        ranks[r].ctx.base[ONO_PB_RESIDUAL] = residuals[r];
+        ranks[r].ctx.base[ONO_PB_GRAD] = grads[r];
+    }
+    int rc = alloc_plan_buffers(ranks, nranks, size, 0, wire);
+    if (!rc) rc = run_plans_local(ranks, s);
+    const hipError_t e = hipStreamSynchronize(s);  // the scratch is freed below
+    free_plan_buffers(ranks);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_error(e, "local plans", __FILE__, __LINE__);
+    return ONO_OK;
+}
+
+int ono_plan_run_local_ps(int nranks, size_t nparams, const float *const *grads, float *const *params,
+                          float *const *shards, float *const *v, float *const *s_, const ono_opt_spec *opt,
+                          float step_size, void *stream) {
+    if (!grads || !params || !shards || !opt || nranks < 2 || nranks > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "bad arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t n = (size_t)nranks, C = (nparams + n - 1) / n;
+    OptLaunch o{opt->kind, opt->lr, opt->momentum, opt->beta1, opt->beta2, opt->eps, step_size, (float)nranks};
+    std::vector<LocalRank> ranks(nranks);
+    std::vector<void *> pads;
+    int rc = ONO_OK;
+    for (int r = 0; r < nranks && !rc; r++) {
+        LocalRank &R = ranks[r];
+        rc = plan_ps_step(R.plan, r, nranks, nparams);
+        R.ctx.base[ONO_PB_GIN] = const_cast<float *>(grads[r]);
+        R.ctx.base[ONO_PB_PARAMS] = params[r];
+        R.ctx.opt = &o;
+        R.ctx.v = v ? v[r] : nullptr;
+        R.ctx.s = s_ ? s_[r] : nullptr;
+        // the padded copies: GPAD zero-filled, PPAD holding every shard (rank r's current shard at r C)
+        void *gpad = nullptr, *ppad = nullptr, *gsh = nullptr;
+        if (!rc && hipMalloc(&gpad, C * n * 4) == hipSuccess) pads.push_back(gpad); else rc = rc ? rc : ONO_E_HIP;
+        if (!rc && hipMalloc(&ppad, C * n * 4) == hipSuccess) pads.push_back(ppad); else rc = rc ? rc : ONO_E_HIP;
+        if (!rc && hipMalloc(&gsh, C * 4) == hipSuccess) pads.push_back(gsh); else rc = rc ? rc : ONO_E_HIP;
+        if (!rc && (hipMemsetAsync(gpad, 0, C * n * 4, s) != hipSuccess || hipMemsetAsync(ppad, 0, C * n * 4, s) != hipSuccess))
+            rc = ONO_E_HIP;
+        const size_t lo = std::min(nparams, (size_t)r * C), len = std::min(nparams, lo + C) - lo;
+        if (!rc && len && hipMemcpyAsync(static_cast<float *>(ppad) + (size_t)r * C, shards[r], len * 4,
+                                         hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = ONO_E_HIP;
+        R.ctx.base[ONO_PB_GPAD] = gpad;
+        R.ctx.base[ONO_PB_PPAD] = ppad;
+        R.ctx.base[ONO_PB_GSHARD] = gsh;
+    }
+    if (rc == ONO_E_HIP) set_error(ONO_E_HIP, "local PS plan scratch");
+    if (!rc) rc = run_plans_local(ranks, s);
+    for (int r = 0; r < nranks && !rc; r++) {  // the updated shard back to the caller's state
+        const size_t lo = std::min(nparams, (size_t)r * C), len = std::min(nparams, lo + C) - lo;
+        if (len && hipMemcpyAsync(shards[r], static_cast<float *>(ranks[r].ctx.base[ONO_PB_PPAD]) + (size_t)r * C,
+                                  len * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = set_error(ONO_E_HIP, "shard copy-back");
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    for (void *p : pads) (void)hipFree(p);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_error(e, "local PS plans", __FILE__, __LINE__);
+    return ONO_OK;
+}
 
 int ono_local_direct_pull_grads(float *const *residuals, float *const *grads, int nranks, size_t n,
                                 int wire, void *stream) {

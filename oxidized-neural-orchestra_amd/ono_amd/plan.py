@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 
 from ._lib import ALGO, WIRE, PlanStep, call
+from . import kernels
 
 KIND = ("group_begin", "send", "recv", "group_end", "allreduce", "reduce_scatter", "all_gather", "kernel",
         "memset", "copy", "fork", "join")
@@ -43,3 +44,27 @@ def buffers(nranks: int, size: int, nparams: int = 0) -> dict:
     c = (C.c_uint64 * len(BUF))()
     call("ono_plan_buffers", nranks, size, nparams, c)
     return {BUF[i]: int(c[i]) for i in range(len(BUF))}
+
+
+def _ptrs(ts):
+    return (C.c_void_p * len(ts))(*[kernels.f32_ptr(t) for t in ts])
+
+
+def run_local(algo: str, wire: str, residuals, grads, segments: int = 1, stream=None) -> None:
+    """Every rank's pull_grads plan run by co-resident ranks on one device
+    (ono_plan_run_local): the N > 1 schedules' device work without RCCL."""
+    n = len(residuals)
+    size = residuals[0].numel()
+    call("ono_plan_run_local", ALGO[algo], WIRE[wire], n, size, segments, _ptrs(residuals), _ptrs(grads),
+         kernels.stream_handle(stream))
+
+
+def run_local_ps(grads, params, shards, opt, step_size: float = 0.0, v=None, s=None, stream=None) -> None:
+    """ono_ps_step's plan for co-resident ranks (ono_plan_run_local_ps); opt
+    is an ono_amd optimizer (its spec()), shards / v / s are per-rank shard
+    tensors updated in place."""
+    n = len(grads)
+    nul = (C.c_void_p * n)()
+    call("ono_plan_run_local_ps", n, grads[0].numel(), _ptrs(grads), _ptrs(params), _ptrs(shards),
+         _ptrs(v) if v is not None else nul, _ptrs(s) if s is not None else nul, C.byref(opt.spec()),
+         float(step_size), kernels.stream_handle(stream))
