@@ -422,8 +422,9 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
 def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     """the device top-k codec (comms/src/sparse/protocol.rs:57-144) on a 64 MiB
     gradient with the threshold at the 90th |g| percentile (~10 % of the values kept, the
-    reference's r = 0.9).  Drop = count pass + scan + write pass + headers, a blocking call (the
-    wire length is needed on the host); bytes = 4 N read + the wire written.  Lift parses the
+    reference's r = 0.9).  Drop = tile images + record scan + move, as a blocking call (the wire
+    length is needed on the host) and stream-ordered back to back; bytes = 4 N read + the wire
+    written.  Lift parses the
     run headers on the host and expands on the device (host buffer in)."""
     import ctypes as C
 
@@ -451,6 +452,20 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
             tev.append(a.elapsed_time(b) * 1e-3)
     td, tdev = sorted(ts)[len(ts) // 2], sorted(tev)[len(tev) // 2]
     wire = bytes(buf[: nb.value].cpu().numpy())
+    # stream-ordered drops back to back (ono_sparse_drop_async: the wire length stays in HBM), one
+    # event pair around K of them: the encoder's own time per drop, without the host round trip
+    nbd = torch.zeros(1, dtype=torch.int64, device="cuda")
+    K = 20
+    ono_amd.sparse.grad_drop_async(g, t, buf, nbd)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(K):
+        ono_amd.sparse.grad_drop_async(g, t, buf, nbd)
+    b.record(stream)
+    b.synchronize()
+    tstream = a.elapsed_time(b) * 1e-3 / K
+    assert int(nbd.item()) == len(wire) and bytes(buf[: len(wire)].cpu().numpy()) == wire
     tl = []
     for r in range(rounds + 1):
         t0 = time.perf_counter()
@@ -487,8 +502,13 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
             "drop": {"ms": round(td * 1e3, 3), "device_ms": round(tdev * 1e3, 3), "algorithmic_bytes": drop_bytes,
                      "achieved_gbs": round(drop_bytes / tdev / 1e9, 1),
                      "frac_of_hbm_peak": round(drop_bytes / tdev / 1e9 / HBM_PEAK_GBS, 4),
+                     "stream_ms": round(tstream * 1e3, 4),
+                     "stream_achieved_gbs": round(drop_bytes / tstream / 1e9, 1),
+                     "stream_frac_of_hbm_peak": round(drop_bytes / tstream / 1e9 / HBM_PEAK_GBS, 4),
                      "note": "ms = wall time of the blocking C call; device_ms = HIP events around it on its "
-                             "stream (count + tile scan + write + headers, then the host read of the totals)"},
+                             "stream (tile images + record scan + move, then the host read of the totals); "
+                             "stream_ms = per drop of %d stream-ordered drops back to back "
+                             "(ono_sparse_drop_async), one event pair" % K},
             "lift": {"ms": round(lt * 1e3, 3), "note": "host wire buffer in (Python bytes): H2D + device parse + "
                                                         "expand, wall time through the Python wrapper"},
             "lift_dev": {"ms": round(dlt * 1e3, 3), "device_ms": round(dlt_ev * 1e3, 3),

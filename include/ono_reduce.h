@@ -137,6 +137,13 @@ int ono_sparse_threshold(float *t_out, const float *g_dev, size_t n, const uint3
 int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t amount);
 int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
                     float threshold, void *stream);
+/* The stream-ordered drop: the same bytes, nothing waits on the host; the
+ * wire length lands in *nbytes_dev (device or host-mapped u64) when the
+ * stream reaches it.  cap must be ono_sparse_max_bytes(n) (ONO_E_SIZE
+ * otherwise).  For a device-side consumer of the stream (an RCCL send of the
+ * frame, a device lift) and for back-to-back timing.                      */
+int ono_sparse_drop_async(uint8_t *buf_dev, size_t cap, uint64_t *nbytes_dev, const float *g_dev, size_t n,
+                          float threshold, void *stream);
 int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
                     void *stream);
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame

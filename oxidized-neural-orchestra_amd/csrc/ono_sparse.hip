@@ -11,10 +11,11 @@
 // and run j (starting at s_j) has its header 8 bytes earlier, with
 //   offset_j = U(s_j) - U(s_{j-1}),  U(i) = i - F(i)  (unkept values before i)
 //   len_j    = F(s_{j+1}) - F(s_j)   (F_total for the last run).
-// Four launches: per-tile counts -> tile scan -> write (block-wide scan with
-// wave shuffles + LDS; values written, run starts record U and F) -> headers,
-// back to back on the stream (the totals stay on the device; the host reads
-// them once, at the end, for the wire length).
+// Three launches (see "encoder" below): each tile's byte range built in LDS
+// and written to a scratch slot -> one scan of the tile records -> each slot
+// moved to its place with the two cross-tile header fields completed.  g is
+// read once; the totals stay on the device (the blocking form reads them once,
+// at the end, for the wire length; the stream-ordered form leaves it in HBM).
 // Decoding is a parallel parse on the device (the record stream is a linked
 // list: each header gives the next one's position), see "Lift" below; the
 // reference's sequential parse on the host remains as the exact fallback and
@@ -25,6 +26,7 @@
 #include <cmath>
 #include <cstring>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -37,6 +39,7 @@ namespace {
 constexpr int kSB = 256;             // threads per block (4 waves)
 constexpr int kEPT = 8;              // elements per thread
 constexpr int kTile = kSB * kEPT;    // 2048 elements per tile
+constexpr int kIT = 128, kIE = kTile / kIT;  // the encoder's tile: 2 waves x 16 values per thread
 
 // half 2.7.1 conversions = the gfx950 cvt instructions, NaN rules included (ono_kernels.hip to_f16)
 __device__ __forceinline__ uint16_t to_f16_sp(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
@@ -45,43 +48,38 @@ __device__ __forceinline__ float from_f16_sp(uint16_t b) { return (float)__built
 // g.abs() >= threshold (NaN never kept, as in Rust)
 __device__ __forceinline__ bool kept(float x, float t) { return fabsf(x) >= t; }
 
-// Flags of a thread's kEPT elements: bit e = kept, plus whether each starts a run.
-// NTL: the count pass loads g plainly so the 64 MiB bucket stays in the Infinity
-// Cache for the write pass, whose nt loads are its last use (70 -> 66 us).
-// The kEPT = 8 values come in as two 16-B loads (g is 16-B aligned on the fast
-// path; `vec` = false uses scalar loads); whether the element before the
-// thread's first one is kept comes from the neighbouring lane (a shuffle), and
-// only lane 0 of each wave reads it from memory.
+// Keep flags of a thread's E values and which of them start a run (the
+// element before the thread's first one is the previous lane's last, taken by
+// a shuffle; lane 0 has it loaded).
 struct Bits {
     uint32_t keep = 0, start = 0;
 };
 typedef float f4s __attribute__((ext_vector_type(4)));
-template <bool NTL>
-__device__ __forceinline__ Bits thread_bits(const float *g, size_t n, float t, size_t base, bool vec,
-                                            float (&x)[kEPT]) {
+
+// The value of lane - 1 (DPP wave_shr:1; lane 0 gets 0): no LDS round trip.
+__device__ __forceinline__ uint32_t lane_before(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+// Inclusive sum over lanes 0..l, all DPP (row_shr 1 / 2 / 4 / 8 within rows
+// of 16, then row_bcast 15 and 31 across rows): six VALU adds.
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+template <int E>
+__device__ __forceinline__ Bits flags_of(const float (&x)[E], float before, size_t n, float t, size_t base) {
     Bits b;
-    if (vec && base + kEPT <= n) {
-        f4s a, c;
-        if constexpr (NTL) {
-            a = __builtin_nontemporal_load((const f4s *)(g + base));
-            c = __builtin_nontemporal_load((const f4s *)(g + base + 4));
-        } else {
-            a = *(const f4s *)(g + base);
-            c = *(const f4s *)(g + base + 4);
-        }
-        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
-    } else {
 #pragma unroll
-        for (int e = 0; e < kEPT; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
-    }
-#pragma unroll
-    for (int e = 0; e < kEPT; e++)
+    for (int e = 0; e < E; e++)
         if (base + e < n && kept(x[e], t)) b.keep |= 1u << e;
-    // kept(element base-1): the previous lane's last flag; lane 0 loads it
-    const int lane = threadIdx.x & 63;
-    uint32_t last = (b.keep >> (kEPT - 1)) & 1u;
-    uint32_t prev = __shfl_up(last, 1, 64);
-    if (lane == 0) prev = base > 0 && base - 1 < n ? (kept(g[base - 1], t) ? 1u : 0u) : 0u;
+    const uint32_t last = (b.keep >> (E - 1)) & 1u;
+    uint32_t prev = lane_before(last);
+    if ((threadIdx.x & 63) == 0) prev = base > 0 && base - 1 < n && kept(before, t) ? 1u : 0u;
     b.start = b.keep & ~((b.keep << 1) | prev);
     return b;
 }
@@ -113,56 +111,6 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
     eb = pb + ib - b;
 }
 
-// The same scan for the per-thread counts of the count / write passes, which
-// are small (kept <= 8, run starts <= 4 of a thread's 8 elements): each bit
-// plane of the count is one wave ballot, and mbcnt counts the set bits below
-// the lane — an exact exclusive wave scan with no cross-lane data movement
-// (7 ballots instead of 12 ds_bpermute round trips of the shuffle ladder).
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-template <int BITS>
-__device__ __forceinline__ void wave_scan_small(uint32_t v, uint32_t &ex, uint32_t &tot) {
-    ex = 0;
-    tot = 0;
-#pragma unroll
-    for (int b = 0; b < BITS; b++) {
-        const uint64_t m = __ballot((v >> b) & 1u);
-        ex += mbcnt64(m) << b;
-        tot += (uint32_t)__popcll(m) << b;
-    }
-}
-__device__ __forceinline__ void block_scan_counts(uint32_t a, uint32_t b, uint32_t &ea, uint32_t &eb, uint32_t &ta,
-                                                  uint32_t &tb) {
-    __shared__ uint32_t wa[kSB / 64], wb[kSB / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t xa, xb, sa, sb;
-    wave_scan_small<4>(a, xa, sa);  // a <= kEPT = 8
-    wave_scan_small<3>(b, xb, sb);  // b <= kEPT / 2 = 4
-    if (lane == 0) { wa[wave] = sa; wb[wave] = sb; }
-    __syncthreads();
-    uint32_t pa = 0, pb = 0;
-    ta = 0;
-    tb = 0;
-#pragma unroll
-    for (int w = 0; w < kSB / 64; w++) {
-        if (w < wave) { pa += wa[w]; pb += wb[w]; }
-        ta += wa[w];
-        tb += wb[w];
-    }
-    ea = pa + xa;
-    eb = pb + xb;
-}
-static_assert(kEPT == 8, "block_scan_counts sizes its bit planes for 8 elements per thread");
-
-__global__ __launch_bounds__(kSB) void sp_count(const float *g, size_t n, float t, uint32_t *tileF, uint32_t *tileS,
-                                                bool vec) {
-    float x[kEPT];
-    Bits b = thread_bits<false>(g, n, t, (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT, vec, x);
-    uint32_t ea, eb, ta, tb;
-    block_scan_counts(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
-    if (threadIdx.x == 0) { tileF[blockIdx.x] = ta; tileS[blockIdx.x] = tb; }
-}
 
 // Exclusive scan of the tile counts in place, one block of kScanT threads,
 // in chunks of kScanT x kScanPer tiles staged through LDS: coalesced global
@@ -209,76 +157,388 @@ __global__ __launch_bounds__(kScanT) void sp_scan_tiles(uint32_t *tileF, uint32_
     if (threadIdx.x == 0) { totals[0] = carry[0]; totals[1] = carry[1]; }
 }
 
-// A tile's output is one contiguous byte range of the wire, from
-// 8 + 8 S0 + 2 F0 to 8 + 8 (S0 + runs) + 2 (F0 + kept) (S0, F0: the tile's
-// prefix).  Values are placed in an LDS image of that range first, then the
-// block writes the range out with consecutive 2-byte stores (coalesced,
-// instead of one scattered store per kept value).  Header slots in the image
-// are left as they are; sp_headers writes them afterwards.
-constexpr int kStageU16 = (8 * (kTile / 2 + 1) + 2 * kTile) / 2;  // worst case: alternating kept/unkept
-__global__ __launch_bounds__(kSB) void sp_write(const float *g, size_t n, float t, const uint32_t *tileF,
-                                                const uint32_t *tileS, uint8_t *buf, uint32_t *RU, uint32_t *RF,
-                                                bool vec) {
-    __shared__ uint16_t stage[kStageU16];
-    __shared__ uint32_t su[kTile / 2 + 1], sf[kTile / 2 + 1];  // the tile's run table rows
-    const size_t base = (size_t)blockIdx.x * kTile + (size_t)threadIdx.x * kEPT;
-    float x[kEPT];  // the values stay in registers from the flag pass (g is read once here)
-    Bits b = thread_bits<true>(g, n, t, base, vec, x);
-    uint32_t ea, eb, ta, tb;
-    block_scan_counts(__popc(b.keep), __popc(b.start), ea, eb, ta, tb);
-    const uint32_t F0 = tileF[blockIdx.x], S0 = tileS[blockIdx.x];
-    uint32_t f = ea, sl = eb;  // this thread's kept values / runs before it, within the tile
-    if (b.keep) {
-#pragma unroll
-        for (int e = 0; e < kEPT; e++) {
-            if (!(b.keep >> e & 1u)) continue;
-            if (b.start >> e & 1u) {
-                const size_t i = base + e;
-                su[sl] = (uint32_t)(i - (F0 + f));  // U(s_j): unkept values before the run
-                sf[sl] = F0 + f;                    // F(s_j)
-                sl++;
-            }
-            stage[4 * sl + f] = to_f16_sp(x[e]);  // byte 8 sl + 2 f of the tile's range
-            f++;
-        }
+// ------------------------------------------------------------- encoder ----
+// Three launches, g read once:
+//  1. sp_image, one workgroup per 2048-value tile: flags, a block scan of the
+//     per-thread counts, and the tile's byte range of the wire built in LDS —
+//     its values, and its run headers with every field that the tile alone
+//     determines — then written to the tile's slot of a scratch image, plus a
+//     16-B record {kept | runs << 16, last kept index + 1, first unkept index,
+//     first / last header position}.
+//  2. sp_scan_rec, one workgroup: exclusive prefix sums of kept and runs (the
+//     tile's place in the wire), the exclusive prefix max of "last kept + 1"
+//     (where the run before the tile's first run ended) and the exclusive
+//     suffix min of "first unkept" (where a run still open at the tile's end
+//     ends).
+//  3. sp_move, one wave per tile: the slot to its place in the wire (2-B
+//     aligned), with the two header fields that depend on other tiles
+//     completed on the way: the first run's offset and the last run's length.
+// The first run's offset is U_local(s_0) + (tile start - P) and the last run's
+// length is (kept from s_last to the tile's end) + (Q - tile end) when the
+// tile's last value is kept (P: last kept index + 1 before the tile, 0 if
+// none; Q: first unkept index after the tile, n if none): a run's offset is
+// the gap since the previous run's end, its length the distance to the first
+// unkept value after its start.
+constexpr int kSlotU16 = 5128;  // the largest tile image, 3 S + 2049 <= 5121 units (S <= 1024), padded to 16 B
+static_assert((kSlotU16 * 2) % 16 == 0, "slots are 16-B aligned");
+
+// Block-wide scans over the threads of a tile (tile-local indices): the
+// exclusive prefix of (kept, runs), the last kept index + 1 before the thread
+// (0: none) and the first unkept index after it (kTile: none), and the tile's
+// totals, last kept + 1 and first unkept — one LDS exchange of wave totals.
+struct TileScan {
+    uint32_t ef, es;              // this thread's exclusive prefix
+    uint32_t tf, ts;              // tile totals
+    uint32_t kept1_before, unkept_after;
+    uint32_t last_kept1, first_unkept;
+};
+__device__ __forceinline__ TileScan tile_scan(uint32_t keep, uint32_t start, uint32_t unkept) {
+    __shared__ uint32_t wf[kIT / 64], ws[kIT / 64], wl[kIT / 64], wu[kIT / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lo = threadIdx.x * kIE;
+    // kept and run starts packed in one word (a wave holds < 2^16 of each):
+    // one DPP scan for both
+    const uint32_t own = __popc(keep) | __popc(start) << 16;
+    const uint32_t inc = wave_incl_sum_dpp(own), exc = inc - own;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    const uint32_t xf = exc & 0xFFFFu, xs = exc >> 16, sf = tot & 0xFFFFu, ss = tot >> 16;
+    // the nearest lane below with a kept value / above with an unkept one:
+    // one ballot and one lane-indexed shuffle each (no scan ladder)
+    const uint32_t k1 = keep ? lo + 32u - __clz(keep) : 0u;                  // last kept + 1 in the thread
+    const uint32_t u1 = unkept ? lo + (uint32_t)(__ffs(unkept) - 1) : kTile;  // first unkept in the thread
+    const uint64_t mk = __ballot(keep != 0), mu = __ballot(unkept != 0);
+    const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
+    const uint64_t kbm = mk & below, uam = mu & above;
+    const int lk = kbm ? 63 - __clzll((long long)kbm) : 0, lu = uam ? __ffsll((unsigned long long)uam) - 1 : 0;
+    const uint32_t ykb = __shfl(k1, lk, 64), yua = __shfl(u1, lu, 64);
+    const uint32_t kb = kbm ? ykb : 0u, ua = uam ? yua : (uint32_t)kTile;
+    const uint32_t wk = __shfl(k1, mk ? 63 - __clzll((long long)mk) : 0, 64);  // all lanes shuffle
+    const uint32_t wuu = __shfl(u1, mu ? __ffsll((unsigned long long)mu) - 1 : 0, 64);
+    if (lane == 0) {  // wave totals
+        wf[wave] = sf;
+        ws[wave] = ss;
+        wl[wave] = mk ? wk : 0u;
+        wu[wave] = mu ? wuu : (uint32_t)kTile;
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < tb; k += kSB) {  // run table rows, coalesced
-        RU[S0 + k] = su[k];
-        RF[S0 + k] = sf[k];
+    TileScan r{xf, xs, 0, 0, kb, ua, 0, kTile};
+#pragma unroll
+    for (int w = 0; w < kIT / 64; w++) {
+        if (w < wave) { r.ef += wf[w]; r.es += ws[w]; r.kept1_before = max(r.kept1_before, wl[w]); }
+        if (w > wave) r.unkept_after = min(r.unkept_after, wu[w]);
+        r.tf += wf[w];
+        r.ts += ws[w];
+        r.last_kept1 = max(r.last_kept1, wl[w]);
+        r.first_unkept = min(r.first_unkept, wu[w]);
     }
-    // the range, 4 bytes per store where aligned (it starts 2-B aligned)
-    const uint32_t nu16 = 4 * tb + ta;  // the range's length in 2-byte units
-    uint16_t *dst = (uint16_t *)(buf + 8 + 8 * (size_t)S0 + 2 * (size_t)F0);
-    const uint32_t h = (uint32_t)(((uintptr_t)dst >> 1) & 1u) < nu16 ? (uint32_t)(((uintptr_t)dst >> 1) & 1u) : nu16;
-    if (threadIdx.x == 0 && h) dst[0] = stage[0];
-    const uint32_t npair = (nu16 - h) / 2;
-    uint32_t *d32 = (uint32_t *)(dst + h);
-    for (uint32_t k = threadIdx.x; k < npair; k += kSB)
-        d32[k] = (uint32_t)stage[h + 2 * k] | (uint32_t)stage[h + 2 * k + 1] << 16;
-    if (threadIdx.x == 0 && h + 2 * npair < nu16) dst[nu16 - 1] = stage[nu16 - 1];
+    return r;
+}
+static_assert(kIE == 16, "tile_scan sizes its bit planes for 16 elements per thread");
+
+// One workgroup per tile: flags, the block scans, then the tile's byte range
+// in LDS — each kept value at 8 S + 2 F, each run's header by the thread that
+// holds its start (offset = start - end of the previous run, length = first
+// unkept after it - start, both tile-local; a run open at either tile edge is
+// completed by sp_move) — and out to the tile's slot.  Records: recA = {kept
+// | runs << 16, last kept + 1 | first unkept << 16} (what the scan needs),
+// recB = {first header | last header << 16, the first run's offset | the
+// last run's length << 16} (what the move completes).
+__global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float t, bool vec, uint16_t *img,
+                                                uint2 *recA, uint2 *recB, int var) {
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
+    __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
+    const size_t tile = blockIdx.x, tile0 = tile * kTile;
+    const uint32_t lo = threadIdx.x * kIE;  // the thread's first element, tile-local
+    const size_t base = tile0 + lo;
+    float x[kIE], before = 0.0f;
+    if ((threadIdx.x & 63) == 0 && base > 0 && base - 1 < n) before = g[base - 1];  // issued with the values
+    if (vec && base + kIE <= n) {  // four 16-B loads per thread: 2 KiB per wave in flight
+#pragma unroll
+        for (int q = 0; q < kIE / 4; q++) {
+            const f4s a = (var & 4) ? *((const f4s *)(g + base) + q) : __builtin_nontemporal_load((const f4s *)(g + base) + q);
+            x[4 * q] = a.x; x[4 * q + 1] = a.y; x[4 * q + 2] = a.z; x[4 * q + 3] = a.w;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < kIE; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
+    }
+    const Bits b = flags_of(x, before, n, t, base);
+    const uint32_t valid = base >= n ? 0u : (n - base >= (size_t)kIE ? 0xFFFFu : (1u << (n - base)) - 1u);
+    const uint32_t unk = valid & ~b.keep;
+    const TileScan ts = tile_scan(b.keep, b.start, unk);
+    const uint32_t R = ts.ts, F = ts.tf;
+    const uint32_t tend_l = (uint32_t)min((size_t)kTile, n - tile0);
+    // the values: one store per element, branch-free — to byte 8 S + 2 F of
+    // the tile's range when kept, else to this thread's spare unit past the
+    // image (no exec-mask branches around 16 conditional stores)
+    if (!(var & 2)) {
+#pragma unroll
+        for (int e = 0; e < kIE; e++) {
+            const uint32_t f = ts.ef + __popc(b.keep & ((1u << e) - 1u));
+            const uint32_t sl = ts.es + __popc(b.start & ((2u << e) - 1u));  // runs started at or before e
+            const uint32_t pos = (b.keep >> e & 1u) ? 4 * sl + f : (uint32_t)kSlotU16 + 2 * threadIdx.x;
+            stage[pos] = to_f16_sp(x[e]);
+        }
+    }
+    // the headers: a loop over this thread's run starts (offset = start - end
+    // of the previous run, length = first unkept after it - start, both
+    // tile-local; runs open at a tile edge are completed by sp_move).  The
+    // stores are volatile LDS stores so that they stay 2-byte stores: merged
+    // into wider ones they would be unaligned LDS accesses.
+    typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
+    lds_u16 *vst = (lds_u16 *)stage;
+    for (uint32_t m = b.start; m; m &= m - 1u) {
+        const int e = __ffs(m) - 1;
+        const uint32_t below = (1u << e) - 1u;
+        const uint32_t f = ts.ef + __popc(b.keep & below), sl = ts.es + __popc(b.start & below);
+        const uint32_t mk = b.keep & below, mu = unk & ~((2u << e) - 1u);
+        const uint32_t prev_end = mk ? lo + 32u - __clz(mk) : ts.kept1_before;
+        const uint32_t next_unkept =
+            mu ? lo + (uint32_t)(__ffs(mu) - 1) : (ts.unkept_after < (uint32_t)kTile ? ts.unkept_after : tend_l);
+        const uint32_t off = lo + e - prev_end, len = next_unkept - (lo + e);
+        const uint32_t p = 4 * sl + f;  // the header, 8 bytes before the run's first value
+        vst[p] = (uint16_t)off;
+        vst[p + 1] = 0;
+        vst[p + 2] = (uint16_t)len;
+        vst[p + 3] = 0;
+        if (sl == 0) rb[0] = p | off << 16;
+        if (sl == R - 1) rb[1] = p | len << 16;
+    }
+    __syncthreads();
+    const uint32_t nu16 = 4 * R + F;
+    uint4 *slot = (uint4 *)(img + tile * kSlotU16);
+    const uint4 *st4 = (const uint4 *)stage;
+    if (!(var & 1))
+        for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) slot[k] = st4[k];
+    if (threadIdx.x == 0) {
+        recA[tile] = make_uint2(F | R << 16, ts.last_kept1 | ts.first_unkept << 16);
+        recB[tile] = R ? make_uint2((rb[0] & 0xFFFFu) | rb[1] << 16, rb[0] >> 16 | (rb[1] & 0xFFFF0000u))
+                       : make_uint2(0u, 0u);
+    }
 }
 
-// R and the kept total come from the device totals (no host round trip); a
-// grid-stride loop sized for the worst case idles past R.
-__global__ __launch_bounds__(kSB) void sp_headers(const uint32_t *RU, const uint32_t *RF, const uint64_t *totals,
-                                                  uint64_t total_len, uint8_t *buf, uint64_t *host_tot) {
-    const size_t R = totals[1];
-    const uint32_t Ftot = (uint32_t)totals[0];
+// Inclusive wave scans over 64 lanes: sum, max (forward) and min (backward).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= d) v = max(v, y);
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_min_rev(uint32_t v) {  // min over this lane and the ones above
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_down(v, d, 64);
+        if (lane + d < 64) v = min(v, y);
+    }
+    return v;
+}
+
+// recA -> pre = {F0, S0, P, Q} per tile (F0 / S0: kept values / runs before
+// the tile; P: last kept index + 1 before it, 0 if none; Q: first unkept
+// index after it, n if none); totals = {kept, runs}.  One workgroup of
+// kScanRecT threads, kScanRecPer consecutive tiles per thread, chunks of
+// kScanRecChunk tiles staged through LDS (coalesced 8-B record loads, 16-B
+// result stores); forward over the chunks (sums, max), then backward (min) —
+// one load and one store per record when the tiles fit one chunk (n <= 2^24).
+constexpr int kScanRecT = 1024, kScanRecPer = 8, kScanRecChunk = kScanRecT * kScanRecPer;
+__global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, size_t ntiles, uint32_t n,
+                                                         uint64_t *totals) {
+    __shared__ uint32_t la[kScanRecChunk], lb[kScanRecChunk], lp[kScanRecChunk], lq[kScanRecChunk];
+    __shared__ uint32_t wa[kScanRecT / 64], wb[kScanRecT / 64], wc[kScanRecT / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lo = threadIdx.x * kScanRecPer;
+    const size_t nch = (ntiles + kScanRecChunk - 1) / kScanRecChunk;
+    const bool single = nch == 1;
+    uint32_t cf = 0, cs = 0, cp = 0;  // carries from the earlier chunks
+    for (size_t c = 0; c < nch; c++) {
+        const size_t c0 = c * kScanRecChunk;
+        const uint32_t m = (uint32_t)min((size_t)kScanRecChunk, ntiles - c0);
+        for (uint32_t i = threadIdx.x; i < kScanRecChunk; i += kScanRecT) {
+            const uint2 r = i < m ? recA[c0 + i] : make_uint2(0u, (uint32_t)kTile << 16);
+            la[i] = r.x;
+            lb[i] = r.y;
+        }
+        __syncthreads();
+        uint32_t sumf = 0, sums = 0, mx = 0;
+        uint32_t lk[kScanRecPer];
+#pragma unroll
+        for (int k = 0; k < kScanRecPer; k++) {
+            const uint32_t a = la[lo + k], l1 = lb[lo + k] & 0xFFFFu;
+            sumf += a & 0xFFFFu;
+            sums += a >> 16;
+            lk[k] = l1 ? (uint32_t)((c0 + lo + k) * kTile) + l1 : 0u;  // global last kept + 1
+            mx = max(mx, lk[k]);
+        }
+        const uint32_t i_f = wave_incl_sum(sumf), i_s = wave_incl_sum(sums), i_m = wave_incl_max(mx);
+        if (lane == 63) { wa[wave] = i_f; wb[wave] = i_s; wc[wave] = i_m; }
+        __syncthreads();
+        uint32_t pf = cf, ps = cs, pm = cp, tf = 0, tsum = 0, tm = 0;
+#pragma unroll
+        for (int w = 0; w < kScanRecT / 64; w++) {
+            if (w < wave) { pf += wa[w]; ps += wb[w]; pm = max(pm, wc[w]); }
+            tf += wa[w];
+            tsum += wb[w];
+            tm = max(tm, wc[w]);
+        }
+        pf += i_f - sumf;  // exclusive, within the wave
+        ps += i_s - sums;
+        const uint32_t wprev = __shfl_up(i_m, 1, 64);
+        if (lane) pm = max(pm, wprev);
+#pragma unroll
+        for (int k = 0; k < kScanRecPer; k++) {  // own entries only: no hazard with other threads
+            const uint32_t a = la[lo + k];
+            la[lo + k] = pf;
+            lp[lo + k] = ps;
+            lq[lo + k] = pm;
+            pf += a & 0xFFFFu;
+            ps += a >> 16;
+            pm = max(pm, lk[k]);
+        }
+        cf += tf;
+        cs += tsum;
+        cp = max(cp, tm);
+        __syncthreads();
+        if (!single)
+            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i] = make_uint4(la[i], lp[i], lq[i], 0u);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { totals[0] = cf; totals[1] = cs; }
+    uint32_t cq = n;  // min of first-unkept over the tiles of the later chunks
+    for (size_t c = nch; c-- > 0;) {
+        const size_t c0 = c * kScanRecChunk;
+        const uint32_t m = (uint32_t)min((size_t)kScanRecChunk, ntiles - c0);
+        if (!single) {
+            for (uint32_t i = threadIdx.x; i < kScanRecChunk; i += kScanRecT)
+                lb[i] = i < m ? recA[c0 + i].y : (uint32_t)kTile << 16;
+            __syncthreads();
+        }
+        uint32_t fu[kScanRecPer], mn = n;
+#pragma unroll
+        for (int k = 0; k < kScanRecPer; k++) {
+            const uint32_t f1 = lb[lo + k] >> 16;
+            fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + lo + k) * kTile) + f1 : n;
+            mn = min(mn, fu[k]);
+        }
+        const uint32_t i_m = wave_incl_min_rev(mn);
+        if (lane == 0) wa[wave] = i_m;
+        __syncthreads();
+        uint32_t q = cq, tq = n;
+#pragma unroll
+        for (int w = 0; w < kScanRecT / 64; w++) {
+            if (w > wave) q = min(q, wa[w]);
+            tq = min(tq, wa[w]);
+        }
+        const uint32_t wnext = __shfl_down(i_m, 1, 64);
+        if (lane < 63) q = min(q, wnext);
+#pragma unroll
+        for (int k = kScanRecPer - 1; k >= 0; k--) {
+            lb[lo + k] = q;
+            q = min(q, fu[k]);
+        }
+        cq = min(cq, tq);
+        __syncthreads();
+        if (single) {
+            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i] = make_uint4(la[i], lp[i], lq[i], lb[i]);
+        } else {
+            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i].w = lb[i];
+        }
+        __syncthreads();
+    }
+}
+
+// One tile's slot -> its place in the wire: nu16 units to byte 8 + 8 S0 +
+// 2 F0, u32 stores inside the range and u16 stores at its ends (neighbouring
+// tiles share those words), the two cross-tile header fields completed on the
+// way.  v: the slot's first 64 * kMoveBatch words, already loaded (lane l
+// holds words l + 64 k).
+constexpr int kMoveBatch = 8;  // words per lane per batch: 1024 units per wave
+__device__ __forceinline__ void move_tile(const uint32_t *src32, uint32_t (&v)[kMoveBatch], uint32_t nu16, uint32_t R,
+                                          uint32_t c0, uint32_t hl, uint32_t off0, uint32_t lenl, uint8_t *dst) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t h = (uint32_t)((uintptr_t)dst >> 1) & 1u;  // the range starts mid-word
+    uint32_t *d32 = (uint32_t *)(dst - 2 * h);
+    uint16_t *d16 = (uint16_t *)d32;
+    const uint32_t nw = (h + nu16 + 1) / 2;
+    uint32_t carry = 0;  // the word before this batch's first one
+    for (uint32_t w0 = 0; w0 < nw; w0 += 64 * kMoveBatch) {
+        if (w0) {  // tiles of more than 1023 units: the next batch (within the slot)
+#pragma unroll
+            for (int k = 0; k < kMoveBatch; k++) v[k] = __builtin_nontemporal_load(src32 + w0 + lane + 64 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < kMoveBatch; k++) {
+            const uint32_t up = lane_before(v[k]);
+            const uint32_t last = k ? (uint32_t)__builtin_amdgcn_readlane((int)v[k - 1], 63) : carry;
+            const uint32_t vp = lane ? up : last;  // word w - 1
+            const uint32_t w = w0 + lane + 64 * k;
+            uint32_t lo16 = h ? vp >> 16 : v[k] & 0xFFFFu, hi16 = h ? v[k] & 0xFFFFu : v[k] >> 16;
+            const int64_t u0 = 2 * (int64_t)w - h;  // slot units u0, u0 + 1
+            if (R) {
+                if (u0 == c0) lo16 = off0 & 0xFFFFu;
+                if (u0 + 1 == c0) hi16 = off0 & 0xFFFFu;
+                if (u0 == c0 + 1) lo16 = off0 >> 16;
+                if (u0 + 1 == c0 + 1) hi16 = off0 >> 16;
+                if (u0 == hl + 2) lo16 = lenl & 0xFFFFu;
+                if (u0 + 1 == hl + 2) hi16 = lenl & 0xFFFFu;
+                if (u0 == hl + 3) lo16 = lenl >> 16;
+                if (u0 + 1 == hl + 3) hi16 = lenl >> 16;
+            }
+            const bool vlo = u0 >= 0 && u0 < nu16, vhi = u0 + 1 < nu16;
+            if (w < nw) {
+                if (vlo && vhi) d32[w] = lo16 | hi16 << 16;
+                else if (vlo) d16[2 * w] = (uint16_t)lo16;
+                else if (vhi) d16[2 * w + 1] = (uint16_t)hi16;
+            }
+        }
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)v[kMoveBatch - 1], 63);
+    }
+}
+
+// One wave per tile: its records and prefix by scalar loads, the slot's
+// first 512 words (most tiles' whole image) issued at the same time, then the
+// move.  Block 0 also writes the u64 total length and publishes the wire
+// length.
+__global__ __launch_bounds__(kSB) void sp_move(const uint16_t *img, const uint2 *recA, const uint2 *recB,
+                                               const uint4 *pre, size_t ntiles, size_t n, const uint64_t *totals,
+                                               uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
-        for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)(total_len >> (16 * q));
-        host_tot[0] = Ftot;  // the wire length's terms, for the caller (host-mapped)
+        for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
+        const uint64_t F = totals[0], R = totals[1];
+        host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
         host_tot[1] = R;
+        if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
     }
-    for (size_t j = (size_t)blockIdx.x * kSB + threadIdx.x; j < R; j += (size_t)gridDim.x * kSB) {
-        uint32_t off = RU[j] - (j ? RU[j - 1] : 0u);
-        uint32_t len = (j + 1 < R ? RF[j + 1] : Ftot) - RF[j];
-        uint8_t *h = buf + 8 + 8 * j + 2 * (size_t)RF[j];
-        *(uint16_t *)(h + 0) = (uint16_t)off;
-        *(uint16_t *)(h + 2) = (uint16_t)(off >> 16);
-        *(uint16_t *)(h + 4) = (uint16_t)len;
-        *(uint16_t *)(h + 6) = (uint16_t)(len >> 16);
-    }
+    const uint32_t lane = threadIdx.x & 63;
+    // wave-uniform (readfirstlane): scalar loads for the records, scalar
+    // base addresses for the slot
+    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
+    if (tile >= ntiles) return;
+    const uint32_t *src32 = (const uint32_t *)(img + tile * kSlotU16);
+    uint32_t v[kMoveBatch];
+#pragma unroll
+    for (int k = 0; k < kMoveBatch; k++) v[k] = __builtin_nontemporal_load(src32 + lane + 64 * k);
+    const uint2 a = recA[tile], hb = recB[tile];
+    const uint4 p = pre[tile];
+    const uint32_t F = a.x & 0xFFFFu, R = a.x >> 16, nu16 = 4 * R + F;
+    if (!nu16) return;
+    const uint32_t tile0 = (uint32_t)(tile * kTile), tend = (uint32_t)min((size_t)tile0 + kTile, n);
+    // the first run's offset and the last run's length (R > 0), completed
+    const uint32_t off0 = (hb.y & 0xFFFFu) + (tile0 - p.z);
+    const uint32_t lenl = (hb.y >> 16) + (tile0 + (a.y & 0xFFFFu) == tend ? p.w - tend : 0u);
+    move_tile(src32, v, nu16, R, hb.x & 0xFFFFu, hb.x >> 16, off0, lenl, buf + 8 + 8 * (size_t)p.y + 2 * (size_t)p.x);
 }
 
 // Fallback lift (after a host parse): value v belongs to run j with
@@ -501,39 +761,42 @@ __global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
 }
 
 // Scratch of the encoder (tile counts, run table, device totals, two host-
-// mapped words for the result), kept per device and grown on demand: the
-// stream-ordered allocations it replaces cost more than the kernels at 64 MiB.
+// mapped words for the result), kept per (device, stream) and grown on
+// demand: the stream-ordered allocations it replaces cost more than the
+// kernels at 64 MiB.  Per stream, so stream-ordered drops on different
+// streams never share it (on one stream they are ordered anyway).
 struct Scratch {
-    size_t tiles_cap = 0, runs_cap = 0;
-    uint32_t *tiles = nullptr, *runs = nullptr;
+    size_t tiles_cap = 0;
+    uint2 *rec = nullptr;     // 2 x tiles_cap: recA, then recB
+    uint4 *pre = nullptr;     // tiles_cap scanned prefixes
+    uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
     uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
 };
 std::mutex g_scratch_mu;
-Scratch g_scratch[64];
+std::map<std::pair<int, hipStream_t>, Scratch> g_scratch;
 
-int scratch_for(size_t ntiles, size_t maxruns, Scratch **out) {
+int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
-    Scratch &sc = g_scratch[dev];
+    Scratch &sc = g_scratch[{dev, stream}];
     if (!sc.totals_dev) {
         ONO_HIP(hipMalloc((void **)&sc.totals_dev, 2 * sizeof(uint64_t)));
         ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
     }
-    if (2 * ntiles + 2 > sc.tiles_cap) {
-        (void)hipFree(sc.tiles);
-        sc.tiles = nullptr;
+    if (ntiles > sc.tiles_cap) {
+        (void)hipFree(sc.rec);
+        (void)hipFree(sc.pre);
+        (void)hipFree(sc.img);
+        sc.rec = nullptr;
+        sc.pre = nullptr;
+        sc.img = nullptr;
         sc.tiles_cap = 0;
-        ONO_HIP(hipMalloc((void **)&sc.tiles, (2 * ntiles + 2) * sizeof(uint32_t)));
-        sc.tiles_cap = 2 * ntiles + 2;
-    }
-    if (2 * maxruns > sc.runs_cap) {
-        (void)hipFree(sc.runs);
-        sc.runs = nullptr;
-        sc.runs_cap = 0;
-        ONO_HIP(hipMalloc((void **)&sc.runs, 2 * maxruns * sizeof(uint32_t)));
-        sc.runs_cap = 2 * maxruns;
+        ONO_HIP(hipMalloc((void **)&sc.rec, 2 * ntiles * sizeof(uint2)));
+        ONO_HIP(hipMalloc((void **)&sc.pre, ntiles * sizeof(uint4)));
+        ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
+        sc.tiles_cap = ntiles;
     }
     *out = &sc;
     return ONO_OK;
@@ -745,55 +1008,87 @@ extern "C" {
 
 size_t ono_sparse_max_bytes(size_t n) { return 8 + 10 * ((n + 1) / 2) + 2 * n; }
 
-int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, float threshold,
-                    void *stream) {
-    if (!nbytes || (n && !g) || !buf) return set_error(ONO_E_ARG, "NULL argument");
-    if (n >= 0xFFFFFFFFull) return set_error(ONO_E_ARG, "sparse codec offsets are u32 (protocol.rs:13-19)");
-    if (cap < 8) return set_error(ONO_E_SIZE, "buffer too small");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+}  // extern "C"
+
+namespace {
+
+// The four launches of the encoder.  nbytes_dev != NULL: the stream-ordered
+// form (the buffer holds the worst case, nothing waits; the headers kernel
+// stores the wire length there).  Otherwise blocking: the host reads the
+// totals at the end (and, for a buffer below the worst case, once before the
+// write pass to check the size).
+int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
+                float threshold, hipStream_t s) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
-    const size_t maxruns = (n + 1) / 2 + 1;
     const bool vec = ((uintptr_t)g & 15u) == 0;
-    // A buffer of the worst-case size cannot overflow: count, scan, write and
-    // headers run back to back and the host reads the totals once at the end.
-    // A smaller buffer needs the exact size first (one extra host round trip).
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
-    std::lock_guard<std::mutex> lk(g_scratch_mu);  // one call at a time per process owns the scratch
+    std::lock_guard<std::mutex> lk(g_scratch_mu);  // the host side of one call at a time
     Scratch *sc = nullptr;
-    int rc = scratch_for(ntiles, maxruns, &sc);
+    int rc = scratch_for(ntiles, s, &sc);
     if (rc) return rc;
-    uint32_t *tileF = sc->tiles, *tileS = sc->tiles + ntiles + 1, *RU = sc->runs, *RF = sc->runs + maxruns;
+    uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
+    uint4 *pre = sc->pre;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
-    tot[0] = tot[1] = 0;
+    if (!nbytes_dev) tot[0] = tot[1] = 0;
     uint64_t *totals = sc->totals_dev;
     hipError_t e = hipSuccess;
     if (ntiles) {
-        hipLaunchKernelGGL(sp_count, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS, vec);
-        hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, tileF, tileS, ntiles, totals);
+        static const int var = getenv("ONO_SP_VARIANT") ? atoi(getenv("ONO_SP_VARIANT")) : 0;
+        hipLaunchKernelGGL(sp_image, dim3((unsigned)ntiles), dim3(kIT), 0, s, g, n, threshold, vec, sc->img, recA,
+                           recB, var);
+        hipLaunchKernelGGL(sp_scan_rec, dim3(1), dim3(kScanRecT), 0, s, recA, pre, ntiles, (uint32_t)n, totals);
     } else {
         e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s);
     }
     if (e == hipSuccess) e = hipGetLastError();
-    if (e == hipSuccess && !worst_case_fits) {
+    if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip)
         hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(1), 0, s, totals, sc->host_tot_dev);
         e = hipStreamSynchronize(s);
         if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
             return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu",
                              (size_t)(8 + 8 * tot[1] + 2 * tot[0]), cap);
     }
-    if (e != hipSuccess) return hip_error(e, "sparse count", __FILE__, __LINE__);
-    if (ntiles)
-        hipLaunchKernelGGL(sp_write, dim3((unsigned)ntiles), dim3(kSB), 0, s, g, n, threshold, tileF, tileS, buf, RU,
-                           RF, vec);
-    const size_t hdr_runs = worst_case_fits ? maxruns : (size_t)tot[1];
-    const size_t hblocks = std::min<size_t>(4096, (hdr_runs + kSB) / kSB);
-    hipLaunchKernelGGL(sp_headers, dim3((unsigned)hblocks), dim3(kSB), 0, s, RU, RF, totals, (uint64_t)n, buf,
-                       sc->host_tot_dev);
+    if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
+    const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
+    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, ntiles, n, totals, buf,
+                       sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
+    if (nbytes_dev) return ONO_OK;
+    e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
     return ONO_OK;
+}
+
+int drop_args(const float *g, size_t n, const uint8_t *buf, size_t cap) {
+    if ((n && !g) || !buf) return set_error(ONO_E_ARG, "NULL argument");
+    if (n >= 0xFFFFFFFFull) return set_error(ONO_E_ARG, "sparse codec offsets are u32 (protocol.rs:13-19)");
+    if (cap < 8) return set_error(ONO_E_SIZE, "buffer too small");
+    return ONO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ono_sparse_drop(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, float threshold,
+                    void *stream) {
+    if (!nbytes) return set_error(ONO_E_ARG, "NULL argument");
+    int rc = drop_args(g, n, buf, cap);
+    if (rc) return rc;
+    return drop_launch(buf, cap, nbytes, nullptr, g, n, threshold, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ono_sparse_drop_async(uint8_t *buf, size_t cap, uint64_t *nbytes_dev, const float *g, size_t n,
+                          float threshold, void *stream) {
+    if (!nbytes_dev) return set_error(ONO_E_ARG, "NULL argument");
+    int rc = drop_args(g, n, buf, cap);
+    if (rc) return rc;
+    if (cap < ono_sparse_max_bytes(n))
+        return set_error(ONO_E_SIZE, "the stream-ordered drop needs the worst-case buffer (%zu bytes, have %zu)",
+                         ono_sparse_max_bytes(n), cap);
+    return drop_launch(buf, cap, nullptr, nbytes_dev, g, n, threshold, reinterpret_cast<hipStream_t>(stream));
 }
 
 int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, size_t nbytes, void *stream) {

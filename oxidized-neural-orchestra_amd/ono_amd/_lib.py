@@ -107,6 +107,7 @@ _SIGS = {
     "ono_direct_chain": (_i, [_fp, _vp, C.POINTER(C.c_void_p), _i, _sz, C.c_float, _i, _i, _vp]),
     "ono_sparse_max_bytes": (_sz, [_sz]),
     "ono_sparse_drop": (_i, [_vp, _sz, C.POINTER(C.c_size_t), _fp, _sz, C.c_float, _vp]),
+    "ono_sparse_drop_async": (_i, [_vp, _sz, _vp, _fp, _sz, C.c_float, _vp]),
     "ono_sparse_lift": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_dev": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_fallbacks": (_sz, []),

@@ -93,6 +93,17 @@ def grad_drop_dev(g: torch.Tensor, threshold: float, stream=None) -> torch.Tenso
     return buf[: nb.value]
 
 
+def grad_drop_async(g: torch.Tensor, threshold: float, buf: torch.Tensor, nbytes: torch.Tensor,
+                    stream=None) -> None:
+    """Stream-ordered grad_drop (ono_sparse_drop_async): buf (uint8, at least
+    ono_sparse_max_bytes(n)) receives the wire bytes and nbytes (one int64 on
+    the device) their length, when the stream gets there; nothing waits."""
+    n = g.numel()
+    assert buf.is_cuda and buf.dtype == torch.uint8 and nbytes.is_cuda and nbytes.dtype == torch.int64
+    call("ono_sparse_drop_async", buf.data_ptr(), buf.numel(), nbytes.data_ptr(), kernels.f32_ptr(g), n,
+         float(threshold), kernels.stream_handle(stream))
+
+
 def grad_lift_dev(buf: torch.Tensor, cap: int | None = None, stream=None) -> torch.Tensor:
     """grad_lift of wire bytes already in HBM (ono_sparse_lift_dev)."""
     assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()

@@ -283,6 +283,62 @@ def test_drop_headers_across_tiles_and_scan_chunks(pattern):
     assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
 
 
+@pytest.mark.parametrize("pattern", ["all_kept", "none_kept", "tile_edges", "clustered", "single_tail"])
+def test_drop_tile_boundary_patterns(pattern):
+    """The encoder's cross-tile header fields (sp_move completes the first
+    run's offset from the kept values before the tile and the last run's
+    length from the unkept values after it): runs that start or end exactly at
+    the 2048-value tile edges, one run over every tile, nothing kept, bursts of
+    runs with long gaps, a lone value at the very end."""
+    n = 3 * 2048 * 5 + 11
+    g = np.zeros(n, np.float32)
+    if pattern == "all_kept":
+        g[:] = 2.0
+    elif pattern == "tile_edges":
+        for k in range(1, n // 2048 + 1):
+            e = 2048 * k
+            g[max(0, e - 3):e] = 1.0          # a run ending at the tile's end
+            if e + 1 < n:
+                g[e + 1:e + 4] = -1.0         # one starting just after the next tile's start
+            if k % 3 == 0 and e < n:
+                g[e - 1:e + 1] = 3.0          # one crossing the edge
+    elif pattern == "clustered":
+        rng = np.random.default_rng(7)
+        for c in rng.integers(0, n - 300, 40):
+            m = rng.random(300) < 0.6
+            g[c:c + 300] = np.where(m, rng.standard_normal(300).astype(np.float32) + 3.0, 0.0)
+    elif pattern == "single_tail":
+        g[-1] = -7.0
+    got = SP.grad_drop_dev(dev(g), 0.5)
+    want = O.grad_drop(g, 0.5)
+    assert bytes(got.cpu().numpy()) == want
+    assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
+
+
+@pytest.mark.parametrize("n", [0, 5, 2048, (1 << 20) + 3])
+def test_drop_async_matches_blocking(n):
+    """ono_sparse_drop_async: the same bytes as the blocking drop, the length
+    in device memory, several drops queued back to back on one stream with
+    no host wait between them; a buffer below the worst case is refused."""
+    L = ono_amd.lib()
+    cap = L.ono_sparse_max_bytes(n)
+    gs = [O.synth(n, SEED + 40 + k, 1) for k in range(3)]
+    ts = [float(np.quantile(np.abs(x), 0.9)) if n else 0.0 for x in gs]
+    bufs = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in gs]
+    nbs = torch.zeros(len(gs), dtype=torch.int64, device="cuda")
+    dgs = [dev(x) for x in gs]
+    torch.cuda.synchronize()
+    for k in range(len(gs)):
+        SP.grad_drop_async(dgs[k], ts[k], bufs[k], nbs[k:k + 1])
+    torch.cuda.synchronize()
+    for k in range(len(gs)):
+        want = O.grad_drop(gs[k], ts[k])
+        assert int(nbs[k].item()) == len(want)
+        assert bytes(bufs[k][: len(want)].cpu().numpy()) == want
+    with pytest.raises(ono_amd.OnoError):
+        SP.grad_drop_async(dgs[0], ts[0], bufs[0][: max(cap - 1, 0)], nbs[:1])
+
+
 # ------------------------------------------------ calculate_threshold on the device
 def _threshold_inputs(n, seed):
     x = O.synth(n, seed, 0)

@@ -28,10 +28,19 @@ for _ in range(K):
 ev1.record()
 torch.cuda.synchronize()
 print(f"drop {ev0.elapsed_time(ev1) / K * 1e3:.1f} us per call between events on the stream")
+buf = torch.empty(L.ono_sparse_max_bytes(n), dtype=torch.uint8, device="cuda")
+nbd = torch.zeros(1, dtype=torch.int64, device="cuda")
+ev0.record()
+for _ in range(K):
+    ono_amd.sparse.grad_drop_async(g, t, buf, nbd)
+ev1.record()
+torch.cuda.synchronize()
+print(f"drop {ev0.elapsed_time(ev1) / K * 1e3:.1f} us per stream-ordered drop, back to back")
+assert int(nbd.item()) == wire.numel() and torch.equal(buf[: wire.numel()], wire)
 out = torch.empty(n, dtype=torch.float32, device="cuda")
 ln = C.c_size_t(0)
 s = torch.cuda.current_stream().cuda_stream
-for _ in range(K):
+for _ in range(K if not os.environ.get("ONO_SP_VARIANT") else 0):  # variants write garbage
     ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
 torch.cuda.synchronize()
 print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
