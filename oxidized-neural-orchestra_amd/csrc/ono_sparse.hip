@@ -71,6 +71,26 @@ __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
     return v;
 }
+// The same shape for max (identity 0) and min (identity ~0: lanes without a
+// source keep `old`).
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_min_dpp(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
 template <int E>
 __device__ __forceinline__ Bits flags_of(const float (&x)[E], float before, size_t n, float t, size_t base) {
     Bits b;
@@ -158,27 +178,29 @@ __global__ __launch_bounds__(kScanT) void sp_scan_tiles(uint32_t *tileF, uint32_
 }
 
 // ------------------------------------------------------------- encoder ----
-// Three launches, g read once:
-//  1. sp_image, one workgroup per 2048-value tile: flags, a block scan of the
-//     per-thread counts, and the tile's byte range of the wire built in LDS —
-//     its values, and its run headers with every field that the tile alone
-//     determines — then written to the tile's slot of a scratch image, plus a
-//     16-B record {kept | runs << 16, last kept index + 1, first unkept index,
-//     first / last header position}.
-//  2. sp_scan_rec, one workgroup: exclusive prefix sums of kept and runs (the
-//     tile's place in the wire), the exclusive prefix max of "last kept + 1"
-//     (where the run before the tile's first run ended) and the exclusive
-//     suffix min of "first unkept" (where a run still open at the tile's end
-//     ends).
+// Three launches, g read once (64 MiB, 10 % kept, MI355X: 19.5 + 9.6 + 10.5
+// us, 40 us per drop back to back; the four-launch count / scan / write /
+// headers design it replaced read g twice and took ~50):
+//  1. sp_image, one 128-thread workgroup per 2048-value tile (16 values per
+//     thread): flags, one LDS exchange of the waves' DPP scans, then the
+//     tile's byte range of the wire built in LDS — its values, and its run
+//     headers with every field that the tile alone determines, written by the
+//     threads that hold the run starts — copied to the tile's slot of a
+//     scratch image (5 B per value), plus two 8-B records: recA = {kept | runs
+//     << 16, last kept + 1 | first unkept << 16}, recB = {first / last header
+//     position, first run's offset | last run's length} (all tile-local).
+//  2. sp_scan_rec, one workgroup: per tile the exclusive prefix sums of kept
+//     and runs (its place in the wire), the exclusive prefix max of "last kept
+//     + 1" (P: where the run before the tile's first run ended) and the
+//     exclusive suffix min of "first unkept" (Q: where a run still open at the
+//     tile's end ends).
 //  3. sp_move, one wave per tile: the slot to its place in the wire (2-B
-//     aligned), with the two header fields that depend on other tiles
-//     completed on the way: the first run's offset and the last run's length.
-// The first run's offset is U_local(s_0) + (tile start - P) and the last run's
-// length is (kept from s_last to the tile's end) + (Q - tile end) when the
-// tile's last value is kept (P: last kept index + 1 before the tile, 0 if
-// none; Q: first unkept index after the tile, n if none): a run's offset is
-// the gap since the previous run's end, its length the distance to the first
-// unkept value after its start.
+//     aligned) in 16-B destination chunks, completing on the way the two
+//     header fields that depend on other tiles: the first run's offset (+=
+//     tile start - P) and, when the tile's last value is kept, the last run's
+//     length (+= Q - tile end).  A run's offset is the gap since the previous
+//     run's end, its length the distance to the first unkept value after its
+//     start.
 constexpr int kSlotU16 = 5128;  // the largest tile image, 3 S + 2049 <= 5121 units (S <= 1024), padded to 16 B
 static_assert((kSlotU16 * 2) % 16 == 0, "slots are 16-B aligned");
 
@@ -244,7 +266,7 @@ static_assert(kIE == 16, "tile_scan sizes its bit planes for 16 elements per thr
 // recB = {first header | last header << 16, the first run's offset | the
 // last run's length << 16} (what the move completes).
 __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float t, bool vec, uint16_t *img,
-                                                uint2 *recA, uint2 *recB, int var) {
+                                                uint2 *recA, uint2 *recB) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
     __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
     const size_t tile = blockIdx.x, tile0 = tile * kTile;
@@ -255,7 +277,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float 
     if (vec && base + kIE <= n) {  // four 16-B loads per thread: 2 KiB per wave in flight
 #pragma unroll
         for (int q = 0; q < kIE / 4; q++) {
-            const f4s a = (var & 4) ? *((const f4s *)(g + base) + q) : __builtin_nontemporal_load((const f4s *)(g + base) + q);
+            const f4s a = __builtin_nontemporal_load((const f4s *)(g + base) + q);
             x[4 * q] = a.x; x[4 * q + 1] = a.y; x[4 * q + 2] = a.z; x[4 * q + 3] = a.w;
         }
     } else {
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float 
     // the values: one store per element, branch-free — to byte 8 S + 2 F of
     // the tile's range when kept, else to this thread's spare unit past the
     // image (no exec-mask branches around 16 conditional stores)
-    if (!(var & 2)) {
+    {
 #pragma unroll
         for (int e = 0; e < kIE; e++) {
             const uint32_t f = ts.ef + __popc(b.keep & ((1u << e) - 1u));
@@ -308,8 +330,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float 
     const uint32_t nu16 = 4 * R + F;
     uint4 *slot = (uint4 *)(img + tile * kSlotU16);
     const uint4 *st4 = (const uint4 *)stage;
-    if (!(var & 1))
-        for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) slot[k] = st4[k];
+    for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) slot[k] = st4[k];
     if (threadIdx.x == 0) {
         recA[tile] = make_uint2(F | R << 16, ts.last_kept1 | ts.first_unkept << 16);
         recB[tile] = R ? make_uint2((rb[0] & 0xFFFFu) | rb[1] << 16, rb[0] >> 16 | (rb[1] & 0xFFFF0000u))
@@ -317,34 +338,6 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float 
     }
 }
 
-// Inclusive wave scans over 64 lanes: sum, max (forward) and min (backward).
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= d) v = max(v, y);
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_min_rev(uint32_t v) {  // min over this lane and the ones above
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_down(v, d, 64);
-        if (lane + d < 64) v = min(v, y);
-    }
-    return v;
-}
 
 // recA -> pre = {F0, S0, P, Q} per tile (F0 / S0: kept values / runs before
 // the tile; P: last kept index + 1 before it, 0 if none; Q: first unkept
@@ -382,7 +375,7 @@ __global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint
             lk[k] = l1 ? (uint32_t)((c0 + lo + k) * kTile) + l1 : 0u;  // global last kept + 1
             mx = max(mx, lk[k]);
         }
-        const uint32_t i_f = wave_incl_sum(sumf), i_s = wave_incl_sum(sums), i_m = wave_incl_max(mx);
+        const uint32_t i_f = wave_incl_sum_dpp(sumf), i_s = wave_incl_sum_dpp(sums), i_m = wave_incl_max_dpp(mx);
         if (lane == 63) { wa[wave] = i_f; wb[wave] = i_s; wc[wave] = i_m; }
         __syncthreads();
         uint32_t pf = cf, ps = cs, pm = cp, tf = 0, tsum = 0, tm = 0;
@@ -395,8 +388,7 @@ __global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint
         }
         pf += i_f - sumf;  // exclusive, within the wave
         ps += i_s - sums;
-        const uint32_t wprev = __shfl_up(i_m, 1, 64);
-        if (lane) pm = max(pm, wprev);
+        pm = max(pm, lane_before(i_m));  // lane 0 gets 0, the identity
 #pragma unroll
         for (int k = 0; k < kScanRecPer; k++) {  // own entries only: no hazard with other threads
             const uint32_t a = la[lo + k];
@@ -425,27 +417,31 @@ __global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint
                 lb[i] = i < m ? recA[c0 + i].y : (uint32_t)kTile << 16;
             __syncthreads();
         }
+        // reversed order: thread t takes the chunk's tiles m-1-8t ... m-8-8t, so
+        // "the tiles after" are the earlier threads' and a forward min scan does
         uint32_t fu[kScanRecPer], mn = n;
 #pragma unroll
         for (int k = 0; k < kScanRecPer; k++) {
-            const uint32_t f1 = lb[lo + k] >> 16;
-            fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + lo + k) * kTile) + f1 : n;
+            const uint32_t idx = lo + k, i = m - 1 - idx;
+            const uint32_t f1 = idx < m ? lb[i] >> 16 : (uint32_t)kTile;
+            fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + i) * kTile) + f1 : n;
             mn = min(mn, fu[k]);
         }
-        const uint32_t i_m = wave_incl_min_rev(mn);
-        if (lane == 0) wa[wave] = i_m;
+        const uint32_t i_m = wave_incl_min_dpp(mn);
+        if (lane == 63) wa[wave] = i_m;
         __syncthreads();
         uint32_t q = cq, tq = n;
 #pragma unroll
         for (int w = 0; w < kScanRecT / 64; w++) {
-            if (w > wave) q = min(q, wa[w]);
+            if (w < wave) q = min(q, wa[w]);
             tq = min(tq, wa[w]);
         }
-        const uint32_t wnext = __shfl_down(i_m, 1, 64);
-        if (lane < 63) q = min(q, wnext);
+        const uint32_t wprev = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)i_m, 0x138, 0xF, 0xF, false);
+        q = min(q, wprev);  // lane 0 keeps ~0, the identity
 #pragma unroll
-        for (int k = kScanRecPer - 1; k >= 0; k--) {
-            lb[lo + k] = q;
+        for (int k = 0; k < kScanRecPer; k++) {
+            const uint32_t idx = lo + k;
+            if (idx < m) lb[m - 1 - idx] = q;
             q = min(q, fu[k]);
         }
         cq = min(cq, tq);
@@ -459,61 +455,96 @@ __global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint
     }
 }
 
-// One tile's slot -> its place in the wire: nu16 units to byte 8 + 8 S0 +
-// 2 F0, u32 stores inside the range and u16 stores at its ends (neighbouring
-// tiles share those words), the two cross-tile header fields completed on the
-// way.  v: the slot's first 64 * kMoveBatch words, already loaded (lane l
-// holds words l + 64 k).
-constexpr int kMoveBatch = 8;  // words per lane per batch: 1024 units per wave
-__device__ __forceinline__ void move_tile(const uint32_t *src32, uint32_t (&v)[kMoveBatch], uint32_t nu16, uint32_t R,
-                                          uint32_t c0, uint32_t hl, uint32_t off0, uint32_t lenl, uint8_t *dst) {
+// One tile's slot -> its place in the wire, in 16-B chunks of the
+// destination: the range starts O units (0..7, uniform) into its first
+// aligned chunk, so destination chunk c takes slot units 8c - O .. 8c - O + 7
+// — the last O units of slot chunk c - 1 (the lane before, by DPP) and the
+// first 8 - O of slot chunk c (this lane).  Whole chunks are one 16-B store;
+// the range's first and last chunk (shared with the neighbouring tiles) are
+// stored unit by unit.  The two completed header fields (slot units c0, c0 + 1
+// and hl + 2, hl + 3) are substituted in registers on the way.
+constexpr int kMoveBatch = 2;  // 16-B slot chunks per lane loaded up front: 1024 units per wave
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldn4(const uint4 *p) {
+    const u4v r = __builtin_nontemporal_load((const u4v *)p);
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+__device__ __forceinline__ uint4 lane_before4(uint4 v) {
+    return make_uint4(lane_before(v.x), lane_before(v.y), lane_before(v.z), lane_before(v.w));
+}
+__device__ __forceinline__ uint4 readlane4(uint4 v, int l) {
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
+                      (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l));
+}
+template <int O>
+__device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveBatch], uint32_t nu16, uint32_t R,
+                                            const uint32_t (&fu)[4], const uint32_t (&fv)[4], uint16_t *base16) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t h = (uint32_t)((uintptr_t)dst >> 1) & 1u;  // the range starts mid-word
-    uint32_t *d32 = (uint32_t *)(dst - 2 * h);
-    uint16_t *d16 = (uint16_t *)d32;
-    const uint32_t nw = (h + nu16 + 1) / 2;
-    uint32_t carry = 0;  // the word before this batch's first one
-    for (uint32_t w0 = 0; w0 < nw; w0 += 64 * kMoveBatch) {
-        if (w0) {  // tiles of more than 1023 units: the next batch (within the slot)
+    const uint32_t nchunks = nu16 ? (O + nu16 + 7) / 8 : 0;
+    // field unit f of the range lands at base16 unit f + O: chunk, word, half
+    uint32_t fc[4], fw[4];
 #pragma unroll
-            for (int k = 0; k < kMoveBatch; k++) v[k] = __builtin_nontemporal_load(src32 + w0 + lane + 64 * k);
-        }
+    for (int j = 0; j < 4; j++) {
+        fc[j] = R ? (fu[j] + O) / 8 : 0xFFFFFFFFu;
+        fw[j] = (fu[j] + O) % 8;  // unit within the chunk
+    }
+    uint4 carry = make_uint4(0, 0, 0, 0);  // slot chunk before this batch's first one
+    auto batch = [&](uint32_t c0b) {
 #pragma unroll
         for (int k = 0; k < kMoveBatch; k++) {
-            const uint32_t up = lane_before(v[k]);
-            const uint32_t last = k ? (uint32_t)__builtin_amdgcn_readlane((int)v[k - 1], 63) : carry;
-            const uint32_t vp = lane ? up : last;  // word w - 1
-            const uint32_t w = w0 + lane + 64 * k;
-            uint32_t lo16 = h ? vp >> 16 : v[k] & 0xFFFFu, hi16 = h ? v[k] & 0xFFFFu : v[k] >> 16;
-            const int64_t u0 = 2 * (int64_t)w - h;  // slot units u0, u0 + 1
-            if (R) {
-                if (u0 == c0) lo16 = off0 & 0xFFFFu;
-                if (u0 + 1 == c0) hi16 = off0 & 0xFFFFu;
-                if (u0 == c0 + 1) lo16 = off0 >> 16;
-                if (u0 + 1 == c0 + 1) hi16 = off0 >> 16;
-                if (u0 == hl + 2) lo16 = lenl & 0xFFFFu;
-                if (u0 + 1 == hl + 2) hi16 = lenl & 0xFFFFu;
-                if (u0 == hl + 3) lo16 = lenl >> 16;
-                if (u0 + 1 == hl + 3) hi16 = lenl >> 16;
+            const uint4 own = v[k];
+            const uint4 up = lane_before4(own);
+            const uint4 last = k ? readlane4(v[k - 1], 63) : carry;
+            const uint4 prev = lane ? up : last;
+            const uint32_t C[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // out word j = concat units 8 - O + 2j, + 1
+                const int sft = 8 - O + 2 * j;
+                if (sft % 2 == 0) o[j] = C[sft / 2];
+                else o[j] = __builtin_amdgcn_alignbit(C[(sft + 1) / 2], C[(sft - 1) / 2], 16);
             }
-            const bool vlo = u0 >= 0 && u0 < nu16, vhi = u0 + 1 < nu16;
-            if (w < nw) {
-                if (vlo && vhi) d32[w] = lo16 | hi16 << 16;
-                else if (vlo) d16[2 * w] = (uint16_t)lo16;
-                else if (vhi) d16[2 * w + 1] = (uint16_t)hi16;
+            const uint32_t c = c0b + lane + 64 * k;
+            if (R) {
+#pragma unroll
+                for (int f = 0; f < 4; f++) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (c == fc[f] && fw[f] / 2 == (uint32_t)j) {
+                            const uint32_t sh = 16 * (fw[f] % 2);
+                            o[j] = (o[j] & ~(0xFFFFu << sh)) | fv[f] << sh;
+                        }
+                    }
+                }
+            }
+            const bool whole = c * 8 >= (uint32_t)O && (size_t)c * 8 + 8 - O <= nu16;
+            if (whole) {
+                const u4v ov = {o[0], o[1], o[2], o[3]};
+                __builtin_nontemporal_store(ov, (u4v *)(base16 + 8 * (size_t)c));
+            } else if (c < nchunks) {  // the range's first / last chunk
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int64_t u = (int64_t)c * 8 + i - O;  // range unit
+                    if (u >= 0 && u < (int64_t)nu16) base16[8 * (size_t)c + i] = (uint16_t)(o[i / 2] >> (16 * (i % 2)));
+                }
             }
         }
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)v[kMoveBatch - 1], 63);
+        carry = readlane4(v[kMoveBatch - 1], 63);
+    };
+    batch(0);  // unconditionally: no branch for the compiler to sink the early loads behind
+    for (uint32_t c0b = 64 * kMoveBatch; c0b < nchunks; c0b += 64 * kMoveBatch) {  // tiles of more than 1023 units
+#pragma unroll
+        for (int k = 0; k < kMoveBatch; k++) v[k] = ldn4(src4 + c0b + lane + 64 * k);
+        batch(c0b);
     }
 }
 
-// One wave per tile: its records and prefix by scalar loads, the slot's
-// first 512 words (most tiles' whole image) issued at the same time, then the
-// move.  Block 0 also writes the u64 total length and publishes the wire
-// length.
-__global__ __launch_bounds__(kSB) void sp_move(const uint16_t *img, const uint2 *recA, const uint2 *recB,
-                                               const uint4 *pre, size_t ntiles, size_t n, const uint64_t *totals,
-                                               uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
+// One wave per tile: its records and prefix by scalar loads, the slot's first
+// 1024 units (most tiles' whole image) issued at the same time, then the move.
+// Block 0 also writes the u64 total length and publishes the wire length.
+__global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) void sp_move(
+    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, size_t ntiles, size_t n,
+    const uint64_t *totals, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
         const uint64_t F = totals[0], R = totals[1];
@@ -522,23 +553,36 @@ __global__ __launch_bounds__(kSB) void sp_move(const uint16_t *img, const uint2 
         if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
     }
     const uint32_t lane = threadIdx.x & 63;
-    // wave-uniform (readfirstlane): scalar loads for the records, scalar
-    // base addresses for the slot
+    // wave-uniform (readfirstlane): scalar base addresses and branches
     const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
     if (tile >= ntiles) return;
-    const uint32_t *src32 = (const uint32_t *)(img + tile * kSlotU16);
-    uint32_t v[kMoveBatch];
+    const uint4 *src4 = (const uint4 *)(img + tile * kSlotU16);
+    uint4 v[kMoveBatch];
 #pragma unroll
-    for (int k = 0; k < kMoveBatch; k++) v[k] = __builtin_nontemporal_load(src32 + lane + 64 * k);
+    for (int k = 0; k < kMoveBatch; k++) v[k] = ldn4(src4 + lane + 64 * k);
     const uint2 a = recA[tile], hb = recB[tile];
     const uint4 p = pre[tile];
     const uint32_t F = a.x & 0xFFFFu, R = a.x >> 16, nu16 = 4 * R + F;
-    if (!nu16) return;
     const uint32_t tile0 = (uint32_t)(tile * kTile), tend = (uint32_t)min((size_t)tile0 + kTile, n);
     // the first run's offset and the last run's length (R > 0), completed
     const uint32_t off0 = (hb.y & 0xFFFFu) + (tile0 - p.z);
     const uint32_t lenl = (hb.y >> 16) + (tile0 + (a.y & 0xFFFFu) == tend ? p.w - tend : 0u);
-    move_tile(src32, v, nu16, R, hb.x & 0xFFFFu, hb.x >> 16, off0, lenl, buf + 8 + 8 * (size_t)p.y + 2 * (size_t)p.x);
+    const uint32_t c0 = hb.x & 0xFFFFu, hl = hb.x >> 16;
+    const uint32_t fu[4] = {c0, c0 + 1, hl + 2, hl + 3};
+    const uint32_t fv[4] = {off0 & 0xFFFFu, off0 >> 16, lenl & 0xFFFFu, lenl >> 16};
+    uint8_t *dst = buf + 8 + 8 * (size_t)p.y + 2 * (size_t)p.x;
+    const uint32_t O = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uintptr_t)dst & 15u) >> 1));
+    uint16_t *base16 = (uint16_t *)(dst - 2 * O);
+    switch (O) {
+    case 0: move_chunks<0>(src4, v, nu16, R, fu, fv, base16); break;
+    case 1: move_chunks<1>(src4, v, nu16, R, fu, fv, base16); break;
+    case 2: move_chunks<2>(src4, v, nu16, R, fu, fv, base16); break;
+    case 3: move_chunks<3>(src4, v, nu16, R, fu, fv, base16); break;
+    case 4: move_chunks<4>(src4, v, nu16, R, fu, fv, base16); break;
+    case 5: move_chunks<5>(src4, v, nu16, R, fu, fv, base16); break;
+    case 6: move_chunks<6>(src4, v, nu16, R, fu, fv, base16); break;
+    default: move_chunks<7>(src4, v, nu16, R, fu, fv, base16); break;
+    }
 }
 
 // Fallback lift (after a host parse): value v belongs to run j with
@@ -1033,9 +1077,8 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     uint64_t *totals = sc->totals_dev;
     hipError_t e = hipSuccess;
     if (ntiles) {
-        static const int var = getenv("ONO_SP_VARIANT") ? atoi(getenv("ONO_SP_VARIANT")) : 0;
         hipLaunchKernelGGL(sp_image, dim3((unsigned)ntiles), dim3(kIT), 0, s, g, n, threshold, vec, sc->img, recA,
-                           recB, var);
+                           recB);
         hipLaunchKernelGGL(sp_scan_rec, dim3(1), dim3(kScanRecT), 0, s, recA, pre, ntiles, (uint32_t)n, totals);
     } else {
         e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s);

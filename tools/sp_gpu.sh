@@ -23,5 +23,5 @@ import csv, glob
 for f in glob.glob('gpurun_out/sp_prof/*kernel_stats.csv'):
     for r in csv.DictReader(open(f)):
         if 'sp_' in r['Name'] or 'sl_' in r['Name']:
-            print(r['Name'].split('(')[0][-40:], r['Calls'], round(float(r['AverageNs'])/1000, 2), round(float(r['MinNs'])/1000, 2), round(float(r['MaxNs'])/1000, 2))
+            print(r['Name'].replace('(anonymous namespace)::', '').split('(')[0][-40:], r['Calls'], round(float(r['AverageNs'])/1000, 2), round(float(r['MinNs'])/1000, 2), round(float(r['MaxNs'])/1000, 2))
 PY
