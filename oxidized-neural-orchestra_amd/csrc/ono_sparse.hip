@@ -178,18 +178,20 @@ __global__ __launch_bounds__(kScanT) void sp_scan_tiles(uint32_t *tileF, uint32_
 }
 
 // ------------------------------------------------------------- encoder ----
-// Three launches, g read once (64 MiB, 10 % kept, MI355X: 19.5 + 9.6 + 10.5
-// us, 40 us per drop back to back; the four-launch count / scan / write /
-// headers design it replaced read g twice and took ~50):
+// Three launches, g read once (64 MiB, 10 % kept, MI355X: about 20 + 7.3 +
+// 10.5 us, 38 us per drop back to back with the gradient read from HBM; the
+// four-launch count / scan / write / headers design it replaced read g twice
+// and took ~50):
 //  1. sp_image, one 128-thread workgroup per 2048-value tile (16 values per
-//     thread): flags, one LDS exchange of the waves' DPP scans, then the
+//     thread, plain 16-B loads): flags, one LDS exchange of the waves' DPP scans, then the
 //     tile's byte range of the wire built in LDS — its values, and its run
 //     headers with every field that the tile alone determines, written by the
 //     threads that hold the run starts — copied to the tile's slot of a
 //     scratch image (5 B per value), plus two 8-B records: recA = {kept | runs
 //     << 16, last kept + 1 | first unkept << 16}, recB = {first / last header
 //     position, first run's offset | last run's length} (all tile-local).
-//  2. sp_scan_rec, one workgroup: per tile the exclusive prefix sums of kept
+//  2. sp_scan_rec, one workgroup per 1024 tiles (two levels, the last
+//     workgroup to arrive makes the chunk carries): per tile the exclusive prefix sums of kept
 //     and runs (its place in the wire), the exclusive prefix max of "last kept
 //     + 1" (P: where the run before the tile's first run ended) and the
 //     exclusive suffix min of "first unkept" (Q: where a run still open at the
@@ -265,25 +267,33 @@ static_assert(kIE == 16, "tile_scan sizes its bit planes for 16 elements per thr
 // | runs << 16, last kept + 1 | first unkept << 16} (what the scan needs),
 // recB = {first header | last header << 16, the first run's offset | the
 // last run's length << 16} (what the move completes).
-__global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float t, bool vec, uint16_t *img,
+__global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, float t, bool vec, uint16_t *img,
                                                 uint2 *recA, uint2 *recB) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
     __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
     const size_t tile = blockIdx.x, tile0 = tile * kTile;
     const uint32_t lo = threadIdx.x * kIE;  // the thread's first element, tile-local
     const size_t base = tile0 + lo;
-    float x[kIE], before = 0.0f;
-    if ((threadIdx.x & 63) == 0 && base > 0 && base - 1 < n) before = g[base - 1];  // issued with the values
-    if (vec && base + kIE <= n) {  // four 16-B loads per thread: 2 KiB per wave in flight
+    float x[kIE];
+    // four 16-B loads per thread, 2 KiB per wave in flight; plain loads: nt
+    // loads measured slower here even from HBM (64 MiB drop over 6 rotating
+    // gradients: 38.2 us with plain loads, 49.9 us with nt)
+    if (vec && base + kIE <= n) {
 #pragma unroll
         for (int q = 0; q < kIE / 4; q++) {
-            const f4s a = __builtin_nontemporal_load((const f4s *)(g + base) + q);
+            const f4s a = *((const f4s *)(g + base) + q);
             x[4 * q] = a.x; x[4 * q + 1] = a.y; x[4 * q + 2] = a.z; x[4 * q + 3] = a.w;
         }
     } else {
 #pragma unroll
         for (int e = 0; e < kIE; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
     }
+    // the value before the wave's first one (lane 0 uses it): a wave-uniform
+    // address, so a scalar load that waits on its own counter — as a vector
+    // load under lane 0's branch it was issued, and waited for, only after
+    // all of the values had landed (+6 us per drop)
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(tile0 + (threadIdx.x & ~63u) * kIE));
+    const float before = wbase ? g[min((size_t)wbase - 1, n - 1)] : 0.0f;
     const Bits b = flags_of(x, before, n, t, base);
     const uint32_t valid = base >= n ? 0u : (n - base >= (size_t)kIE ? 0xFFFFu : (1u << (n - base)) - 1u);
     const uint32_t unk = valid & ~b.keep;
@@ -341,117 +351,110 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *g, size_t n, float 
 
 // recA -> pre = {F0, S0, P, Q} per tile (F0 / S0: kept values / runs before
 // the tile; P: last kept index + 1 before it, 0 if none; Q: first unkept
-// index after it, n if none); totals = {kept, runs}.  One workgroup of
-// kScanRecT threads, kScanRecPer consecutive tiles per thread, chunks of
-// kScanRecChunk tiles staged through LDS (coalesced 8-B record loads, 16-B
-// result stores); forward over the chunks (sums, max), then backward (min) —
-// one load and one store per record when the tiles fit one chunk (n <= 2^24).
-constexpr int kScanRecT = 1024, kScanRecPer = 8, kScanRecChunk = kScanRecT * kScanRecPer;
-__global__ __launch_bounds__(kScanRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, size_t ntiles, uint32_t n,
-                                                         uint64_t *totals) {
-    __shared__ uint32_t la[kScanRecChunk], lb[kScanRecChunk], lp[kScanRecChunk], lq[kScanRecChunk];
-    __shared__ uint32_t wa[kScanRecT / 64], wb[kScanRecT / 64], wc[kScanRecT / 64];
+// index after it, n if none), in two levels within one launch: each
+// workgroup scans a chunk of kRecChunk tiles (LDS-staged, DPP wave scans;
+// the suffix min as a forward scan over the chunk reversed) into chunk-local
+// prefixes and publishes the chunk's aggregate; the workgroup that arrives
+// last (one agent-scope counter, one arrival per workgroup) turns the
+// aggregates into per-chunk carries and the totals.  sp_move adds its
+// chunk's carry.
+constexpr int kRecT = 256, kRecPer = 4, kRecChunk = kRecT * kRecPer;  // 1024 tiles per workgroup
+__global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, uint4 *agg, uint4 *carry,
+                                                      uint32_t *counter, size_t ntiles, uint32_t n, uint64_t *totals) {
+    __shared__ uint32_t la[kRecChunk], lb[kRecChunk];
+    __shared__ uint32_t rf[kRecChunk], rs[kRecChunk], rp[kRecChunk], rq[kRecChunk];
+    __shared__ uint32_t wa[kRecT / 64], wb[kRecT / 64], wc[kRecT / 64], wd[kRecT / 64];
+    __shared__ uint32_t is_last;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t lo = threadIdx.x * kScanRecPer;
-    const size_t nch = (ntiles + kScanRecChunk - 1) / kScanRecChunk;
-    const bool single = nch == 1;
-    uint32_t cf = 0, cs = 0, cp = 0;  // carries from the earlier chunks
-    for (size_t c = 0; c < nch; c++) {
-        const size_t c0 = c * kScanRecChunk;
-        const uint32_t m = (uint32_t)min((size_t)kScanRecChunk, ntiles - c0);
-        for (uint32_t i = threadIdx.x; i < kScanRecChunk; i += kScanRecT) {
-            const uint2 r = i < m ? recA[c0 + i] : make_uint2(0u, (uint32_t)kTile << 16);
-            la[i] = r.x;
-            lb[i] = r.y;
-        }
-        __syncthreads();
-        uint32_t sumf = 0, sums = 0, mx = 0;
-        uint32_t lk[kScanRecPer];
-#pragma unroll
-        for (int k = 0; k < kScanRecPer; k++) {
-            const uint32_t a = la[lo + k], l1 = lb[lo + k] & 0xFFFFu;
-            sumf += a & 0xFFFFu;
-            sums += a >> 16;
-            lk[k] = l1 ? (uint32_t)((c0 + lo + k) * kTile) + l1 : 0u;  // global last kept + 1
-            mx = max(mx, lk[k]);
-        }
-        const uint32_t i_f = wave_incl_sum_dpp(sumf), i_s = wave_incl_sum_dpp(sums), i_m = wave_incl_max_dpp(mx);
-        if (lane == 63) { wa[wave] = i_f; wb[wave] = i_s; wc[wave] = i_m; }
-        __syncthreads();
-        uint32_t pf = cf, ps = cs, pm = cp, tf = 0, tsum = 0, tm = 0;
-#pragma unroll
-        for (int w = 0; w < kScanRecT / 64; w++) {
-            if (w < wave) { pf += wa[w]; ps += wb[w]; pm = max(pm, wc[w]); }
-            tf += wa[w];
-            tsum += wb[w];
-            tm = max(tm, wc[w]);
-        }
-        pf += i_f - sumf;  // exclusive, within the wave
-        ps += i_s - sums;
-        pm = max(pm, lane_before(i_m));  // lane 0 gets 0, the identity
-#pragma unroll
-        for (int k = 0; k < kScanRecPer; k++) {  // own entries only: no hazard with other threads
-            const uint32_t a = la[lo + k];
-            la[lo + k] = pf;
-            lp[lo + k] = ps;
-            lq[lo + k] = pm;
-            pf += a & 0xFFFFu;
-            ps += a >> 16;
-            pm = max(pm, lk[k]);
-        }
-        cf += tf;
-        cs += tsum;
-        cp = max(cp, tm);
-        __syncthreads();
-        if (!single)
-            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i] = make_uint4(la[i], lp[i], lq[i], 0u);
-        __syncthreads();
+    const size_t c0 = (size_t)blockIdx.x * kRecChunk;
+    const uint32_t m = (uint32_t)min((size_t)kRecChunk, ntiles - c0);
+    for (uint32_t i = threadIdx.x; i < kRecChunk; i += kRecT) {
+        const uint2 r = i < m ? recA[c0 + i] : make_uint2(0u, (uint32_t)kTile << 16);
+        la[i] = r.x;
+        lb[i] = r.y;
     }
-    if (threadIdx.x == 0) { totals[0] = cf; totals[1] = cs; }
-    uint32_t cq = n;  // min of first-unkept over the tiles of the later chunks
-    for (size_t c = nch; c-- > 0;) {
-        const size_t c0 = c * kScanRecChunk;
-        const uint32_t m = (uint32_t)min((size_t)kScanRecChunk, ntiles - c0);
-        if (!single) {
-            for (uint32_t i = threadIdx.x; i < kScanRecChunk; i += kScanRecT)
-                lb[i] = i < m ? recA[c0 + i].y : (uint32_t)kTile << 16;
-            __syncthreads();
-        }
-        // reversed order: thread t takes the chunk's tiles m-1-8t ... m-8-8t, so
-        // "the tiles after" are the earlier threads' and a forward min scan does
-        uint32_t fu[kScanRecPer], mn = n;
+    __syncthreads();
+    const uint32_t lo = threadIdx.x * kRecPer;
+    // forward: this thread's tiles lo .. lo + 3
+    uint32_t sumf = 0, sums = 0, mx = 0, lk[kRecPer], cnt[kRecPer];
 #pragma unroll
-        for (int k = 0; k < kScanRecPer; k++) {
-            const uint32_t idx = lo + k, i = m - 1 - idx;
-            const uint32_t f1 = idx < m ? lb[i] >> 16 : (uint32_t)kTile;
-            fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + i) * kTile) + f1 : n;
-            mn = min(mn, fu[k]);
-        }
-        const uint32_t i_m = wave_incl_min_dpp(mn);
-        if (lane == 63) wa[wave] = i_m;
-        __syncthreads();
-        uint32_t q = cq, tq = n;
+    for (int k = 0; k < kRecPer; k++) {
+        cnt[k] = la[lo + k];
+        const uint32_t l1 = lb[lo + k] & 0xFFFFu;
+        sumf += cnt[k] & 0xFFFFu;
+        sums += cnt[k] >> 16;
+        lk[k] = l1 ? (uint32_t)((c0 + lo + k) * kTile) + l1 : 0u;  // global last kept + 1
+        mx = max(mx, lk[k]);
+    }
+    // backward, as a forward scan over the chunk reversed: tiles m-1-lo .. m-4-lo
+    uint32_t fu[kRecPer], mn = n;
 #pragma unroll
-        for (int w = 0; w < kScanRecT / 64; w++) {
-            if (w < wave) q = min(q, wa[w]);
-            tq = min(tq, wa[w]);
-        }
-        const uint32_t wprev = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)i_m, 0x138, 0xF, 0xF, false);
-        q = min(q, wprev);  // lane 0 keeps ~0, the identity
+    for (int k = 0; k < kRecPer; k++) {
+        const uint32_t idx = lo + k, i = m - 1 - idx;
+        const uint32_t f1 = idx < m ? lb[i] >> 16 : (uint32_t)kTile;
+        fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + i) * kTile) + f1 : n;
+        mn = min(mn, fu[k]);
+    }
+    const uint32_t i_f = wave_incl_sum_dpp(sumf), i_s = wave_incl_sum_dpp(sums);
+    const uint32_t i_m = wave_incl_max_dpp(mx), i_u = wave_incl_min_dpp(mn);
+    if (lane == 63) { wa[wave] = i_f; wb[wave] = i_s; wc[wave] = i_m; wd[wave] = i_u; }
+    __syncthreads();
+    uint32_t pf = 0, ps = 0, pm = 0, q = n, tf = 0, tsum = 0, tm = 0, tq = n;
 #pragma unroll
-        for (int k = 0; k < kScanRecPer; k++) {
-            const uint32_t idx = lo + k;
-            if (idx < m) lb[m - 1 - idx] = q;
-            q = min(q, fu[k]);
+    for (int w = 0; w < kRecT / 64; w++) {
+        if (w < wave) { pf += wa[w]; ps += wb[w]; pm = max(pm, wc[w]); q = min(q, wd[w]); }
+        tf += wa[w];
+        tsum += wb[w];
+        tm = max(tm, wc[w]);
+        tq = min(tq, wd[w]);
+    }
+    pf += i_f - sumf;  // exclusive, within the wave
+    ps += i_s - sums;
+    pm = max(pm, lane_before(i_m));  // lane 0 gets 0, the identity
+    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)i_u, 0x138, 0xF, 0xF, false));  // lane 0: ~0
+#pragma unroll
+    for (int k = 0; k < kRecPer; k++) {
+        rf[lo + k] = pf;
+        rs[lo + k] = ps;
+        rp[lo + k] = pm;
+        pf += cnt[k] & 0xFFFFu;
+        ps += cnt[k] >> 16;
+        pm = max(pm, lk[k]);
+        const uint32_t idx = lo + k;
+        if (idx < m) rq[m - 1 - idx] = q;
+        q = min(q, fu[k]);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += kRecT) pre[c0 + i] = make_uint4(rf[i], rs[i], rp[i], rq[i]);
+    // the chunk's aggregate, then one arrival; the last workgroup makes the carries
+    if (threadIdx.x == 0) {
+        agg[blockIdx.x] = make_uint4(tf, tsum, tm, tq);
+        const uint32_t before = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = before == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x;
+        uint32_t cf = 0, cs = 0, cm = 0;
+        for (uint32_t g = 0; g < G; g++) {  // forward carries (atomic loads: never a stale cached line)
+            const uint32_t af = __hip_atomic_load(&agg[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t as = __hip_atomic_load(&agg[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t am = __hip_atomic_load(&agg[g].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            carry[g] = make_uint4(cf, cs, cm, 0u);
+            cf += af;
+            cs += as;
+            cm = max(cm, am);
         }
-        cq = min(cq, tq);
-        __syncthreads();
-        if (single) {
-            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i] = make_uint4(la[i], lp[i], lq[i], lb[i]);
-        } else {
-            for (uint32_t i = threadIdx.x; i < m; i += kScanRecT) pre[c0 + i].w = lb[i];
+        uint32_t cq = n;
+        for (uint32_t g = G; g-- > 0;) {  // backward carries
+            carry[g].w = cq;
+            cq = min(cq, __hip_atomic_load(&agg[g].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         }
-        __syncthreads();
+        totals[0] = cf;
+        totals[1] = cs;
+        __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next drop
     }
 }
 
@@ -543,8 +546,8 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
 // 1024 units (most tiles' whole image) issued at the same time, then the move.
 // Block 0 also writes the u64 total length and publishes the wire length.
 __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) void sp_move(
-    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, size_t ntiles, size_t n,
-    const uint64_t *totals, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
+    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, const uint4 *carry, size_t ntiles,
+    size_t n, const uint64_t *totals, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
         const uint64_t F = totals[0], R = totals[1];
@@ -561,7 +564,8 @@ __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
     for (int k = 0; k < kMoveBatch; k++) v[k] = ldn4(src4 + lane + 64 * k);
     const uint2 a = recA[tile], hb = recB[tile];
-    const uint4 p = pre[tile];
+    const uint4 pl = pre[tile], cr = carry[tile / kRecChunk];  // chunk-local prefix + the chunk's carry
+    const uint4 p = make_uint4(pl.x + cr.x, pl.y + cr.y, max(pl.z, cr.z), min(pl.w, cr.w));
     const uint32_t F = a.x & 0xFFFFu, R = a.x >> 16, nu16 = 4 * R + F;
     const uint32_t tile0 = (uint32_t)(tile * kTile), tend = (uint32_t)min((size_t)tile0 + kTile, n);
     // the first run's offset and the last run's length (R > 0), completed
@@ -812,7 +816,8 @@ __global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
 struct Scratch {
     size_t tiles_cap = 0;
     uint2 *rec = nullptr;     // 2 x tiles_cap: recA, then recB
-    uint4 *pre = nullptr;     // tiles_cap scanned prefixes
+    uint4 *pre = nullptr;     // tiles_cap chunk-local prefixes, then 2 x (tiles_cap / kRecChunk + 1): aggregates, carries
+    uint32_t *counter = nullptr;  // the record scan's arrival counter (zero between drops)
     uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
     uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
 };
@@ -825,6 +830,8 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
     Scratch &sc = g_scratch[{dev, stream}];
     if (!sc.totals_dev) {
+        ONO_HIP(hipMalloc((void **)&sc.counter, sizeof(uint32_t)));
+        ONO_HIP(hipMemset(sc.counter, 0, sizeof(uint32_t)));
         ONO_HIP(hipMalloc((void **)&sc.totals_dev, 2 * sizeof(uint64_t)));
         ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
@@ -838,7 +845,7 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
         sc.img = nullptr;
         sc.tiles_cap = 0;
         ONO_HIP(hipMalloc((void **)&sc.rec, 2 * ntiles * sizeof(uint2)));
-        ONO_HIP(hipMalloc((void **)&sc.pre, ntiles * sizeof(uint4)));
+        ONO_HIP(hipMalloc((void **)&sc.pre, (ntiles + 2 * (ntiles / kRecChunk + 1)) * sizeof(uint4)));
         ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
         sc.tiles_cap = ntiles;
     }
@@ -1071,7 +1078,8 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     int rc = scratch_for(ntiles, s, &sc);
     if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
-    uint4 *pre = sc->pre;
+    const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
+    uint4 *pre = sc->pre, *agg = sc->pre + sc->tiles_cap, *carry = agg + (sc->tiles_cap / kRecChunk + 1);
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     uint64_t *totals = sc->totals_dev;
@@ -1079,7 +1087,8 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (ntiles) {
         hipLaunchKernelGGL(sp_image, dim3((unsigned)ntiles), dim3(kIT), 0, s, g, n, threshold, vec, sc->img, recA,
                            recB);
-        hipLaunchKernelGGL(sp_scan_rec, dim3(1), dim3(kScanRecT), 0, s, recA, pre, ntiles, (uint32_t)n, totals);
+        hipLaunchKernelGGL(sp_scan_rec, dim3((unsigned)nchunks), dim3(kRecT), 0, s, recA, pre, agg, carry,
+                           sc->counter, ntiles, (uint32_t)n, totals);
     } else {
         e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s);
     }
@@ -1093,7 +1102,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, ntiles, n, totals, buf,
+    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, carry, ntiles, n, totals, buf,
                        sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
