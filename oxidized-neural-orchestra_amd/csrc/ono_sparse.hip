@@ -257,7 +257,7 @@ __device__ __forceinline__ TileScan tile_scan(uint32_t keep, uint32_t start, uin
     }
     return r;
 }
-static_assert(kIE == 16, "tile_scan sizes its bit planes for 16 elements per thread");
+static_assert(kIE <= 32, "a thread's flags are one 32-bit mask; its counts are packed as 16-bit halves");
 
 // One workgroup per tile: flags, the block scans, then the tile's byte range
 // in LDS — each kept value at 8 S + 2 F, each run's header by the thread that
@@ -295,7 +295,8 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(tile0 + (threadIdx.x & ~63u) * kIE));
     const float before = wbase ? g[min((size_t)wbase - 1, n - 1)] : 0.0f;
     const Bits b = flags_of(x, before, n, t, base);
-    const uint32_t valid = base >= n ? 0u : (n - base >= (size_t)kIE ? 0xFFFFu : (1u << (n - base)) - 1u);
+    const uint32_t full = kIE >= 32 ? 0xFFFFFFFFu : (1u << (kIE & 31)) - 1u;
+    const uint32_t valid = base >= n ? 0u : (n - base >= (size_t)kIE ? full : (1u << (n - base)) - 1u);
     const uint32_t unk = valid & ~b.keep;
     const TileScan ts = tile_scan(b.keep, b.start, unk);
     const uint32_t R = ts.ts, F = ts.tf;
