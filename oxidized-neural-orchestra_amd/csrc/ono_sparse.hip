@@ -132,51 +132,6 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
 }
 
 
-// Exclusive scan of the tile counts in place, one block of kScanT threads,
-// in chunks of kScanT x kScanPer tiles staged through LDS: coalesced global
-// loads into LDS, each thread scans its kScanPer contiguous tiles there, one
-// block-wide scan of the per-thread sums, coalesced stores back.
-// totals[0] = kept values, totals[1] = runs.
-constexpr int kScanT = 1024, kScanPer = 8, kScanChunk = kScanT * kScanPer;
-__global__ __launch_bounds__(kScanT) void sp_scan_tiles(uint32_t *tileF, uint32_t *tileS, size_t ntiles,
-                                                        uint64_t *totals) {
-    __shared__ uint32_t lf[kScanChunk], ls[kScanChunk];
-    __shared__ uint32_t carry[2];
-    if (threadIdx.x == 0) { carry[0] = 0; carry[1] = 0; }
-    for (size_t c0 = 0; c0 < ntiles; c0 += kScanChunk) {
-        const size_t m = ntiles - c0 < (size_t)kScanChunk ? ntiles - c0 : (size_t)kScanChunk;
-        for (size_t i = threadIdx.x; i < kScanChunk; i += kScanT) {
-            lf[i] = i < m ? tileF[c0 + i] : 0u;
-            ls[i] = i < m ? tileS[c0 + i] : 0u;
-        }
-        __syncthreads();
-        const int lo = threadIdx.x * kScanPer;
-        uint32_t sf = 0, ss = 0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; k++) { sf += lf[lo + k]; ss += ls[lo + k]; }
-        uint32_t ef, es, tf, ts;
-        block_scan2<kScanT>(sf, ss, ef, es, tf, ts);
-        ef += carry[0];
-        es += carry[1];
-#pragma unroll
-        for (int k = 0; k < kScanPer; k++) {
-            const uint32_t a = lf[lo + k], b = ls[lo + k];
-            lf[lo + k] = ef;
-            ls[lo + k] = es;
-            ef += a;
-            es += b;
-        }
-        __syncthreads();
-        for (size_t i = threadIdx.x; i < m; i += kScanT) {
-            tileF[c0 + i] = lf[i];
-            tileS[c0 + i] = ls[i];
-        }
-        if (threadIdx.x == 0) { carry[0] += tf; carry[1] += ts; }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) { totals[0] = carry[0]; totals[1] = carry[1]; }
-}
-
 // ------------------------------------------------------------- encoder ----
 // Three launches, g read once (64 MiB, 10 % kept, MI355X: about 20 + 7.3 +
 // 10.5 us, 38 us per drop back to back with the gradient read from HBM; the
@@ -621,185 +576,392 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 }
 
 // ---------------------------------------------------------------- lift ----
-// The record stream is cut into segments of kSeg bytes.  sl_starts picks, per
-// segment, the first 2-byte position whose next kLook records are all
-// plausible (a speculative record start; segment 0 starts at the true head,
-// byte 8).  sl_walk follows the records from each start until it lands on a
-// later segment's start (marking it reached) or the end of the stream.  The
-// speculation is checked, not trusted: the walks are exactly the sequential
-// parse iff every speculative start was reached and no walk failed (records
-// form a successor chain, so a walk that lands on a start has joined the true
-// chain there; the earliest start off the chain can only be reached from the
-// chain, so it stays unreached).  Otherwise `bad` is raised and the host
-// parses sequentially — also how malformed input gets the reference's error
-// messages.  Each walk's sum of (offset + length) is scanned (block-wide in
-// sl_walk, across blocks by sp_scan_tiles) to give the element index its
-// records start at; sl_place walks again and writes the values of short runs
-// itself, and queues runs longer than kShort for sl_long (one workgroup per
-// run).
-constexpr int kSeg = 128, kLook = 4, kShort = 16;
+// The record stream is a linked list (each header's run length gives the next
+// header's position), cut into segments of kSeg bytes.  Three launches:
+//  1. sl_index, one workgroup per window of kLW segments (32 KiB of stream
+//     staged in LDS with one coalesced pass): each thread picks its segment's
+//     first 2-byte position whose next kLook records are all plausible (a
+//     speculative record start; segment 0 starts at the true head, byte 8),
+//     then walks the records from there in LDS until it lands on a later
+//     segment's start (stamping that segment reached with this call's epoch)
+//     or the end, noting each record (position, element offset within the
+//     walk, length, and a run of at most two values whole).  A block scan of
+//     the walks' sums of (offset + length) gives each segment's element index
+//     within the window.  The workgroups also zero g[0, total) between them.
+//  2. sl_place, 16 lanes per segment: the window's prefix, the checks, and
+//     each noted record placed by one lane (runs longer than kShortP queued
+//     in chunks; no record is walked again).
+// (64 MiB gradient at 10 % kept on MI355X: 40 + 27 + 4 us against 81 us of
+// kernels for the six-launch design it replaced; the walks are a chain of
+// dependent LDS reads per thread, so sl_index is latency-bound.  Tried and
+// dropped: the zero-fill on a side stream (event cost > overlap), a
+// tile-image fill that re-walks the records per 4096-value tile (58 us: ~10
+// walking lanes per workgroup), gap-zeroing by the records' lanes instead of
+// a zero-fill (50 us: per-lane scalar stores).)
+//  3. sl_long: the queued chunks, one workgroup each.
+// The speculation is checked, not trusted: the walks are exactly the
+// sequential parse iff every speculative start was reached and no walk failed
+// (records form a successor chain, so a walk that lands on a start has joined
+// the true chain there; the earliest start off the chain can only be reached
+// from the chain, so it stays unreached).  Otherwise `bad` (a host-mapped
+// word, this call's epoch) is raised and the host parses sequentially — also
+// how malformed input gets the reference's error messages.
+constexpr int kSeg = 128, kLook = 4;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kLW = 256;                      // sl_index: threads = segments per window
+constexpr size_t kWin = (size_t)kLW * kSeg;   // 32 KiB of stream per window
+constexpr int kMarg = 1024;                   // staged past the window (the last segments' look-ahead)
+constexpr int kRecK = 32;                     // records kept per segment walk (the rest walked again)
+constexpr int kShortP = 32;                   // runs up to this long are placed by one lane
+constexpr int kLongChunk = 4096;              // longer runs: queued chunks, one workgroup each
 
-__device__ __forceinline__ uint32_t ld32(const uint8_t *b, size_t p) {  // p even, b 2-B aligned
-    const uint16_t *h = (const uint16_t *)(b + p);
-    return (uint32_t)h[0] | (uint32_t)h[1] << 16;
+// The stream's u16 units: [lo, lo + 2 n16) from LDS, every other one from
+// global memory (p even, b 2-B aligned).  The two pointers carry their address
+// spaces, so the two loads cannot be merged into one flat load through a
+// selected pointer (which the compiler otherwise does: a flat access to LDS has
+// the vector-memory latency).
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+typedef __attribute__((address_space(1))) const uint16_t glb_u16;
+struct Bytes {
+    const uint8_t *b;
+    lds_u16 *lds;
+    size_t lo, n16;
+    // [p, p + nb) lies in the staged range (p even; p - lo wraps below lo)
+    __device__ __forceinline__ bool staged(size_t p, size_t nb) const {
+        const size_t d = p - lo;
+        return d < 2 * n16 && nb <= 2 * n16 - d;
+    }
+    // A record header (offset, length): one range check, then four loads
+    // issued together from one memory or the other.
+    __device__ __forceinline__ void hdr(size_t p, uint32_t &off, uint32_t &len) const {
+        uint32_t h0, h1, h2, h3;
+        if (staged(p, 8)) {
+            lds_u16 *q = lds + ((p - lo) >> 1);
+            h0 = q[0]; h1 = q[1]; h2 = q[2]; h3 = q[3];
+        } else {
+            glb_u16 *q = (glb_u16 *)(b + p);
+            h0 = q[0]; h1 = q[1]; h2 = q[2]; h3 = q[3];
+        }
+        off = h0 | h1 << 16;
+        len = h2 | h3 << 16;
+    }
+    // n f16 values from p, widened, into dst[0, n)
+    __device__ __forceinline__ void values(size_t p, uint32_t n, float *dst) const {
+        if (staged(p, 2 * (size_t)n)) {
+            lds_u16 *q = lds + ((p - lo) >> 1);
+            for (uint32_t i = 0; i < n; i++) dst[i] = from_f16_sp(q[i]);
+        } else {
+            glb_u16 *q = (glb_u16 *)(b + p);
+            for (uint32_t i = 0; i < n; i++) dst[i] = from_f16_sp(q[i]);
+        }
+    }
+    __device__ __forceinline__ uint16_t u16s(size_t p) const { return lds[(p - lo) >> 1]; }  // staged(p, 2)
+    __device__ __forceinline__ uint32_t hdr32(size_t p) const {                             // staged(p, 4)
+        lds_u16 *q = lds + ((p - lo) >> 1);
+        return (uint32_t)q[0] | (uint32_t)q[1] << 16;
+    }
+    __device__ __forceinline__ float value(size_t p) const {
+        return from_f16_sp(staged(p, 2) ? lds[(p - lo) >> 1] : *(glb_u16 *)(b + p));
+    }
+};
+__device__ __forceinline__ lds_u16 *as_lds(const uint16_t *p) { return (lds_u16 *)p; }
+
+// u16 units [lo, lo + 2 n16) of b (at most MAXB bytes) into lds (8-B
+// aligned): 8-B loads when b + lo is 8-B aligned, 4-B loads when 4-B aligned,
+// else 2-B loads.  Every load of a thread is issued before the first LDS
+// store (one memory latency, not one per load).
+template <int NT, int MAXB>
+__device__ __forceinline__ void stage_bytes(uint16_t *lds, const uint8_t *b, size_t lo, size_t n16) {
+    const uint8_t *src = b + lo;
+    const uintptr_t a = (uintptr_t)src;
+    size_t done = 0;
+    if ((a & 7) == 0) {
+        constexpr int K = (MAXB / 8 + NT - 1) / NT;
+        const size_t n8 = n16 / 4;
+        uint2 v[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const size_t i = threadIdx.x + (size_t)k * NT;
+            if (i < n8) v[k] = ((const uint2 *)src)[i];
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const size_t i = threadIdx.x + (size_t)k * NT;
+            if (i < n8) ((uint2 *)lds)[i] = v[k];
+        }
+        done = 4 * n8;
+    } else if ((a & 3) == 0) {
+        constexpr int K = (MAXB / 4 + NT - 1) / NT;
+        const size_t n4 = n16 / 2;
+        uint32_t v[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const size_t i = threadIdx.x + (size_t)k * NT;
+            if (i < n4) v[k] = ((const uint32_t *)src)[i];
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const size_t i = threadIdx.x + (size_t)k * NT;
+            if (i < n4) ((uint32_t *)lds)[i] = v[k];
+        }
+        done = 2 * n4;
+    }
+    for (size_t i = done + threadIdx.x; i < n16; i += NT) lds[i] = ((const uint16_t *)src)[i];
 }
-__device__ __forceinline__ uint16_t ld16(const uint8_t *b, size_t p) { return *(const uint16_t *)(b + p); }
 
-// g[0, total) = 0 (grad.fill(0); resize(total, 0)) with total read from the
-// stream's first 8 bytes on the device, so the host need not wait for it.
-// tot[0] = total; flags: [0] bad, [1] queued long runs, [2] total > cap (then
-// nothing is written and every later kernel stands down through flags[0]).
-__global__ __launch_bounds__(kSB) void sl_zero(float *g, const uint8_t *b, size_t cap, int vec, uint64_t *tot,
-                                               uint32_t *flags, uint64_t *host_word) {
+__device__ __forceinline__ uint64_t stream_total(const uint8_t *b) {
     uint64_t total = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) total |= (uint64_t)ld16(b, 2 * q) << (16 * q);
-    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x, stride = (size_t)gridDim.x * kSB;
-    if (t == 0) {
-        tot[0] = total;
-        host_word[1] = total;
-        flags[0] = total > cap ? 1u : 0u;
-        flags[1] = 0;
-        flags[2] = total > cap ? 1u : 0u;
-    }
-    if (total > cap) return;
-    if (vec) {
-        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (size_t i = t; i < total / 4; i += stride) *(f4s *)(g + 4 * i) = z;
-        for (size_t i = 4 * (total / 4) + t; i < total; i += stride) g[i] = 0.0f;
-    } else {
-        for (size_t i = t; i < total; i += stride) g[i] = 0.0f;
-    }
+    for (int q = 0; q < 4; q++) total |= (uint64_t)*(const uint16_t *)(b + 2 * q) << (16 * q);
+    return total;
 }
 
-__global__ __launch_bounds__(kSB) void sl_starts(const uint8_t *b, size_t nbytes, const uint64_t *tot, size_t S,
-                                                 uint32_t *p0, uint32_t *reached) {
-    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
-    if (t >= S) return;
-    const uint64_t total = tot[0];
-    reached[t] = 0;
-    if (t == 0) { p0[0] = 8; return; }
-    const size_t lo = 8 + t * kSeg, hi = lo + kSeg < nbytes ? lo + kSeg : nbytes;
+// A speculation refuted or a malformed stream: the host parses sequentially.
+__device__ __forceinline__ void raise_bad(uint64_t *host_word, uint32_t epoch) {
+    *(volatile uint64_t *)host_word = epoch;
+}
+
+// Segment s's speculative record start: the first 2-byte position whose next
+// kLook records are plausible (kNone: none).  A start whose records run past
+// the stream is no start; nor is one with a run of >= 2^16 values: a header
+// read 2 B off its true position takes a half of the run length as the high
+// half of its own (so >= 2^16), and such a jump lands on a true header about
+// one time in five, after which every look-ahead record is valid.  Runs are
+// maximal in grad_drop's output, so a record after the first is >= 1 value
+// past the previous run: offset 0 is no start either (zero-filled payload
+// reads as offset 0).  A true start refused here only leaves its segment to
+// the previous walk.
+__device__ uint32_t seg_start(const Bytes &src, size_t s, size_t nbytes, uint64_t total) {
+    if (s == 0) return 8;
+    const size_t lo = 8 + s * kSeg, hi = lo + kSeg < nbytes ? lo + kSeg : nbytes;
     for (size_t p = lo; p < hi; p += 2) {
         size_t q = p;
         uint64_t acc = 0;
         bool ok = true;
         for (int k = 0; k < kLook && q != nbytes; k++) {
             if (nbytes - q < 8) { ok = false; break; }
-            const uint32_t off = ld32(b, q), len = ld32(b, q + 4);
-            // A start whose records run past the stream is no start; nor is one
-            // with a run of >= 2^16 values: a header read 2 B off its true
-            // position takes a half of the run length as the high half of its
-            // own (so >= 2^16), and such a jump lands on a true header about one
-            // time in five, after which every look-ahead record is valid.  Runs
-            // are maximal in grad_drop's output, so a record after the first is
-            // >= 1 value past the previous run: offset 0 is no start either
-            // (zero-filled payload reads as offset 0).  A true start refused
-            // here only leaves its segment to the previous walk.
+            uint32_t off, len;
+            src.hdr(q, off, len);
             if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
             acc += (uint64_t)off + len;
             if (acc > total) { ok = false; break; }
             q += 8 + 2 * (size_t)len;
         }
-        if (ok) { p0[t] = (uint32_t)p; return; }
+        if (ok) return (uint32_t)p;
     }
-    p0[t] = kNone;
+    return kNone;
 }
 
-// per segment: gsum[t] = sum of (offset + length) over its records;
-// per block: bsum[block] = the block's total (scanned afterwards)
-__global__ __launch_bounds__(kSB) void sl_walk(const uint8_t *b, size_t nbytes, const uint64_t *tot, size_t S,
-                                               const uint32_t *p0, uint32_t *reached, uint32_t *gsum, uint32_t *bsum,
-                                               uint32_t *bscratch, uint32_t *flags) {
-    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
-    const uint64_t total = tot[0];
+// Block-wide sum of a u64 (the same value in every thread).
+template <int NT>
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v) {
+    __shared__ uint64_t ws[NT / 64];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t t = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) t += ws[w];
+    __syncthreads();
+    return t;
+}
+
+// Per segment s (sl_index): p0 (its speculative start or kNone), gpre (the
+// element index its records start from, within its window), the stamps of the
+// starts its walk landed on (reached = this call's epoch), and its records:
+// rcnt = how many, ent[s K + j] = {byte position, the run's element offset
+// within the walk, length, its first two values} for the first K; per window:
+// wsum.
+__global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes, size_t S, size_t cap, float *g,
+                                                int vec, uint32_t epoch, uint32_t *p0g, uint32_t *gpre,
+                                                uint32_t *rcnt, uint4 *ent, uint32_t *reached, uint32_t *wsum,
+                                                uint32_t *qcount, uint64_t *host_word) {
+    __shared__ uint2 lw8[(kWin + kMarg) / 8];
+    __shared__ uint32_t lp0[kLW];
+    uint16_t *lw = (uint16_t *)lw8;
+    const size_t w = blockIdx.x, s0 = w * kLW, s = s0 + threadIdx.x;
+    const size_t lo = 8 + w * kWin, hi = lo + kWin + kMarg < nbytes ? lo + kWin + kMarg : nbytes;
+    const uint64_t total = stream_total(b);
+    if (w == 0 && threadIdx.x == 0) *qcount = 0;  // sl_place's long-run queue
+    if (total <= cap) {  // this workgroup's share of g[0, total) = 0 (grad.fill(0); resize(total, 0))
+        const size_t W = gridDim.x;
+        if (vec) {
+            const size_t n4 = total / 4, a = n4 * w / W, z = n4 * (w + 1) / W;
+            const f4s zero = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (size_t i = a + threadIdx.x; i < z; i += kLW) __builtin_nontemporal_store(zero, (f4s *)g + i);
+            if (w == W - 1)
+                for (size_t i = 4 * n4 + threadIdx.x; i < total; i += kLW) g[i] = 0.0f;
+        } else {
+            const size_t a = total * w / W, z = total * (w + 1) / W;
+            for (size_t i = a + threadIdx.x; i < z; i += kLW) g[i] = 0.0f;
+        }
+    }
+    stage_bytes<kLW, kWin + kMarg>(lw, b, lo, (hi - lo) / 2);
+    __syncthreads();
+    const Bytes src{b, as_lds(lw), lo, (hi - lo) / 2};
+    const uint32_t mine = s < S ? seg_start(src, s, nbytes, total) : kNone;
+    lp0[threadIdx.x] = mine;
+    __syncthreads();
     uint64_t sum = 0;
-    if (t < S && p0[t] != kNone) {
-        size_t pos = p0[t];
-        const size_t segend = 8 + (t + 1) * kSeg;
+    uint32_t cnt = 0;
+    if (mine != kNone) {
+        size_t pos = mine;
+        const size_t segend = 8 + (s + 1) * kSeg;
+        uint4 *my = ent + s * kRecK;
         for (;;) {
             if (pos == nbytes) break;  // the end of the stream
             if (pos >= segend) {
                 const size_t u = (pos - 8) / kSeg;
-                const uint32_t pu = u < S ? p0[u] : kNone;
-                if (pu != kNone && pos == pu) { reached[u] = 1; break; }
-                if (pu != kNone && pos > pu) { flags[0] = 1; break; }  // stepped over a start: not a record
+                const uint32_t pu =
+                    u >= S ? kNone : (u - s0 < (size_t)kLW ? lp0[u - s0] : seg_start(src, u, nbytes, total));
+                if (pu != kNone && pos == pu) { reached[u] = epoch; break; }
+                if (pu != kNone && pos > pu) { raise_bad(host_word, epoch); break; }  // stepped over a start
             }
-            if (nbytes - pos < 8) { flags[0] = 1; break; }
-            const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
-            if ((nbytes - pos - 8) / 2 < len) { flags[0] = 1; break; }
+            if (nbytes - pos < 8) { raise_bad(host_word, epoch); break; }
+            uint32_t off, len;
+            src.hdr(pos, off, len);
+            if ((nbytes - pos - 8) / 2 < len) { raise_bad(host_word, epoch); break; }
+            if (cnt < (uint32_t)kRecK) {
+                // a run of at most two values rides along whole (most runs are
+                // that short): bit 0 of the (even) position says so
+                uint32_t v01 = 0, whole = 0;
+                if (len <= 2 && src.staged(pos + 8, 2 * (size_t)len)) {
+                    whole = 1;
+                    v01 = len == 2 ? src.hdr32(pos + 8) : len == 1 ? (uint32_t)src.u16s(pos + 8) : 0u;
+                }
+                my[cnt] = make_uint4((uint32_t)pos | whole, (uint32_t)(sum + off), len, v01);
+            }
+            cnt++;
             sum += (uint64_t)off + len;
-            if (sum > total) { flags[0] = 1; break; }
+            if (sum > total) { raise_bad(host_word, epoch); break; }
             pos += 8 + 2 * (size_t)len;
         }
     }
-    if (t < S) gsum[t] = (uint32_t)sum;
     uint32_t ea, eb, ta, tb;
-    block_scan2((uint32_t)sum, 0u, ea, eb, ta, tb);
-    if (threadIdx.x == 0) { bsum[blockIdx.x] = ta; bscratch[blockIdx.x] = 0; }
+    block_scan2<kLW>((uint32_t)sum, 0u, ea, eb, ta, tb);
+    if (s < S) {
+        p0g[s] = mine;
+        gpre[s] = ea;
+        rcnt[s] = cnt;
+    }
+    if (threadIdx.x == 0) wsum[w] = ta;
 }
 
-__device__ __forceinline__ void put_run(float *g, const uint8_t *b, uint32_t gi, size_t vpos, uint32_t len,
-                                        uint32_t *longq, uint32_t qcap, uint32_t *flags) {
-    if (len <= (uint32_t)kShort) {
-        for (uint32_t i = 0; i < len; i++) g[gi + i] = from_f16_sp(ld16(b, vpos + 2 * i));
-    } else {
-        const uint32_t k = atomicAdd(&flags[1], 1u);
-        if (k >= qcap) { flags[0] = 1; return; }  // only off-chain walks can overfill it
-        longq[3 * k] = gi;
-        longq[3 * k + 1] = (uint32_t)vpos;
-        longq[3 * k + 2] = len;
+// A run of n values from stream byte vp into g[gi ..]: short runs by the
+// thread itself, longer ones as queued chunks of kLongChunk values for sl_long.
+__device__ __forceinline__ void put_run(float *g, const uint8_t *b, size_t gi, size_t vp, uint32_t n, uint4 *queue,
+                                        uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint32_t epoch) {
+    glb_u16 *q = (glb_u16 *)(b + vp);
+    if (n <= (uint32_t)kShortP) {
+        for (uint32_t i = 0; i < n; i++) g[gi + i] = from_f16_sp(q[i]);
+        return;
+    }
+    const uint32_t nc = (n + kLongChunk - 1) / kLongChunk;
+    const uint32_t k = atomicAdd(qcount, nc);
+    if (k + nc > qcap || k + nc < k) { raise_bad(host_word, epoch); return; }  // only a refuted stream overfills it
+    for (uint32_t c = 0; c < nc; c++) {
+        const size_t o = (size_t)c * kLongChunk;
+        queue[k + c] = make_uint4((uint32_t)(gi + o), (uint32_t)(vp + 2 * o), min((uint32_t)kLongChunk, n - (uint32_t)o),
+                                  0u);
     }
 }
 
-// bsum: exclusive scan over blocks (sp_scan_tiles)
-__global__ __launch_bounds__(kSB) void sl_place(float *g, const uint8_t *b, size_t nbytes, const uint64_t *tot,
-                                                size_t S, const uint32_t *p0, const uint32_t *reached,
-                                                const uint32_t *gsum, const uint32_t *bsum, uint32_t *longq,
-                                                uint32_t qcap, uint32_t *flags) {
-    const size_t t = (size_t)blockIdx.x * kSB + threadIdx.x;
-    const uint64_t total = tot[0];
-    const uint32_t mine = t < S ? gsum[t] : 0u;
-    uint32_t ea, eb, ta, tb;
-    block_scan2(mine, 0u, ea, eb, ta, tb);
-    if (flags[0] || t >= S || p0[t] == kNone) return;  // a failed walk: nothing to place
-    if (t > 0 && !reached[t]) { flags[0] = 1; return; }  // a speculative start off the chain
-    // the same records sl_walk visited (it checked every one against the
-    // stream's bounds), stopping where it stopped
-    uint64_t gi = (uint64_t)bsum[blockIdx.x] + ea;
-    size_t pos = p0[t];
-    const size_t segend = 8 + (t + 1) * kSeg;
-    for (;;) {
-        if (pos == nbytes) break;
-        if (pos >= segend) {
-            const size_t u = (pos - 8) / kSeg;
-            const uint32_t pu = u < S ? p0[u] : kNone;
-            if (pu != kNone && pos >= pu) break;
+// kPG lanes per segment: the window's prefix (a sum over the earlier windows'
+// totals), the speculation check (every start reached), the total check (the
+// records' offsets and lengths sum to at most the stream's total length:
+// every record lies in [0, total), protocol.rs:127-129), then each record of
+// the segment's walk placed by one lane (g was zeroed by sl_index).
+constexpr int kPT = 256, kPG = 16, kPSeg = kPT / kPG;  // 16 segments per workgroup
+static_assert(kLW % kPSeg == 0, "a workgroup's segments share a window");
+__global__ __launch_bounds__(kPT) void sl_place(float *g, const uint8_t *b, size_t nbytes, size_t S, size_t cap,
+                                                uint32_t epoch, const uint32_t *p0g, const uint32_t *gpre,
+                                                const uint32_t *rcnt, const uint4 *ent, const uint32_t *reached,
+                                                const uint32_t *wsum, uint4 *queue, uint32_t *qcount, uint32_t qcap,
+                                                uint64_t *host_word) {
+    const uint64_t total = stream_total(b);
+    if (blockIdx.x == 0 && threadIdx.x == 0) host_word[1] = total;
+    if (total > cap) return;  // ONO_E_SIZE: nothing is written
+    const size_t sb = (size_t)blockIdx.x * kPSeg, w = sb / kLW, s = sb + threadIdx.x / kPG;
+    const uint32_t lane = threadIdx.x % kPG;
+    const uint32_t p = s < S ? p0g[s] : kNone;
+    const uint32_t gp = s < S ? gpre[s] : 0u, cnt = s < S ? rcnt[s] : 0u;
+    const uint32_t rc = s < S && lane == 0 ? reached[s] : 0u;
+    // the lane's two records, loaded with the rest (no dependence on the prefix)
+    const uint4 *my = ent + s * kRecK;
+    uint4 r[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (s < S) {
+        r[0] = my[lane];
+        r[1] = my[lane + kPG];
+    }
+    constexpr int U = 4;  // wsum loads in flight per thread per step
+    uint64_t part = 0;
+    for (size_t j0 = 0; j0 < w; j0 += U * kPT) {
+        uint32_t v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) {
+            const size_t j = j0 + k * kPT + threadIdx.x;
+            v[k] = j < w ? wsum[j] : 0u;
         }
-        const uint32_t off = ld32(b, pos), len = ld32(b, pos + 4);
-        gi += off;
-        if (gi > total || total - gi < len) { flags[0] = 1; return; }  // protocol.rs:127-129 (host reports it)
-        put_run(g, b, (uint32_t)gi, pos + 8, len, longq, qcap, flags);
-        gi += len;
-        pos += 8 + 2 * (size_t)len;
+#pragma unroll
+        for (int k = 0; k < U; k++) part += v[k];
+    }
+    const uint64_t wp = block_sum64<kPT>(part);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && wp + wsum[w] > total) raise_bad(host_word, epoch);
+    if (p == kNone) return;
+    if (lane == 0 && s > 0 && rc != epoch) raise_bad(host_word, epoch);  // a speculative start off the chain
+    const uint64_t E = wp + gp;
+    const uint32_t m = min(cnt, (uint32_t)kRecK);
+    static_assert(kRecK == 2 * kPG, "two records per lane");
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t j = lane + k * kPG;
+        if (j >= m) break;
+        const uint64_t gi = E + r[k].y;
+        const uint32_t len = r[k].z;
+        if (gi > total || total - gi < len) { raise_bad(host_word, epoch); continue; }  // (never written past total)
+        if (r[k].x & 1u) {  // carried whole
+            if (len >= 1) g[gi] = from_f16_sp((uint16_t)r[k].w);
+            if (len == 2) g[gi + 1] = from_f16_sp((uint16_t)(r[k].w >> 16));
+        } else {
+            put_run(g, b, gi, (size_t)r[k].x + 8, len, queue, qcount, qcap, host_word, epoch);
+        }
+    }
+    if (cnt > (uint32_t)kRecK && lane == 0) {
+        // a walk of more than kRecK records (a true start refused nearby): the
+        // rest walked again from the last stored one, stopping where sl_index stopped
+        const uint4 e = my[kRecK - 1];  // the last stored record: {position, run start in the walk, length}
+        size_t pos = (e.x & ~1u) + 8 + 2 * (size_t)e.z;
+        uint64_t cur = (uint64_t)e.y + e.z;
+        const size_t segend = 8 + (s + 1) * kSeg;
+        for (;;) {
+            if (pos >= nbytes) break;
+            if (pos >= segend) {
+                const size_t u = (pos - 8) / kSeg;
+                const uint32_t pu = u >= S ? kNone : p0g[u];
+                if (pu != kNone && pos >= pu) break;
+            }
+            if (nbytes - pos < 8) break;
+            glb_u16 *h = (glb_u16 *)(b + pos);
+            const uint32_t off = (uint32_t)h[0] | (uint32_t)h[1] << 16, len = (uint32_t)h[2] | (uint32_t)h[3] << 16;
+            if ((nbytes - pos - 8) / 2 < len) break;
+            const uint64_t gi = E + cur + off;
+            if (gi > total || total - gi < len) { raise_bad(host_word, epoch); break; }
+            put_run(g, b, gi, pos + 8, len, queue, qcount, qcap, host_word, epoch);
+            cur += (uint64_t)off + len;
+            pos += 8 + 2 * (size_t)len;
+        }
     }
 }
 
-// runs longer than kShort: one workgroup per queued run
-__global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const uint32_t *longq,
-                                               const uint32_t *flags, uint64_t *host_word) {
-    const uint32_t bad = flags[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // every kernel that raises them has run
-        host_word[0] = bad;
-        host_word[2] = flags[2];
-    }
-    if (bad) return;
-    const uint32_t nq = flags[1];  // <= qcap when bad is clear
+// Queued chunks of long runs, one workgroup each (grid-stride).
+__global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const uint4 *queue,
+                                               const uint32_t *qcount, uint32_t qcap) {
+    const uint32_t nq = min(*qcount, qcap);
     for (uint32_t k = blockIdx.x; k < nq; k += gridDim.x) {
-        const uint32_t gi = longq[3 * k], len = longq[3 * k + 2];
-        const size_t vpos = longq[3 * k + 1];
-        for (uint32_t i = threadIdx.x; i < len; i += kSB) g[gi + i] = from_f16_sp(ld16(b, vpos + 2 * i));
+        const uint4 e = queue[k];
+        glb_u16 *q = (glb_u16 *)(b + e.y);
+        for (uint32_t i = threadIdx.x; i < e.z; i += kSB) g[(size_t)e.x + i] = from_f16_sp(q[i]);
     }
 }
 
@@ -855,10 +1017,14 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
 }
 
 struct LiftScratch {
-    size_t seg_cap = 0, rec_cap = 0, buf_cap = 0;
-    uint32_t *seg = nullptr, *rec = nullptr, *flags = nullptr;
+    size_t seg_cap = 0, win_cap = 0, q_cap = 0, buf_cap = 0;
+    uint32_t *seg = nullptr;   // 4 x seg_cap: p0, gpre, rcnt, reached (epoch stamps, zeroed when allocated)
+    uint4 *ent = nullptr;      // kRecK x seg_cap: the walks' records
+    uint32_t *win = nullptr;   // wsum (W), then the long-run queue's count
+    uint4 *queue = nullptr;    // q_cap chunks of long runs
+    uint32_t epoch = 0;
     uint8_t *buf = nullptr;
-    uint64_t *totals = nullptr, *host_word = nullptr, *host_word_dev = nullptr;
+    uint64_t *host_word = nullptr, *host_word_dev = nullptr;  // [0] bad (= epoch), [1] total
 };
 LiftScratch g_lift[64];
 std::atomic<size_t> g_lift_fallbacks{0};
@@ -953,42 +1119,57 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
     LiftScratch &L = g_lift[dev];
-    const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, nblk = S ? (S + kSB - 1) / kSB : 0;
-    const size_t qcap = (nbytes - 8) / (8 + 2 * (kShort + 1)) + 1;  // runs longer than kShort fit this many
-    if (!L.flags) {
-        ONO_HIP(hipMalloc((void **)&L.flags, 4 * sizeof(uint32_t)));
-        ONO_HIP(hipHostMalloc((void **)&L.host_word, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, W = (S + kLW - 1) / kLW;
+    if (!L.host_word) {
+        ONO_HIP(hipHostMalloc((void **)&L.host_word, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&L.host_word_dev, L.host_word, 0));
-        ONO_HIP(hipMalloc((void **)&L.totals, 4 * sizeof(uint64_t)));  // [0] total, [1..2] scan totals
     }
-    int rc = grow(&L.seg, L.seg_cap, 3 * S + 2 * nblk + 4);
-    if (!rc) rc = grow(&L.rec, L.rec_cap, 3 * qcap);
+    bool restamp = false;
+    if (S > L.seg_cap) {
+        (void)hipFree(L.seg);
+        (void)hipFree(L.ent);
+        L.seg = nullptr;
+        L.ent = nullptr;
+        L.seg_cap = 0;
+        ONO_HIP(hipMalloc((void **)&L.seg, 4 * S * sizeof(uint32_t)));
+        ONO_HIP(hipMalloc((void **)&L.ent, kRecK * S * sizeof(uint4)));
+        L.seg_cap = S;
+        restamp = true;
+    }
+    const size_t Wg = std::max<size_t>(1, W);  // (one workgroup zero-fills an empty stream's gradient)
+    int rc = grow(&L.win, L.win_cap, Wg + 1);
+    // chunks of runs longer than kShortP: at most one per kLongChunk values plus one per such run
+    // chunks of runs longer than kShortP: at most one per kLongChunk values plus one per such run
+    const size_t qcap = (nbytes - 8) / (8 + 2 * (kShortP + 1)) + cap / kLongChunk + 1;
+    if (!rc) rc = grow(&L.queue, L.q_cap, qcap);
     if (rc) return rc;
-    uint32_t *p0 = L.seg, *reached = L.seg + S, *gsum = L.seg + 2 * S, *bsum = L.seg + 3 * S,
-             *bscr = L.seg + 3 * S + nblk;
-    volatile uint64_t *word = L.host_word;
-    word[0] = 1;
-    word[1] = word[2] = 0;
-    const int vec = ((uintptr_t)g & 15) == 0;
-    const unsigned zb = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (cap / 4 + kSB - 1) / kSB));
-    hipLaunchKernelGGL(sl_zero, dim3(zb), dim3(kSB), 0, s, g, dbuf, cap, vec, L.totals, L.flags, L.host_word_dev);
-    if (S) {
-        hipLaunchKernelGGL(sl_starts, dim3((unsigned)nblk), dim3(kSB), 0, s, dbuf, nbytes, L.totals, S, p0, reached);
-        hipLaunchKernelGGL(sl_walk, dim3((unsigned)nblk), dim3(kSB), 0, s, dbuf, nbytes, L.totals, S, p0, reached,
-                           gsum, bsum, bscr, L.flags);
-        hipLaunchKernelGGL(sp_scan_tiles, dim3(1), dim3(kScanT), 0, s, bsum, bscr, nblk, L.totals + 1);
-        hipLaunchKernelGGL(sl_place, dim3((unsigned)nblk), dim3(kSB), 0, s, g, dbuf, nbytes, L.totals, S, p0, reached,
-                           gsum, bsum, L.rec, (uint32_t)qcap, L.flags);
+    if (++L.epoch == 0) {  // stamps of 2^32 lifts ago could match again
+        L.epoch = 1;
+        restamp = true;
     }
-    const unsigned lb = (unsigned)std::min<size_t>(1024, qcap);
-    hipLaunchKernelGGL(sl_long, dim3(lb), dim3(kSB), 0, s, g, dbuf, L.rec, L.flags, L.host_word_dev);
+    const size_t C = L.seg_cap;
+    uint32_t *p0 = L.seg, *gpre = L.seg + C, *rcnt = L.seg + 2 * C, *reached = L.seg + 3 * C;
+    if (restamp) ONO_HIP(hipMemsetAsync(reached, 0, C * sizeof(uint32_t), s));
+    uint32_t *wsum = L.win, *qcount = L.win + Wg;
+    volatile uint64_t *word = L.host_word;
+    word[0] = 0;
+    word[1] = 0;
+    const uint32_t epoch = L.epoch;
+    const int vec = ((uintptr_t)g & 15) == 0;
+    hipLaunchKernelGGL(sl_index, dim3((unsigned)Wg), dim3(kLW), 0, s, dbuf, nbytes, S, cap, g, vec, epoch, p0, gpre,
+                       rcnt, L.ent, reached, wsum, qcount, L.host_word_dev);
+    hipLaunchKernelGGL(sl_place, dim3((unsigned)std::max<size_t>(1, (S + kPSeg - 1) / kPSeg)), dim3(kPT), 0, s, g,
+                       dbuf, nbytes, S, cap, epoch, p0, gpre, rcnt, L.ent, reached, wsum, L.queue, qcount,
+                       (uint32_t)qcap, L.host_word_dev);
+    hipLaunchKernelGGL(sl_long, dim3((unsigned)std::min<size_t>(2048, qcap)), dim3(kSB), 0, s, g, dbuf, L.queue,
+                       qcount, (uint32_t)qcap);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
     const uint64_t total = word[1];
-    if (word[2]) return size_error(total);
+    if (total > cap) return size_error(total);
     *out_len = total;
-    if (word[0] == 0) return ONO_OK;
+    if (word[0] != epoch) return ONO_OK;
     // speculation missed or the stream is malformed: the sequential parse decides
     g_lift_fallbacks.fetch_add(1);
     ONO_HIP(hipMemsetAsync(g, 0, total * sizeof(float), s));

@@ -54,7 +54,18 @@ del G
 out = torch.empty(n, dtype=torch.float32, device="cuda")
 ln = C.c_size_t(0)
 s = torch.cuda.current_stream().cuda_stream
-for _ in range(K if not os.environ.get("ONO_SP_VARIANT") else 0):  # variants write garbage
-    ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
+KL = K if not os.environ.get("ONO_SP_VARIANT") else 0  # variants write garbage
+ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
 torch.cuda.synchronize()
+t0 = time.perf_counter()
+ev0.record()
+for _ in range(KL):
+    ono_amd._lib.call("ono_sparse_lift_dev", out.data_ptr(), n, C.byref(ln), wire.data_ptr(), wire.numel(), s)
+ev1.record()
+torch.cuda.synchronize()
+if KL:
+    print(f"lift_dev {(time.perf_counter() - t0) / KL * 1e6:.1f} us per blocking call, "
+          f"{ev0.elapsed_time(ev1) / KL * 1e3:.1f} us between events")
+    ref = ono_amd.sparse.grad_lift(bytes(wire.cpu().numpy()), n)
+    print("lift_dev equals the host-stream lift:", bool(torch.equal(out.view(torch.int32), ref.view(torch.int32))))
 print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
