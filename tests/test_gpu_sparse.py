@@ -383,3 +383,71 @@ def test_threshold_argument_errors():
         SP.threshold(g[:10], 1.5)
     with pytest.raises(ono_amd.InvalidArgument):
         SP.threshold(g[:10], 0.4, np.array([3, 10], np.uint32))  # index out of range
+
+
+# ------------------------------------------------- lift: three-launch paths ----
+def _lift_into(buf_dev: torch.Tensor, out: torch.Tensor, cap: int) -> int:
+    import ctypes as C
+
+    ln = C.c_size_t(0)
+    rc = ono_amd.lib().ono_sparse_lift_dev(out.data_ptr(), cap, C.byref(ln), buf_dev.data_ptr(), buf_dev.numel(),
+                                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rc == 0, ono_amd.lib().ono_last_error()
+    return ln.value
+
+
+@pytest.mark.parametrize("n,r", [(70001, 0.9), (1 << 20, 0.5), (4099, 0.0)])
+def test_lift_dev_leaves_values_past_total_untouched(n, r):
+    """cap > total: g[0, total) is the lift (zeros between the runs), g[total, cap) keeps what it held
+    (protocol.rs:96-144 resizes the caller's vector to total)."""
+    g = O.synth(n, SEED + 41, 2)
+    t = max(float(np.quantile(np.abs(g), r)), 6.103515625e-05) if r > 0 else 0.0
+    wire = SP.grad_drop_dev(dev(g), t)
+    cap = n + 3000
+    out = torch.full((cap,), 9.0, dtype=torch.float32, device="cuda")
+    assert _lift_into(wire, out, cap) == n
+    assert_bitexact(out[:n].cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=n))
+    assert torch.all(out[n:] == 9.0)
+
+
+@pytest.mark.parametrize("lens", [[4096], [4097], [8192 + 33], [33, 32, 31, 4096 * 3 + 1], [1, 2, 3] * 50])
+def test_lift_dev_long_runs_across_chunks(lens):
+    """Runs longer than one lane's share (> 32 values) go through the chunk queue, including runs that
+    are whole multiples of the 4096-value chunk and one value past it."""
+    rng = np.random.default_rng(sum(lens))
+    parts, total = [], 0
+    body = []
+    for ln in lens:
+        off = int(rng.integers(1, 40))
+        body.append(np.array([off, ln], np.uint32).tobytes())
+        body.append(rng.integers(0, 0x7C00, ln).astype(np.uint16).tobytes())  # finite f16 values
+        total += off + ln
+    total += 7
+    b = np.uint64(total).tobytes() + b"".join(body)
+    want = O.grad_lift(b, cap=total)
+    out = torch.full((total,), 5.0, dtype=torch.float32, device="cuda")
+    assert _lift_into(to_dev(b), out, total) == total
+    assert_bitexact(out.cpu().numpy(), want)
+
+
+def test_lift_dev_walks_longer_than_the_noted_records():
+    """Offsets of 0 after the first record refuse every speculative start, so segment 0's walk spans the
+    whole stream: records past the 32 it notes are walked again by sl_place's overflow path."""
+    rng = np.random.default_rng(3)
+    nrec = 3000
+    lens = rng.integers(1, 4, nrec)
+    offs = np.zeros(nrec, np.int64)
+    offs[0] = 5
+    body = []
+    for o, ln in zip(offs, lens):
+        body.append(np.array([o, ln], np.uint32).tobytes())
+        body.append(rng.integers(0, 0x7C00, ln).astype(np.uint16).tobytes())
+    total = int(offs.sum() + lens.sum()) + 11
+    b = np.uint64(total).tobytes() + b"".join(body)
+    L = ono_amd.lib()
+    before = L.ono_sparse_lift_fallbacks()
+    out = torch.empty(total, dtype=torch.float32, device="cuda")
+    assert _lift_into(to_dev(b), out, total) == total
+    assert L.ono_sparse_lift_fallbacks() == before  # the parallel parse held (one walk, verified)
+    assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
