@@ -591,7 +591,7 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 //  2. sl_place, 16 lanes per segment: the window's prefix, the checks, and
 //     each noted record placed by one lane (runs longer than kShortP queued
 //     in chunks; no record is walked again).
-// (64 MiB gradient at 10 % kept on MI355X: 40 + 27 + 4 us against 81 us of
+// (64 MiB gradient at 10 % kept on MI355X: 37 + 27 + 4 us against 81 us of
 // kernels for the six-launch design it replaced; the walks are a chain of
 // dependent LDS reads per thread, so sl_index is latency-bound.  Tried and
 // dropped: the zero-fill on a side stream (event cost > overlap), a
@@ -784,19 +784,6 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
     const size_t lo = 8 + w * kWin, hi = lo + kWin + kMarg < nbytes ? lo + kWin + kMarg : nbytes;
     const uint64_t total = stream_total(b);
     if (w == 0 && threadIdx.x == 0) *qcount = 0;  // sl_place's long-run queue
-    if (total <= cap) {  // this workgroup's share of g[0, total) = 0 (grad.fill(0); resize(total, 0))
-        const size_t W = gridDim.x;
-        if (vec) {
-            const size_t n4 = total / 4, a = n4 * w / W, z = n4 * (w + 1) / W;
-            const f4s zero = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (size_t i = a + threadIdx.x; i < z; i += kLW) __builtin_nontemporal_store(zero, (f4s *)g + i);
-            if (w == W - 1)
-                for (size_t i = 4 * n4 + threadIdx.x; i < total; i += kLW) g[i] = 0.0f;
-        } else {
-            const size_t a = total * w / W, z = total * (w + 1) / W;
-            for (size_t i = a + threadIdx.x; i < z; i += kLW) g[i] = 0.0f;
-        }
-    }
     stage_bytes<kLW, kWin + kMarg>(lw, b, lo, (hi - lo) / 2);
     __syncthreads();
     const Bytes src{b, as_lds(lw), lo, (hi - lo) / 2};
@@ -846,6 +833,21 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
         rcnt[s] = cnt;
     }
     if (threadIdx.x == 0) wsum[w] = ta;
+    // this workgroup's share of g[0, total) = 0 (grad.fill(0); resize(total, 0)), after the walks: stores
+    // issued before the staging loads would hold them up (one vmcnt counter for both)
+    if (total <= cap) {
+        const size_t W = gridDim.x;
+        if (vec) {
+            const size_t n4 = total / 4, a = n4 * w / W, z = n4 * (w + 1) / W;
+            const f4s zero = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (size_t i = a + threadIdx.x; i < z; i += kLW) __builtin_nontemporal_store(zero, (f4s *)g + i);
+            if (w == W - 1)
+                for (size_t i = 4 * n4 + threadIdx.x; i < total; i += kLW) g[i] = 0.0f;
+        } else {
+            const size_t a = total * w / W, z = total * (w + 1) / W;
+            for (size_t i = a + threadIdx.x; i < z; i += kLW) g[i] = 0.0f;
+        }
+    }
 }
 
 // A run of n values from stream byte vp into g[gi ..]: short runs by the
