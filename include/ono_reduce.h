@@ -149,8 +149,9 @@ int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *bu
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame
  * received into device memory); same results and errors as ono_sparse_lift.
  * Both parse on the device: speculative record starts per 128-B segment,
- * verified walks, scan, expand; the reference's sequential host parse runs
- * only when the speculation is refuted or the stream is malformed.          */
+ * verified walks that note every record, one lane per record placing its
+ * run; the reference's sequential host parse runs only when the speculation
+ * is refuted or the stream is malformed.  g[total, cap) is left untouched.  */
 int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
                         void *stream);
 /* lifts so far (this process) that took the sequential host parse        */
