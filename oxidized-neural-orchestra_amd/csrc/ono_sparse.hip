@@ -310,17 +310,15 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
 // index after it, n if none), in two levels within one launch: each
 // workgroup scans a chunk of kRecChunk tiles (LDS-staged, DPP wave scans;
 // the suffix min as a forward scan over the chunk reversed) into chunk-local
-// prefixes and publishes the chunk's aggregate; the workgroup that arrives
-// last (one agent-scope counter, one arrival per workgroup) turns the
-// aggregates into per-chunk carries and the totals.  sp_move adds its
-// chunk's carry.
-constexpr int kRecT = 256, kRecPer = 4, kRecChunk = kRecT * kRecPer;  // 1024 tiles per workgroup
-__global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, uint4 *agg, uint4 *carry,
-                                                      uint32_t *counter, size_t ntiles, uint32_t n, uint64_t *totals) {
+// prefixes and publishes the chunk's aggregate.  Each sp_move wave folds the
+// aggregates before / after its chunk into the chunk's carry itself (no
+// arrival counter, no serial pass over the chunks).
+constexpr int kRecT = 256, kRecPer = 2, kRecChunk = kRecT * kRecPer;  // 512 tiles per workgroup
+__global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, uint4 *agg, size_t ntiles,
+                                                      uint32_t n) {
     __shared__ uint32_t la[kRecChunk], lb[kRecChunk];
     __shared__ uint32_t rf[kRecChunk], rs[kRecChunk], rp[kRecChunk], rq[kRecChunk];
     __shared__ uint32_t wa[kRecT / 64], wb[kRecT / 64], wc[kRecT / 64], wd[kRecT / 64];
-    __shared__ uint32_t is_last;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t c0 = (size_t)blockIdx.x * kRecChunk;
     const uint32_t m = (uint32_t)min((size_t)kRecChunk, ntiles - c0);
@@ -382,36 +380,44 @@ __global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *p
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < m; i += kRecT) pre[c0 + i] = make_uint4(rf[i], rs[i], rp[i], rq[i]);
-    // the chunk's aggregate, then one arrival; the last workgroup makes the carries
-    if (threadIdx.x == 0) {
-        agg[blockIdx.x] = make_uint4(tf, tsum, tm, tq);
-        const uint32_t before = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = before == gridDim.x - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!is_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (threadIdx.x == 0) {
-        const uint32_t G = gridDim.x;
-        uint32_t cf = 0, cs = 0, cm = 0;
-        for (uint32_t g = 0; g < G; g++) {  // forward carries (atomic loads: never a stale cached line)
-            const uint32_t af = __hip_atomic_load(&agg[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t as = __hip_atomic_load(&agg[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t am = __hip_atomic_load(&agg[g].z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            carry[g] = make_uint4(cf, cs, cm, 0u);
-            cf += af;
-            cs += as;
-            cm = max(cm, am);
+    if (threadIdx.x == 0) agg[blockIdx.x] = make_uint4(tf, tsum, tm, tq);  // the chunk's aggregate
+}
+
+// The carry of chunk c (sp_scan_rec's aggregates, G chunks): kept values and
+// runs before it, the last kept index + 1 before it (max), the first unkept
+// index after it (min, n if none) — one wave, its lanes over the chunks.
+__device__ __forceinline__ uint4 chunk_carry(const uint4 *agg, uint32_t G, uint32_t c, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t f = 0, r = 0, m = 0, q = n;
+    for (uint32_t j0 = 0; j0 < G; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const uint4 a = j < G ? agg[j] : make_uint4(0u, 0u, 0u, n);
+        if (j < c) {
+            f += a.x;
+            r += a.y;
+            m = max(m, a.z);
+        } else if (j > c) {
+            q = min(q, a.w);
         }
-        uint32_t cq = n;
-        for (uint32_t g = G; g-- > 0;) {  // backward carries
-            carry[g].w = cq;
-            cq = min(cq, __hip_atomic_load(&agg[g].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        }
-        totals[0] = cf;
-        totals[1] = cs;
-        __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next drop
     }
+    f = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(f), 63);
+    r = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(r), 63);
+    m = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(m), 63);
+    q = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(q), 63);
+    return make_uint4(f, r, m, q);
+}
+
+// The totals (kept values, runs) over all chunks, by one wave.
+__device__ __forceinline__ uint2 chunk_totals(const uint4 *agg, uint32_t G) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t f = 0, r = 0;
+    for (uint32_t j = lane; j < G; j += 64) {
+        const uint4 a = agg[j];
+        f += a.x;
+        r += a.y;
+    }
+    return make_uint2((uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(f), 63),
+                      (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(r), 63));
 }
 
 // One tile's slot -> its place in the wire, in 16-B chunks of the
@@ -502,14 +508,18 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
 // 1024 units (most tiles' whole image) issued at the same time, then the move.
 // Block 0 also writes the u64 total length and publishes the wire length.
 __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) void sp_move(
-    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, const uint4 *carry, size_t ntiles,
-    size_t n, const uint64_t *totals, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
-        for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
-        const uint64_t F = totals[0], R = totals[1];
-        host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
-        host_tot[1] = R;
-        if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
+    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, const uint4 *agg, size_t ntiles,
+    size_t n, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
+    const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
+        const uint2 t = chunk_totals(agg, G);
+        if (threadIdx.x == 0) {
+            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
+            const uint64_t F = t.x, R = t.y;
+            host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
+            host_tot[1] = R;
+            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
+        }
     }
     const uint32_t lane = threadIdx.x & 63;
     // wave-uniform (readfirstlane): scalar base addresses and branches
@@ -520,7 +530,7 @@ __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
     for (int k = 0; k < kMoveBatch; k++) v[k] = ldn4(src4 + lane + 64 * k);
     const uint2 a = recA[tile], hb = recB[tile];
-    const uint4 pl = pre[tile], cr = carry[tile / kRecChunk];  // chunk-local prefix + the chunk's carry
+    const uint4 pl = pre[tile], cr = chunk_carry(agg, G, (uint32_t)(tile / kRecChunk), (uint32_t)n);  // + carry
     const uint4 p = make_uint4(pl.x + cr.x, pl.y + cr.y, max(pl.z, cr.z), min(pl.w, cr.w));
     const uint32_t F = a.x & 0xFFFFu, R = a.x >> 16, nu16 = 4 * R + F;
     const uint32_t tile0 = (uint32_t)(tile * kTile), tend = (uint32_t)min((size_t)tile0 + kTile, n);
@@ -967,13 +977,16 @@ __global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const
     }
 }
 
-// the totals into the host-mapped words (the exact-size path of a small buffer)
-__global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
-    host_tot[0] = totals[0];
-    host_tot[1] = totals[1];
+// the totals into the host-mapped words (the exact-size path of a small buffer), one wave
+__global__ void sp_totals_out(const uint4 *agg, uint32_t G, uint64_t *host_tot) {
+    const uint2 t = chunk_totals(agg, G);
+    if (threadIdx.x == 0) {
+        host_tot[0] = t.x;
+        host_tot[1] = t.y;
+    }
 }
 
-// Scratch of the encoder (tile counts, run table, device totals, two host-
+// Scratch of the encoder (tile records, prefixes, the tile images, two host-
 // mapped words for the result), kept per (device, stream) and grown on
 // demand: the stream-ordered allocations it replaces cost more than the
 // kernels at 64 MiB.  Per stream, so stream-ordered drops on different
@@ -981,10 +994,9 @@ __global__ void sp_totals_out(const uint64_t *totals, uint64_t *host_tot) {
 struct Scratch {
     size_t tiles_cap = 0;
     uint2 *rec = nullptr;     // 2 x tiles_cap: recA, then recB
-    uint4 *pre = nullptr;     // tiles_cap chunk-local prefixes, then 2 x (tiles_cap / kRecChunk + 1): aggregates, carries
-    uint32_t *counter = nullptr;  // the record scan's arrival counter (zero between drops)
+    uint4 *pre = nullptr;     // tiles_cap chunk-local prefixes, then the chunk aggregates
     uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
-    uint64_t *totals_dev = nullptr, *host_tot = nullptr, *host_tot_dev = nullptr;
+    uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;
 };
 std::mutex g_scratch_mu;
 std::map<std::pair<int, hipStream_t>, Scratch> g_scratch;
@@ -994,10 +1006,7 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
     Scratch &sc = g_scratch[{dev, stream}];
-    if (!sc.totals_dev) {
-        ONO_HIP(hipMalloc((void **)&sc.counter, sizeof(uint32_t)));
-        ONO_HIP(hipMemset(sc.counter, 0, sizeof(uint32_t)));
-        ONO_HIP(hipMalloc((void **)&sc.totals_dev, 2 * sizeof(uint64_t)));
+    if (!sc.host_tot) {
         ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
     }
@@ -1263,22 +1272,19 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
     const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
-    uint4 *pre = sc->pre, *agg = sc->pre + sc->tiles_cap, *carry = agg + (sc->tiles_cap / kRecChunk + 1);
+    uint4 *pre = sc->pre, *agg = sc->pre + sc->tiles_cap;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     if (!nbytes_dev) tot[0] = tot[1] = 0;
-    uint64_t *totals = sc->totals_dev;
     hipError_t e = hipSuccess;
     if (ntiles) {
         hipLaunchKernelGGL(sp_image, dim3((unsigned)ntiles), dim3(kIT), 0, s, g, n, threshold, vec, sc->img, recA,
                            recB);
-        hipLaunchKernelGGL(sp_scan_rec, dim3((unsigned)nchunks), dim3(kRecT), 0, s, recA, pre, agg, carry,
-                           sc->counter, ntiles, (uint32_t)n, totals);
-    } else {
-        e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s);
+        hipLaunchKernelGGL(sp_scan_rec, dim3((unsigned)nchunks), dim3(kRecT), 0, s, recA, pre, agg, ntiles,
+                           (uint32_t)n);
     }
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip)
-        hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(1), 0, s, totals, sc->host_tot_dev);
+        hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, agg, (uint32_t)nchunks, sc->host_tot_dev);
         e = hipStreamSynchronize(s);
         if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
             return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu",
@@ -1286,7 +1292,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, carry, ntiles, n, totals, buf,
+    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, agg, ntiles, n, buf,
                        sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
