@@ -762,6 +762,31 @@ __device__ uint32_t seg_start(const Bytes &src, size_t s, size_t nbytes, uint64_
     return kNone;
 }
 
+// seg_start over the staged bytes alone, 32-bit positions: kUnknown when a
+// candidate's look-ahead leaves them (then seg_start decides).
+constexpr uint32_t kUnknown = 0xFFFFFFFEu;
+__device__ uint32_t seg_start_lds(lds_u16 *L, uint32_t lo, uint32_t lim, uint32_t s, uint32_t nbytes, uint64_t total) {
+    if (s == 0) return 8;
+    const uint32_t a = 8 + s * kSeg, hi = a + kSeg < nbytes ? a + kSeg : nbytes;
+    for (uint32_t p = a; p < hi; p += 2) {
+        uint32_t q = p;
+        uint64_t acc = 0;
+        bool ok = true;
+        for (int k = 0; k < kLook && q != nbytes; k++) {
+            if (nbytes - q < 8) { ok = false; break; }
+            if (q < lo || q + 8 > lim) return kUnknown;
+            lds_u16 *h = L + ((q - lo) >> 1);
+            const uint32_t off = (uint32_t)h[0] | (uint32_t)h[1] << 16, len = (uint32_t)h[2] | (uint32_t)h[3] << 16;
+            if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
+            acc += (uint64_t)off + len;
+            if (acc > total) { ok = false; break; }
+            q += 8 + 2 * len;
+        }
+        if (ok) return p;
+    }
+    return kNone;
+}
+
 // Block-wide sum of a u64 (the same value in every thread).
 template <int NT>
 __device__ __forceinline__ uint64_t block_sum64(uint64_t v) {
@@ -797,7 +822,11 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
     stage_bytes<kLW, kWin + kMarg>(lw, b, lo, (hi - lo) / 2);
     __syncthreads();
     const Bytes src{b, as_lds(lw), lo, (hi - lo) / 2};
-    const uint32_t mine = s < S ? seg_start(src, s, nbytes, total) : kNone;
+    // (device-path streams are below 4 GiB: 32-bit positions in the LDS loops)
+    const uint32_t lo32 = (uint32_t)lo, lim = (uint32_t)(lo + 2 * src.n16), nb32 = (uint32_t)nbytes;
+    lds_u16 *L = as_lds(lw);
+    uint32_t mine = s < S ? seg_start_lds(L, lo32, lim, (uint32_t)s, nb32, total) : kNone;
+    if (mine == kUnknown) mine = seg_start(src, s, nbytes, total);  // look-ahead past the staged bytes
     lp0[threadIdx.x] = mine;
     __syncthreads();
     uint64_t sum = 0;
@@ -806,7 +835,46 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
         size_t pos = mine;
         const size_t segend = 8 + (s + 1) * kSeg;
         uint4 *my = ent + s * kRecK;
-        for (;;) {
+        bool done = false;
+        {  // the walk while every record is staged and every start it meets is in this window:
+           // LDS reads only (no memory wait in the loop), 32-bit positions
+            // Every exit condition is computed first and tested once (the reads are clamped into the
+            // staged bytes), so a step is one divergent branch, not six.
+            uint32_t p = mine;
+            const uint32_t seg32 = (uint32_t)segend, s032 = (uint32_t)s0, S32 = (uint32_t)S;
+            for (;;) {
+                const bool end = p == nb32, cross = p >= seg32;
+                const uint32_t u = (p - 8) / kSeg, ui = u - s032;
+                const bool inwin = ui < (uint32_t)kLW, live = cross && u < S32;
+                const uint32_t pu = lp0[inwin ? ui : 0u];
+                const bool has = live && inwin && pu != kNone;
+                const bool land = has && p == pu, over = has && p > pu, leave = live && !inwin;
+                const bool hdr_ok = nb32 - p >= 8 && p + 8 <= lim;
+                const uint32_t pc = hdr_ok ? p : lo32;
+                lds_u16 *q = L + ((pc - lo32) >> 1);
+                const uint32_t off = (uint32_t)q[0] | (uint32_t)q[1] << 16, len = (uint32_t)q[2] | (uint32_t)q[3] << 16;
+                const bool len_ok = (nb32 - pc - 8) / 2 >= len;
+                if (end || land || over || leave || !hdr_ok || !len_ok) {
+                    // the end, a start (joined), a stepped-over start: done; a header not staged or
+                    // truncated, another window's start: the general walk takes over
+                    if (land) reached[u] = epoch;
+                    if (over) raise_bad(host_word, epoch);
+                    done = end || land || over;
+                    break;
+                }
+                if (cnt < (uint32_t)kRecK) {
+                    const bool whole = len <= 2 && p + 8 + 2 * len <= lim;
+                    const uint32_t v01 = len == 2 ? (uint32_t)q[4] | (uint32_t)q[5] << 16 : len == 1 ? (uint32_t)q[4] : 0u;
+                    my[cnt] = make_uint4(p | (whole ? 1u : 0u), (uint32_t)(sum + off), len, whole ? v01 : 0u);
+                }
+                cnt++;
+                sum += (uint64_t)off + len;
+                if (sum > total) { raise_bad(host_word, epoch); done = true; break; }
+                p += 8 + 2 * len;
+            }
+            pos = p;
+        }
+        for (; !done;) {
             if (pos == nbytes) break;  // the end of the stream
             if (pos >= segend) {
                 const size_t u = (pos - 8) / kSeg;
