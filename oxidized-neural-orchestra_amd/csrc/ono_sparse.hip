@@ -597,18 +597,18 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 //     or the end, noting each record (position, element offset within the
 //     walk, length, and a run of at most two values whole).  A block scan of
 //     the walks' sums of (offset + length) gives each segment's element index
-//     within the window.  The workgroups also zero g[0, total) between them.
-//  2. sl_place, 16 lanes per segment: the window's prefix, the checks, and
-//     each noted record placed by one lane (runs longer than kShortP queued
-//     in chunks; no record is walked again).
-// (64 MiB gradient at 10 % kept on MI355X: 37 + 27 + 4 us against 81 us of
-// kernels for the six-launch design it replaced; the walks are a chain of
+//     within the window.
+//  2. sl_place, a workgroup per 16 segments: the window's prefix, the checks,
+//     and the group's whole range of g written with its values and zeros
+//     (built in LDS and stored once when it is at most kImg values).
+//  3. sl_long: queued chunks (long runs outside an image, wide gaps).
+// (64 MiB gradient at 10 % kept on MI355X: 27 + 29 + 4 us against 81 us of
+// kernels for the six-launch design it replaced; the walks are chains of
 // dependent LDS reads per thread, so sl_index is latency-bound.  Tried and
 // dropped: the zero-fill on a side stream (event cost > overlap), a
 // tile-image fill that re-walks the records per 4096-value tile (58 us: ~10
-// walking lanes per workgroup), gap-zeroing by the records' lanes instead of
-// a zero-fill (50 us: per-lane scalar stores).)
-//  3. sl_long: the queued chunks, one workgroup each.
+// walking lanes per workgroup), gap-zeroing by the records' lanes (50 us:
+// per-lane scalar stores), a first-record mask of every position (+12 us).)
 // The speculation is checked, not trusted: the walks are exactly the
 // sequential parse iff every speculative start was reached and no walk failed
 // (records form a successor chain, so a walk that lands on a start has joined
@@ -808,8 +808,8 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v) {
 // rcnt = how many, ent[s K + j] = {byte position, the run's element offset
 // within the walk, length, its first two values} for the first K; per window:
 // wsum.
-__global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes, size_t S, size_t cap, float *g,
-                                                int vec, uint32_t epoch, uint32_t *p0g, uint32_t *gpre,
+__global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes, size_t S, uint32_t epoch,
+                                                uint32_t *p0g, uint32_t *gpre,
                                                 uint32_t *rcnt, uint4 *ent, uint32_t *reached, uint32_t *wsum,
                                                 uint32_t *qcount, uint64_t *host_word) {
     __shared__ uint2 lw8[(kWin + kMarg) / 8];
@@ -911,54 +911,92 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
         rcnt[s] = cnt;
     }
     if (threadIdx.x == 0) wsum[w] = ta;
-    // this workgroup's share of g[0, total) = 0 (grad.fill(0); resize(total, 0)), after the walks: stores
-    // issued before the staging loads would hold them up (one vmcnt counter for both)
-    if (total <= cap) {
-        const size_t W = gridDim.x;
-        if (vec) {
-            const size_t n4 = total / 4, a = n4 * w / W, z = n4 * (w + 1) / W;
-            const f4s zero = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (size_t i = a + threadIdx.x; i < z; i += kLW) __builtin_nontemporal_store(zero, (f4s *)g + i);
-            if (w == W - 1)
-                for (size_t i = 4 * n4 + threadIdx.x; i < total; i += kLW) g[i] = 0.0f;
-        } else {
-            const size_t a = total * w / W, z = total * (w + 1) / W;
-            for (size_t i = a + threadIdx.x; i < z; i += kLW) g[i] = 0.0f;
-        }
-    }
 }
 
-// A run of n values from stream byte vp into g[gi ..]: short runs by the
-// thread itself, longer ones as queued chunks of kLongChunk values for sl_long.
-__device__ __forceinline__ void put_run(float *g, const uint8_t *b, size_t gi, size_t vp, uint32_t n, uint4 *queue,
-                                        uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint32_t epoch) {
-    glb_u16 *q = (glb_u16 *)(b + vp);
-    if (n <= (uint32_t)kShortP) {
-        for (uint32_t i = 0; i < n; i++) g[gi + i] = from_f16_sp(q[i]);
-        return;
-    }
-    const uint32_t nc = (n + kLongChunk - 1) / kLongChunk;
+// A span of g for sl_long as chunks of kLongChunk: zeros (kind 1) or the f16
+// values from stream byte vp on (kind 0).  Reserved with one atomic (rare:
+// long runs, and the gaps of groups spanning more than kZeroMax values).
+__device__ __forceinline__ void queue_span(size_t dst, size_t vp, size_t n, uint32_t kind, uint4 *queue,
+                                           uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint32_t epoch) {
+    if (n == 0) return;
+    const uint32_t nc = (uint32_t)((n + kLongChunk - 1) / kLongChunk);
     const uint32_t k = atomicAdd(qcount, nc);
     if (k + nc > qcap || k + nc < k) { raise_bad(host_word, epoch); return; }  // only a refuted stream overfills it
     for (uint32_t c = 0; c < nc; c++) {
         const size_t o = (size_t)c * kLongChunk;
-        queue[k + c] = make_uint4((uint32_t)(gi + o), (uint32_t)(vp + 2 * o), min((uint32_t)kLongChunk, n - (uint32_t)o),
-                                  0u);
+        queue[k + c] = make_uint4((uint32_t)(dst + o), (uint32_t)(vp + 2 * o), (uint32_t)min((size_t)kLongChunk, n - o),
+                                  kind);
     }
 }
 
-// kPG lanes per segment: the window's prefix (a sum over the earlier windows'
-// totals), the speculation check (every start reached), the total check (the
-// records' offsets and lengths sum to at most the stream's total length:
-// every record lies in [0, total), protocol.rs:127-129), then each record of
-// the segment's walk placed by one lane (g was zeroed by sl_index).
+// sl_place: workgroup shape, the largest range built in LDS, its long-run queue, the widest range it zeroes
 constexpr int kPT = 256, kPG = 16, kPSeg = kPT / kPG;  // 16 segments per workgroup
+constexpr int kImg = 4096, kLQ = 32;
+constexpr size_t kZeroMax = 1u << 20;
 static_assert(kLW % kPSeg == 0, "a workgroup's segments share a window");
+
+// Where a record's values go: the LDS image of the group's range (dense
+// groups), or g itself (wide groups).  Runs longer than kShortP: the LDS
+// queue of the workgroup (image) or sl_long's queue (g).
+struct Place {
+    float *g;
+    const uint8_t *b;
+    uint64_t ea;     // the group's first element (image index 0)
+    float *img;      // nullptr: write g
+    uint32_t *lq, *lqn;  // LDS queue of long runs: {image index, stream byte, count} x kLQ
+    uint4 *queue;
+    uint32_t *qcount, qcap;
+    uint64_t *host_word;
+    uint32_t epoch;
+    __device__ void run(uint64_t gi, size_t vp, uint32_t n, bool carried, uint32_t v01) const {
+        if (carried) {
+            float *d = img ? img + (gi - ea) : g + gi;
+            if (n >= 1) d[0] = from_f16_sp((uint16_t)v01);
+            if (n == 2) d[1] = from_f16_sp((uint16_t)(v01 >> 16));
+            return;
+        }
+        glb_u16 *q = (glb_u16 *)(b + vp);
+        if (n <= (uint32_t)kShortP) {
+            float *d = img ? img + (gi - ea) : g + gi;
+            for (uint32_t i = 0; i < n; i++) d[i] = from_f16_sp(q[i]);
+            return;
+        }
+        if (img) {
+            const uint32_t k = atomicAdd(lqn, 1u);
+            if (k < (uint32_t)kLQ) {
+                lq[3 * k] = (uint32_t)(gi - ea);
+                lq[3 * k + 1] = (uint32_t)vp;
+                lq[3 * k + 2] = n;
+                return;
+            }
+            for (uint32_t i = 0; i < n; i++) img[gi - ea + i] = from_f16_sp(q[i]);  // (queue full: rare)
+            return;
+        }
+        queue_span(gi, vp, n, 0u, queue, qcount, qcap, host_word, epoch);
+    }
+};
+
+// kPG lanes per segment, kPSeg segments per workgroup (a "group"): the
+// window's prefix (a sum over the earlier windows' totals), the speculation
+// check (every start reached), the total check (the records' offsets and
+// lengths sum to at most the stream's total length: every record lies in
+// [0, total), protocol.rs:127-129), then the group's range of g, [E of its
+// first segment, E of the next group's) — the tail up to total for the last —
+// written with every value and zero in it (grad.fill(0); resize(total, 0);
+// the runs: protocol.rs:96-144):
+//  * up to kImg values (nearly every group at 10 % kept): built in LDS (zeros,
+//    then each noted record placed by one lane) and stored once, coalesced;
+//  * up to kZeroMax: zeroed in g by the workgroup, then the values scattered;
+//  * wider (a long gap in a sparse stream): the gaps before the records and
+//    the tail queued as zero chunks for sl_long, the values scattered.
 __global__ __launch_bounds__(kPT) void sl_place(float *g, const uint8_t *b, size_t nbytes, size_t S, size_t cap,
-                                                uint32_t epoch, const uint32_t *p0g, const uint32_t *gpre,
+                                                int vec, uint32_t epoch, const uint32_t *p0g, const uint32_t *gpre,
                                                 const uint32_t *rcnt, const uint4 *ent, const uint32_t *reached,
                                                 const uint32_t *wsum, uint4 *queue, uint32_t *qcount, uint32_t qcap,
                                                 uint64_t *host_word) {
+    __shared__ f4s img4[kImg / 4];
+    float *img = (float *)img4;
+    __shared__ uint32_t lq[3 * kLQ], lqn;
     const uint64_t total = stream_total(b);
     if (blockIdx.x == 0 && threadIdx.x == 0) host_word[1] = total;
     if (total > cap) return;  // ONO_E_SIZE: nothing is written
@@ -967,6 +1005,9 @@ __global__ __launch_bounds__(kPT) void sl_place(float *g, const uint8_t *b, size
     const uint32_t p = s < S ? p0g[s] : kNone;
     const uint32_t gp = s < S ? gpre[s] : 0u, cnt = s < S ? rcnt[s] : 0u;
     const uint32_t rc = s < S && lane == 0 ? reached[s] : 0u;
+    const size_t sn = sb + kPSeg;  // the next group's first segment
+    const bool last = sn >= S, wend = !last && sn % kLW == 0;
+    const uint32_t gpn = !last && !wend ? gpre[sn] : 0u, wsw = S > 0 ? wsum[w] : 0u, gpa = S > 0 ? gpre[sb] : 0u;
     // the lane's two records, loaded with the rest (no dependence on the prefix)
     const uint4 *my = ent + s * kRecK;
     uint4 r[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
@@ -987,27 +1028,63 @@ __global__ __launch_bounds__(kPT) void sl_place(float *g, const uint8_t *b, size
         for (int k = 0; k < U; k++) part += v[k];
     }
     const uint64_t wp = block_sum64<kPT>(part);
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && wp + wsum[w] > total) raise_bad(host_word, epoch);
-    if (p == kNone) return;
-    if (lane == 0 && s > 0 && rc != epoch) raise_bad(host_word, epoch);  // a speculative start off the chain
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && wp + wsw > total) raise_bad(host_word, epoch);
+    if (p != kNone && lane == 0 && s > 0 && rc != epoch) raise_bad(host_word, epoch);  // a start off the chain
+    // the group's range (uniform); a refuted stream may give nonsense: clamp into [0, total]
+    const uint64_t ea = min(S > 0 ? wp + gpa : 0, total);
+    uint64_t eb = last ? total : wend ? wp + wsw : wp + gpn;
+    eb = max(min(eb, total), ea);
+    const uint64_t R = eb - ea;
+    // the image starts at the 16-B boundary at or below ea (g 16-B aligned: whole-vector LDS reads and stores)
+    const uint64_t ia = vec ? ea & ~3ull : ea;
+    const int mode = eb - ia <= (uint64_t)kImg ? 0 : R <= (uint64_t)kZeroMax ? 1 : 2;  // image / zero + scatter / queue
+    if (threadIdx.x == 0) lqn = 0;
+    if (mode == 0) {
+        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(eb - ia + 3) / 4; i += kPT) img4[i] = z;
+    } else if (mode == 1) {
+        if (vec) {
+            const uint64_t a4 = (ea + 3) / 4, z4 = eb / 4;
+            const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (a4 < z4) {
+                for (uint64_t i = a4 + threadIdx.x; i < z4; i += kPT) __builtin_nontemporal_store(z, (f4s *)g + i);
+                if (threadIdx.x < 4 * a4 - ea) g[ea + threadIdx.x] = 0.0f;
+                if (threadIdx.x < eb - 4 * z4) g[4 * z4 + threadIdx.x] = 0.0f;
+            } else {
+                for (uint64_t i = ea + threadIdx.x; i < eb; i += kPT) g[i] = 0.0f;
+            }
+        } else {
+            for (uint64_t i = ea + threadIdx.x; i < eb; i += kPT) g[i] = 0.0f;
+        }
+    }
+    __syncthreads();  // the zeros before the values (mode 1: the zero stores have completed)
+    const Place P{g, b, ia, mode == 0 ? img : nullptr, lq, &lqn, queue, qcount, qcap, host_word, epoch};
     const uint64_t E = wp + gp;
-    const uint32_t m = min(cnt, (uint32_t)kRecK);
+    const uint32_t m = p != kNone ? min(cnt, (uint32_t)kRecK) : 0u;
     static_assert(kRecK == 2 * kPG, "two records per lane");
+    // mode 2: where each record's gap starts (the run before it ended): record j - 1's end by
+    // shuffles within the segment's 16 lanes (record j is lane j % 16's r[0] or r[1]), E for the first
+    const uint32_t end0 = r[0].y + r[0].z, end1 = r[1].y + r[1].z;
+    const uint32_t prev0 = (uint32_t)__shfl((int)end0, (int)((lane + kPG - 1) % kPG), kPG);
+    const uint32_t prev1 = (uint32_t)__shfl((int)end1, (int)((lane + kPG - 1) % kPG), kPG);
+    const uint64_t from[2] = {lane == 0 ? E : E + prev0, lane == 0 ? E + prev0 : E + prev1};
+    uint64_t stream_end = ~0ull;  // the end of the stream's last run, if this thread holds it
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const uint32_t j = lane + k * kPG;
         if (j >= m) break;
         const uint64_t gi = E + r[k].y;
         const uint32_t len = r[k].z;
-        if (gi > total || total - gi < len) { raise_bad(host_word, epoch); continue; }  // (never written past total)
-        if (r[k].x & 1u) {  // carried whole
-            if (len >= 1) g[gi] = from_f16_sp((uint16_t)r[k].w);
-            if (len == 2) g[gi + 1] = from_f16_sp((uint16_t)(r[k].w >> 16));
-        } else {
-            put_run(g, b, gi, (size_t)r[k].x + 8, len, queue, qcount, qcap, host_word, epoch);
+        const size_t pos = r[k].x & ~1u;
+        if (gi > total || total - gi < len || gi < ea || gi + len > eb) {  // (never outside the range)
+            raise_bad(host_word, epoch);
+            continue;
         }
+        if (mode == 2) queue_span(from[k], 0, gi - from[k], 1u, queue, qcount, qcap, host_word, epoch);
+        P.run(gi, pos + 8, len, r[k].x & 1u, r[k].w);
+        if (pos + 8 + 2 * (size_t)len == nbytes) stream_end = gi + len;
     }
-    if (cnt > (uint32_t)kRecK && lane == 0) {
+    if (cnt > (uint32_t)kRecK && lane == 0 && p != kNone) {
         // a walk of more than kRecK records (a true start refused nearby): the
         // rest walked again from the last stored one, stopping where sl_index stopped
         const uint4 e = my[kRecK - 1];  // the last stored record: {position, run start in the walk, length}
@@ -1026,22 +1103,58 @@ __global__ __launch_bounds__(kPT) void sl_place(float *g, const uint8_t *b, size
             const uint32_t off = (uint32_t)h[0] | (uint32_t)h[1] << 16, len = (uint32_t)h[2] | (uint32_t)h[3] << 16;
             if ((nbytes - pos - 8) / 2 < len) break;
             const uint64_t gi = E + cur + off;
-            if (gi > total || total - gi < len) { raise_bad(host_word, epoch); break; }
-            put_run(g, b, gi, pos + 8, len, queue, qcount, qcap, host_word, epoch);
+            if (gi > total || total - gi < len || gi < ea || gi + len > eb) { raise_bad(host_word, epoch); break; }
+            if (mode == 2) queue_span(E + cur, 0, off, 1u, queue, qcount, qcap, host_word, epoch);
+            P.run(gi, pos + 8, len, false, 0u);
+            if (pos + 8 + 2 * (size_t)len == nbytes) stream_end = gi + len;
             cur += (uint64_t)off + len;
             pos += 8 + 2 * (size_t)len;
         }
     }
+    // mode 2: the tail after the stream's last run (or all of g when there are no records)
+    if (mode == 2 && stream_end != ~0ull) queue_span(stream_end, 0, total - stream_end, 1u, queue, qcount, qcap,
+                                                      host_word, epoch);
+    if (mode == 2 && S == 0 && threadIdx.x == 0) queue_span(0, 0, total, 1u, queue, qcount, qcap, host_word, epoch);
+    if (mode != 0) return;
+    __syncthreads();  // the image's short runs and the long-run queue
+    const uint32_t nl = min(lqn, (uint32_t)kLQ);
+    for (uint32_t k = 0; k < nl; k++) {  // long runs: the whole workgroup copies each
+        const uint32_t a = lq[3 * k], vp = lq[3 * k + 1], n = lq[3 * k + 2];
+        glb_u16 *q = (glb_u16 *)(b + vp);
+        for (uint32_t i = threadIdx.x; i < n; i += kPT) img[a + i] = from_f16_sp(q[i]);
+    }
+    __syncthreads();
+    // the range out, coalesced: whole 16-B vectors of the image where they lie inside [ea, eb), the
+    // elements of the first and last vector that do one by one
+    const uint32_t n = (uint32_t)(eb - ia), nv = (n + 3) / 4;
+    const uint32_t skip = (uint32_t)(ea - ia);  // image elements before ea (another group's)
+    if (vec) {
+        for (uint32_t i = threadIdx.x; i < nv; i += kPT) {
+            const uint32_t e0 = 4 * i;
+            if (e0 >= skip && e0 + 4 <= n) {
+                __builtin_nontemporal_store(img4[i], (f4s *)(g + ia) + i);
+            } else {
+                for (uint32_t k = 0; k < 4; k++)
+                    if (e0 + k >= skip && e0 + k < n) g[ia + e0 + k] = img[e0 + k];
+            }
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += kPT) g[ia + i] = img[i];
+    }
 }
 
-// Queued chunks of long runs, one workgroup each (grid-stride).
+// Queued chunks of long runs and of wide groups' gaps, one workgroup each (grid-stride).
 __global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const uint4 *queue,
                                                const uint32_t *qcount, uint32_t qcap) {
     const uint32_t nq = min(*qcount, qcap);
     for (uint32_t k = blockIdx.x; k < nq; k += gridDim.x) {
         const uint4 e = queue[k];
-        glb_u16 *q = (glb_u16 *)(b + e.y);
-        for (uint32_t i = threadIdx.x; i < e.z; i += kSB) g[(size_t)e.x + i] = from_f16_sp(q[i]);
+        if (e.w) {  // zeros
+            for (uint32_t i = threadIdx.x; i < e.z; i += kSB) g[(size_t)e.x + i] = 0.0f;
+        } else {
+            glb_u16 *q = (glb_u16 *)(b + e.y);
+            for (uint32_t i = threadIdx.x; i < e.z; i += kSB) g[(size_t)e.x + i] = from_f16_sp(q[i]);
+        }
     }
 }
 
@@ -1215,11 +1328,12 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
         L.seg_cap = S;
         restamp = true;
     }
-    const size_t Wg = std::max<size_t>(1, W);  // (one workgroup zero-fills an empty stream's gradient)
+    const size_t Wg = std::max<size_t>(1, W);  // (an empty stream still gets one: it resets the long-run queue)
     int rc = grow(&L.win, L.win_cap, Wg + 1);
     // chunks of runs longer than kShortP: at most one per kLongChunk values plus one per such run
-    // chunks of runs longer than kShortP: at most one per kLongChunk values plus one per such run
-    const size_t qcap = (nbytes - 8) / (8 + 2 * (kShortP + 1)) + cap / kLongChunk + 1;
+    // queued chunks: of runs longer than kShortP (one per kLongChunk values plus one per such run) and of
+    // the gaps of groups wider than kZeroMax (one per kLongChunk zeros plus one per record, and the tail)
+    const size_t qcap = (nbytes - 8) / 8 + (nbytes - 8) / (8 + 2 * (kShortP + 1)) + 2 * (cap / kLongChunk) + 4;
     if (!rc) rc = grow(&L.queue, L.q_cap, qcap);
     if (rc) return rc;
     if (++L.epoch == 0) {  // stamps of 2^32 lifts ago could match again
@@ -1235,10 +1349,10 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     word[1] = 0;
     const uint32_t epoch = L.epoch;
     const int vec = ((uintptr_t)g & 15) == 0;
-    hipLaunchKernelGGL(sl_index, dim3((unsigned)Wg), dim3(kLW), 0, s, dbuf, nbytes, S, cap, g, vec, epoch, p0, gpre,
-                       rcnt, L.ent, reached, wsum, qcount, L.host_word_dev);
+    hipLaunchKernelGGL(sl_index, dim3((unsigned)Wg), dim3(kLW), 0, s, dbuf, nbytes, S, epoch, p0, gpre, rcnt, L.ent,
+                       reached, wsum, qcount, L.host_word_dev);
     hipLaunchKernelGGL(sl_place, dim3((unsigned)std::max<size_t>(1, (S + kPSeg - 1) / kPSeg)), dim3(kPT), 0, s, g,
-                       dbuf, nbytes, S, cap, epoch, p0, gpre, rcnt, L.ent, reached, wsum, L.queue, qcount,
+                       dbuf, nbytes, S, cap, vec, epoch, p0, gpre, rcnt, L.ent, reached, wsum, L.queue, qcount,
                        (uint32_t)qcap, L.host_word_dev);
     hipLaunchKernelGGL(sl_long, dim3((unsigned)std::min<size_t>(2048, qcap)), dim3(kSB), 0, s, g, dbuf, L.queue,
                        qcount, (uint32_t)qcap);

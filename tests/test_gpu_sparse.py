@@ -451,3 +451,27 @@ def test_lift_dev_walks_longer_than_the_noted_records():
     assert _lift_into(to_dev(b), out, total) == total
     assert L.ono_sparse_lift_fallbacks() == before  # the parallel parse held (one walk, verified)
     assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+@pytest.mark.parametrize("offs,lens,tail", [
+    ([], [], 3_000_000),                                   # no records: g is all tail (queued zero chunks)
+    ([1_500_000, 2_000_000, 10], [5, 40, 1], 2_500_000),  # gaps wider than a workgroup zeroes itself
+    ([200_000, 300_000, 7, 1], [3, 50, 2, 4100], 90_000),  # a group zeroed by its workgroup, then scattered
+    ([3, 1, 4, 1, 5], [9, 2, 6, 5, 3], 5),                  # a small range built in LDS
+])
+def test_lift_dev_range_modes(offs, lens, tail):
+    """Every element of g[0, total) is written exactly once, whatever a group's range: an LDS image for
+    small ranges, zero-then-scatter for medium ones, queued zero chunks for wide gaps and tails."""
+    rng = np.random.default_rng(len(offs) + tail)
+    body, total = [], 0
+    for o, ln in zip(offs, lens):
+        body.append(np.array([o, ln], np.uint32).tobytes())
+        body.append(rng.integers(0, 0x7C00, ln).astype(np.uint16).tobytes())
+        total += o + ln
+    total += tail
+    b = np.uint64(total).tobytes() + b"".join(body)
+    want = O.grad_lift(b, cap=total)
+    out = torch.full((total + 64,), 3.0, dtype=torch.float32, device="cuda")
+    assert _lift_into(to_dev(b), out, total + 64) == total
+    assert_bitexact(out[:total].cpu().numpy(), want)
+    assert torch.all(out[total:] == 3.0)
