@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int 
 //     and the group's whole range of g written with its values and zeros
 //     (built in LDS and stored once when it is at most kImg values).
 //  3. sl_long: queued chunks (long runs outside an image, wide gaps).
-// (64 MiB gradient at 10 % kept on MI355X: 27 + 29 + 4 us against 81 us of
+// (64 MiB gradient at 10 % kept on MI355X: 26 + 29.5 + 4 us against 81 us of
 // kernels for the six-launch design it replaced; the walks are chains of
 // dependent LDS reads per thread, so sl_index is latency-bound.  Tried and
 // dropped: the zero-fill on a side stream (event cost > overlap), a
@@ -768,21 +768,40 @@ constexpr uint32_t kUnknown = 0xFFFFFFFEu;
 __device__ uint32_t seg_start_lds(lds_u16 *L, uint32_t lo, uint32_t lim, uint32_t s, uint32_t nbytes, uint64_t total) {
     if (s == 0) return 8;
     const uint32_t a = 8 + s * kSeg, hi = a + kSeg < nbytes ? a + kSeg : nbytes;
-    for (uint32_t p = a; p < hi; p += 2) {
-        uint32_t q = p;
-        uint64_t acc = 0;
-        bool ok = true;
-        for (int k = 0; k < kLook && q != nbytes; k++) {
-            if (nbytes - q < 8) { ok = false; break; }
-            if (q < lo || q + 8 > lim) return kUnknown;
-            lds_u16 *h = L + ((q - lo) >> 1);
-            const uint32_t off = (uint32_t)h[0] | (uint32_t)h[1] << 16, len = (uint32_t)h[2] | (uint32_t)h[3] << 16;
-            if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
-            acc += (uint64_t)off + len;
-            if (acc > total) { ok = false; break; }
-            q += 8 + 2 * len;
+    // Candidates four at a time: their first-record tests share one read of 14 bytes (independent
+    // of each other, so one LDS latency), and only the survivors, in order, walk their look-ahead.
+    for (uint32_t p0 = a; p0 < hi; p0 += 8) {
+        if (p0 < lo || p0 + 14 > lim) return kUnknown;  // (not all staged: seg_start decides)
+        lds_u16 *h = L + ((p0 - lo) >> 1);
+        uint32_t u[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++) u[i] = h[i];
+        uint32_t cand = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t p = p0 + 2 * c, off = u[c] | u[c + 1] << 16, len = u[c + 2] | u[c + 3] << 16;
+            const bool ok = p < hi && nbytes - p >= 8 && off != 0 && len < 0x10000u && (nbytes - p - 8) / 2 >= len;
+            cand |= (ok ? 1u : 0u) << c;
         }
-        if (ok) return p;
+        while (cand) {
+            const uint32_t c = (uint32_t)__builtin_ctz(cand);
+            cand &= cand - 1;
+            const uint32_t p = p0 + 2 * c;
+            uint32_t q = p;
+            uint64_t acc = 0;
+            bool ok = true;
+            for (int k = 0; k < kLook && q != nbytes; k++) {
+                if (nbytes - q < 8) { ok = false; break; }
+                if (q < lo || q + 8 > lim) return kUnknown;
+                lds_u16 *hq = L + ((q - lo) >> 1);
+                const uint32_t off = (uint32_t)hq[0] | (uint32_t)hq[1] << 16, len = (uint32_t)hq[2] | (uint32_t)hq[3] << 16;
+                if (off == 0 || len >= 0x10000u || (nbytes - q - 8) / 2 < len) { ok = false; break; }
+                acc += (uint64_t)off + len;
+                if (acc > total) { ok = false; break; }
+                q += 8 + 2 * len;
+            }
+            if (ok) return p;
+        }
     }
     return kNone;
 }
