@@ -117,7 +117,11 @@ class Ctl:
         if world > 1:
             import torch.distributed as dist
             if not dist.is_initialized():
-                dist.init_process_group("gloo", rank=rank, world_size=world)
+                rdv = os.environ.get("ONO_BENCH_RDV")  # file:// rendezvous of the xGMI children (no port to race for)
+                if rdv:
+                    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=rdv)
+                else:
+                    dist.init_process_group("gloo", rank=rank, world_size=world)
             self.dist = dist
 
     def barrier(self) -> None:
@@ -1012,16 +1016,15 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
     handles over their own gloo group) and time both wires; a child that hangs
     or faults is killed at --xgmi-timeout and recorded, the parent's line
     survives.  Returns {"xgmi:f32": {...}, "xgmi:f16": {...}} from child rank 0."""
-    import socket
+    import shutil
     import subprocess
+    import tempfile
 
     n = coresident or world
-    port = None
-    if rank == 0:
-        with socket.socket() as sk:
-            sk.bind(("127.0.0.1", 0))
-            port = str(sk.getsockname()[1]).encode()
-    port = ctl.bcast_bytes(port).decode()
+    rdv_dir = None
+    if rank == 0:  # the children's gloo rendezvous: a fresh file on this node (a free port could be taken)
+        rdv_dir = tempfile.mkdtemp(prefix="ono_bench_rdv_").encode()
+    rdv_dir = ctl.bcast_bytes(rdv_dir).decode()
     import torch
     if torch.cuda.is_available():
         torch.cuda.synchronize()  # nothing of the parent's in flight while the children run
@@ -1029,13 +1032,13 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
            str(args.steps), "--warmup", str(args.warmup), "--bucket-mib", str(args.bucket_mib),
            "--sweep-mib", getattr(args, "sweep_mib", "")]
     procs = []
-    # The children rendezvous on their own port with rank 0 hosting the store:
-    # drop torchrun's agent-store settings (TORCHELASTIC_USE_AGENT_STORE=True
-    # would make every child a client of a store nobody serves on that port).
+    # The children rendezvous through their own file store: drop torchrun's
+    # agent-store settings (TORCHELASTIC_USE_AGENT_STORE=True would make every
+    # child a client of a store nobody serves).
     base_env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     for r in (range(n) if coresident else [rank]):
         env = dict(base_env, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+                   ONO_BENCH_RDV="file://" + os.path.join(rdv_dir, "store"))
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     deadline = time.time() + args.xgmi_timeout
     outs = []
@@ -1048,6 +1051,8 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
             err = f"killed after {args.xgmi_timeout:.0f} s; " + (err or "")
         outs.append((p.returncode, out, err))
     ctl.barrier()
+    if rank == 0:
+        shutil.rmtree(rdv_dir, ignore_errors=True)
     if rank != 0:
         return {}
     rc, out, err = outs[0]

@@ -13,9 +13,10 @@ is NaN — payload propagation through a + b is compiler-defined in the referenc
 """
 import json
 import os
-import socket
+import shutil
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -23,17 +24,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull", **env_extra) -> list:
-    port = _port()
+    # gloo rendezvous through a fresh file: a port picked free here could be taken by another
+    # process on the box before the ranks bind it (EADDRINUSE seen once in a round-2 session)
+    rdv_dir = tempfile.mkdtemp(prefix="ono_xgmi_rdv_")
+    rdv = "file://" + os.path.join(rdv_dir, "store")
     env = dict(os.environ, ONO_XGMI_TIMEOUT_S="10", PYTHONUNBUFFERED="1", ONO_XGMI_GATHER=gather, ONO_XGMI_DIAG="1",
                **env_extra)
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), str(port),
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "xgmi_worker.py"), str(r), str(n), rdv,
                                json.dumps(cases)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True) for r in range(n)]
     outs = []
@@ -47,6 +45,7 @@ def run_ranks(n: int, cases: list, timeout: float = 240.0, gather: str = "pull",
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        shutil.rmtree(rdv_dir, ignore_errors=True)
     return outs
 
 

@@ -7,7 +7,7 @@ loads/stores, flag barriers), with HBM standing in for the xGMI links.  The
 64-byte handles travel over a gloo group (the control channel the reference
 would use is its ring TCP links).
 
-usage: python xgmi_worker.py RANK NRANKS PORT CASES_JSON
+usage: python xgmi_worker.py RANK NRANKS (PORT | file://PATH) CASES_JSON
 Prints one JSON line: {"rank": r, "results": [{"case": ..., "ok": bool, "msg": str}, ...]}.
 """
 import json
@@ -219,10 +219,12 @@ def run_timeout(rank: int, n: int, how: str = "env") -> str | None:
 
 
 def main() -> int:
-    rank, n, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    rank, n, rdv = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     cases = json.loads(sys.argv[4])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=n, init_method=f"tcp://127.0.0.1:{port}")
+    # rendezvous through a file the parent made unique (no port to collide with), or a port
+    init = rdv if rdv.startswith("file://") else f"tcp://127.0.0.1:{int(rdv)}"
+    dist.init_process_group("gloo", rank=rank, world_size=n, init_method=init)
     results = []
     for case in cases:
         try:
