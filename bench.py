@@ -463,8 +463,8 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     gs = [g] + [ono_amd.kernels.synth(torch.empty(n, dtype=torch.float32, device="cuda"), SEED + j, 7)
                 for j in range(1, NG)]
     tg = [t] + [float(torch.quantile(x[: 1 << 20].abs().float(), 0.9).item()) for x in gs[1:]]
-    for j in range(NG):
-        ono_amd.sparse.grad_drop_async(gs[j], tg[j], buf, nbd)
+    for i in range(K):  # one untimed pass of the same loop first (clocks and caches as in the timed one)
+        ono_amd.sparse.grad_drop_async(gs[i % NG], tg[i % NG], buf, nbd)
     ono_amd.sparse.grad_drop_async(g, t, buf, nbd)
     torch.cuda.synchronize()
     assert int(nbd.item()) == len(wire) and bytes(buf[: len(wire)].cpu().numpy()) == wire
