@@ -655,23 +655,10 @@ struct Bytes {
         off = h0 | h1 << 16;
         len = h2 | h3 << 16;
     }
-    // n f16 values from p, widened, into dst[0, n)
-    __device__ __forceinline__ void values(size_t p, uint32_t n, float *dst) const {
-        if (staged(p, 2 * (size_t)n)) {
-            lds_u16 *q = lds + ((p - lo) >> 1);
-            for (uint32_t i = 0; i < n; i++) dst[i] = from_f16_sp(q[i]);
-        } else {
-            glb_u16 *q = (glb_u16 *)(b + p);
-            for (uint32_t i = 0; i < n; i++) dst[i] = from_f16_sp(q[i]);
-        }
-    }
     __device__ __forceinline__ uint16_t u16s(size_t p) const { return lds[(p - lo) >> 1]; }  // staged(p, 2)
     __device__ __forceinline__ uint32_t hdr32(size_t p) const {                             // staged(p, 4)
         lds_u16 *q = lds + ((p - lo) >> 1);
         return (uint32_t)q[0] | (uint32_t)q[1] << 16;
-    }
-    __device__ __forceinline__ float value(size_t p) const {
-        return from_f16_sp(staged(p, 2) ? lds[(p - lo) >> 1] : *(glb_u16 *)(b + p));
     }
 };
 __device__ __forceinline__ lds_u16 *as_lds(const uint16_t *p) { return (lds_u16 *)p; }
