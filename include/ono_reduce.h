@@ -225,7 +225,10 @@ int ono_ring_pull_grads(ono_ring *ring, void *stream);
 int ono_ring_pull_grads_dev(ono_ring *ring, float *residual_dev, float *grad_dev, size_t n,
                             void *stream);
 /* host-fed form (the reference's buffers live in host memory and arrive on
- * TCP): chunked H2D -> reduce -> D2H pipeline on three streams; blocking.    */
+ * TCP): chunked H2D -> reduce -> D2H pipeline on three streams; blocking.
+ * The exact schedules (HOPS, DIRECT, XGMI) pipeline sub-rounds (a slice of
+ * every chunk each, ono_plan_pull_grads_sub), so every element keeps its
+ * owner and chain; a TCP ring and the sparse mode run whole buckets.        */
 int ono_ring_pull_grads_host(ono_ring *ring, float *residual_host, float *grad_host, size_t n);
 /* Page-lock long-lived caller buckets (the reference's WorkerRingManager
  * Vec<f32>s live as long as the manager) so pull_grads_host DMAs them in
@@ -479,6 +482,15 @@ typedef struct {
  * steps; *count = the plan's length (call with cap 0 to size it).           */
 int ono_plan_pull_grads(int algo, int wire, int pos, int nranks, size_t size, int segments, ono_plan_step *steps,
                         size_t cap, size_t *count);
+/* sub-round sub_index of a host-fed HOPS / DIRECT round (what
+ * ono_ring_pull_grads_host runs for those schedules): elements
+ * [j sub, (j + 1) sub) of every chunk, sub = sub_elems rounded down to a
+ * multiple of 64 (at least 64); steps over empty slices are left out on both
+ * sides.  The sub-rounds in order equal the whole-bucket round bit for bit.  */
+int ono_plan_pull_grads_sub(int algo, int wire, int pos, int nranks, size_t size, size_t sub_elems, size_t sub_index,
+                            ono_plan_step *steps, size_t cap, size_t *count);
+/* how many sub-rounds of sub_elems per chunk cover a bucket (0: no plan)    */
+size_t ono_plan_sub_rounds(int nranks, size_t size, size_t sub_elems);
 /* ono_ps_step of rank pos over the RCCL communicator (reduce-scatter, fused
  * update, all-gather; shards of ceil(nparams / nranks), zero-padded)        */
 int ono_plan_ps_step(int pos, int nranks, size_t nparams, ono_plan_step *steps, size_t cap, size_t *count);
@@ -494,6 +506,10 @@ int ono_plan_buffers(int nranks, size_t size, size_t nparams, uint64_t *counts);
  * pull_grads: residuals[r], grads[r] are rank r's buckets of `size`.        */
 int ono_plan_run_local(int algo, int wire, int nranks, size_t size, int segments, float *const *residuals,
                        float *const *grads, void *stream);
+/* the host-fed sub-rounds of ono_plan_pull_grads_sub run one after another
+ * by co-resident ranks, as ono_plan_run_local runs whole rounds (nranks >= 2) */
+int ono_plan_run_local_sub(int algo, int wire, int nranks, size_t size, size_t sub_elems, float *const *residuals,
+                           float *const *grads, void *stream);
 /* ono_ps_step's plan: grads[r] (nparams) in, params[r] (nparams) out; shards[r]
  * is rank r's shard of the parameters (split at ceil(nparams / nranks)) and
  * its optimizer state v[r], s[r] (may be NULL for GD), updated in place;

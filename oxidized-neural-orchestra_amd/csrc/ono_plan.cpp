@@ -93,21 +93,31 @@ public:
 
 int mod(int x, int n) { return ((x % n) + n) % n; }
 
+// The part of every chunk one round works on: st[c], ln[c] (the whole chunks
+// for a whole-bucket round; a slice of each for a host-fed sub-round).  Steps
+// over an empty piece are left out on both sides of every exchange.
+struct Pieces {
+    std::vector<size_t> st, ln;
+    size_t slot;  // the receive-slot stride of the direct schedule (the largest chunk + 4)
+    bool whole;   // the pieces are the chunks themselves
+};
+
 // worker_ring.rs:112-204 as ncclSend/ncclRecv pairs, the fused codec kernels
 // between hops (see ono_ring.cpp's header for the kernel <-> line mapping).
-void hops(Builder &b, int wire, int pos, int n, const std::vector<size_t> &off) {
-    auto len = [&](int c) { return (uint64_t)(off[c + 1] - off[c]); };
-    auto slot = [&](int w, int c) { return Ref{ONO_PB_WIRE0 + w, ph(off[c])}; };
-    auto at = [&](int buf, int c) { return Ref{buf, off[c]}; };
+void hops(Builder &b, int wire, int pos, int n, const Pieces &pc) {
+    auto len = [&](int c) { return (uint64_t)pc.ln[c]; };
+    auto slot = [&](int w, int c) { return Ref{ONO_PB_WIRE0 + w, ph(pc.st[c])}; };
+    auto at = [&](int buf, int c) { return Ref{buf, pc.st[c]}; };
     const int next = mod(pos + 1, n), prev = mod(pos - 1, n);
     const float fn = (float)n;
-    b.kernel(ONO_POP_ENCODE_ZERO, {slot(0, pos), at(ONO_PB_RESIDUAL, pos)}, len(pos), wire);
+    if (len(pos)) b.kernel(ONO_POP_ENCODE_ZERO, {slot(0, pos), at(ONO_PB_RESIDUAL, pos)}, len(pos), wire);
     for (int st = 0; st < n - 1; st++) {  // scatter: out slot 0, in slot 1
         const int cs = mod(pos - st, n), cr = mod(pos - st - 1, n);
         b.group_begin();
-        b.p2p(ONO_PLAN_SEND, next, slot(0, cs), len(cs), wire);
-        b.p2p(ONO_PLAN_RECV, prev, slot(1, cr), len(cr), wire);
+        if (len(cs)) b.p2p(ONO_PLAN_SEND, next, slot(0, cs), len(cs), wire);
+        if (len(cr)) b.p2p(ONO_PLAN_RECV, prev, slot(1, cr), len(cr), wire);
         b.group_end();
+        if (!len(cr)) continue;
         if (st < n - 2)
             b.kernel(ONO_POP_ADD_ENCODE_ZERO, {slot(0, cr), at(ONO_PB_RESIDUAL, cr), slot(1, cr)}, len(cr), wire);
         else
@@ -118,10 +128,10 @@ void hops(Builder &b, int wire, int pos, int n, const std::vector<size_t> &off) 
     for (int j = 0; j < n - 1; j++) {
         const int cs = mod(pos + 1 - j, n), cr = mod(pos - j, n);
         b.group_begin();
-        b.p2p(ONO_PLAN_SEND, next, slot(bo, cs), len(cs), wire);
-        b.p2p(ONO_PLAN_RECV, prev, slot(bi, cr), len(cr), wire);
+        if (len(cs)) b.p2p(ONO_PLAN_SEND, next, slot(bo, cs), len(cs), wire);
+        if (len(cr)) b.p2p(ONO_PLAN_RECV, prev, slot(bi, cr), len(cr), wire);
         b.group_end();
-        b.kernel(ONO_POP_DECODE_SCALE, {at(ONO_PB_GRAD, cr), slot(bi, cr)}, len(cr), wire, fn);
+        if (len(cr)) b.kernel(ONO_POP_DECODE_SCALE, {at(ONO_PB_GRAD, cr), slot(bi, cr)}, len(cr), wire, fn);
         std::swap(bo, bi);
     }
 }
@@ -129,40 +139,49 @@ void hops(Builder &b, int wire, int pos, int n, const std::vector<size_t> &off) 
 // The direct schedule (ono_ring.cpp): all-to-all of chunk slices, the owner's
 // chain kernel in the reference order, the residual zeroed on the side stream
 // beside the all-gather of the owned chunk.
-void direct(Builder &b, int wire, int pos, int n, size_t size, const std::vector<size_t> &off) {
-    auto len = [&](int c) { return (uint64_t)(off[c + 1] - off[c]); };
-    const size_t slot = off[1] - off[0] + 4;
+void direct(Builder &b, int wire, int pos, int n, size_t size, const Pieces &pc) {
+    auto len = [&](int c) { return (uint64_t)pc.ln[c]; };
+    const size_t slot = pc.slot;
     const int c = mod(pos + 1, n);
     const bool f16 = wire == ONO_WIRE_F16;
+    const size_t sc = pc.st[c];
     b.group_begin();  // 1. rank q receives every rank's slice of the chunk it owns, c_q = q + 1
     for (int q = 0; q < n; q++) {
         if (q == pos) continue;
         const int cq = mod(q + 1, n), k = mod(q - c, n);
-        b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_RESIDUAL, off[cq]}, len(cq), ONO_WIRE_F32);
-        b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_RBUF, (uint64_t)k * slot + ph(off[c])}, len(c), ONO_WIRE_F32);
+        if (len(cq)) b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_RESIDUAL, pc.st[cq]}, len(cq), ONO_WIRE_F32);
+        if (len(c)) b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_RBUF, (uint64_t)k * slot + ph(sc)}, len(c), ONO_WIRE_F32);
     }
     b.group_end();
     // 2. the chain c, c+1, ..., c+n-1 (the owner's own slice last), grad = p / n
-    ono_plan_step &s = b.kernel(ONO_POP_DIRECT, {Ref{ONO_PB_GRAD, off[c]}, f16 ? Ref{ONO_PB_MSG, ph(off[c])} : kNone},
-                                len(c), wire, (float)n);
-    for (int k = 0; k < n - 1; k++) Builder::ref(s, 2 + k, Ref{ONO_PB_RBUF, (uint64_t)k * slot + ph(off[c])});
-    Builder::ref(s, 2 + n - 1, Ref{ONO_PB_RESIDUAL, off[c]});
-    s.flag = 0;  // zero the own slice only
+    if (len(c)) {
+        ono_plan_step &s = b.kernel(ONO_POP_DIRECT, {Ref{ONO_PB_GRAD, sc}, f16 ? Ref{ONO_PB_MSG, ph(sc)} : kNone},
+                                    len(c), wire, (float)n);
+        for (int k = 0; k < n - 1; k++) Builder::ref(s, 2 + k, Ref{ONO_PB_RBUF, (uint64_t)k * slot + ph(sc)});
+        Builder::ref(s, 2 + n - 1, Ref{ONO_PB_RESIDUAL, sc});
+        s.flag = 0;  // zero the own slice only
+    }
     // 3. the sent slices are zeroed on the side stream
     b.fork();
-    if (off[c] > 0) b.memset(Ref{ONO_PB_RESIDUAL, 0}, off[c], 1);
-    if (off[c + 1] < size) b.memset(Ref{ONO_PB_RESIDUAL, off[c + 1]}, size - off[c + 1], 1);
+    if (pc.whole) {
+        if (sc > 0) b.memset(Ref{ONO_PB_RESIDUAL, 0}, sc, 1);
+        if (sc + len(c) < size) b.memset(Ref{ONO_PB_RESIDUAL, sc + len(c)}, size - (sc + len(c)), 1);
+    } else {
+        for (int q = 0; q < n; q++)
+            if (q != c && len(q)) b.memset(Ref{ONO_PB_RESIDUAL, pc.st[q]}, len(q), 1);
+    }
     // 4. all-gather of the owned chunk: f32 values, or the f16 message decoded on arrival
     b.group_begin();
     for (int q = 0; q < n; q++) {
         if (q == pos) continue;
         const int cq = mod(q + 1, n);
         if (f16) {
-            b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_MSG, ph(off[c])}, len(c), ONO_WIRE_F16);
-            b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_GSTAGE, (uint64_t)q * slot + ph(off[cq])}, len(cq), ONO_WIRE_F16);
+            if (len(c)) b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_MSG, ph(sc)}, len(c), ONO_WIRE_F16);
+            if (len(cq))
+                b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_GSTAGE, (uint64_t)q * slot + ph(pc.st[cq])}, len(cq), ONO_WIRE_F16);
         } else {
-            b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_GRAD, off[c]}, len(c), ONO_WIRE_F32);
-            b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_GRAD, off[cq]}, len(cq), ONO_WIRE_F32);
+            if (len(c)) b.p2p(ONO_PLAN_SEND, q, Ref{ONO_PB_GRAD, sc}, len(c), ONO_WIRE_F32);
+            if (len(cq)) b.p2p(ONO_PLAN_RECV, q, Ref{ONO_PB_GRAD, pc.st[cq]}, len(cq), ONO_WIRE_F32);
         }
     }
     b.group_end();
@@ -170,8 +189,9 @@ void direct(Builder &b, int wire, int pos, int n, size_t size, const std::vector
         for (int q = 0; q < n; q++) {
             if (q == pos) continue;
             const int cq = mod(q + 1, n);
+            if (!len(cq)) continue;
             b.kernel(ONO_POP_DECODE_SCALE,
-                     {Ref{ONO_PB_GRAD, off[cq]}, Ref{ONO_PB_GSTAGE, (uint64_t)q * slot + ph(off[cq])}}, len(cq),
+                     {Ref{ONO_PB_GRAD, pc.st[cq]}, Ref{ONO_PB_GSTAGE, (uint64_t)q * slot + ph(pc.st[cq])}}, len(cq),
                      ONO_WIRE_F16, (float)n);
         }
     b.join();
@@ -214,22 +234,57 @@ int plan_pull_grads(std::vector<ono_plan_step> &out, int algo, int wire, int pos
         return set_error(ONO_E_ARG, "no plan for pos %d of %d ranks", pos, n);
     if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
     if (size < (size_t)n) return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, n);
-    const std::vector<size_t> off = split_chunks(size, (size_t)n);
     Builder b;
-    switch (algo) {
-    case ONO_ALGO_ALLREDUCE:
+    if (algo == ONO_ALGO_ALLREDUCE) {
         if (wire != ONO_WIRE_F32) return set_error(ONO_E_ARG, "an RCCL all-reduce cannot carry the f16 wire semantics");
         allreduce(b, n, size, segments);
-        break;
+        out.swap(b.steps);
+        return ONO_OK;
+    }
+    return plan_pull_grads_sub(out, algo, wire, pos, n, size, 0, 0);
+}
+
+size_t plan_sub_elems(size_t sub_elems) { return std::max<size_t>(64, sub_elems / 64 * 64); }
+
+size_t plan_sub_rounds(int n, size_t size, size_t sub_elems) {
+    if (n < 1 || size < (size_t)n) return 0;
+    const std::vector<size_t> off = split_chunks(size, (size_t)n);
+    const size_t maxc = off[1] - off[0], sub = plan_sub_elems(sub_elems);
+    return std::max<size_t>(1, (maxc + sub - 1) / sub);
+}
+
+int plan_pull_grads_sub(std::vector<ono_plan_step> &out, int algo, int wire, int pos, int n, size_t size,
+                        size_t sub_elems, size_t j) {
+    if (n < 2 || pos < 0 || pos >= n) return set_error(ONO_E_ARG, "no plan for pos %d of %d ranks", pos, n);
+    if (wire != ONO_WIRE_F32 && wire != ONO_WIRE_F16) return set_error(ONO_E_ARG, "wire=%d", wire);
+    if (size < (size_t)n) return set_error(ONO_E_SIZE, "bucket of %zu elements cannot be split over %d ranks", size, n);
+    const std::vector<size_t> off = split_chunks(size, (size_t)n);
+    Pieces pc;
+    pc.slot = off[1] - off[0] + 4;
+    pc.whole = sub_elems == 0;
+    pc.st.resize(n);
+    pc.ln.resize(n);
+    // sub-round j: elements [j sub, (j + 1) sub) of every chunk (sub a multiple of 64, so every
+    // piece keeps its chunk's 4-element phase); every element keeps its owner and its chain
+    const size_t sub = pc.whole ? 0 : plan_sub_elems(sub_elems);
+    if (!pc.whole && j >= plan_sub_rounds(n, size, sub_elems))
+        return set_error(ONO_E_ARG, "sub-round %zu of %zu", j, plan_sub_rounds(n, size, sub_elems));
+    for (int c = 0; c < n; c++) {
+        const size_t L = off[c + 1] - off[c], lo = pc.whole ? 0 : std::min(L, j * sub);
+        pc.st[c] = off[c] + lo;
+        pc.ln[c] = pc.whole ? L : std::min(L - lo, sub);
+    }
+    Builder b;
+    switch (algo) {
     case ONO_ALGO_HOPS:
-        hops(b, wire, pos, n, off);
+        hops(b, wire, pos, n, pc);
         break;
     case ONO_ALGO_DIRECT:
         if (n > ONO_MAX_INPUTS) return set_error(ONO_E_ARG, "direct schedule supports up to %d ranks", ONO_MAX_INPUTS);
-        direct(b, wire, pos, n, size, off);
+        direct(b, wire, pos, n, size, pc);
         break;
     default:
-        return set_error(ONO_E_ARG, "no exchange plan for algo %d", algo);
+        return set_error(ONO_E_ARG, "no %s plan for algo %d", pc.whole ? "exchange" : "sub-round", algo);
     }
     out.swap(b.steps);
     return ONO_OK;
@@ -291,6 +346,20 @@ int ono_plan_pull_grads(int algo, int wire, int pos, int nranks, size_t size, in
     b.steps.swap(p);
     return emit(b, steps, cap, count);
 }
+
+int ono_plan_pull_grads_sub(int algo, int wire, int pos, int nranks, size_t size, size_t sub_elems, size_t sub_index,
+                            ono_plan_step *steps, size_t cap, size_t *count) {
+    if (!count) return set_error(ONO_E_ARG, "count is NULL");
+    if (sub_elems == 0) return set_error(ONO_E_ARG, "sub_elems is 0 (the whole bucket: ono_plan_pull_grads)");
+    std::vector<ono_plan_step> p;
+    int rc = plan_pull_grads_sub(p, algo, wire, pos, nranks, size, sub_elems, sub_index);
+    if (rc) return rc;
+    Builder b;
+    b.steps.swap(p);
+    return emit(b, steps, cap, count);
+}
+
+size_t ono_plan_sub_rounds(int nranks, size_t size, size_t sub_elems) { return plan_sub_rounds(nranks, size, sub_elems); }
 
 int ono_plan_ps_step(int pos, int nranks, size_t nparams, ono_plan_step *steps, size_t cap, size_t *count) {
     if (!count) return set_error(ONO_E_ARG, "count is NULL");

@@ -596,6 +596,77 @@ extern "C" int ono_ring_unregister_host(ono_ring *r, void *p) {
     return set_error(ONO_E_ARG, "pointer was not registered");
 }
 
+// Host-fed round of the exact RCCL schedules (HOPS, DIRECT), as the xGMI form
+// does it (ono_xgmi.cpp): sub-round j takes elements [j sub, (j+1) sub) of
+// every chunk, so every element keeps its owner and its chain (the result is
+// the whole-bucket round's bit for bit) while the H2D of sub-round j+1
+// (hstream), the exchange of j (cstream) and the D2H of j-1 (dstream) overlap.
+// The host residual is zeroed once its sub-round has reached HBM.
+static int exact_pull_grads_host(ono_ring *r, int algo, float *res_host, float *grad_host) {
+    int rc = algo == ONO_ALGO_DIRECT ? alloc_direct(r) : ONO_OK;
+    if (rc) return rc;
+    const size_t want = std::max<size_t>(1, host_chunk_elems() / (size_t)r->n);
+    const size_t S = plan_sub_rounds(r->n, r->size, want), sub = plan_sub_elems(want);
+    if ((rc = ensure_events(r, S))) return rc;
+    const int n = r->n;
+    std::vector<size_t> st(n), ln(n);
+    auto piece = [&](size_t j) {
+        for (int q = 0; q < n; q++) {
+            const size_t L = r->off[q + 1] - r->off[q], lo = std::min(L, j * sub);
+            st[q] = r->off[q] + lo;
+            ln[q] = std::min(L - lo, sub);
+        }
+    };
+    PlanCtx c;
+    c.wire = r->wire;
+    c.base[ONO_PB_RESIDUAL] = r->residual;
+    c.base[ONO_PB_GRAD] = r->grad;
+    c.base[ONO_PB_WIRE0] = r->wbuf[0];
+    c.base[ONO_PB_WIRE1] = r->wbuf[1];
+    c.base[ONO_PB_RBUF] = r->rbuf;
+    c.base[ONO_PB_GSTAGE] = r->gstage;
+    c.base[ONO_PB_MSG] = r->msg;
+    auto zero_host = [&](size_t j) -> int {  // sub-round j has reached HBM: zero its host residual
+        ONO_HIP(hipEventSynchronize(r->ev_h[j]));
+        piece(j);
+        for (int q = 0; q < n; q++)
+            if (ln[q]) memset(res_host + st[q], 0, ln[q] * sizeof(float));
+        return ONO_OK;
+    };
+    auto rounds = [&]() -> int {
+        std::vector<ono_plan_step> plan;
+        for (size_t j = 0; j < S; j++) {
+            piece(j);
+            for (int q = 0; q < n; q++)
+                if (ln[q])
+                    ONO_HIP(hipMemcpyAsync(r->residual + st[q], res_host + st[q], ln[q] * sizeof(float),
+                                           hipMemcpyHostToDevice, r->hstream));
+            ONO_HIP(hipEventRecord(r->ev_h[j], r->hstream));
+            ONO_HIP(hipStreamWaitEvent(r->cstream, r->ev_h[j], 0));
+            int rc2 = plan_pull_grads_sub(plan, algo, r->wire, r->pos, n, r->size, want, j);
+            if (!rc2) rc2 = run_plan(r, plan, c, r->cstream);
+            if (rc2) return rc2;
+            ONO_HIP(hipEventRecord(r->ev_c[j], r->cstream));
+            ONO_HIP(hipStreamWaitEvent(r->dstream, r->ev_c[j], 0));
+            for (int q = 0; q < n; q++)
+                if (ln[q])
+                    ONO_HIP(hipMemcpyAsync(grad_host + st[q], r->grad + st[q], ln[q] * sizeof(float),
+                                           hipMemcpyDeviceToHost, r->dstream));
+            ONO_HIP(hipEventRecord(r->ev_d[j], r->dstream));
+            if (j > 0 && (rc2 = zero_host(j - 1))) return rc2;
+        }
+        return zero_host(S - 1);
+    };
+    rc = rounds();
+    // every copy into or out of the caller's buffers is done before we return, failed or not
+    const hipError_t e1 = hipStreamSynchronize(r->hstream), e2 = hipStreamSynchronize(r->cstream),
+                     e3 = hipStreamSynchronize(r->dstream);
+    if (rc) return rc;
+    for (hipError_t e : {e1, e2, e3})
+        if (e != hipSuccess) return hip_error(e, "host-fed exchange round", __FILE__, __LINE__);
+    return ONO_OK;
+}
+
 int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t n) {
     if (!r || !res_host || !grad_host) return set_error(ONO_E_ARG, "NULL argument");
     if (n != r->size) return set_error(ONO_E_SIZE, "buffer of %zu elements, ring of %zu", n, r->size);
@@ -608,7 +679,10 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
 
     if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // sub-round pipeline (ono_xgmi.cpp)
         return xgmi_pull_grads_host(r, res_host, grad_host, CH);
-    if (r->n > 1 && resolved_algo(r) != ONO_ALGO_ALLREDUCE) {  // whole-bucket exact schedules
+    const int algo = resolved_algo(r);
+    if (r->n > 1 && (algo == ONO_ALGO_HOPS || algo == ONO_ALGO_DIRECT) && r->fd_next < 0 && r->sparse_r <= 0.0f)
+        return exact_pull_grads_host(r, algo, res_host, grad_host);  // sub-round pipeline
+    if (r->n > 1 && algo != ONO_ALGO_ALLREDUCE) {  // whole-bucket: the TCP edge (its own pieces), sparse mode
         ONO_HIP(hipMemcpyAsync(r->residual, res_host, bytes, hipMemcpyHostToDevice, r->cstream));
         int rc = pull_grads_impl(r, r->residual, r->grad, r->cstream);
         if (rc) return rc;
@@ -1020,6 +1094,34 @@ int ono_plan_run_local(int algo, int wire, int nranks, size_t size, int segments
     free_plan_buffers(ranks);
     if (rc) return rc;
     if (e != hipSuccess) return hip_error(e, "local plans", __FILE__, __LINE__);
+    return ONO_OK;
+}
+
+int ono_plan_run_local_sub(int algo, int wire, int nranks, size_t size, size_t sub_elems, float *const *residuals,
+                           float *const *grads, void *stream) {
+    if (!residuals || !grads || nranks < 2 || nranks > ONO_MAX_INPUTS)
+        return set_error(ONO_E_ARG, "nranks must be in [2, %d]", ONO_MAX_INPUTS);
+    if (sub_elems == 0) return set_error(ONO_E_ARG, "sub_elems is 0 (the whole bucket: ono_plan_run_local)");
+    for (int r = 0; r < nranks; r++)
+        if (!residuals[r] || !grads[r]) return set_error(ONO_E_ARG, "NULL bucket for rank %d", r);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::vector<LocalRank> ranks(nranks);
+    for (int r = 0; r < nranks; r++) {
+        ranks[r].ctx.base[ONO_PB_RESIDUAL] = residuals[r];
+        ranks[r].ctx.base[ONO_PB_GRAD] = grads[r];
+    }
+    int rc = alloc_plan_buffers(ranks, nranks, size, 0, wire);
+    const size_t S = rc ? 0 : plan_sub_rounds(nranks, size, sub_elems);
+    for (size_t j = 0; !rc && j < S; j++) {  // the sub-rounds one after another, as the host-fed round orders them
+        for (int r = 0; r < nranks && !rc; r++) rc = plan_pull_grads_sub(ranks[r].plan, algo, wire, r, nranks, size,
+                                                                         sub_elems, j);
+        for (auto &R : ranks) R.pc = 0;
+        if (!rc) rc = run_plans_local(ranks, s);
+    }
+    const hipError_t e = hipStreamSynchronize(s);  // the scratch is freed below
+    free_plan_buffers(ranks);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_error(e, "local sub-round plans", __FILE__, __LINE__);
     return ONO_OK;
 }
 

@@ -173,6 +173,9 @@ _SIGS = {
     "ono_ps_step": (_i, [_vp, _fp, _fp, _vp]),
     "ono_plan_pull_grads": (_i, [_i, _i, _i, _i, _sz, _i, _vp, _sz, C.POINTER(C.c_size_t)]),
     "ono_plan_ps_step": (_i, [_i, _i, _sz, _vp, _sz, C.POINTER(C.c_size_t)]),
+    "ono_plan_pull_grads_sub": (_i, [_i, _i, _i, _i, _sz, _sz, _sz, _vp, _sz, C.POINTER(C.c_size_t)]),
+    "ono_plan_sub_rounds": (_sz, [_i, _sz, _sz]),
+    "ono_plan_run_local_sub": (_i, [_i, _i, _i, _sz, _sz, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _vp]),
     "ono_plan_buffers": (_i, [_i, _sz, _sz, C.POINTER(C.c_uint64)]),
     "ono_plan_run_local": (_i, [_i, _i, _i, _sz, _i, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _vp]),
     "ono_plan_run_local_ps": (_i, [_i, _sz, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),

@@ -36,6 +36,16 @@ def pull_grads(algo: str, wire: str, pos: int, nranks: int, size: int, segments:
     return _steps("ono_plan_pull_grads", ALGO[algo], WIRE[wire], pos, nranks, size, segments)
 
 
+def pull_grads_sub(algo: str, wire: str, pos: int, nranks: int, size: int, sub_elems: int, j: int) -> list[dict]:
+    """Sub-round j of a host-fed HOPS / DIRECT round (ono_plan_pull_grads_sub)."""
+    return _steps("ono_plan_pull_grads_sub", ALGO[algo], WIRE[wire], pos, nranks, size, sub_elems, j)
+
+
+def sub_rounds(nranks: int, size: int, sub_elems: int) -> int:
+    from ._lib import lib
+    return int(lib().ono_plan_sub_rounds(nranks, size, sub_elems))
+
+
 def ps_step(pos: int, nranks: int, nparams: int) -> list[dict]:
     return _steps("ono_plan_ps_step", pos, nranks, nparams)
 
@@ -56,6 +66,14 @@ def run_local(algo: str, wire: str, residuals, grads, segments: int = 1, stream=
     n = len(residuals)
     size = residuals[0].numel()
     call("ono_plan_run_local", ALGO[algo], WIRE[wire], n, size, segments, _ptrs(residuals), _ptrs(grads),
+         kernels.stream_handle(stream))
+
+
+def run_local_sub(algo: str, wire: str, residuals, grads, sub_elems: int, stream=None) -> None:
+    """The host-fed sub-rounds (ono_plan_run_local_sub) by co-resident ranks."""
+    n = len(residuals)
+    size = residuals[0].numel()
+    call("ono_plan_run_local_sub", ALGO[algo], WIRE[wire], n, size, sub_elems, _ptrs(residuals), _ptrs(grads),
          kernels.stream_handle(stream))
 
 

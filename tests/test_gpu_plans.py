@@ -43,6 +43,24 @@ def test_exact_plans_vs_oracle(algo, wire, n, length):
         assert not res[r].cpu().numpy().view(np.uint32).any(), f"rank {r}: residual not zeroed"
 
 
+@pytest.mark.parametrize("algo", ["hops", "direct"])
+@pytest.mark.parametrize("wire", ["f16", "f32"])
+@pytest.mark.parametrize("n,length,sub", [(2, 109386, 4096), (3, 2 ** 18 + 5, 1 << 14), (5, 65541, 64),
+                                          (8, 1000003, 1 << 16)])
+def test_host_fed_sub_rounds_vs_oracle(algo, wire, n, length, sub):
+    """The host-fed HOPS / DIRECT round's sub-rounds (ono_ring_pull_grads_host cuts the round into a
+    slice of every chunk each) run on the device one after another: bit-exact with the whole round."""
+    ins = [O.synth(length, SEED + 31, r) for r in range(n)]
+    res = [dev(x) for x in ins]
+    grads = [torch.full_like(r, 7.0) for r in res]
+    P.run_local_sub(algo, wire, res, grads, sub)
+    torch.cuda.synchronize()
+    want, _ = O.ring_pull_grads(ins, wire)
+    for r in range(n):
+        assert_bitexact(grads[r].cpu().numpy(), want[r], f"{algo}/{wire} rank {r}")
+        assert not res[r].cpu().numpy().view(np.uint32).any(), f"rank {r}: residual not zeroed"
+
+
 @pytest.mark.parametrize("segments", [1, 4])
 @pytest.mark.parametrize("n,length", [(2, (1 << 22) + 5), (3, 1000003), (8, (1 << 22) + 7)])
 def test_allreduce_plan_segments(segments, n, length):

@@ -313,6 +313,48 @@ def test_pull_grads_plans_vs_oracle(n, algo, wire):
             assert_bitexact(bufs[r]["residual"], er[r], f"{algo}/{wire} n={n} size={size} residual {r}")
 
 
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 16])
+@pytest.mark.parametrize("algo,wire", [("hops", "f16"), ("hops", "f32"), ("direct", "f16"), ("direct", "f32")])
+@pytest.mark.parametrize("sub", [64, 100, 1000])
+def test_host_fed_sub_round_plans_vs_oracle(n, algo, wire, sub):
+    """The host-fed HOPS / DIRECT round as sub-rounds (a 64-multiple slice of
+    every chunk each, empty slices left out on both sides): each sub-round's
+    plans match up across ranks, stay in bounds and race nothing, and the
+    sub-rounds in order give the whole-bucket result bit for bit."""
+    for size in (n, 1000 * n + 3, 4099):
+        if size < n:
+            continue
+        x = [O.synth(size, SEED + 29, r) for r in range(n)]
+        S = P.sub_rounds(n, size, sub)
+        maxc = -(-size // n)
+        assert S == max(1, -(-maxc // max(64, sub // 64 * 64)))
+        sizes, bufs = pull_buffers(n, size, wire, x)
+        cov = [np.zeros(size, bool) for _ in range(n)]
+        for j in range(S):
+            plans = [P.pull_grads_sub(algo, wire, r, n, size, sub, j) for r in range(n)]
+            for p in plans:
+                check_bounds(p, sizes)
+                check_streams(p)
+            covered = execute(plans, bufs, wire)
+            for r in range(n):
+                cov[r] |= covered[r]
+        eg, er = O.ring_pull_grads(x, wire)
+        for r in range(n):
+            assert cov[r].all(), f"{algo}/{wire} n={n} size={size} sub={sub}: rank {r}'s grad not covered"
+            assert_bitexact(bufs[r]["grad"], eg[r], f"{algo}/{wire} n={n} size={size} sub={sub} grad {r}")
+            assert_bitexact(bufs[r]["residual"], er[r], f"{algo}/{wire} n={n} size={size} sub={sub} residual {r}")
+
+
+def test_sub_round_plan_errors():
+    with pytest.raises(ono_amd.InvalidArgument):
+        P.pull_grads_sub("allreduce", "f32", 0, 2, 1000, 64, 0)  # the all-reduce is pipelined in chunks already
+    with pytest.raises(ono_amd.InvalidArgument):
+        P.pull_grads_sub("hops", "f16", 0, 2, 1000, 64, P.sub_rounds(2, 1000, 64))  # past the last sub-round
+    with pytest.raises(ono_amd.InvalidArgument):
+        P.pull_grads_sub("hops", "f16", 0, 2, 1000, 0, 0)
+    assert P.sub_rounds(4, 3, 64) == 0
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 13, 16])
 @pytest.mark.parametrize("segments", [1, 2, 4, 7])
 def test_allreduce_plans(n, segments):
