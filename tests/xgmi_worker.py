@@ -101,6 +101,17 @@ def run_case(rank: int, n: int, case: dict) -> str | None:
                     msg += f" own/n={int((got[bad] == own).sum())}"
                     lo, hi = int(bad.min()), int(bad.max())
                     msg += f" span=[{lo},{hi}]"
+                    # contiguous runs of wrong elements (page-sized runs point at address translation,
+                    # scattered ones at ordering); host-fed: does the ring's device staging hold the
+                    # right values (then the D2H copy is what went wrong)?
+                    cuts = np.flatnonzero(np.diff(bad) != 1)
+                    starts = np.concatenate(([bad[0]], bad[cuts + 1]))
+                    ends = np.concatenate((bad[cuts], [bad[-1]])) + 1
+                    runs = [(int(a), int(b - a)) for a, b in zip(starts, ends)]
+                    msg += f" runs={len(runs)} first_runs={runs[:6]}"
+                    if form in ("host", "host_registered"):
+                        dev = ring.grad.cpu().numpy()
+                        msg += f" dev_right={int(O.same_or_both_nan(dev[bad], expect[rank][bad]).sum())}"
                 return msg
             if bits(res_after).any():
                 return f"round {rd}: residual not zeroed ({np.count_nonzero(bits(res_after))} left)"
