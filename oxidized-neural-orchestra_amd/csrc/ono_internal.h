@@ -9,6 +9,9 @@
 
 #include "ono_reduce.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace ono {
 
 // Records a thread-local error message and returns `code`.
@@ -35,6 +38,20 @@ Scale make_scale(float divisor);
 // split_chunks (worker/src/middlewares/mod.rs:15-59): offsets of min(len, n) chunks
 std::vector<size_t> split_chunks(size_t len, size_t n);
 inline size_t ph(size_t off) { return off & 3u; }  // phase-match wire slots to chunk starts
+
+// Events that order a kernel's output before a copy on another stream (D2H by
+// a DMA engine, which reads memory past the GPU's L2): recorded with an
+// explicit system-scope release, so the kernel's dirty L2 lines are written
+// back before the copy starts whatever the runtime's default release scope.
+// ONO_COPY_EVENT_RELEASE=default leaves the scope to the runtime (measurement).
+inline unsigned copy_event_flags() {
+    static const unsigned f = [] {
+        const char *e = getenv("ONO_COPY_EVENT_RELEASE");
+        return e && !strcmp(e, "default") ? (unsigned)hipEventDisableTiming
+                                          : (unsigned)(hipEventDisableTiming | hipEventReleaseToSystem);
+    }();
+    return f;
+}
 
 // ---- kernel launchers (ono_kernels.hip); return hipSuccess or the launch error
 hipError_t launch_sum_scale(float *out, const float *const *ins, int k, size_t n, float divisor,

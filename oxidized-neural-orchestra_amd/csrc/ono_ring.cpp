@@ -554,8 +554,8 @@ static bool is_registered(ono_ring *r, const void *p, size_t bytes) {
 static int ensure_events(ono_ring *r, size_t nchunks) {
     for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
         while (v->size() < nchunks) {
-            hipEvent_t ev;
-            ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            hipEvent_t ev;  // ev_c: a chunk's result, read next by the D2H copy
+            ONO_HIP(hipEventCreateWithFlags(&ev, v == &r->ev_c ? copy_event_flags() : hipEventDisableTiming));
             v->push_back(ev);
         }
     return ONO_OK;

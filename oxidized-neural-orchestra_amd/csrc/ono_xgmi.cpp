@@ -370,8 +370,8 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     const size_t sub = std::max<size_t>(64, sub_elems / (size_t)n / 64 * 64);  // keeps the 4-element phases
     const size_t S = (r->maxc + sub - 1) / sub;
     while (x->ev.size() < 3 * S) {
-        hipEvent_t ev;
-        ONO_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipEvent_t ev;  // 3 j + 1: sub-round j's result, read next by the D2H copy
+        ONO_HIP(hipEventCreateWithFlags(&ev, x->ev.size() % 3 == 1 ? copy_event_flags() : hipEventDisableTiming));
         x->ev.push_back(ev);
     }
     std::vector<size_t> st(n), ln(n);
