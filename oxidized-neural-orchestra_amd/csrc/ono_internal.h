@@ -5,12 +5,11 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "ono_reduce.h"
-
-#include <cstdlib>
-#include <cstring>
 
 namespace ono {
 
