@@ -177,6 +177,32 @@ template <class Sh> void L_shot2(const Args &a, size_t nvec) {
     hipLaunchKernelGGL(k_shot2<Sh>, dim3((unsigned)((nvec + 127) / 128)), dim3(64), 0, g_s, a, nvec);
 }
 
+// f16 decode with 8 values per lane (one 16-B load) and both f32 stores
+// wave-contiguous (1 KiB each): lane l stores values 4l..4l+3 and 256+4l..,
+// which lanes l/2 and 32 + l/2 loaded (two dwords each, picked by l's parity)
+__global__ __launch_bounds__(64) void k_dec8(Args a, size_t nblk) {
+    const size_t blk = blockIdx.x;
+    if (blk >= nblk) return;
+    const int l = threadIdx.x;
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 h = ldn((const u4 *)a.in[0] + blk * 64 + l);
+    const int s0 = l >> 1, s1 = 32 + (l >> 1);
+    const bool odd = l & 1;
+    const uint32_t x0 = __shfl((int)h.x, s0), x1 = __shfl((int)h.y, s0), x2 = __shfl((int)h.z, s0),
+                   x3 = __shfl((int)h.w, s0);
+    const uint32_t y0 = __shfl((int)h.x, s1), y1 = __shfl((int)h.y, s1), y2 = __shfl((int)h.z, s1),
+                   y3 = __shfl((int)h.w, s1);
+    const uint32_t p0 = odd ? x2 : x0, p1 = odd ? x3 : x1, q0 = odd ? y2 : y0, q1 = odd ? y3 : y1;
+    const f4 r0 = {dec1((uint16_t)p0), dec1((uint16_t)(p0 >> 16)), dec1((uint16_t)p1), dec1((uint16_t)(p1 >> 16))};
+    const f4 r1 = {dec1((uint16_t)q0), dec1((uint16_t)(q0 >> 16)), dec1((uint16_t)q1), dec1((uint16_t)(q1 >> 16))};
+    stn((f4 *)a.out + blk * 128 + l, r0 * 0.125f);
+    stn((f4 *)a.out + blk * 128 + 64 + l, r1 * 0.125f);
+}
+void L_dec8(const Args &a, size_t nvec) {
+    const size_t nblk = nvec / 128;  // 512 values per wave (N a multiple of 512 here)
+    hipLaunchKernelGGL(k_dec8, dim3((unsigned)nblk), dim3(64), 0, g_s, a, nblk);
+}
+
 template <class Sh> void add_rows(std::vector<Row> &rows, const char *shape, int per_set) {
     const double b = Sh::bytes_per_elem * (double)N;
     rows.push_back({std::string(shape) + " loop", b, per_set, L_loop<Sh>, {}});
@@ -299,6 +325,9 @@ int main(int argc, char **argv) {
         add("chain8 L1 LO1 S0", 44, 10, L_run<ChainShape<1, 1, 0>>);
         add("chain8 L1 LO1 S1", 44, 10, L_run<ChainShape<1, 1, 1>>);
         add("chain8 L0 LO0 S0", 44, 10, L_run<ChainShape<0, 0, 0>>);
+    } else if (argc > 3 && !strcmp(argv[3], "dec8")) {
+        rows.push_back({"dec shot", DecShape::bytes_per_elem * (double)N, 2, L_shot<DecShape>, {}});
+        rows.push_back({"dec8 shuffled", DecShape::bytes_per_elem * (double)N, 2, L_dec8, {}});
     } else if (argc > 3 && !strcmp(argv[3], "skew")) {
         for (size_t sk : {(size_t)0, (size_t)256, (size_t)2048, (size_t)4096, (size_t)8192, (size_t)65536 + 512}) {
             char nm[64];
