@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ONO_ABI_VERSION 1
+#define ONO_ABI_VERSION 2
 #define ONO_UID_BYTES 128 /* sizeof(ncclUniqueId) */
 #define ONO_MAX_INPUTS 16 /* max k of ono_sum_scale_f32 */
 
@@ -182,24 +182,35 @@ int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device
  * are the reference's byte for byte ([u64 BE len][u32 BE kind][payload],
  * comms/src/protocol/msg.rs:120-191): DenseGrad (kind 1/2, f16 LE) or, with
  * ono_ring_set_sparse, SparseGrad (kind 3/4), so MI355X workers and reference
- * Rust workers of either serializer form one ring.  Errors: a frame of
- * another valid kind (0 control, 5 params, 6 data chunk) or of the wrong
- * length -> ONO_E_PROTO ("Received an invalid worker event"); a kind byte
- * >= 7 (msg.rs:187), a malformed sparse stream, a socket failure -> ONO_E_IO.
- * f16 wire, hop schedule; the hop arithmetic runs in HBM (fused codec
- * kernels), one D2H + H2D of the chunk per hop.                              */
+ * Rust workers of either serializer form one ring.  A received gradient of
+ * another length than the hop's chunk is added over the shorter length in the
+ * scatter (the zip of worker_ring.rs:141-143) and refused in the gather
+ * (ONO_E_PROTO; the reference's copy_from_slice at :200 panics).  Any other
+ * frame fails as WorkerHandle::recv_event + the ring would
+ * (ono_worker_event_check): ONO_E_PROTO "Received an invalid worker event" for
+ * the worker events Upgraded / Disconnect / Done / ReportLoss, ONO_E_IO for a
+ * kind byte >= 7 (msg.rs:187), "Unexpected message from worker" (params, data
+ * chunks, other commands), "loss diverged", malformed JSON, a malformed sparse
+ * stream and socket failures.  f16 wire, hop schedule; the hop arithmetic runs
+ * in HBM (fused codec kernels), one D2H + H2D of the chunk per hop.          */
 int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int device, int fd_prev,
                         int fd_next);
 /* The SparseCapable serializer of this worker (SerializerSpec sparse_capable{r};
- * Compressor::compress, comms/src/handles/compressor.rs:71-98): every chunk it
- * pushes is sent as a SparseGrad frame (kind 3) of its values with
- * |g| >= t, t = calculate_threshold(chunk, r); the scatter then zeroes only the
- * sent values of the residual (worker_ring.rs:126-133) and the gather keeps
- * only the sent values in grad (:177-193).  ratio in (0, 1]; 0 = the Base
- * (dense f16) serializer.  TCP rings only (n > 1): inside a node the dense
- * schedules move fewer bytes than a sparse stream is worth.  Every worker
- * accepts both gradient kinds whatever its own serializer
- * (handles/worker.rs:102-108).  `seed` starts the default sampler's stream.   */
+ * Compressor::compress, comms/src/handles/compressor.rs:71-98): for every chunk
+ * it pushes, t = calculate_threshold(chunk, r) and the grad_drop stream of the
+ * values with |g| >= t; that stream goes out as a SparseGrad frame (kind 3)
+ * when it is no longer than the chunk's f16 payload (2 bytes per value, :79),
+ * else the chunk goes out as a DenseGrad of f16(chunk) (:84-89).  The ring
+ * takes the branch push_grad's result selects (worker_ring.rs:125-134,
+ * 177-193): after a SparseGrad the scatter zeroes only the sent values of the
+ * residual and the gather keeps only the sent values in grad, leaving the
+ * owned residual chunk as it is (the reset at :178-184 is commented out, so it
+ * keeps the reduced sum into the next round); after a DenseGrad the scatter
+ * zeroes the chunk and the gather zeroes the owned residual at j == 0.  ratio
+ * in (0, 1]; 0 = the Base (dense f16) serializer.  TCP rings only (n > 1):
+ * inside a node the dense schedules move fewer bytes than a sparse stream is
+ * worth.  Every worker accepts both gradient kinds whatever its own serializer
+ * (handles/worker.rs:102-108).  `seed` starts the default sampler's stream.  */
 int ono_ring_set_sparse(ono_ring *ring, float ratio, uint64_t seed);
 /* Draws the threshold sample of one push: `amount` = min(len, 16384) distinct
  * indices of [0, len) into idx; return 0 on success.  Called for every sparse
@@ -210,6 +221,17 @@ int ono_ring_set_sparse(ono_ring *ring, float ratio, uint64_t seed);
  * NULL restores the default (ono_sparse_sample_default).                     */
 typedef int (*ono_sample_fn)(void *ctx, size_t len, uint32_t *idx, size_t amount);
 int ono_ring_set_sampler(ono_ring *ring, ono_sample_fn fn, void *ctx);
+/* WorkerHandle::recv_event's verdict on one received frame of this kind byte
+ * (comms/src/handles/worker.rs:82-130, protocol/msg.rs:160-191) as the ring
+ * sees it: ONO_OK for a gradient (kinds 1-4); kind 0 parses the JSON Command
+ * (serde's externally tagged snake_case form) — Upgraded / Disconnect / Done /
+ * a finite ReportLoss -> ONO_E_PROTO "Received an invalid worker event"
+ * (worker_ring.rs:136-138), a ReportLoss with a null (NaN) loss -> ONO_E_IO
+ * "loss diverged: NaN or Inf detected", another command -> ONO_E_IO
+ * "Unexpected message from worker", malformed JSON or an unknown command ->
+ * ONO_E_IO (the serde error); kinds 5 / 6 -> ONO_E_IO "Unexpected message from
+ * worker"; kind >= 7 -> ONO_E_IO "Received an invalid kind byte".  Host only.  */
+int ono_worker_event_check(uint32_t kind, const uint8_t *payload, size_t nbytes);
 int ono_ring_destroy(ono_ring *ring);
 /* the owned buckets (device pointers): grad = WorkerRingManager.grad,
  * residual = WorkerRingManager.residual                                      */
@@ -262,9 +284,14 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
 /* A ring with no collective library at all (ONO_ALGO_XGMI only): create,
  * export this rank's handle, pass every rank's handle (nranks x
  * ONO_XGMI_HANDLE_BYTES, rank order) to connect.  The handles travel out of
- * band, like the RCCL id.  Destroy is collective (a final barrier keeps this
- * rank's region mapped until every peer is done with it).                    */
-#define ONO_XGMI_HANDLE_BYTES 64 /* sizeof(hipIpcMemHandle_t) */
+ * band, like the RCCL id.  A handle is the region's IPC handle (64 bytes), the
+ * region's random 64-bit ring id and its size; connect maps every peer region,
+ * checks that every page of each mapping shows that peer's ring id (a stale
+ * import -> ONO_E_IO), and returns once every rank has connected (a device
+ * barrier).  Destroy is collective: each rank marks every peer region it is
+ * done with, closes its imports, and frees its own region once all peers have
+ * marked it (or the timeout passed).                                          */
+#define ONO_XGMI_HANDLE_BYTES 128 /* hipIpcMemHandle_t + ring id + region bytes + zero */
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
 int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);

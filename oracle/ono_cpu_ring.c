@@ -15,12 +15,17 @@
  * Timed region = the pull_grads() rounds only (residual refill is outside).
  *
  * Serializer: Base (dense f16, default) or, with --sparse R, SparseCapable{R}
- * (compressor.rs:71-98): every push is a SparseGrad frame (kind 3) of the
- * values with |g| >= calculate_threshold(chunk, R) (protocol.rs:33-86; sample
- * from ono_ref_sample_default at --sparse-seed above 16384 values); the scatter
- * zeroes only the sent values (worker_ring.rs:126-133), the gather keeps only
- * the sent values (:177-193).  Either serializer receives both kinds: a
- * SparseGrad lifts into the zero-filled decode buffer (handles/worker.rs:102-108).
+ * (compressor.rs:71-98): every push computes t = calculate_threshold(chunk, R)
+ * (protocol.rs:33-49; sample from ono_ref_sample_default at --sparse-seed above
+ * 16384 values) and the grad_drop stream of the values with |g| >= t
+ * (:57-86); the stream goes out as a SparseGrad frame (kind 3) when it is no
+ * longer than 2 bytes per value (compressor.rs:79), else the chunk goes out as
+ * a DenseGrad (:84-89).  The ring follows the push (worker_ring.rs:125-134,
+ * 177-193): sparse -> the scatter zeroes only the sent values, the gather keeps
+ * only the sent values in grad and leaves the owned residual alone; dense ->
+ * the scatter zeroes the chunk, the gather zeroes the owned residual at j == 0.
+ * Either serializer receives both kinds: a SparseGrad lifts into the
+ * zero-filled decode buffer (handles/worker.rs:102-108).
  *
  * usage: ono_cpu_ring --ranks N --len L --rounds R [--seed S] [--check] [--no-pin]
  * prints one JSON line: {"ranks":..,"len":..,"rounds":..,"s_per_round":..,"gib_s":..,"check":..}
@@ -129,21 +134,26 @@ static void set_nb(int fd) {
 
 
 /* push_grad (handles/worker.rs:157-174): the frame of this worker's serializer
- * for chunk ch; *t = the SparseCapable threshold (unused for Base). */
+ * for chunk ch; *sparse = 1 when it is a SparseGrad (push_grad's Some(*t)),
+ * 0 for a DenseGrad (None). */
 static size_t push_frame(worker_t *w, const float *ch, size_t cl, uint16_t *comp, uint8_t *frame, uint32_t *sidx,
-                         float *t) {
-    if (w->ratio <= 0.0f) {
-        ono_ref_f16_encode(comp, ch, cl);
-        return ono_ref_frame_dense(frame, comp, cl, 0);
+                         float *t, int *sparse) {
+    *sparse = 0;
+    if (w->ratio > 0.0f) {
+        const size_t m = cl < 16384 ? cl : 16384;
+        if (cl > 16384) ono_ref_sample_default(&w->state, cl, sidx, m);
+        *t = ono_ref_sparse_threshold_sample(ch, cl, cl > 16384 ? sidx : NULL, m, w->ratio);
+        size_t nb = ono_ref_grad_drop(frame + 12, ch, cl, *t);
+        if (nb <= cl * 2) { /* compressor.rs:79 */
+            uint64_t len = 4 + (uint64_t)nb;
+            for (int q = 0; q < 8; q++) frame[q] = (uint8_t)(len >> (56 - 8 * q));
+            frame[8] = 0; frame[9] = 0; frame[10] = 0; frame[11] = 3; /* SparseGrad, is_last = false */
+            *sparse = 1;
+            return 12 + nb;
+        }
     }
-    const size_t m = cl < 16384 ? cl : 16384;
-    if (cl > 16384) ono_ref_sample_default(&w->state, cl, sidx, m);
-    *t = ono_ref_sparse_threshold_sample(ch, cl, cl > 16384 ? sidx : NULL, m, w->ratio);
-    size_t nb = ono_ref_grad_drop(frame + 12, ch, cl, *t);
-    uint64_t len = 4 + (uint64_t)nb;
-    for (int q = 0; q < 8; q++) frame[q] = (uint8_t)(len >> (56 - 8 * q));
-    frame[8] = 0; frame[9] = 0; frame[10] = 0; frame[11] = 3; /* SparseGrad, is_last = false */
-    return 12 + nb;
+    ono_ref_f16_encode(comp, ch, cl); /* compress_dense_grad, compressor.rs:106-118 */
+    return ono_ref_frame_dense(frame, comp, cl, 0);
 }
 
 /* recv_event (handles/worker.rs:82-108): a DenseGrad decodes, a SparseGrad
@@ -201,13 +211,17 @@ static void *worker_main(void *arg) {
         for (int s = 0; s < n - 1; s++) {
             size_t cl = off[i + 1] - off[i];
             float t = 0.0f;
-            size_t fl = push_frame(w, w->residual + off[i], cl, comp, frame, sidx, &t);
+            int sparse = 0;
+            size_t fl = push_frame(w, w->residual + off[i], cl, comp, frame, sidx, &t, &sparse);
             size_t got = 0;
             if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, cap, &got)) {
                 fprintf(stderr, "xchg failed\n"); exit(3);
             }
-            if (w->ratio <= 0.0f) memset(w->residual + off[i], 0, cl * sizeof(float));
-            else for (size_t j = 0; j < cl; j++) if (fabsf(w->residual[off[i] + j]) >= t) w->residual[off[i] + j] = 0.0f;
+            if (sparse) { /* worker_ring.rs:126-132 */
+                for (size_t j = 0; j < cl; j++) if (fabsf(w->residual[off[i] + j]) >= t) w->residual[off[i] + j] = 0.0f;
+            } else {      /* :133 */
+                memset(w->residual + off[i], 0, cl * sizeof(float));
+            }
             i = (i + n - 1) % n;
             size_t m = recv_grad((const uint8_t *)inbuf, got, dec, off[i + 1] - off[i]);
             float *ch = w->residual + off[i];
@@ -223,14 +237,17 @@ static void *worker_main(void *arg) {
             for (int j = 0; j < n - 1; j++) {
                 size_t cl = off[i + 1] - off[i];
                 float t = 0.0f;
-                size_t fl = push_frame(w, w->grad + off[i], cl, comp, frame, sidx, &t);
+                int sparse = 0;
+                size_t fl = push_frame(w, w->grad + off[i], cl, comp, frame, sidx, &t, &sparse);
                 size_t got = 0;
                 if (xchg(fd_next, fd_prev, frame, fl, (uint8_t *)inbuf, cap, &got)) {
                     fprintf(stderr, "xchg failed\n"); exit(3);
                 }
-                if (w->ratio > 0.0f)
+                if (sparse) { /* :177-190; the owned residual is not reset (:178-184 commented out) */
                     for (size_t q = 0; q < cl; q++) if (fabsf(w->grad[off[i] + q]) < t) w->grad[off[i] + q] = 0.0f;
-                if (j == 0) memset(w->residual + off[i], 0, cl * sizeof(float));
+                } else if (j == 0) { /* :191-193 */
+                    memset(w->residual + off[i], 0, cl * sizeof(float));
+                }
                 i = (i + n - 1) % n;
                 size_t m = recv_grad((const uint8_t *)inbuf, got, dec, off[i + 1] - off[i]);
                 if (m != off[i + 1] - off[i]) { fprintf(stderr, "gather: chunk length mismatch\n"); exit(3); }

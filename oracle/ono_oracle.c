@@ -169,25 +169,59 @@ int ono_ref_ring_pull_grads(float *const *residual, float *const *grad, int n, s
     return 0;
 }
 
-/* One push of a chunk by a worker with serializer `ratio` (0 = Base): the
- * values the receiver ends up with (its decode, or its lift into a zero-filled
- * buffer) in msg; the threshold in *t (dense: +inf, nothing is "unsent").    */
-static void push_chunk(const float *ch, size_t cl, float ratio, uint64_t *state, float *msg, float *t) {
-    if (ratio <= 0.0f) {
-        for (size_t i = 0; i < cl; i++) msg[i] = ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i]));
-        *t = -1.0f;
-        return;
+/* Bytes grad_drop_into writes for `ch` at threshold t (protocol.rs:57-86):
+ * the u64 total, then per run of |g| >= t an offset, a length and 2 B per value. */
+static size_t drop_bytes(const float *ch, size_t cl, float t) {
+    size_t nb = 8, i = 0;
+    while (i < cl) {
+        if (fabsf(ch[i]) >= t) {
+            size_t s = i;
+            while (i < cl && fabsf(ch[i]) >= t) i++;
+            nb += 8 + 2 * (i - s);
+        } else {
+            i++;
+        }
     }
-    const size_t m = cl < 16384 ? cl : 16384;
-    uint32_t *idx = NULL;
-    if (cl > 16384) {
-        idx = (uint32_t *)malloc(m * sizeof(uint32_t));
-        ono_ref_sample_default(state, cl, idx, m);
+    return nb;
+}
+
+/* One push_grad of chunk ch by a worker with serializer `ratio` (0 = Base),
+ * handles/worker.rs:157-174 over Compressor::compress (compressor.rs:71-98):
+ *   Base:            DenseGrad f16(ch)                              -> None
+ *   SparseCapable:   t = calculate_threshold(ch, r) (the sampler state
+ *                    advances whatever is sent); grad_drop_into(ch, t); if the
+ *                    stream is no longer than the f16 payload, len * 2 bytes
+ *                    (:79), a SparseGrad                            -> Some(t)
+ *                    else the DenseGrad of f16(ch) (:84-89)         -> None
+ * msg = the values the receiver's recv_event hands the ring: the decoded f16
+ * payload, or the lift into a zero-filled buffer (worker.rs:84-108).
+ * Returns 1 when the push was sparse (Some(t)), 0 when dense (None).        */
+static int push_chunk(const float *ch, size_t cl, float ratio, uint64_t *state, float *msg, float *t) {
+    *t = 0.0f;
+    if (ratio > 0.0f) {
+        const size_t m = cl < 16384 ? cl : 16384;
+        uint32_t *idx = NULL;
+        if (cl > 16384) {
+            idx = (uint32_t *)malloc(m * sizeof(uint32_t));
+            ono_ref_sample_default(state, cl, idx, m);
+        }
+        *t = ono_ref_sparse_threshold_sample(ch, cl, idx, m, ratio);
+        free(idx);
+        if (drop_bytes(ch, cl, *t) <= cl * 2) { /* compressor.rs:79 */
+            for (size_t i = 0; i < cl; i++)
+                msg[i] = fabsf(ch[i]) >= *t ? ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i])) : 0.0f;
+            return 1;
+        }
     }
-    *t = ono_ref_sparse_threshold_sample(ch, cl, idx, m, ratio);
-    free(idx);
-    for (size_t i = 0; i < cl; i++)
-        msg[i] = fabsf(ch[i]) >= *t ? ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i])) : 0.0f;
+    for (size_t i = 0; i < cl; i++) msg[i] = ono_ref_f16_to_f32(ono_ref_f32_to_f16(ch[i]));
+    return 0;
+}
+
+int ono_ref_sparse_push_is_sparse(const float *ch, size_t cl, float ratio, uint64_t *state, float *t) {
+    float *msg = (float *)malloc(sizeof(float) * (cl ? cl : 1));
+    int sp = push_chunk(ch, cl, ratio, state, msg, t);
+    free(msg);
+    return sp;
 }
 
 int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, int n, size_t len,
@@ -207,9 +241,11 @@ int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, i
             int c = idx[r];
             float *ch = residual[r] + off[c];
             size_t cl = off[c + 1] - off[c];
-            push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r]);
-            if (ratio[r] <= 0.0f) memset(ch, 0, cl * sizeof(float));               /* :133 */
-            else for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) >= thr[r]) ch[i] = 0.0f; /* :128-131 */
+            if (push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r])) {
+                for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) >= thr[r]) ch[i] = 0.0f; /* :126-132 */
+            } else {
+                memset(ch, 0, cl * sizeof(float)); /* :133 */
+            }
         }
         for (int r = 0; r < n; r++) {
             int p = (r + n - 1) % n;
@@ -217,7 +253,7 @@ int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, i
             int c = idx[r];
             float *ch = residual[r] + off[c];
             size_t cl = off[c + 1] - off[c];
-            for (size_t i = 0; i < cl; i++) ch[i] += msg[(size_t)p * maxc + i]; /* :141-143 */
+            for (size_t i = 0; i < cl; i++) ch[i] += msg[(size_t)p * maxc + i]; /* :140-143 */
         }
     }
     /* gather (worker_ring.rs:155-204) */
@@ -227,26 +263,29 @@ int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, i
         memcpy(grad[r] + off[c], residual[r] + off[c], (off[c + 1] - off[c]) * sizeof(float)); /* :166 */
     }
     if (n == 1) {
-        memset(residual[0] + off[idx[0]], 0, (off[idx[0] + 1] - off[idx[0]]) * sizeof(float));
+        memset(residual[0] + off[idx[0]], 0, (off[idx[0] + 1] - off[idx[0]]) * sizeof(float)); /* :168-171 */
     } else {
         for (int j = 0; j < n - 1; j++) {
             for (int r = 0; r < n; r++) {
                 int c = idx[r];
                 float *ch = grad[r] + off[c];
                 size_t cl = off[c + 1] - off[c];
-                push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r]);
-                if (ratio[r] > 0.0f)
-                    for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) < thr[r]) ch[i] = 0.0f; /* :183-187 */
-                if (j == 0) memset(residual[r] + off[c], 0, cl * sizeof(float));            /* :191-193 */
+                if (push_chunk(ch, cl, ratio[r], &state[r], msg + (size_t)r * maxc, &thr[r])) {
+                    /* :177-190 — the owned residual is NOT reset (the zeroing is
+                     * commented out at :178-184): it keeps the reduced sum */
+                    for (size_t i = 0; i < cl; i++) if (fabsf(ch[i]) < thr[r]) ch[i] = 0.0f;
+                } else if (j == 0) {
+                    memset(residual[r] + off[c], 0, cl * sizeof(float)); /* :191-193 */
+                }
             }
             for (int r = 0; r < n; r++) {
                 int p = (r + n - 1) % n;
                 idx[r] = (idx[r] + n - 1) % n;
                 int c = idx[r];
-                memcpy(grad[r] + off[c], msg + (size_t)p * maxc, (off[c + 1] - off[c]) * sizeof(float)); /* :200 */
+                memcpy(grad[r] + off[c], msg + (size_t)p * maxc, (off[c + 1] - off[c]) * sizeof(float)); /* :199-200 */
             }
         }
-        for (int r = 0; r < n; r++) ono_ref_normalize(grad[r], len, (size_t)n);
+        for (int r = 0; r < n; r++) ono_ref_normalize(grad[r], len, (size_t)n); /* :101-105 */
     }
     free(off); free(msg); free(thr); free(idx);
     return 0;

@@ -49,15 +49,26 @@ size_t ono_ref_split_chunks(size_t len, size_t n, size_t *offsets);
 int ono_ref_ring_pull_grads(float *const *residual, float *const *grad, int nranks,
                             size_t len, int wire);
 /* The same round with each worker's serializer: ratio[r] == 0 -> Base (dense
- * f16 DenseGrad), ratio[r] in (0, 1] -> SparseCapable{ratio[r]}: every push
- * sends the values with |g| >= calculate_threshold(chunk, ratio) (sample drawn
- * with ono_ref_sample_default at state[r] above 16384 values; state advanced),
- * the scatter zeroes only the sent values (worker_ring.rs:126-133), the
- * gather keeps only the sent values in grad (:177-193).  Receivers add
- * (scatter) or copy (gather) the decoded / lifted chunk: a SparseGrad lifts
- * into a zero-filled buffer (comms/src/handles/worker.rs:102-108).          */
+ * f16 DenseGrad), ratio[r] in (0, 1] -> SparseCapable{ratio[r]}
+ * (Compressor::compress, comms/src/handles/compressor.rs:71-98): every push
+ * computes t = calculate_threshold(chunk, ratio) (sample drawn with
+ * ono_ref_sample_default at state[r] above 16384 values; state advanced) and
+ * the grad_drop stream; the push is a SparseGrad only when that stream is no
+ * longer than the chunk's f16 payload (len * 2 bytes, :79), else a DenseGrad.
+ * The ring then takes the branch push_grad's result selects
+ * (worker_ring.rs:125-134, 177-193):
+ *   scatter: sparse -> zero the sent values (|g| >= t); dense -> zero the chunk;
+ *   gather:  sparse -> grad keeps only the sent values (|g| < t -> 0) and the
+ *            owned residual chunk is left as it is (:178-184 commented out);
+ *            dense at j == 0 -> zero the owned residual chunk.
+ * Receivers add (scatter) or copy (gather) the decoded / lifted chunk: a
+ * SparseGrad lifts into a zero-filled buffer (handles/worker.rs:102-108).   */
 int ono_ref_ring_pull_grads_sparse(float *const *residual, float *const *grad, int nranks, size_t len,
                                    const float *ratio, uint64_t *state);
+/* One push of chunk ch by a worker of serializer `ratio`: 1 if it goes out as a
+ * SparseGrad (threshold in *t), 0 if as a DenseGrad; the sampler state advances
+ * as in the ring.                                                            */
+int ono_ref_sparse_push_is_sparse(const float *ch, size_t cl, float ratio, uint64_t *state, float *t);
 
 /* ---- sum-and-scale: out[i] = (((in0+in1)+in2)+...)/divisor ------------------
  * The f32-wire ring's per-chunk arithmetic (worker_ring.rs:141-143 then

@@ -86,6 +86,9 @@ def lib():
         L.ono_ref_ring_pull_grads_sparse.restype = C.c_int
         L.ono_ref_ring_pull_grads_sparse.argtypes = [C.POINTER(_fp), C.POINTER(_fp), C.c_int, C.c_size_t,
                                                      C.POINTER(C.c_float), C.POINTER(C.c_uint64)]
+        L.ono_ref_sparse_push_is_sparse.restype = C.c_int
+        L.ono_ref_sparse_push_is_sparse.argtypes = [_fp, C.c_size_t, C.c_float, C.POINTER(C.c_uint64),
+                                                    C.POINTER(C.c_float)]
         _lib = L
     return _lib
 
@@ -150,6 +153,16 @@ def ring_pull_grads_sparse(residuals: list[np.ndarray], ratios, states):
     if lib().ono_ref_ring_pull_grads_sparse(rp, gp, n, length, rat, st) != 0:
         raise ValueError("reference panics: fewer chunks than ranks")
     return grads, res, [st[i] for i in range(n)]
+
+
+def sparse_push(chunk: np.ndarray, ratio: float, state: int = 0):
+    """What a SparseCapable{ratio} worker's push_grad sends for `chunk`
+    (compressor.rs:71-98): (is_sparse, threshold, next sampler state)."""
+    ch = np.ascontiguousarray(chunk, dtype=np.float32)
+    st = C.c_uint64(state & (2 ** 64 - 1))
+    t = C.c_float(0.0)
+    sp = lib().ono_ref_sparse_push_is_sparse(_f(ch), ch.size, ratio, C.byref(st), C.byref(t))
+    return bool(sp), float(t.value), st.value
 
 
 def sample_default(state: int, length: int, amount: int):

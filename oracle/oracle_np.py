@@ -12,6 +12,8 @@ Reference (lminervino18/oxidized-neural-orchestra):
   averaging      machine_learning/src/param_manager.rs:183-188
   store          parameter_server/src/storage/blocking/{store,shard}.rs
   optimizers     machine_learning/src/optimization/*.rs
+  sparse codec   comms/src/sparse/protocol.rs:33-144
+  serializer     comms/src/handles/compressor.rs:71-98, handles/worker.rs:157-174
 """
 from __future__ import annotations
 
@@ -115,6 +117,176 @@ def ring_pull_grads(residuals: list[np.ndarray], wire: str = "f16"):
     f = F32(n)
     grads = [(g / f).astype(F32) for g in grads]
     return grads, res
+
+
+# ------------------------------------------------------------------ sparse codec
+SAMPLE_SIZE_MAX = 1 << 14                 # protocol.rs:21
+MIN_POSITIVE_F16 = F32(6.103515625e-05)   # f16::MIN_POSITIVE (protocol.rs:22)
+_G64 = 0x9E3779B97F4A7C15
+_MASK64 = (1 << 64) - 1
+
+
+def _mix64_int(z: int) -> int:
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _MASK64
+    return z ^ (z >> 31)
+
+
+def sample_default(state: int, length: int, amount: int):
+    """The library's stand-in for rand's index::sample (Floyd over splitmix64):
+    (indices in draw order, next state).  amount == length draws nothing."""
+    if amount >= length:
+        return np.arange(length, dtype=np.uint32), state
+    seen, out = set(), []
+    for j in range(length - amount, length):
+        state = (state + _G64) & _MASK64
+        t = _mix64_int(state) % (j + 1)
+        if t in seen:
+            t = j
+        seen.add(t)
+        out.append(t)
+    return np.array(out, dtype=np.uint32), state
+
+
+def calculate_threshold(residual: np.ndarray, r: float, sample_idx) -> F32:
+    """protocol.rs:33-49 over the drawn sample (the k-th order statistic does
+    not depend on the order the sample is drawn in)."""
+    if residual.size == 0:
+        return F32(0)
+    bits = residual.view(np.uint32)[np.asarray(sample_idx, dtype=np.int64)] & np.uint32(0x7FFFFFFF)  # abs
+    m = bits.size
+    with np.errstate(invalid="ignore"):
+        kf = F32(m) * (F32(1) - F32(r))          # f32 arithmetic
+    k = 0 if not (kf > 0) else int(kf)            # `as usize`: truncates, saturates at 0 (NaN -> 0)
+    k = min(max(k, 0), m - 1)
+    # total_cmp on non-negative values (NaN above +inf) is the order of the bit patterns
+    x = np.sort(bits)[k].view(F32)
+    return F32(np.fmax(x, MIN_POSITIVE_F16))     # f32::max ignores NaN
+
+
+def grad_drop(residual: np.ndarray, threshold) -> bytes:
+    """grad_drop_into (protocol.rs:57-86): [u64 LE len] then, per run of
+    |g| >= threshold, [u32 LE offset from the previous run's end][u32 LE run]
+    [f16 LE values]."""
+    g = np.ascontiguousarray(residual, dtype=F32)
+    keep = np.abs(g) >= F32(threshold)
+    edges = np.flatnonzero(np.diff(np.concatenate(([False], keep, [False])).astype(np.int8)))
+    starts, ends = edges[0::2], edges[1::2]
+    parts = [np.uint64(g.size).tobytes()]
+    last_end = 0
+    h = f32_to_f16_bits(g)
+    for a, b in zip(starts.tolist(), ends.tolist()):
+        parts.append(np.array([a - last_end, b - a], dtype="<u4").tobytes())
+        parts.append(h[a:b].astype("<u2").tobytes())
+        last_end = b
+    return b"".join(parts)
+
+
+def grad_lift(buf: bytes) -> np.ndarray:
+    """grad_lift_into (protocol.rs:96-144) into a fresh buffer; raises the
+    reference's error strings."""
+    if len(buf) < 8:
+        raise ValueError("The given sparse buffer is smaller than TOTAL_LEN_SIZE")
+    total = int.from_bytes(buf[:8], "little")
+    g = np.zeros(total, dtype=F32)
+    body = buf[8:]
+    gi = bi = 0
+    while bi < len(body):
+        if bi + 4 > len(body):
+            raise ValueError("Missing index bytes at grad lift")
+        gi += int.from_bytes(body[bi:bi + 4], "little")
+        bi += 4
+        if bi + 4 > len(body):
+            raise ValueError("Missing chunk length bytes at grad lift")
+        cl = int.from_bytes(body[bi:bi + 4], "little")
+        bi += 4
+        if gi > total or total - gi < cl:
+            raise ValueError("Gradient chunk exceeds target vector bounds")
+        if bi + 2 * cl > len(body):
+            raise ValueError("Truncated float data")
+        g[gi:gi + cl] = f16_bits_to_f32(np.frombuffer(body[bi:bi + 2 * cl], dtype="<u2"))
+        bi += 2 * cl
+        gi += cl
+    return g
+
+
+def push_grad(chunk: np.ndarray, ratio: float, state: int):
+    """WorkerHandle::push_grad (handles/worker.rs:157-174) over
+    Compressor::compress (compressor.rs:71-98): returns (what the receiver's
+    recv_event hands its ring, Some(threshold) -> float or None -> None, the
+    sampler state after the push, the wire payload's kind 1 or 3)."""
+    if ratio > 0:
+        m = min(chunk.size, SAMPLE_SIZE_MAX)
+        if chunk.size > SAMPLE_SIZE_MAX:
+            idx, state = sample_default(state, chunk.size, m)
+        else:
+            idx = np.arange(chunk.size)
+        t = calculate_threshold(chunk, ratio, idx)
+        buf = grad_drop(chunk, t)
+        if len(buf) <= chunk.size * 2:          # compressor.rs:79
+            return grad_lift(buf), t, state, 3
+    return quantize_f16(chunk), None, state, 1
+
+
+def ring_pull_grads_sparse(residuals: list[np.ndarray], ratios, states):
+    """One pull_grads() round of every worker, each with its own serializer
+    (ratio 0 = Base), written from worker_ring.rs:112-204 as the reference
+    states it.  Returns (grads, residuals_after, states_after)."""
+    n = len(residuals)
+    length = residuals[0].size
+    chunks = split_chunks(length, n)
+    if len(chunks) < n:
+        raise ValueError("reference panics: fewer chunks than ranks")
+    res = [np.array(r, dtype=F32, copy=True) for r in residuals]
+    grads = [np.zeros(length, dtype=F32) for _ in range(n)]
+    st = list(states)
+    i = list(range(n))
+    for _ in range(n - 1):                       # scatter, :121-144
+        events = []
+        for r in range(n):
+            lo, hi = chunks[i[r]]
+            ev, sent, st[r], _ = push_grad(res[r][lo:hi], ratios[r], st[r])
+            events.append(ev)
+            ch = res[r][lo:hi]
+            if sent is not None:                 # :126-132
+                ch[np.abs(ch) >= sent] = F32(0)
+            else:                                # :133
+                ch[:] = F32(0)
+        for r in range(n):
+            i[r] = (i[r] + n - 1) % n            # :140
+            lo, hi = chunks[i[r]]
+            agg = events[(r - 1) % n]
+            k = min(hi - lo, agg.size)           # the zip stops at the shorter
+            res[r][lo:lo + k] += agg[:k]
+    for r in range(n):                           # gather, :163-166
+        i[r] = (r + 1) % n
+        lo, hi = chunks[i[r]]
+        grads[r][lo:hi] = res[r][lo:hi]
+    if n == 1:                                   # :168-171
+        lo, hi = chunks[i[0]]
+        res[0][lo:hi] = F32(0)
+        return grads, res, st
+    for j in range(n - 1):                       # :173-201
+        events = []
+        for r in range(n):
+            lo, hi = chunks[i[r]]
+            ev, sent, st[r], _ = push_grad(grads[r][lo:hi], ratios[r], st[r])
+            events.append(ev)
+            if sent is not None:                 # :177-190 (the residual is not touched)
+                ch = grads[r][lo:hi]
+                ch[np.abs(ch) < sent] = F32(0)
+            elif j == 0:                         # :191-193
+                res[r][lo:hi] = F32(0)
+        for r in range(n):
+            i[r] = (i[r] + n - 1) % n            # :199
+            lo, hi = chunks[i[r]]
+            acc = events[(r - 1) % n]
+            if acc.size != hi - lo:
+                raise ValueError("copy_from_slice panics on a length mismatch")
+            grads[r][lo:hi] = acc                # :200
+    f = F32(n)                                   # :101-105
+    grads = [(g / f).astype(F32) for g in grads]
+    return grads, res, st
 
 
 def sum_scale(ins: list[np.ndarray], divisor: float) -> np.ndarray:

@@ -16,6 +16,9 @@ namespace ono {
 // Records a thread-local error message and returns `code`.
 int set_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int hip_error(hipError_t e, const char *what, const char *file, int line);
+// WorkerHandle::recv_event's verdict on a frame of this kind (ono_msg.cpp):
+// ONO_OK for a gradient (kinds 1-4), else the reference's error class
+int worker_event_check(uint32_t kind, const uint8_t *payload, size_t n);
 
 #define ONO_HIP(expr)                                                                  \
     do {                                                                               \
@@ -115,6 +118,19 @@ struct XBarrier {
 hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s);
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s);
 hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s);
+// Connect verification (ono_xgmi.cpp): stamp the ring id at the start of every
+// page of a region (page 0: at id_off), and read them back through an import
+// (bad[p] = 1 where page p shows anything else).
+hipError_t launch_xgmi_stamp(uint8_t *region, size_t npages, size_t id_off, uint64_t id, hipStream_t s);
+hipError_t launch_xgmi_verify(const uint8_t *region, size_t npages, size_t id_off, uint64_t id, uint8_t *bad,
+                              hipStream_t s);
+// Teardown markers: lane q != pos stores peer_id[q] into peer_done[q][pos].
+struct XSignal {
+    uint64_t *peer_done[ONO_MAX_INPUTS];
+    uint64_t peer_id[ONO_MAX_INPUTS];
+    int n, pos;
+};
+hipError_t launch_xgmi_signal(const XSignal &sig, hipStream_t s);
 
 // PS shard update (storage/blocking/shard.rs:74-92 + optimization/*.rs), fused:
 //   g /= nworkers (if > 1); optimizer step on w (state v, s); g = 0 when zero_grad

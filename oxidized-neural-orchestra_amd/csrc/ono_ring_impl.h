@@ -131,7 +131,7 @@ struct ono_ring {
     // pushed chunk (0 = the Base dense serializer); the sampler draws the
     // threshold sample above 16384 values (default: ono_sparse_sample_default
     // over sample_state); sp_dev holds this worker's encoded frame in HBM,
-    // sp_tmp a lifted incoming chunk
+    // sp_tmp (sp_tmp_cap values) an incoming chunk that is not a whole-chunk DenseGrad
     float sparse_r = 0.0f;
     uint64_t sample_state = 0;
     ono_sample_fn sampler = nullptr;
@@ -140,6 +140,7 @@ struct ono_ring {
     uint8_t *sp_dev = nullptr;
     size_t sp_dev_cap = 0;
     float *sp_tmp = nullptr;
+    size_t sp_tmp_cap = 0;
     // small-frame TCP rings: the wire buffers are pinned host frames the codec
     // kernels read and write in place (no D2H / H2D per hop); zc[b] + 16 is the
     // payload base, so a frame's 12-byte header sits just before its payload

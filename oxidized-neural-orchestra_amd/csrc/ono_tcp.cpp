@@ -10,22 +10,32 @@
 //   3 / 4  SparseGrad (is_last false / true): the grad_drop stream
 //          [u64 LE total][{u32 LE offset, u32 LE run, f16 LE x run}*]
 //          (comms/src/sparse/protocol.rs:57-86)
-//   0 control (JSON), 5 params, 6 data chunk: valid messages but not a
-//          gradient — the ring's "Received an invalid worker event"
-//          (worker_ring.rs:136-138, :195-197) -> ONO_E_PROTO
+//   0 control (JSON), 5 params, 6 data chunk: WorkerHandle::recv_event's
+//          verdict (ono_msg.cpp): a worker event the ring rejects ->
+//          ONO_E_PROTO "Received an invalid worker event" (worker_ring.rs:136-138),
+//          "loss diverged", "Unexpected message from worker" or the serde
+//          error -> ONO_E_IO (handles/worker.rs:82-130)
 //   >= 7   Msg::deserialize's invalid_kind_byte io::Error (msg.rs:187) -> ONO_E_IO
 // A worker receives either gradient kind whatever its own serializer is
 // (WorkerHandle::recv_event lifts SparseGrad into the handle's zero-filled
 // buffer, comms/src/handles/worker.rs:102-108), so MI355X workers share a
-// ring with reference workers of either serializer.
+// ring with reference workers of either serializer.  A gradient of another
+// length than the hop's chunk is added over the shorter length in the scatter
+// (the zip of worker_ring.rs:141-143) and refused in the gather, where the
+// reference's copy_from_slice (:200) panics.
 //
 // Serializers of this worker (its push_grad, handles/worker.rs:157-174):
 //   Base (default)       DenseGrad of f16(chunk) (compressor.rs:106-118)
-//   SparseCapable{r}     (ono_ring_set_sparse) SparseGrad of the chunk's
-//                        values with |g| >= t, t = calculate_threshold(chunk, r)
-//                        (protocol.rs:33-49), and the ring's sparse branches:
-//                        scatter zeroes only the sent values (worker_ring.rs:126-133),
-//                        gather keeps only the sent values in grad (:177-193).
+//   SparseCapable{r}     (ono_ring_set_sparse) t = calculate_threshold(chunk, r)
+//                        (protocol.rs:33-49) and the grad_drop stream; the
+//                        SparseGrad goes out only when that stream is no longer
+//                        than the f16 payload (2 bytes per value), else the
+//                        DenseGrad of f16(chunk) (compressor.rs:79-89).  The ring
+//                        takes the branch the push selects (worker_ring.rs:125-134,
+//                        177-193): scatter zeroes the sent values (sparse) or the
+//                        chunk (dense); gather keeps only the sent values in grad
+//                        and leaves the owned residual as it is (sparse), or zeroes
+//                        the owned residual at j == 0 (dense).
 //
 // One hop = the fused kernel (or the sparse encoder) writes the payload, it
 // comes down to a pinned frame in pieces (D2H + one event per piece) and a
@@ -66,6 +76,7 @@ enum : uint32_t {
     KIND_SPARSE = 3,
     KIND_SPARSE_LAST = 4,
     KIND_MAX_VALID = 6,
+    KIND_DENSE_OTHER = 16,  // (internal) a DenseGrad of another length than the hop's chunk
 };
 
 size_t tcp_block_bytes() {  // env ONO_TCP_BLOCK_KIB (default 4 MiB), read once per ring
@@ -113,15 +124,16 @@ struct Outgoing {
     size_t pieces = 0;  // 0: complete
 };
 
-// Where the previous worker's frame goes.  A DenseGrad must carry exactly
-// dense_bytes (this hop's chunk); it lands at dense_host and, when dense_dev is
-// set, goes up to HBM piece by piece.  A SparseGrad lands in r->sp_rx (host).
+// Where the previous worker's frame goes.  A DenseGrad of exactly
+// dense_bytes (this hop's chunk) lands at dense_host and, when dense_dev is
+// set, goes up to HBM piece by piece; every other frame (a DenseGrad of
+// another length, a SparseGrad, a non-gradient message) lands whole in
+// r->sp_rx (host) for the hop to judge.
 struct Incoming {
     size_t dense_bytes = 0;
     uint8_t *dense_host = nullptr;
     uint8_t *dense_dev = nullptr;
-    size_t sparse_cap = 0;
-    uint32_t kind = 0;  // result: KIND_DENSE or KIND_SPARSE
+    uint32_t kind = 0;  // result: KIND_DENSE, KIND_DENSE_OTHER, KIND_SPARSE, or the kind byte 0 / 5 / 6
     size_t bytes = 0;   // result: payload bytes
 };
 
@@ -165,42 +177,40 @@ struct TcpRecv {
         uint64_t l = 0;
         for (int i = 0; i < 8; i++) l = (l << 8) | hdr[i];
         const uint32_t kind = hdr[11];  // Header::from_be_bytes(..) as u8 (msg.rs:168)
-        if (kind > KIND_MAX_VALID) {     // msg.rs:187: invalid_kind_byte
-            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "invalid kind byte %u", kind); return false;
+        if (kind > KIND_MAX_VALID) {     // msg.rs:105-110, 187
+            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "Received an invalid kind byte %u", kind); return false;
         }
-        if (l < 4) {
-            e.code = ONO_E_IO; snprintf(e.msg, sizeof e.msg, "frame of %llu bytes has no header", (unsigned long long)l);
+        if (l < 4) {  // msg.rs:98-103, 161-163
+            e.code = ONO_E_IO;
+            snprintf(e.msg, sizeof e.msg, "The given buffer is too small %llu, must at least be 4 bytes",
+                     (unsigned long long)l);
             return false;
         }
         const uint64_t pay = l - 4;
+        dst = nullptr;
+        dev = nullptr;
         if (kind == KIND_DENSE || kind == KIND_DENSE_LAST) {
-            if (pay != in.dense_bytes) {  // the hop's chunk (worker_ring.rs:141-143, :200)
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (%llu payload bytes, expected %zu)",
-                         (unsigned long long)pay, in.dense_bytes);
+            if (pay % 2) {  // bytemuck::cast_slice to f16 (msg.rs:175) cannot split a value
+                e.code = ONO_E_IO;
+                snprintf(e.msg, sizeof e.msg, "DenseGrad payload of %llu bytes is not a whole number of f16 values",
+                         (unsigned long long)pay);
                 return false;
             }
-            dst = in.dense_host;
-            dev = in.dense_dev;
-            in.kind = KIND_DENSE;
-        } else if (kind == KIND_SPARSE || kind == KIND_SPARSE_LAST) {
-            if (pay > in.sparse_cap) {  // longer than any grad_drop of this hop's chunk
-                e.code = ONO_E_PROTO;
-                snprintf(e.msg, sizeof e.msg,
-                         "Received an invalid worker event (sparse payload of %llu bytes, at most %zu)",
-                         (unsigned long long)pay, in.sparse_cap);
-                return false;
+            if (pay == in.dense_bytes) {
+                dst = in.dense_host;
+                dev = in.dense_dev;
+                in.kind = KIND_DENSE;
+            } else {
+                in.kind = KIND_DENSE_OTHER;
             }
+        } else {
+            in.kind = (kind == KIND_SPARSE || kind == KIND_SPARSE_LAST) ? KIND_SPARSE : kind;
+        }
+        if (!dst) {  // the whole payload to host memory
             if (int rc = grow_pinned(&r->sp_rx, &r->sp_rx_cap, std::max<size_t>(pay, 8))) {
                 e.code = rc; snprintf(e.msg, sizeof e.msg, "%s", ono_last_error()); return false;
             }
             dst = r->sp_rx;
-            dev = nullptr;
-            in.kind = KIND_SPARSE;
-        } else {  // a control message, params or a data chunk where a gradient is required
-            e.code = ONO_E_PROTO;
-            snprintf(e.msg, sizeof e.msg, "Received an invalid worker event (kind %u)", kind);
-            return false;
         }
         in.bytes = (size_t)pay;
         need = 12 + (size_t)pay;
@@ -373,9 +383,14 @@ private:
         return settle(o);
     }
 
-    // SparseCapable serializer: t = calculate_threshold(chunk, r), then the
-    // SparseGrad of grad_drop(chunk, t) (compressor.rs:71-98)
-    int out_sparse(const float *chunk, size_t L, float &t, Outgoing &o) {
+    // SparseCapable serializer, Compressor::compress (compressor.rs:71-98):
+    // t = calculate_threshold(chunk, r), the grad_drop stream of the chunk;
+    // a SparseGrad if the stream is at most 2 bytes per value (:79), else the
+    // DenseGrad of f16(chunk) (:84-89) — encoded into slot(0, c) and, in the
+    // scatter (zero_chunk), fused with the dense branch's chunks[i].fill(0.0)
+    // (worker_ring.rs:133).  sparse = push_grad's Some(t) / None.
+    int out_sparse(float *chunk, int c, bool zero_chunk, float &t, bool &sparse, Outgoing &o) {
+        const size_t L = len(c);
         int rc = threshold(chunk, L, t);
         if (rc) return rc;
         const size_t cap = ono_sparse_max_bytes(L);
@@ -388,6 +403,12 @@ private:
         }
         size_t nb = 0;
         if ((rc = ono_sparse_drop(r_->sp_dev, cap, &nb, chunk, L, t, s_))) return rc;
+        sparse = nb <= 2 * L;
+        if (!sparse) {
+            if (zero_chunk) ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, c), chunk, L, s_));
+            else ONO_K(r_, s_, launch_encode<uint16_t>(slot(0, c), chunk, L, s_));
+            return out_dense(0, c, o);
+        }
         if ((rc = grow_pinned(&r_->tx, &r_->tx_cap, 12 + nb))) return rc;
         o = Outgoing{};
         put_header(r_->tx, nb, KIND_SPARSE);
@@ -423,36 +444,72 @@ private:
             in.dense_host = r_->rx + 12;
             in.dense_dev = reinterpret_cast<uint8_t *>(slot(b, c));
         }
-        in.sparse_cap = ono_sparse_max_bytes(len(c));
         return in;
     }
     int ensure_rx() {
         return grow_pinned(&r_->rx, &r_->rx_cap, 12 + 2 * (r_->maxc + 4));
     }
-
-    // A received SparseGrad lifted into dst (zero-filled + the runs), which
-    // must be this hop's chunk length (the reference's zip / copy_from_slice)
-    int lift(const Incoming &in, float *dst, int c) {
-        uint64_t total = 0;
-        for (int q = 0; q < 8 && q < (int)in.bytes; q++) total |= (uint64_t)r_->sp_rx[q] << (8 * q);
-        if (in.bytes >= 8 && total != len(c))
-            return set_error(ONO_E_PROTO, "Received an invalid worker event (sparse gradient of %llu values, expected %zu)",
-                             (unsigned long long)total, len(c));
-        size_t got = 0;
-        int rc = ono_sparse_lift(dst, len(c), &got, r_->sp_rx, in.bytes, s_);
-        // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
-        if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
-        return rc;
-    }
-    int tmp() {
-        if (!r_->sp_tmp) ONO_HIP(hipMalloc((void **)&r_->sp_tmp, (r_->maxc + 4) * sizeof(float)));
+    // scratch of at least `elems` values at every 4-element phase
+    int tmp(size_t elems) {
+        if (r_->sp_tmp_cap >= elems + 4) return ONO_OK;
+        (void)hipFree(r_->sp_tmp);
+        r_->sp_tmp = nullptr;
+        r_->sp_tmp_cap = 0;
+        const size_t cap = std::max(elems, r_->maxc) + 4;
+        ONO_HIP(hipMalloc((void **)&r_->sp_tmp, cap * sizeof(float)));
+        r_->sp_tmp_cap = cap;
         return ONO_OK;
     }
     // phase-matched scratch for chunk c
     float *tmp_for(int c) const { return r_->sp_tmp + ph(off(c)); }
 
-    // ---- Base serializer: the fused codec kernels (ono_ring.cpp's hop ring)
-    // with a lift in between when the previous worker sent a SparseGrad.
+    // An incoming frame that is not a whole-chunk DenseGrad, as the reference
+    // hands it to the hop (WorkerHandle::recv_event, handles/worker.rs:82-130):
+    // its values in device memory, vals[0, k).  A non-gradient message fails
+    // with recv_event's / the ring's error.  The scatter adds over the shorter
+    // of the two lengths (the zip, worker_ring.rs:141-143); the gather needs
+    // the hop's chunk length exactly (copy_from_slice, :200, panics on any other).
+    int incoming(const Incoming &in, int c, bool gather, const float **vals, size_t *k) {
+        const size_t L = len(c);
+        if (in.kind != KIND_DENSE_OTHER && in.kind != KIND_SPARSE)
+            return worker_event_check(in.kind, r_->sp_rx, in.bytes);
+        if (in.kind == KIND_DENSE_OTHER) {
+            const size_t m = in.bytes / 2;
+            if (gather)
+                return set_error(ONO_E_PROTO, "Received an invalid worker event (a gradient of %zu values for a chunk "
+                                 "of %zu; the reference's copy_from_slice panics)", m, L);
+            *k = std::min(m, L);
+            int rc = tmp(L);
+            if (rc) return rc;
+            uint16_t *h = slot(1, c);  // free: the stream work that read it has run
+            if (zc_) memcpy(h, r_->sp_rx, 2 * *k);
+            else ONO_HIP(hipMemcpyAsync(h, r_->sp_rx, 2 * *k, hipMemcpyHostToDevice, s_));
+            ONO_K(r_, s_, launch_decode_scale<uint16_t>(tmp_for(c), h, *k, 1.0f, s_));
+            *vals = tmp_for(c);
+            return ONO_OK;
+        }
+        uint64_t total = 0;  // SparseGrad: grad_lift_into resizes to the stream's total (protocol.rs:102-106)
+        for (int q = 0; q < 8 && q < (int)in.bytes; q++) total |= (uint64_t)r_->sp_rx[q] << (8 * q);
+        if (in.bytes >= 8 && gather && total != L)
+            return set_error(ONO_E_PROTO, "Received an invalid worker event (a gradient of %llu values for a chunk "
+                             "of %zu; the reference's copy_from_slice panics)", (unsigned long long)total, L);
+        if (in.bytes >= 8 && total > (uint64_t(1) << 36))
+            return set_error(ONO_E_IO, "sparse gradient of %llu values: capacity overflow", (unsigned long long)total);
+        const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
+        int rc = tmp(std::max(cap, L));
+        if (rc) return rc;
+        size_t got = 0;
+        rc = ono_sparse_lift(tmp_for(c), cap, &got, r_->sp_rx, in.bytes, s_);
+        // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
+        if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
+        if (rc) return rc;
+        *k = std::min(got, L);
+        *vals = tmp_for(c);
+        return ONO_OK;
+    }
+
+    // ---- Base serializer: the fused codec kernels (ono_ring.cpp's hop ring);
+    // an incoming frame that is not a whole-chunk DenseGrad is taken apart first.
     int pull_dense(float *res, float *grad) {
         int rc = ensure_rx();
         if (rc) return rc;
@@ -473,8 +530,10 @@ private:
                                                               len(cr), fn, s_));
                 continue;
             }
-            if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
-            ONO_K(r_, s_, launch_acc(res + off(cr), tmp_for(cr), len(cr), s_, true));  // :141-143
+            const float *v = nullptr;
+            size_t k = 0;
+            if ((rc = incoming(in, cr, false, &v, &k))) return rc;
+            ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
             if (!last) {
                 ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, cr), res + off(cr), len(cr), s_));
             } else {  // grad = x / n, the f16 message, residual = 0 (add_finish without the add)
@@ -491,34 +550,41 @@ private:
             if ((rc = out_dense(bo, cs, o)) || (rc = xchg(o, in))) return rc;
             if (in.kind == KIND_DENSE) {
                 ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(bi, cr), len(cr), fn, s_));
-            } else {  // :200 copies the lifted chunk; the next hop forwards its f16 image
-                if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
-                ONO_K(r_, s_, launch_scale_zero(grad + off(cr), tmp_for(cr), len(cr), fn, nullptr, s_));
-                ONO_K(r_, s_, launch_encode<uint16_t>(slot(bi, cr), tmp_for(cr), len(cr), s_));
+            } else {  // :200 copies the received chunk; the next hop forwards its f16 image
+                const float *v = nullptr;
+                size_t k = 0;
+                if ((rc = incoming(in, cr, true, &v, &k))) return rc;
+                ONO_K(r_, s_, launch_scale_zero(grad + off(cr), v, len(cr), fn, nullptr, s_));
+                ONO_K(r_, s_, launch_encode<uint16_t>(slot(bi, cr), v, len(cr), s_));
             }
             std::swap(bo, bi);
         }
         return ONO_OK;
     }
 
-    // ---- SparseCapable serializer (worker_ring.rs:112-204 with the sparse
-    // branches): unfused — each hop's threshold is taken over the chunk as the
-    // reference holds it, so the division by n waits for the end (:101-105).
+    // ---- SparseCapable serializer (worker_ring.rs:112-204 with the branches
+    // push_grad's result selects): unfused — each push's threshold is taken
+    // over the chunk as the reference holds it, so the division by n waits
+    // for the end (:101-105).
     int pull_sparse(float *res, float *grad) {
         int rc = ensure_rx();
         if (rc) return rc;
         float t = 0.0f;
+        bool sparse = false;
         for (int st = 0; st < n_ - 1; st++) {  // scatter (:112-147)
             const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            if ((rc = out_sparse(res + off(cs), len(cs), t, o)) || (rc = xchg(o, in))) return rc;
-            if ((rc = ono_sparse_mask(res + off(cs), len(cs), t, 1, s_))) return rc;  // :128-131: sent values leave
+            if ((rc = out_sparse(res + off(cs), cs, true, t, sparse, o)) || (rc = xchg(o, in))) return rc;
+            // :126-132 sent values leave; a dense push (:133) zeroed the chunk in its encoder
+            if (sparse && (rc = ono_sparse_mask(res + off(cs), len(cs), t, 1, s_))) return rc;
             if (in.kind == KIND_DENSE) {
                 ONO_K(r_, s_, launch_decode_add<uint16_t>(res + off(cr), slot(1, cr), len(cr), s_));
             } else {
-                if ((rc = tmp()) || (rc = lift(in, tmp_for(cr), cr))) return rc;
-                ONO_K(r_, s_, launch_acc(res + off(cr), tmp_for(cr), len(cr), s_, true));
+                const float *v = nullptr;
+                size_t k = 0;
+                if ((rc = incoming(in, cr, false, &v, &k))) return rc;
+                ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
             }
         }
         const int own = mod(pos_ + 1);  // gather (:155-204)
@@ -528,13 +594,19 @@ private:
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            if ((rc = out_sparse(grad + off(cs), len(cs), t, o)) || (rc = xchg(o, in))) return rc;
-            if ((rc = ono_sparse_mask(grad + off(cs), len(cs), t, 0, s_))) return rc;  // :183-187: keep the sent
-            if (j == 0) ONO_HIP(hipMemsetAsync(res + off(own), 0, len(own) * sizeof(float), s_));  // :191-193
+            if ((rc = out_sparse(grad + off(cs), cs, false, t, sparse, o)) || (rc = xchg(o, in))) return rc;
+            if (sparse) {  // :177-190: keep the sent values; the owned residual stays (:178-184 commented out)
+                if ((rc = ono_sparse_mask(grad + off(cs), len(cs), t, 0, s_))) return rc;
+            } else if (j == 0) {  // :191-193
+                ONO_HIP(hipMemsetAsync(res + off(own), 0, len(own) * sizeof(float), s_));
+            }
             if (in.kind == KIND_DENSE) {
                 ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(1, cr), len(cr), 1.0f, s_));
-            } else if ((rc = lift(in, grad + off(cr), cr))) {
-                return rc;
+            } else {
+                const float *v = nullptr;
+                size_t k = 0;
+                if ((rc = incoming(in, cr, true, &v, &k))) return rc;
+                ONO_HIP(hipMemcpyAsync(grad + off(cr), v, len(cr) * sizeof(float), hipMemcpyDeviceToDevice, s_));
             }
         }
         ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105

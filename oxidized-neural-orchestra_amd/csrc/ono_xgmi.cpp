@@ -28,6 +28,24 @@
 // links at once.  No stream synchronisation or host round trip per round: the
 // barriers are device-side flag exchanges with a timeout.
 //
+// Connect is verified, teardown is ordered (round 3).  Every region carries a
+// random 64-bit ring id: in its flag page and at the start of every 4 KiB
+// page, stamped before the handle leaves the process; the handle blob that
+// travels to the peers (ONO_XGMI_HANDLE_BYTES) holds the IPC handle, the id
+// and the region's size.  An importer reads every page's stamp through its
+// new mapping before the first round (a device barrier at the end of connect
+// keeps every rank from writing a peer region until all importers have
+// checked): a mapping that shows anything else — memory of an earlier region
+// of that peer, from an import the runtime kept or recycled — is an ONO_E_IO
+// at connect time instead of wrong data in a later round.  Destroy no longer
+// frees a region that peers may still map: each rank, once its own work is
+// done, stores the owner's id into a teardown slot of every peer region it
+// imported, then closes those imports; an owner frees its region only when
+// every peer's marker is there (or the timeout passed).  Round 2 freed the
+// region right after a barrier, while peers still held imports of it, and
+// re-created rings in the same processes (the host-fed test's one recorded
+// wrong result came from the second ring of the process).
+//
 // Reuse safety without a third barrier: a rank writes peer q's rbuf in round
 // r+1 only after passing barrier 4 of round r, which q reaches after its step 3
 // (the only reader of its rbuf); it overwrites its own obuf (round r+1 step 3)
@@ -35,18 +53,30 @@
 // step 5 (the only remote reader of obuf).
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <random>
+#include <thread>
 
 #include "ono_internal.h"
 #include "ono_ring_impl.h"
 
-static_assert(sizeof(hipIpcMemHandle_t) == ONO_XGMI_HANDLE_BYTES, "IPC handle size");
+static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
 
 namespace ono {
 
-constexpr size_t kFlagBytes = 4096;  // flag slots (n x u64) at the start of the region
+constexpr size_t kFlagBytes = 4096;  // flag page: barrier slots (n x u64) at offset 0,
+constexpr size_t kDoneOff = 1024;    //   teardown markers (n x u64),
+constexpr size_t kIdOff = 2048;      //   the region's ring id
+constexpr size_t kPage = 4096;       // every later page starts with the id until the first round
+// the handle blob: [hipIpcMemHandle_t][u64 ring id][u64 region bytes][zero]
+constexpr size_t kBlobId = sizeof(hipIpcMemHandle_t), kBlobBytes = kBlobId + 8;
+static_assert(kBlobBytes + 8 <= ONO_XGMI_HANDLE_BYTES, "handle blob layout");
 
 struct XgmiState {
     uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
@@ -60,7 +90,11 @@ struct XgmiState {
     uint32_t *err = nullptr;          // host-mapped: set by a barrier that timed out
     uint32_t *err_dev = nullptr;
     uint64_t timeout_ticks = 0;
+    double timeout_s = 0;
     std::vector<hipEvent_t> ev;       // host-fed sub-round pipeline: H2D / round / D2H per sub-round
+    uint64_t id = 0;                  // this region's ring id (stamped, sent in the handle blob)
+    size_t bytes = 0;                 // this region's size
+    std::vector<uint64_t> peer_id;    // every peer region's id, from its blob
 };
 
 }  // namespace ono
@@ -70,6 +104,18 @@ using namespace ono;
 namespace {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint64_t fresh_ring_id() {
+    static std::atomic<uint64_t> counter{0};
+    std::random_device rd;
+    uint64_t z = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 20) ^
+                 (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^
+                 (counter.fetch_add(1) * 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return z ? z : 1;
+}
 
 int xgmi_alloc(ono_ring *r) {
     if (r->xgmi) return ONO_OK;
@@ -84,9 +130,12 @@ int xgmi_alloc(ono_ring *r) {
     const char *gm = getenv("ONO_XGMI_GATHER");
     x->push_gather = gm && strcmp(gm, "push") == 0;
     const size_t bytes = x->push_gather ? x->gat_off + rb : x->gat_off;
+    x->bytes = bytes;
+    x->id = fresh_ring_id();
     ONO_HIP(hipExtMallocWithFlags((void **)&x->xbuf, bytes, hipDeviceMallocUncached));
-    ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0
-    ONO_HIP(hipDeviceSynchronize());              // zeroed before the handle leaves this process
+    ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0, no teardown markers
+    ONO_HIP(launch_xgmi_stamp(x->xbuf, (bytes + kPage - 1) / kPage, kIdOff, x->id, nullptr));
+    ONO_HIP(hipDeviceSynchronize());              // zeroed and stamped before the handle leaves this process
     x->peer.assign(r->n, nullptr);
     x->peer[r->pos] = x->xbuf;
     ONO_HIP(hipHostMalloc((void **)&x->err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
@@ -117,6 +166,7 @@ void xgmi_set_timeout(ono_ring *r) {
     const char *e = getenv("ONO_XGMI_TIMEOUT_S");
     const double secs = r->xgmi_timeout_s > 0 ? r->xgmi_timeout_s : e && atof(e) > 0 ? atof(e) : kDefaultTimeoutS;
     x->timeout_ticks = (uint64_t)(secs * khz * 1000.0);
+    x->timeout_s = secs;
 }
 
 }  // namespace ono
@@ -133,20 +183,84 @@ uint8_t *gslot_of(const XgmiState *x, uint8_t *region_q, int o, int q) {
     return region_q + x->gat_off + (size_t)(o < q ? o : o - 1) * x->slot * sizeof(float);
 }
 
+int barrier(ono_ring *r, hipStream_t s);
+
+void make_blob(const XgmiState *x, const hipIpcMemHandle_t &h, uint8_t *blob) {
+    memset(blob, 0, ONO_XGMI_HANDLE_BYTES);
+    memcpy(blob, &h, sizeof h);
+    memcpy(blob + kBlobId, &x->id, 8);
+    const uint64_t b = x->bytes;
+    memcpy(blob + kBlobBytes, &b, 8);
+}
+
+// Every page of peer q's region as mapped here must show the id q stamped.
+int verify_import(ono_ring *r, int q, uint64_t id, size_t bytes) {
+    XgmiState *x = r->xgmi;
+    const size_t npages = (bytes + kPage - 1) / kPage;
+    uint8_t *bad_dev = nullptr;
+    ONO_HIP(hipMalloc((void **)&bad_dev, npages));
+    std::vector<uint8_t> bad(npages);
+    hipError_t e = launch_xgmi_verify(x->peer[q], npages, kIdOff, id, bad_dev, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(bad.data(), bad_dev, npages, hipMemcpyDeviceToHost);
+    (void)hipFree(bad_dev);
+    if (e != hipSuccess) return hip_error(e, "exchange region verification", __FILE__, __LINE__);
+    size_t nbad = 0, first = npages;
+    for (size_t p = 0; p < npages; p++)
+        if (bad[p]) { nbad++; first = std::min(first, p); }
+    if (nbad)
+        return set_error(ONO_E_IO,
+                         "xGMI connect: rank %d's exchange region as mapped here shows another region's memory "
+                         "(%zu of %zu pages lack ring id %016llx, first page %zu): a stale IPC import",
+                         q, nbad, npages, (unsigned long long)id, first);
+    return ONO_OK;
+}
+
 int xgmi_connect(ono_ring *r, const uint8_t *handles) {
     XgmiState *x = r->xgmi;
     if (x->connected) return ONO_OK;
     DeviceGuard g(r->device);
-    for (int q = 0; q < r->n; q++) {
+    x->peer_id.assign(r->n, 0);
+    x->peer_id[r->pos] = x->id;
+    int rc = ONO_OK;
+    for (int q = 0; q < r->n && rc == ONO_OK; q++) {
         if (q == r->pos) continue;
+        const uint8_t *blob = handles + (size_t)q * ONO_XGMI_HANDLE_BYTES;
         hipIpcMemHandle_t h;
-        memcpy(&h, handles + (size_t)q * ONO_XGMI_HANDLE_BYTES, sizeof h);
+        memcpy(&h, blob, sizeof h);
+        uint64_t id = 0, bytes = 0;
+        memcpy(&id, blob + kBlobId, 8);
+        memcpy(&bytes, blob + kBlobBytes, 8);
+        if (id == 0 || bytes != x->bytes) {
+            rc = set_error(ONO_E_ARG, "xGMI connect: rank %d's handle is not an exchange region of this ring "
+                           "(id %016llx, %llu bytes; expected %zu)", q, (unsigned long long)id,
+                           (unsigned long long)bytes, x->bytes);
+            break;
+        }
         void *p = nullptr;
         hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) return hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
+        if (e != hipSuccess) {
+            rc = hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
+            break;
+        }
         x->peer[q] = static_cast<uint8_t *>(p);
+        x->peer_id[q] = id;
+        rc = verify_import(r, q, id, (size_t)bytes);
+    }
+    if (rc) {  // leave no import behind: a later connect starts over
+        for (int q = 0; q < r->n; q++)
+            if (q != r->pos && x->peer[q]) {
+                (void)hipIpcCloseMemHandle(x->peer[q]);
+                x->peer[q] = nullptr;
+            }
+        return rc;
     }
     x->connected = true;
+    // No rank writes a peer's region before every importer has checked its
+    // stamps: a barrier that every rank passes only once all are connected.
+    if ((rc = barrier(r, nullptr))) return rc;
+    ONO_HIP(hipDeviceSynchronize());
+    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
+        return set_error(ONO_E_IO, "xGMI connect: a peer did not connect within the timeout");
     return ONO_OK;
 }
 
@@ -160,7 +274,7 @@ int xgmi_connect_over_rccl(ono_ring *r, hipStream_t s) {
     std::vector<uint8_t> all((size_t)r->n * H);
     hipIpcMemHandle_t h;
     ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
-    memcpy(all.data() + (size_t)r->pos * H, &h, H);
+    make_blob(r->xgmi, h, all.data() + (size_t)r->pos * H);
     uint8_t *d = nullptr;
     ONO_HIP(hipMalloc((void **)&d, all.size()));
     hipError_t e = hipMemcpyAsync(d + (size_t)r->pos * H, all.data() + (size_t)r->pos * H, H, hipMemcpyHostToDevice, s);
@@ -436,19 +550,49 @@ void xgmi_abort(ono_ring *r) {
     if (r->xgmi && r->xgmi->err) __atomic_store_n(r->xgmi->err, 2u, __ATOMIC_RELEASE);
 }
 
-// Teardown is collective: a final barrier keeps this rank's region mapped
-// until every peer has finished reading it (a peer still pulling from a freed
-// region would fault).  A peer that never arrives costs the timeout, no more.
+// Teardown is collective and ordered: a region is freed only after every
+// peer has said it is done with it.  Once this rank's own work is complete
+// (device synchronised: its last pushes into and pulls from peer regions are
+// over), it stores each peer's ring id into that peer's teardown slot `pos`
+// (system-scope stores through the import), then closes its imports; it then
+// waits until its own region holds its id in every peer's slot and frees it.
+// A peer that never arrives costs the timeout, no more; after a barrier
+// timeout or an abort nobody waits.
 void xgmi_free(ono_ring *r) {
     XgmiState *x = r->xgmi;
     if (!x) return;
     DeviceGuard g(r->device);
-    if (x->connected && !__atomic_load_n(x->err, __ATOMIC_ACQUIRE)) {
-        (void)hipDeviceSynchronize();
-        if (barrier(r, r->cstream) == ONO_OK) (void)hipStreamSynchronize(r->cstream);
+    // after a barrier timeout or an abort this rank does not wait, but still
+    // releases its peers' regions so that they do not wait for it
+    bool wait = x->connected && !__atomic_load_n(x->err, __ATOMIC_ACQUIRE);
+    if (x->connected) {
+        bool ok = hipDeviceSynchronize() == hipSuccess;
+        XSignal sig{};
+        for (int q = 0; q < r->n; q++) {
+            sig.peer_done[q] = q == r->pos ? nullptr : reinterpret_cast<uint64_t *>(x->peer[q] + kDoneOff);
+            sig.peer_id[q] = x->peer_id[q];
+        }
+        sig.n = r->n;
+        sig.pos = r->pos;
+        ok = ok && launch_xgmi_signal(sig, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+        wait &= ok;
     }
     for (int q = 0; q < (int)x->peer.size(); q++)
         if (q != r->pos && x->peer[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
+    if (wait) {  // every peer's marker in this region (uncached: a D2H copy reads what landed)
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<uint64_t> done(r->n);
+        for (;;) {
+            if (hipMemcpy(done.data(), x->xbuf + kDoneOff, r->n * sizeof(uint64_t), hipMemcpyDeviceToHost) !=
+                hipSuccess)
+                break;
+            bool all = true;
+            for (int q = 0; q < r->n; q++) all &= q == r->pos || done[q] == x->id;
+            if (all || r->aborted.load()) break;
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > x->timeout_s) break;
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
     for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
     (void)hipFree(x->xbuf);
     if (x->err) (void)hipHostFree(x->err);
@@ -493,7 +637,7 @@ int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
     DeviceGuard g(r->device);
     hipIpcMemHandle_t h;
     ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
-    memcpy(handle, &h, sizeof h);
+    make_blob(r->xgmi, h, handle);
     return ONO_OK;
 }
 
@@ -508,6 +652,7 @@ int ono_ring_check(const ono_ring *r) {
 int ono_ring_set_xgmi_timeout(ono_ring *r, double seconds) {
     if (!r) return set_error(ONO_E_ARG, "ring is NULL");
     if (!(seconds >= 0) || seconds > 1e7) return set_error(ONO_E_ARG, "timeout %g s", seconds);
+    std::lock_guard<std::mutex> lk(r->mu);  // a round in flight reads the ticks under the same lock
     r->xgmi_timeout_s = seconds;
     xgmi_set_timeout(r);  // later barriers use it (an allocated region keeps its flags)
     return ONO_OK;

@@ -149,6 +149,26 @@ __global__ __launch_bounds__(64) void xbarrier_kernel(XBarrier b) {
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
 }
 
+// Ring-id stamps of a fresh exchange region, lane p -> page p (page 0: the id
+// slot of the flag page); verification reads them back through an import.
+constexpr size_t kXPage = 4096;
+__global__ __launch_bounds__(64) void xstamp_kernel(uint8_t *region, uint64_t npages, uint64_t id_off, uint64_t id) {
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (p < npages) st_sys(reinterpret_cast<uint64_t *>(region + (p ? p * kXPage : id_off)), id);
+    peer_stores_done();
+}
+__global__ __launch_bounds__(64) void xverify_kernel(const uint8_t *region, uint64_t npages, uint64_t id_off,
+                                                     uint64_t id, uint8_t *bad) {
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (p < npages) bad[p] = ld_sys(reinterpret_cast<const uint64_t *>(region + (p ? p * kXPage : id_off))) != id;
+}
+// Teardown: lane q tells peer q that this rank is done with its region.
+__global__ __launch_bounds__(64) void xsignal_kernel(XSignal sg) {
+    const int q = threadIdx.x;
+    if (q < sg.n && q != sg.pos) st_sys(sg.peer_done[q] + sg.pos, sg.peer_id[q]);
+    peer_stores_done();
+}
+
 template <class Op>
 hipError_t launch_segs(const Op &op, XSegs g, hipStream_t s) {
     uint32_t tiles = 0;
@@ -191,6 +211,27 @@ hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t
     case SCALE_RECIP: return launch_segs(PullF32Op<SCALE_RECIP>{sc.v}, g, s);
     default: return launch_segs(PullF32Op<SCALE_DIV>{sc.v}, g, s);
     }
+}
+
+hipError_t launch_xgmi_stamp(uint8_t *region, size_t npages, size_t id_off, uint64_t id, hipStream_t s) {
+    if (npages == 0) return hipSuccess;
+    hipLaunchKernelGGL(xstamp_kernel, dim3((unsigned)((npages + 63) / 64)), dim3(64), 0, s, region, (uint64_t)npages,
+                       (uint64_t)id_off, id);
+    return hipGetLastError();
+}
+
+hipError_t launch_xgmi_verify(const uint8_t *region, size_t npages, size_t id_off, uint64_t id, uint8_t *bad,
+                              hipStream_t s) {
+    if (npages == 0) return hipSuccess;
+    hipLaunchKernelGGL(xverify_kernel, dim3((unsigned)((npages + 63) / 64)), dim3(64), 0, s, region,
+                       (uint64_t)npages, (uint64_t)id_off, id, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_xgmi_signal(const XSignal &sig, hipStream_t s) {
+    if (sig.n < 1 || sig.n > ONO_MAX_INPUTS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xsignal_kernel, dim3(1), dim3(64), 0, s, sig);
+    return hipGetLastError();
 }
 
 hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s) {

@@ -22,7 +22,7 @@ OPT_KIND = {"gd": 0, "momentum": 1, "adam": 2, "add": 3}
 STORE_KIND = {"blocking": 0, "wild": 1}
 SYNC_KIND = {"barrier": 0, "nonblocking": 1}
 UID_BYTES = 128
-XGMI_HANDLE_BYTES = 64
+XGMI_HANDLE_BYTES = 128
 MAX_INPUTS = 16
 PHASES = ("kernel", "rccl", "xgmi_scatter", "xgmi_barrier", "xgmi_gather")  # ono_phase
 
@@ -115,6 +115,7 @@ _SIGS = {
     "ono_sparse_threshold": (_i, [C.POINTER(C.c_float), _fp, _sz, _vp, _sz, C.c_float, _vp]),
     "ono_sparse_sample_default": (_i, [C.POINTER(C.c_uint64), _sz, _vp, _sz]),
     "ono_ring_set_sparse": (_i, [_vp, C.c_float, _u64]),
+    "ono_worker_event_check": (_i, [C.c_uint32, C.c_char_p, _sz]),
     "ono_ring_set_sampler": (_i, [_vp, _vp, _vp]),
     "ono_ring_unique_id": (_i, [C.c_char_p]),
     "ono_ring_create": (_i, [C.POINTER(C.c_void_p), _i, _i, _sz, _i, C.c_char_p, _i]),
@@ -205,10 +206,17 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.ono_abi_version() != 1:
+        if L.ono_abi_version() != 2:
             raise ImportError("libono_reduce.so ABI mismatch")
         _lib = L
     return _lib
+
+
+def worker_event_check(kind: int, payload: bytes) -> None:
+    """WorkerHandle::recv_event's verdict on one frame as the ring sees it
+    (comms/src/handles/worker.rs:82-130): returns for a gradient, raises the
+    reference's error class otherwise."""
+    check(lib().ono_worker_event_check(kind, payload, len(payload)))
 
 
 def check(rc: int) -> None:

@@ -135,7 +135,7 @@ class WorkerRingManager:
                   wire: str = "f32", device: int | None = None) -> "WorkerRingManager":
         """The xGMI peer-access schedule with no collective library: every rank
         exports its exchange region and maps its peers' (ONO_ALGO_XGMI).
-        `allgather(bytes) -> list[bytes]` moves the 64-byte handles between the
+        `allgather(bytes) -> list[bytes]` moves the 128-byte handles between the
         ranks in rank order — any control channel (the reference's ring links,
         a gloo group, a pipe).  Every rank must construct (and close) together."""
         nranks = addrs if isinstance(addrs, int) else len(addrs)
@@ -146,7 +146,7 @@ class WorkerRingManager:
             call("ono_ring_xgmi_handle", self._h, buf)
             handles = allgather(buf.raw)
             if len(handles) != nranks or any(len(x) != XGMI_HANDLE_BYTES for x in handles):
-                raise ValueError("allgather must return one 64-byte handle per rank")
+                raise ValueError(f"allgather must return one {XGMI_HANDLE_BYTES}-byte handle per rank")
             call("ono_ring_xgmi_connect", self._h, b"".join(handles))
         return self
 

@@ -3,7 +3,7 @@
 // a native Rust worker binary per GPU would use it.
 //
 // The parent forks n workers before anything touches the GPU; each worker
-// creates its ring (ono_ring_create_xgmi), sends its 64-byte handle up a pipe,
+// creates its ring (ono_ring_create_xgmi), sends its 128-byte handle up a pipe,
 // receives all n handles back (the parent plays the out-of-band control
 // channel — the reference's ring links), connects, and runs host-fed rounds
 // (ono_ring_pull_grads_host on registered host buckets, both wires), each

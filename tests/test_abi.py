@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_device_count():
     L = ono_amd.lib()
-    assert L.ono_abi_version() == 1
+    assert L.ono_abi_version() == 2
     c = C.c_int(-1)
     assert L.ono_device_count(C.byref(c)) == 0
     assert c.value >= 0

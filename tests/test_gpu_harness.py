@@ -27,7 +27,7 @@ XGMI_HARNESS = os.path.join(NATIVE, "ono_xgmi_harness")
 @pytest.mark.parametrize("nranks,length", [(2, 109386), (4, 300007)])
 def test_cpp_xgmi_harness_one_process_per_rank(nranks, length):
     """tests/native/ono_xgmi_harness.cpp: a C++ parent forks one worker process per
-    rank (before any HIP call), relays the 64-byte handles over pipes, and
+    rank (before any HIP call), relays the 128-byte handles over pipes, and
     every worker runs host-fed rounds of the xGMI ring for both wires through
     the C ABI, bit-exact with the C oracle (all ranks on device 0 here)."""
     if not os.path.exists(XGMI_HARNESS):

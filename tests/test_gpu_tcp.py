@@ -16,11 +16,16 @@ sockets):
 * the reference's failure behaviour: an invalid event is InvalidWorkerEvent
   (worker_ring.rs:136-138), a closed peer is an io error, abort() unblocks;
 * the SparseCapable serializer (ono_ring_set_sparse): SparseGrad frames
-  (kind 3, comms/src/protocol/msg.rs:175-178) on the wire, the ring's sparse
-  branches (worker_ring.rs:126-133, 177-193), and every worker accepting
-  both gradient kinds (handles/worker.rs:102-108) — all-GPU and mixed rings
-  with reference-style CPU workers of either serializer, bit-exact with the
-  restatement (oracle ono_ref_ring_pull_grads_sparse).
+  (kind 3, comms/src/protocol/msg.rs:175-178) when the stream is at most 2
+  bytes per value, else the DenseGrad fallback (compressor.rs:79-89); the
+  ring's branches per push (worker_ring.rs:126-133, 177-193: after a sparse
+  gather push the owned residual is kept), and every worker accepting both
+  gradient kinds (handles/worker.rs:102-108) — all-GPU and mixed rings with
+  reference-style CPU workers of either serializer, bit-exact on grad and
+  residual with the restatements (oracle ono_ref_ring_pull_grads_sparse and
+  the independent numpy one, which agree);
+* a scatter gradient of another length is added over the shorter length (the
+  zip, :141-143); every non-gradient frame fails with recv_event's error class.
 """
 import socket
 import threading
@@ -255,31 +260,113 @@ def test_tcp_ring_wire_bytes():
         close_all(s for p in pairs for s in p)
 
 
-@pytest.mark.parametrize("kind,err", [(0, "proto"), (5, "proto"), (6, "proto"), (7, "io"), (200, "io")])
-def test_tcp_ring_frame_kinds(kind, err):
-    """A control message (0), params (5) or a data chunk (6) where a gradient
-    is required is the ring's InvalidWorkerEvent (worker_ring.rs:136-138);
-    kind bytes >= 7 fail Msg::deserialize with invalid_kind_byte (msg.rs:187),
-    an io::Error.  (Kinds 3/4 are SparseGrad — accepted, see the sparse tests.)"""
+def frame(kind: int, payload: bytes) -> bytes:
+    return (4 + len(payload)).to_bytes(8, "big") + kind.to_bytes(4, "big") + payload
+
+
+# (kind, payload, error class, message) — WorkerHandle::recv_event
+# (comms/src/handles/worker.rs:82-130) + the ring (worker_ring.rs:136-138)
+EVENT_CASES = [
+    (0, b'"upgraded"', "proto", "invalid worker event"),
+    (0, b'"disconnect"', "proto", "invalid worker event"),
+    (0, b'{"done": null}', "proto", "invalid worker event"),
+    (0, b'{"report_loss": {"losses": [0.25, 1.5]}}', "proto", "invalid worker event"),
+    (0, b'{"report_loss": {"losses": [0.25, null]}}', "io", "loss diverged"),
+    (0, b'"ping"', "io", "Unexpected message"),
+    (0, b'{"share_dataset_size": {"size": 3}}', "io", "Unexpected message"),
+    (0, b'{"report_loss": {"losses": [1, }', "io", "control message"),
+    (0, b'"no_such_command"', "io", "unknown variant"),
+    (0, b'', "io", "control message"),
+    (5, b"\0" * 16, "io", "Unexpected message"),
+    (6, b"\0" * 16, "io", "Unexpected message"),
+    (7, b"\0" * 16, "io", "invalid kind byte"),
+    (200, b"", "io", "invalid kind byte"),
+    (0x101, b"\0" * 10, "proto", "invalid worker event"),  # the kind is the header's low byte: 1, wrong length
+]
+
+
+@pytest.mark.parametrize("kind,payload,err,text", EVENT_CASES)
+@pytest.mark.parametrize("phase", ["scatter", "gather"])
+def test_tcp_ring_worker_event_classes(kind, payload, err, text, phase):
+    """A frame that is not the expected gradient fails with the reference's
+    error class and message: a worker event the ring rejects is
+    InvalidWorkerEvent, everything recv_event itself refuses (the serde error,
+    "loss diverged", "Unexpected message from worker", an invalid kind byte)
+    is an io::Error.  Checked in both phases of the round."""
     length = 10001
     w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED + 1, 0))
+    (a, b), (c, d) = O.split_chunks(length, 2)
     try:
         recv_frame(from_gpu)
-        (a, b) = O.split_chunks(length, 2)[1]
-        bad = bytearray(O.frame_dense(O.f16_encode(np.zeros(b - a, np.float32))))
-        bad[11] = kind
-        to_gpu.sendall(bytes(bad))
+        if kind == 0x101 and phase == "scatter":
+            pytest.skip("a shorter DenseGrad is the zip in the scatter (test_tcp_ring_scatter_zip)")
+        if phase == "gather":  # a good scatter frame first, then the bad one in the gather
+            to_gpu.sendall(O.frame_dense(O.f16_encode(O.synth(length, SEED + 1, 1)[c:d])))
+            recv_frame(from_gpu)
+        to_gpu.sendall(frame(kind, payload))
         w.join(60)
         want = ono_amd.InvalidWorkerEvent if err == "proto" else ono_amd.IoError
         assert isinstance(w.err, want), w.err
+        assert text in str(w.err), w.err
     finally:
         close_all(s for p in pairs for s in p)
 
 
+def test_worker_event_check_matches_the_ring():
+    """The host-side verdict (ono_worker_event_check) is what the ring raises."""
+    for kind, payload, err, text in EVENT_CASES:
+        if kind == 0x101:
+            continue
+        want = ono_amd.InvalidWorkerEvent if err == "proto" else ono_amd.IoError
+        with pytest.raises(want, match=text):
+            ono_amd.worker_event_check(kind & 0xFF, payload)
+    ono_amd.worker_event_check(1, b"\0\0")
+
+
+@pytest.mark.parametrize("form,delta", [("dense", -3), ("dense", 5), ("sparse", -2), ("sparse", 4)])
+def test_tcp_ring_scatter_zip(form, delta):
+    """A scatter gradient of another length than the hop's chunk is added over
+    the shorter of the two (the zip of worker_ring.rs:141-143): the rest of the
+    chunk keeps its value, values past the chunk are dropped."""
+    length = 10001
+    x = O.synth(length, SEED + 11, 0)
+    y = O.synth(length, SEED + 11, 1)
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, x)
+    (a, b), (c, d) = O.split_chunks(length, 2)
+    m = d - c + delta
+    peer = y[c:c + m] if delta < 0 else np.concatenate([y[c:d], y[:delta]])
+    try:
+        recv_frame(from_gpu)
+        if form == "dense":
+            to_gpu.sendall(O.frame_dense(O.f16_encode(peer)))
+        else:
+            to_gpu.sendall(frame_sparse(O.grad_drop(peer, O.sparse_threshold(peer, 0.1))))
+        g_frame = recv_frame(from_gpu)  # the owner's gather push of chunk 1
+        to_gpu.sendall(O.frame_dense(O.f16_encode(y[a:b])))  # rank 1's gather push of chunk 0
+        w.join(60)
+        assert w.err is None, w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+    lifted = (O.f16_decode(O.f16_encode(peer)) if form == "dense"
+              else O.grad_lift(O.grad_drop(peer, O.sparse_threshold(peer, 0.1)), m))
+    k = min(m, d - c)
+    own = x[c:d].copy()
+    own[:k] = own[:k] + lifted[:k]
+    assert g_frame == O.frame_dense(O.f16_encode(own))
+    exp_grad = np.concatenate([O.f16_decode(O.f16_encode(y[a:b])), own]) / np.float32(2)
+    assert_bitexact(w.grad, exp_grad.astype(np.float32), "grad")
+    assert not w.residual.view(np.uint32).any()
+
+
 def test_tcp_ring_wrong_length_is_invalid_event():
+    """A gather DenseGrad of another length than the chunk: the reference's
+    copy_from_slice (worker_ring.rs:200) panics; here InvalidWorkerEvent."""
     length = 10001
     w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
+    (a, b), (c, d) = O.split_chunks(length, 2)
     try:
+        recv_frame(from_gpu)
+        to_gpu.sendall(O.frame_dense(O.f16_encode(np.zeros(d - c, np.float32))))
         recv_frame(from_gpu)
         to_gpu.sendall(O.frame_dense(np.zeros(7, np.uint16)))
         w.join(60)
@@ -328,9 +415,9 @@ def oracle_rounds(x_rounds, ratios, seeds):
     return g, res
 
 
-@pytest.mark.parametrize("n,length,ratios", [(2, 10001, [0.4, 0.4]), (2, 70001, [0.1, 0.9]),
-                                             (3, 40000, [0.25, 0.0, 0.6]), (4, 109386, [0.3, 0.3, 0.0, 1.0]),
-                                             (5, 4099, [0.5, 0.0, 0.0, 0.2, 0.7])])
+@pytest.mark.parametrize("n,length,ratios", [(2, 10001, [0.4, 0.1]), (2, 70001, [0.1, 0.9]),
+                                             (3, 40000, [0.05, 0.0, 0.6]), (4, 109386, [0.1, 0.3, 0.0, 1.0]),
+                                             (5, 4099, [0.5, 0.0, 0.0, 0.1, 0.05]), (3, 60000, [0.1, 0.15, 0.05])])
 @pytest.mark.parametrize("zero_copy", [True, False])
 def test_tcp_ring_sparse_socketpairs_vs_oracle(n, length, ratios, zero_copy, monkeypatch):
     """All-GPU rings of SparseCapable and Base workers (chunks below and above
@@ -358,7 +445,7 @@ def test_tcp_ring_sparse_host_fed_and_sampler_callback():
     """The host-fed form, and a caller-installed sampler (the boundary a Rust
     integration uses to draw rand's index::sample): here a Python sampler that
     draws the stand-in stream, so the restatement still applies."""
-    n, length, ratios = 3, 60000, [0.3, 0.3, 0.3]
+    n, length, ratios = 3, 60000, [0.1, 0.3, 0.05]
     seeds = [5, 6, 7]
     ins = inputs_for(n, length, 2, SEED + 43)
 
@@ -384,10 +471,11 @@ def test_tcp_ring_sparse_host_fed_and_sampler_callback():
         assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
 
 
-@pytest.mark.parametrize("n,cpu_ranks,length,ratios", [(2, (1,), 109386, [0.4, 0.4]),
-                                                       (3, (1,), 40000, [0.0, 0.25, 0.5]),
-                                                       (4, (1, 3), 65539, [0.3, 0.0, 0.6, 0.1]),
-                                                       (5, (2, 3), 4099, [0.0, 0.9, 0.2, 0.0, 0.5])])
+@pytest.mark.parametrize("n,cpu_ranks,length,ratios", [(2, (1,), 109386, [0.1, 0.1]),
+                                                       (2, (1,), 109386, [0.4, 0.05]),
+                                                       (3, (1,), 40000, [0.0, 0.05, 0.5]),
+                                                       (4, (1, 3), 65539, [0.3, 0.0, 0.1, 0.1]),
+                                                       (5, (2, 3), 4099, [0.0, 0.9, 0.1, 0.0, 0.05])])
 def test_tcp_ring_sparse_mixed_with_reference_workers(n, cpu_ranks, length, ratios):
     """MI355X workers and reference-style CPU workers, each with its own
     serializer (SparseCapable or Base), in one loopback ring: bit-exact."""
@@ -429,56 +517,107 @@ def test_tcp_ring_sparse_mixed_with_reference_workers(n, cpu_ranks, length, rati
         assert_bitexact(got[r][1], er[r], f"residual rank {r}")
 
 
-def test_tcp_ring_sparse_wire_bytes_and_lift_of_peer_frame():
-    """The first frame of a SparseCapable MI355X worker is the reference's
-    SparseGrad of grad_drop(chunk, calculate_threshold(chunk, r)); a SparseGrad
-    the peer sends back is lifted and added (scatter) like the reference's."""
-    length, r = 20000, 0.4
+def expect_push(chunk, r, state=0):
+    """The frame a SparseCapable{r} worker pushes for `chunk` (compressor.rs:71-98)."""
+    sparse, t, state = O.sparse_push(chunk, r, state)
+    if sparse:
+        return frame_sparse(O.grad_drop(chunk, t)), t, state
+    return O.frame_dense(O.f16_encode(chunk)), None, state
+
+
+@pytest.mark.parametrize("r", [0.05, 0.1, 0.3, 0.9, 1.0])
+def test_tcp_ring_sparse_wire_bytes_and_lift_of_peer_frame(r):
+    """The frames of a SparseCapable MI355X worker are the reference's: the
+    SparseGrad of grad_drop(chunk, calculate_threshold(chunk, r)) when that
+    stream is at most 2 bytes per value, else the DenseGrad of f16(chunk)
+    (compressor.rs:79-89) — r = 0.3 and above go dense on this distribution.
+    A SparseGrad the peer sends back is lifted and added (scatter), and the
+    owner's residual follows the push (worker_ring.rs:126-133, 177-193)."""
+    length = 20000
     x = O.synth(length, SEED + 3, 0)
     links, pairs = socketpair_links(2)
     w = GpuWorker(0, 2, length, [x], *links[0], sparse=(r, 0))
     w.start()
     from_gpu, to_gpu = links[1]
+    (a, b), (c, d) = O.split_chunks(length, 2)
+    y = O.synth(length, SEED + 3, 1)
+    ty = O.sparse_threshold(y[c:d], 0.1)
     try:
-        frame = recv_frame(from_gpu)
-        (a, b) = O.split_chunks(length, 2)[0]
-        t = O.sparse_threshold(x[a:b], r)
-        assert frame == frame_sparse(O.grad_drop(x[a:b], t))
-        # the peer (rank 1) answers with its own sparse chunk 1, then takes the gather frame
-        (c, d) = O.split_chunks(length, 2)[1]
-        y = O.synth(length, SEED + 3, 1)
-        ty = O.sparse_threshold(y[c:d], 0.6)
-        to_gpu.sendall(frame_sparse(O.grad_drop(y[c:d], ty)))
+        f0 = recv_frame(from_gpu)
+        exp0, t0, _ = expect_push(x[a:b], r)
+        assert f0 == exp0
+        assert f0[8:12] == ((3 if t0 is not None else 1)).to_bytes(4, "big")
+        to_gpu.sendall(frame_sparse(O.grad_drop(y[c:d], ty)))  # rank 1's sparse chunk 1
         g_frame = recv_frame(from_gpu)  # rank 0's gather push of its owned chunk 1
-        assert g_frame[8:12] == (3).to_bytes(4, "big")
-        to_gpu.close()
+        to_gpu.sendall(O.frame_dense(O.f16_encode(y[a:b])))
         w.join(60)
+        assert w.err is None, w.err
     finally:
         close_all(s for p in pairs for s in p)
-    # rank 0's chunk 1 = x + lift(peer); the gather push carries grad_drop of it
     owned = x[c:d] + O.grad_lift(O.grad_drop(y[c:d], ty), d - c)
-    t1 = O.sparse_threshold(owned, r)
-    assert g_frame == frame_sparse(O.grad_drop(owned, t1))
+    exp_g, t1, _ = expect_push(owned, r)
+    assert g_frame == exp_g
+    res0 = x[a:b].copy()
+    if t0 is not None:
+        res0[np.abs(res0) >= t0] = 0
+    else:
+        res0[:] = 0
+    assert_bitexact(w.residual[a:b], res0, "scatter chunk residual")
+    # the owned chunk: kept after a sparse gather push (:178-184), zeroed after a dense one (:191-193)
+    assert_bitexact(w.residual[c:d], owned if t1 is not None else np.zeros_like(owned), "owned residual")
+    g1 = owned.copy()
+    if t1 is not None:
+        g1[np.abs(g1) < t1] = 0
+    assert_bitexact(w.grad[c:d], (g1 / np.float32(2)).astype(np.float32), "owned grad")
 
 
-@pytest.mark.parametrize("payload,err", [("total", "proto"), ("short", "io"), ("overrun", "io"), ("huge", "proto")])
-def test_tcp_ring_sparse_bad_frames(payload, err):
-    """A SparseGrad whose total is not the hop's chunk, or whose stream is
-    malformed (the lift's errors, protocol.rs:96-144) or longer than any
-    encoding of the chunk."""
+@pytest.mark.parametrize("payload,phase,err", [("short", "scatter", "io"), ("overrun", "scatter", "io"),
+                                               ("tiny", "scatter", "io"), ("total", "gather", "proto"),
+                                               ("short", "gather", "io")])
+def test_tcp_ring_sparse_bad_frames(payload, phase, err):
+    """A malformed sparse stream fails with the lift's io::Error
+    (protocol.rs:96-144, recv_event's map_err); a well-formed one whose total
+    is not the chunk length is fine in the scatter (the zip) but cannot be
+    copied in the gather (copy_from_slice panics in the reference:
+    InvalidWorkerEvent here)."""
     length = 10001
     w, (from_gpu, to_gpu), pairs = start_two_rank(length, O.synth(length, SEED, 0))
-    (a, b) = O.split_chunks(length, 2)[1]
-    m = b - a
+    (a, b), (c, d) = O.split_chunks(length, 2)
+    m = (b - a) if phase == "gather" else (d - c)
     body = {"total": (m + 1).to_bytes(8, "little"),
             "short": m.to_bytes(8, "little") + b"\x00\x00\x00",
+            "tiny": b"\x01\x02",
             "overrun": m.to_bytes(8, "little") + (m - 1).to_bytes(4, "little") + (5).to_bytes(4, "little") + b"\0" * 10,
-            "huge": m.to_bytes(8, "little") + b"\0" * (8 * m)}[payload]  # > any grad_drop of m values
+            }[payload]
     try:
         recv_frame(from_gpu)
+        if phase == "gather":
+            to_gpu.sendall(O.frame_dense(O.f16_encode(np.zeros(d - c, np.float32))))
+            recv_frame(from_gpu)
         to_gpu.sendall(frame_sparse(body))
         w.join(60)
         want = ono_amd.InvalidWorkerEvent if err == "proto" else ono_amd.IoError
         assert isinstance(w.err, want), w.err
     finally:
         close_all(s for p in pairs for s in p)
+
+
+def test_tcp_ring_sparse_zero_length_runs_accepted():
+    """A stream of many empty runs is valid for the reference (every record
+    passes grad_lift_into's checks) whatever its length: the chunk lifts to
+    zeros, so the scatter adds nothing."""
+    length = 10001
+    x = O.synth(length, SEED + 2, 0)
+    w, (from_gpu, to_gpu), pairs = start_two_rank(length, x)
+    (a, b), (c, d) = O.split_chunks(length, 2)
+    m = d - c
+    try:
+        recv_frame(from_gpu)
+        to_gpu.sendall(frame_sparse(m.to_bytes(8, "little") + b"\0" * (8 * m)))
+        g_frame = recv_frame(from_gpu)
+        to_gpu.sendall(O.frame_dense(O.f16_encode(np.zeros(b - a, np.float32))))
+        w.join(60)
+        assert w.err is None, w.err
+    finally:
+        close_all(s for p in pairs for s in p)
+    assert g_frame == O.frame_dense(O.f16_encode(x[c:d]))

@@ -1,7 +1,7 @@
 """GPU parity of the xGMI peer-access schedule (ONO_ALGO_XGMI) against the oracle.
 
 n ranks run as n processes (tests/xgmi_worker.py), each owning a ring created
-with ono_ring_create_xgmi and connected through the 64-byte IPC handles of its
+with ono_ring_create_xgmi and connected through the 128-byte handles (IPC handle + ring id + size) of its
 peers — the production multi-process path.  On the one-GPU box every rank
 lives on cuda:0, so the mapped peer regions are IPC imports of the same
 device.  Checked bit for bit against the oracle's reference ring
@@ -104,6 +104,19 @@ def test_xgmi_host_fed_sub_round_pipeline(n):
              for w in ("f32", "f16") for f in ("host", "host_registered")]
     cases += [{"length": 4 * n + 1, "wire": "f16", "form": "host", "rounds": 1}]
     check(run_ranks(n, cases, ONO_HOST_CHUNK_MIB="1"))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_xgmi_recreate_rings_in_the_same_processes(n):
+    """Round 2's one wrong host-fed result came from the second ring of the
+    processes (the first torn down, the peers' regions re-imported).  Rings are
+    now created, used and destroyed six times in the same processes: every
+    connect checks each peer mapping page by page against the peer's ring id
+    (a stale import fails there with IoError), teardown frees a region only
+    after every peer has released it, and each cycle's host-fed sub-round
+    round is bit-exact."""
+    check(run_ranks(n, [{"kind": "recreate", "cycles": 6, "wire": "f16"},
+                        {"kind": "recreate", "cycles": 2, "wire": "f32"}], ONO_HOST_CHUNK_MIB="1"))
 
 
 def test_xgmi_timing_phases():

@@ -1,18 +1,30 @@
-"""The sparse ring mode on the CPU: oracle restatement, stand-in sampler and
+"""The sparse ring mode on the CPU: oracle restatements, stand-in sampler and
 the reference-style CPU ring workers (no GPU).
 
-Reference behaviour restated (see oracle/ono_oracle.c ono_ref_ring_pull_grads_sparse):
-  * SparseCapable{r} pushes a SparseGrad of the chunk's values with
-    |g| >= calculate_threshold(chunk, r) (comms/src/sparse/protocol.rs:33-86,
-    compressor.rs:71-98);
-  * scatter zeroes only the sent values (worker_ring.rs:126-133); gather keeps
-    only the sent values in grad (:177-193);
+Reference behaviour (read from the reference for round 3; restated twice, in
+C — oracle/ono_oracle.c ono_ref_ring_pull_grads_sparse — and independently in
+numpy — oracle/oracle_np.py ring_pull_grads_sparse, written line by line from
+worker_ring.rs:112-204 and compressor.rs:71-98):
+  * SparseCapable{r}'s push computes t = calculate_threshold(chunk, r) and the
+    grad_drop stream of the values with |g| >= t (comms/src/sparse/protocol.rs:
+    33-86); the stream goes out as a SparseGrad only when it is no longer than
+    the chunk's f16 payload, 2 bytes per value (compressor.rs:79); otherwise the
+    push is a DenseGrad of f16(chunk) (:84-89) and push_grad returns None
+    (handles/worker.rs:157-174);
+  * after a SparseGrad the scatter zeroes only the sent values
+    (worker_ring.rs:126-132) and the gather keeps only the sent values in grad
+    while the owned residual chunk is left as it is (:177-190; the reset at
+    :178-184 is commented out); after a DenseGrad the scatter zeroes the chunk
+    (:133) and the gather zeroes the owned residual at j == 0 (:191-193);
   * a receiver lifts a SparseGrad into a zero-filled buffer, then adds
     (scatter) or copies (gather) it (comms/src/handles/worker.rs:102-108).
 Parity status: the threshold, codec and frames are pinned by the reference's
 KATs (protocol.rs:150-223, sparse/tests.rs:13-59); the sparse ring's
 composition has no reference test (parity unpinned, like the dense ring), and
 above 16384 values the sample comes from a stand-in sampler, not rand 0.9.4.
+Round 2's restatement missed the dense fallback and reset the owned residual
+after a sparse push; both restatements here were rewritten from the reference
+text and agree bit for bit.
 """
 import numpy as np
 import pytest
@@ -20,6 +32,7 @@ import pytest
 import ono_amd
 from conftest import SEED, assert_bitexact
 from oracle import oracle as O
+from oracle import oracle_np as N
 
 
 def test_threshold_sample_matches_full_and_kat():
@@ -64,30 +77,100 @@ def test_sparse_ring_all_base_is_the_dense_ring(n, length):
     assert st == [11] * n
 
 
-@pytest.mark.parametrize("n,length,ratios", [(2, 20000, [0.4, 0.4]), (3, 40000, [0.25, 0.0, 0.9]),
-                                             (4, 4099, [1.0, 0.5, 0.5, 0.1])])
+@pytest.mark.parametrize("r,kind", [(0.1, 3), (0.3, 1), (0.4, 1), (0.6, 1), (0.9, 1), (1.0, 1)])
+def test_push_kind_on_the_synthetic_distribution(r, kind):
+    """The config-1 chunk (54,693 values of the §8(d) distribution): only r = 0.1
+    keeps the stream under 2 bytes per value; every larger ratio goes out as a
+    DenseGrad (compressor.rs:79-89).  Both restatements agree."""
+    x = O.synth(109386, SEED, 0)[:54693]
+    sparse, t, _ = O.sparse_push(x, r, 0)
+    _, sent, _, k = N.push_grad(x, r, 0)
+    assert k == kind and sparse == (kind == 3)
+    assert (sent is None) == (kind == 1)
+    drop = O.grad_drop(x, t)
+    assert (len(drop) <= 2 * x.size) == (kind == 3)
+    assert drop == N.grad_drop(x, t)
+
+
+def test_push_kat_alternating_goes_dense():
+    """A hand-built chunk whose every other value reaches the threshold: each
+    kept value costs a 10-byte run (8 B header + 2 B), 8 + 5 L bytes > 2 L, so
+    the SparseCapable push is a DenseGrad of f16(chunk); with the runs joined
+    (a kept block) the same values fit and go sparse."""
+    L = 64
+    alt = np.where(np.arange(L) % 2 == 0, 1.0, 0.25).astype(np.float32)
+    # r = 0.5: k = 32 -> the 33rd smallest |g| = 1.0 is the threshold
+    assert O.sparse_threshold(alt, 0.5) == 1.0
+    assert len(O.grad_drop(alt, 1.0)) == 8 + 32 * 10 > 2 * L
+    sparse, t, _ = O.sparse_push(alt, 0.5, 0)
+    assert not sparse and t == 1.0
+    block = np.sort(alt)[::-1].copy()  # 32 x 1.0 then 32 x 0.25: one run
+    assert len(O.grad_drop(block, 1.0)) == 8 + 8 + 64 <= 2 * L
+    sparse, t, _ = O.sparse_push(block, 0.5, 0)
+    assert sparse and t == 1.0
+    # the ring: rank 0's first push of the alternating chunk is dense, so the
+    # chunk is zeroed whole (worker_ring.rs:133), unlike a sparse push
+    x = [np.concatenate([alt, alt]), np.concatenate([block, block])]
+    g, res, _ = O.ring_pull_grads_sparse(x, [0.5, 0.5], [0, 0])
+    g2, res2, _ = N.ring_pull_grads_sparse(x, [0.5, 0.5], [0, 0])
+    for r in range(2):
+        assert_bitexact(g[r], g2[r], f"grad {r}")
+        assert_bitexact(res[r], res2[r], f"residual {r}")
+    assert not res[0][:L].any(), "a DenseGrad push zeroes the whole chunk"
+    assert res[1][L:].any(), "a SparseGrad push leaves the unsent values"
+
+
+@pytest.mark.parametrize("n,length,ratios", [(2, 109386, [0.1, 0.1]), (2, 109386, [0.3, 0.9]),
+                                             (2, 20000, [0.4, 0.4]), (3, 40000, [0.25, 0.0, 0.9]),
+                                             (4, 4099, [1.0, 0.5, 0.5, 0.1]), (4, 70001, [0.0, 0.3, 0.0, 1.0]),
+                                             (5, 4099, [0.5, 0.0, 0.0, 0.2, 0.7]), (3, 60000, [0.05, 0.1, 0.15])])
+def test_sparse_ring_c_equals_numpy(n, length, ratios):
+    """The C restatement and the independent numpy one (written from the
+    reference text) agree bit for bit on grads, residuals and sampler states."""
+    seeds = [7 * r + 1 for r in range(n)]
+    x = [O.synth(length, SEED + 5, r) for r in range(n)]
+    g, res, st = O.ring_pull_grads_sparse(x, ratios, seeds)
+    g2, res2, st2 = N.ring_pull_grads_sparse(x, ratios, seeds)
+    for r in range(n):
+        assert_bitexact(g[r], g2[r], f"grad {r}")
+        assert_bitexact(res[r], res2[r], f"residual {r}")
+    assert st == st2
+
+
+@pytest.mark.parametrize("n,length,ratios", [(2, 20000, [0.1, 0.1]), (3, 40000, [0.05, 0.0, 0.1]),
+                                             (4, 4099, [1.0, 0.5, 0.5, 0.1]), (2, 20000, [0.4, 0.4])])
 def test_sparse_ring_semantics(n, length, ratios):
-    """Properties of the restated sparse round that hold whatever the sample:
-    a sparse worker's residual keeps exactly what it did not send, values
-    below f16::MIN_POSITIVE are never sent, every replica of a chunk holds
-    values that are f16-exact (after the ÷n) or the owner's f32, and a worker
-    whose serializer is Base zeroes what it sent."""
+    """Properties of the round that hold whatever the sample: after a sparse
+    gather push the owned residual chunk still holds the reduced sum (it is not
+    reset); after a dense one it is zero; a sparse scatter push leaves exactly
+    the unsent values; a Base worker ends with a zero residual."""
     x = [O.synth(length, SEED + 5, r) for r in range(n)]
     g, res, _ = O.ring_pull_grads_sparse(x, ratios, list(range(n)))
     chunks = O.split_chunks(length, n)
+    st = list(range(n))
     for r in range(n):
         own = (r + 1) % n
         a, b = chunks[own]
-        assert not res[r][a:b].any(), "the owned chunk's residual is reset at gather j = 0"
         if ratios[r] == 0.0:
             assert not res[r].any(), "Base serializer: every sent chunk is zeroed"
-        else:
+            continue
+        # the scatter's first push is the rank's own-index chunk, unchanged
+        sl = slice(*chunks[r])
+        first_sparse, _, _ = O.sparse_push(x[r][sl], ratios[r], st[r])
+        if first_sparse:
             tiny = np.abs(x[r]) < np.float32(6.103515625e-05)
-            sent_chunk = chunks[r]  # scatter step 0 sends the rank's own-index chunk unchanged
-            sl = slice(*sent_chunk)
             assert_bitexact(res[r][sl][tiny[sl]], x[r][sl][tiny[sl]], "sub-f16 values stay in the residual")
             kept = res[r][sl] != 0
             assert_bitexact(res[r][sl][kept], x[r][sl][kept], "unsent values stay as they were")
+        else:
+            assert not res[r][sl].any(), "a dense push zeroes the chunk"
+        # the owner's chunk: grad = sum / n (f32) before the gather's mask; the
+        # residual keeps the sum after a sparse push, zero after a dense one
+        owned_sum = res[r][a:b]
+        if owned_sum.any():
+            kept = g[r][a:b] != 0
+            assert_bitexact(g[r][a:b][kept], (owned_sum / np.float32(n)).astype(np.float32)[kept],
+                            "the owner's kept values are the residual's sum / n")
 
 
 def free_port() -> int:

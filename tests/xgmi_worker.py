@@ -4,7 +4,7 @@ Every rank is its own process (as on an 8-GPU node: one process per GPU); on
 the one-GPU test box all ranks share cuda:0, so the peer regions they map are
 IPC imports of the same device — the same code path (export, import, peer
 loads/stores, flag barriers), with HBM standing in for the xGMI links.  The
-64-byte handles travel over a gloo group (the control channel the reference
+128-byte handles travel over a gloo group (the control channel the reference
 would use is its ring TCP links).
 
 usage: python xgmi_worker.py RANK NRANKS (PORT | file://PATH) CASES_JSON
@@ -229,6 +229,41 @@ def run_timeout(rank: int, n: int, how: str = "env") -> str | None:
         ring.close()
 
 
+def run_recreate(rank: int, n: int, case: dict) -> str | None:
+    """Create, use and destroy an xGMI ring several times in the same processes
+    (the situation of round 2's one wrong host-fed result: the second ring of a
+    process).  Every connect verifies each peer mapping page by page against
+    the ring id in that peer's handle (a stale import is an IoError at
+    connect); every cycle runs the host-fed sub-round round bit-exact."""
+    cycles, length = case.get("cycles", 6), case.get("length", (1 << 20) + 3)
+    seen, repeats = set(), 0
+    for cyc in range(cycles):
+        blobs = {}
+
+        def ag(b: bytes) -> list:
+            blobs["mine"] = b
+            return allgather(b)
+        ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, ag, wire=case.get("wire", "f16"))
+        try:
+            ipc = blobs["mine"][:64]
+            repeats += ipc in seen  # the same IPC handle bytes as an earlier region of this process
+            seen.add(ipc)
+            ins = [O.synth(length, SEED + 1000 * cyc, r) for r in range(n)]
+            expect, _ = O.ring_pull_grads(ins, case.get("wire", "f16"))
+            res_h = np.ascontiguousarray(ins[rank]).copy()
+            grad_h = np.full(length, 7.0, np.float32)
+            ring.pull_grads_host(res_h, grad_h)
+            bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
+            if bad.size:
+                return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats so far {repeats})"
+            if bits(res_h).any():
+                return f"cycle {cyc}: host residual not zeroed"
+        finally:
+            ring.close()
+    print(json.dumps({"rank": rank, "recreate_ipc_handle_repeats": repeats, "cycles": cycles}), file=sys.stderr)
+    return None
+
+
 def main() -> int:
     rank, n, rdv = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     cases = json.loads(sys.argv[4])
@@ -241,7 +276,8 @@ def main() -> int:
         try:
             kind = case.get("kind", "ring")
             msg = run_timeout(rank, n, case.get("how", "env")) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
-                run_timing(rank, n) if kind == "timing" else run_case(rank, n, case)
+                run_timing(rank, n) if kind == "timing" else run_recreate(rank, n, case) if kind == "recreate" else \
+                run_case(rank, n, case)
         except Exception as e:  # reported, the parent asserts
             msg = f"{type(e).__name__}: {e}"
         results.append({"case": case, "ok": msg is None, "msg": msg or ""})
