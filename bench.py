@@ -222,7 +222,8 @@ def pmc_traffic(kernel_substr: str, elems: int) -> dict | None:
             continue
         for k in d.get("kernels", []):
             if kernel_substr in k.get("name", "") and k.get("elems") == elems:
-                best = dict(k, source=os.path.relpath(f, ROOT))
+                best = dict(k, source=os.path.relpath(f, ROOT), commit=d.get("commit", "unknown"),
+                            session=d.get("session") or "a builder session")
     return best
 
 
@@ -865,6 +866,9 @@ def main(argv=None) -> int:
         }
         if pmc:
             extra["roofline"]["traffic_source"] = pmc["source"]
+            extra["roofline"]["traffic_provenance"] = (
+                f"committed profile {pmc['source']}@{pmc.get('commit', 'unknown')} "
+                f"({pmc.get('session', 'a builder session')}); not measured in this run")
     else:
         extra["roofline"] = xgmi_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo, args.steps)
         if link:
@@ -917,6 +921,13 @@ def main(argv=None) -> int:
             leg("sparse_codec", lambda: sparse_codec(torch, ono_amd))
         if not args.no_cpu_baseline:
             leg("cpu_baseline", lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
+        lr = extra.get("local_reduce", {})
+        fr = {k: lr[k]["frac_of_hbm_peak"] for k in ("k2", "k4", "k8") if isinstance(lr.get(k), dict)}
+        if fr:  # the reduce kernel's bar (north_star: >= 80 % of HBM) beside the N = 1 copy-kernel frac
+            extra["roofline"]["reduce_kernel"] = {
+                "kernel": "sum_scale_f32, 64 MiB, k = 2 / 4 / 8 inputs (BASELINE config 2)",
+                "frac": fr, "frac_min": min(fr.values()), "north_star_target_frac": 0.80,
+                "timing": lr.get("timing")}
 
     value = world * bucket_bytes * args.steps / elapsed / GIB
     line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,

@@ -232,7 +232,20 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
 }
 
 // ============================================================== ops =======
-// sum-and-scale over K inputs (K compile-time), left fold in input order
+// sum-and-scale over K inputs (K compile-time), left fold in input order.
+// Read-once inputs (NTL) at the 64 MiB bucket of BASELINE config 2, measured
+// in round 3 (tools/sum_variants.hip, profiles/r03_sum_variants.txt; same box,
+// medians of 3-5 passes):
+//   K >= 4: ONE load in flight per wave (each input's vector requested once
+//           the previous one has returned): K = 8 99.9 -> 94.9 us (0.755 ->
+//           0.796 of 8 TB/s), K = 4 56.4 -> 53.7 us (0.743 -> 0.782).  All K
+//           loads issued at once — what the compiler does by itself — is the
+//           slowest form; two or three in flight measured like all of them.
+//           (Found through a load-order rotation that happened to serialize
+//           its loads through one register set.)
+//   K == 2: the two inputs land in LDS by LDS-DMA (global_load_lds_dwordx4
+//           nt, no VGPR round trip) and are added from there: 32.3 -> 32.0 us
+//           (0.778 -> 0.787); one load in flight measured no different there.
 struct Ptrs {
     const float *p[ONO_MAX_INPUTS];
 };
@@ -252,10 +265,32 @@ template <int K, int M, bool NTL> struct SumScaleOp {
         else return ld((const f4 *)(in.p[j] + i));
     }
     __device__ __forceinline__ R load(size_t i) const {
-        f4 a = get(0, i);
+        if constexpr (NTL && K == 2) {
+            __shared__ f4 lds[2][kBlock];  // lane l's 16 B of input j land at lds[j][l]
 #pragma unroll
-        for (int j = 1; j < K; j++) a += get(j, i);
-        return a;
+            for (int j = 0; j < 2; j++)
+                __builtin_amdgcn_global_load_lds((const void *)(in.p[j] + i),
+                                                 (__attribute__((address_space(3))) void *)&lds[j][0], 16, 0, 2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return lds[0][threadIdx.x] + lds[1][threadIdx.x];
+        } else if constexpr (NTL && K >= 4) {
+            // one load in flight per wave: each input's vector is requested
+            // once the previous one has returned (fold in input order)
+            f4 a = get(0, i);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int j = 1; j < K; j++) {
+                const f4 x = get(j, i);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                a += x;
+            }
+            return a;
+        } else {
+            f4 a = get(0, i);
+#pragma unroll
+            for (int j = 1; j < K; j++) a += get(j, i);
+            return a;
+        }
     }
     __device__ __forceinline__ void store(size_t i, R a) const { st_nt((f4 *)(out + i), scl4<M>(a, v)); }
 };

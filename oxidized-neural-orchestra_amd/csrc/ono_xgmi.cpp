@@ -28,23 +28,29 @@
 // links at once.  No stream synchronisation or host round trip per round: the
 // barriers are device-side flag exchanges with a timeout.
 //
-// Connect is verified, teardown is ordered (round 3).  Every region carries a
-// random 64-bit ring id: in its flag page and at the start of every 4 KiB
-// page, stamped before the handle leaves the process; the handle blob that
-// travels to the peers (ONO_XGMI_HANDLE_BYTES) holds the IPC handle, the id
-// and the region's size.  An importer reads every page's stamp through its
-// new mapping before the first round (a device barrier at the end of connect
-// keeps every rank from writing a peer region until all importers have
-// checked): a mapping that shows anything else — memory of an earlier region
-// of that peer, from an import the runtime kept or recycled — is an ONO_E_IO
-// at connect time instead of wrong data in a later round.  Destroy no longer
-// frees a region that peers may still map: each rank, once its own work is
-// done, stores the owner's id into a teardown slot of every peer region it
-// imported, then closes those imports; an owner frees its region only when
-// every peer's marker is there (or the timeout passed).  Round 2 freed the
-// region right after a barrier, while peers still held imports of it, and
-// re-created rings in the same processes (the host-fed test's one recorded
-// wrong result came from the second ring of the process).
+// Connect is verified, teardown is ordered, and no exchange region is ever
+// freed or unmapped while the process lives (round 3).  Every region carries a
+// random 64-bit ring id, stamped at the start of every 4 KiB page before its
+// handle leaves the process; the handle blob (ONO_XGMI_HANDLE_BYTES) holds the
+// IPC handle, the ring id, the layout's size and a per-region uid.  An
+// importer reads every page's stamp through its mapping before the first
+// round (a device barrier at the end of connect keeps every rank from writing
+// a peer region until all importers have checked): a mapping that shows
+// another region's memory is an ONO_E_IO at connect time.  That check is what
+// found the cause of round 2's one wrong host-fed result: with regions freed
+// at destroy and re-imported by the next ring of the same processes, the HIP
+// IPC path on this image handed out mappings with a few pages (9 of 1,026 in
+// the recorded case) still backed by an earlier region's memory — after the
+// exporter's new IPC handle had repeated the bytes of one it had exported
+// before (the test logs the repeats).  So regions are pooled per process: a
+// destroyed ring's region (flags reset, re-stamped) serves the next ring that
+// fits in it, a new one is allocated only when none fits, and importers keep
+// every peer region they mapped (keyed by its uid) for reuse instead of
+// closing it — no handle, virtual address or mapping is ever recycled.
+// Destroy stays collective: each rank, once its own work is done, stores the
+// owner's id into a teardown slot of every peer region it mapped; an owner
+// returns its region to the pool only when every peer's marker is there (or
+// the timeout passed), so a region is never reset while a peer still uses it.
 //
 // Reuse safety without a third barrier: a rank writes peer q's rbuf in round
 // r+1 only after passing barrier 4 of round r, which q reaches after its step 3
@@ -59,6 +65,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -75,8 +82,29 @@ constexpr size_t kDoneOff = 1024;    //   teardown markers (n x u64),
 constexpr size_t kIdOff = 2048;      //   the region's ring id
 constexpr size_t kPage = 4096;       // every later page starts with the id until the first round
 // the handle blob: [hipIpcMemHandle_t][u64 ring id][u64 region bytes][zero]
-constexpr size_t kBlobId = sizeof(hipIpcMemHandle_t), kBlobBytes = kBlobId + 8;
-static_assert(kBlobBytes + 8 <= ONO_XGMI_HANDLE_BYTES, "handle blob layout");
+constexpr size_t kBlobId = sizeof(hipIpcMemHandle_t), kBlobBytes = kBlobId + 8, kBlobUid = kBlobBytes + 8,
+                 kBlobAlloc = kBlobUid + 8;
+static_assert(kBlobAlloc + 8 <= ONO_XGMI_HANDLE_BYTES, "handle blob layout");
+
+// The process's exchange regions (never freed: see the header comment) and
+// the peer regions it has mapped (never unmapped), under one lock.
+struct PooledRegion {
+    int device;
+    uint8_t *ptr;
+    size_t bytes;
+    uint64_t uid;
+    hipIpcMemHandle_t handle;
+    bool busy;
+};
+struct MappedPeer {
+    int device;
+    uint64_t uid;
+    size_t bytes;
+    uint8_t *ptr;
+};
+std::mutex g_pool_mu;
+std::vector<PooledRegion> g_regions;
+std::vector<MappedPeer> g_mapped;
 
 struct XgmiState {
     uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
@@ -92,8 +120,11 @@ struct XgmiState {
     uint64_t timeout_ticks = 0;
     double timeout_s = 0;
     std::vector<hipEvent_t> ev;       // host-fed sub-round pipeline: H2D / round / D2H per sub-round
-    uint64_t id = 0;                  // this region's ring id (stamped, sent in the handle blob)
-    size_t bytes = 0;                 // this region's size
+    uint64_t id = 0;                  // this ring's id (stamped into the region, sent in the handle blob)
+    size_t bytes = 0;                 // the layout's size (every rank of the ring computes the same)
+    size_t alloc = 0;                 // the pooled region's size (>= bytes)
+    uint64_t uid = 0;                 // the pooled region's uid
+    hipIpcMemHandle_t handle{};       // its IPC handle
     std::vector<uint64_t> peer_id;    // every peer region's id, from its blob
 };
 
@@ -132,7 +163,32 @@ int xgmi_alloc(ono_ring *r) {
     const size_t bytes = x->push_gather ? x->gat_off + rb : x->gat_off;
     x->bytes = bytes;
     x->id = fresh_ring_id();
-    ONO_HIP(hipExtMallocWithFlags((void **)&x->xbuf, bytes, hipDeviceMallocUncached));
+    {  // the smallest free pooled region that fits, else a new one
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        PooledRegion *best = nullptr;
+        for (auto &pr : g_regions)
+            if (!pr.busy && pr.device == r->device && pr.bytes >= bytes && (!best || pr.bytes < best->bytes))
+                best = &pr;
+        if (!best) {
+            PooledRegion pr{};
+            pr.device = r->device;
+            pr.bytes = align_up(bytes, kPage);
+            pr.uid = fresh_ring_id();
+            ONO_HIP(hipExtMallocWithFlags((void **)&pr.ptr, pr.bytes, hipDeviceMallocUncached));
+            hipError_t e = hipIpcGetMemHandle(&pr.handle, pr.ptr);
+            if (e != hipSuccess) {
+                (void)hipFree(pr.ptr);
+                return hip_error(e, "hipIpcGetMemHandle (exchange region)", __FILE__, __LINE__);
+            }
+            g_regions.push_back(pr);
+            best = &g_regions.back();
+        }
+        best->busy = true;
+        x->xbuf = best->ptr;
+        x->alloc = best->bytes;
+        x->uid = best->uid;
+        x->handle = best->handle;
+    }
     ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0, no teardown markers
     ONO_HIP(launch_xgmi_stamp(x->xbuf, (bytes + kPage - 1) / kPage, kIdOff, x->id, nullptr));
     ONO_HIP(hipDeviceSynchronize());              // zeroed and stamped before the handle leaves this process
@@ -185,12 +241,31 @@ uint8_t *gslot_of(const XgmiState *x, uint8_t *region_q, int o, int q) {
 
 int barrier(ono_ring *r, hipStream_t s);
 
-void make_blob(const XgmiState *x, const hipIpcMemHandle_t &h, uint8_t *blob) {
+void make_blob(const XgmiState *x, uint8_t *blob) {
     memset(blob, 0, ONO_XGMI_HANDLE_BYTES);
-    memcpy(blob, &h, sizeof h);
+    memcpy(blob, &x->handle, sizeof x->handle);
     memcpy(blob + kBlobId, &x->id, 8);
-    const uint64_t b = x->bytes;
+    const uint64_t b = x->bytes, a = x->alloc;
     memcpy(blob + kBlobBytes, &b, 8);
+    memcpy(blob + kBlobUid, &x->uid, 8);
+    memcpy(blob + kBlobAlloc, &a, 8);
+}
+
+// peer region `uid` as mapped in this process: the mapping made for an
+// earlier ring, else a new import (kept for the life of the process)
+int map_peer(ono_ring *r, const hipIpcMemHandle_t &h, uint64_t uid, size_t alloc, uint8_t **out) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (const auto &m : g_mapped)
+        if (m.device == r->device && m.uid == uid && m.bytes == alloc) {
+            *out = m.ptr;
+            return ONO_OK;
+        }
+    void *p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
+    g_mapped.push_back({r->device, uid, alloc, static_cast<uint8_t *>(p)});
+    *out = static_cast<uint8_t *>(p);
+    return ONO_OK;
 }
 
 // Every page of peer q's region as mapped here must show the id q stamped.
@@ -227,31 +302,26 @@ int xgmi_connect(ono_ring *r, const uint8_t *handles) {
         const uint8_t *blob = handles + (size_t)q * ONO_XGMI_HANDLE_BYTES;
         hipIpcMemHandle_t h;
         memcpy(&h, blob, sizeof h);
-        uint64_t id = 0, bytes = 0;
+        uint64_t id = 0, bytes = 0, uid = 0, alloc = 0;
         memcpy(&id, blob + kBlobId, 8);
         memcpy(&bytes, blob + kBlobBytes, 8);
-        if (id == 0 || bytes != x->bytes) {
+        memcpy(&uid, blob + kBlobUid, 8);
+        memcpy(&alloc, blob + kBlobAlloc, 8);
+        if (id == 0 || uid == 0 || bytes != x->bytes || alloc < bytes) {
             rc = set_error(ONO_E_ARG, "xGMI connect: rank %d's handle is not an exchange region of this ring "
                            "(id %016llx, %llu bytes; expected %zu)", q, (unsigned long long)id,
                            (unsigned long long)bytes, x->bytes);
             break;
         }
-        void *p = nullptr;
-        hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-            rc = hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
-            break;
-        }
-        x->peer[q] = static_cast<uint8_t *>(p);
+        uint8_t *p = nullptr;
+        if ((rc = map_peer(r, h, uid, (size_t)alloc, &p))) break;
+        x->peer[q] = p;
         x->peer_id[q] = id;
         rc = verify_import(r, q, id, (size_t)bytes);
     }
-    if (rc) {  // leave no import behind: a later connect starts over
+    if (rc) {  // the mappings stay in the process's table (never unmapped); this ring is not connected
         for (int q = 0; q < r->n; q++)
-            if (q != r->pos && x->peer[q]) {
-                (void)hipIpcCloseMemHandle(x->peer[q]);
-                x->peer[q] = nullptr;
-            }
+            if (q != r->pos) x->peer[q] = nullptr;
         return rc;
     }
     x->connected = true;
@@ -272,9 +342,7 @@ int xgmi_connect_over_rccl(ono_ring *r, hipStream_t s) {
     if (!r->comm) return set_error(ONO_E_ARG, "xGMI ring not connected: call ono_ring_xgmi_connect first");
     const size_t H = ONO_XGMI_HANDLE_BYTES;
     std::vector<uint8_t> all((size_t)r->n * H);
-    hipIpcMemHandle_t h;
-    ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
-    make_blob(r->xgmi, h, all.data() + (size_t)r->pos * H);
+    make_blob(r->xgmi, all.data() + (size_t)r->pos * H);
     uint8_t *d = nullptr;
     ONO_HIP(hipMalloc((void **)&d, all.size()));
     hipError_t e = hipMemcpyAsync(d + (size_t)r->pos * H, all.data() + (size_t)r->pos * H, H, hipMemcpyHostToDevice, s);
@@ -550,14 +618,15 @@ void xgmi_abort(ono_ring *r) {
     if (r->xgmi && r->xgmi->err) __atomic_store_n(r->xgmi->err, 2u, __ATOMIC_RELEASE);
 }
 
-// Teardown is collective and ordered: a region is freed only after every
-// peer has said it is done with it.  Once this rank's own work is complete
-// (device synchronised: its last pushes into and pulls from peer regions are
-// over), it stores each peer's ring id into that peer's teardown slot `pos`
-// (system-scope stores through the import), then closes its imports; it then
-// waits until its own region holds its id in every peer's slot and frees it.
-// A peer that never arrives costs the timeout, no more; after a barrier
-// timeout or an abort nobody waits.
+// Teardown is collective and ordered: a region goes back to the pool (where
+// the next ring resets its flags) only after every peer has said it is done
+// with it.  Once this rank's own work is complete (device synchronised: its
+// last pushes into and pulls from peer regions are over), it stores each
+// peer's ring id into that peer's teardown slot `pos` (system-scope stores
+// through its mapping, which stays in the process's table); it then waits
+// until its own region holds its id in every peer's slot.  A peer that never
+// arrives costs the timeout, no more; after a barrier timeout or an abort this
+// rank does not wait.
 void xgmi_free(ono_ring *r) {
     XgmiState *x = r->xgmi;
     if (!x) return;
@@ -577,8 +646,6 @@ void xgmi_free(ono_ring *r) {
         ok = ok && launch_xgmi_signal(sig, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
         wait &= ok;
     }
-    for (int q = 0; q < (int)x->peer.size(); q++)
-        if (q != r->pos && x->peer[q]) (void)hipIpcCloseMemHandle(x->peer[q]);
     if (wait) {  // every peer's marker in this region (uncached: a D2H copy reads what landed)
         const auto t0 = std::chrono::steady_clock::now();
         std::vector<uint64_t> done(r->n);
@@ -594,7 +661,11 @@ void xgmi_free(ono_ring *r) {
         }
     }
     for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
-    (void)hipFree(x->xbuf);
+    {  // the region goes back to the pool; peer mappings stay in the process's table
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (auto &pr : g_regions)
+            if (pr.ptr == x->xbuf) pr.busy = false;
+    }
     if (x->err) (void)hipHostFree(x->err);
     delete x;
     r->xgmi = nullptr;
@@ -634,10 +705,7 @@ int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
     if (r->n == 1) return ONO_OK;
     int rc = xgmi_alloc(r);
     if (rc) return rc;
-    DeviceGuard g(r->device);
-    hipIpcMemHandle_t h;
-    ONO_HIP(hipIpcGetMemHandle(&h, r->xgmi->xbuf));
-    make_blob(r->xgmi, h, handle);
+    make_blob(r->xgmi, handle);
     return ONO_OK;
 }
 

@@ -157,5 +157,24 @@ def test_optimizer_and_sum_scale_stream_non_temporal(kernels):
         for k, code in _one_shot(kernels, op).items():
             if op == "SumScaleOp" and not re.search(r"SumScaleOpILi\d+ELi\dELb1E", k):
                 continue  # the in-place form (out aliases an input) keeps plain loads
-            loads = _vec_loads(code)
+            loads = _vec_loads(code) + [i for i in code if i.startswith("global_load_lds_dwordx")]
             assert loads and all(" nt" in i for i in loads), f"{k}: {loads}"
+
+
+def test_sum_scale_load_forms(kernels):
+    """Round 3: K = 2 reads its inputs by LDS-DMA (two
+    global_load_lds_dwordx4 nt, no VGPR loads); K >= 4 keeps ONE vector load
+    in flight per wave: its K nt loads are each followed by vmcnt(0) before the
+    next is issued."""
+    ks = {k: v for k, v in _one_shot(kernels, "SumScaleOp").items() if re.search(r"SumScaleOpILi\d+ELi\dELb1E", k)}
+    assert ks
+    for k, code in ks.items():
+        K = int(re.search(r"SumScaleOpILi(\d+)E", k).group(1))
+        glds = [i for i in code if i.startswith("global_load_lds_dwordx4")]
+        vec = [n for n, i in enumerate(code) if i.startswith("global_load_dwordx4")]
+        if K == 2:
+            assert len(glds) == 2 and not vec, f"{k}: {glds} {vec}"
+        elif K >= 4:
+            assert len(vec) == K and not glds, f"{k}: {len(vec)} vector loads"
+            for a_, b_ in zip(vec, vec[1:]):
+                assert any(code[j] == "s_waitcnt vmcnt(0)" for j in range(a_ + 1, b_)), f"{k}: two loads in flight"

@@ -246,7 +246,7 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
         ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, ag, wire=case.get("wire", "f16"))
         try:
             ipc = blobs["mine"][:64]
-            repeats += ipc in seen  # the same IPC handle bytes as an earlier region of this process
+            repeats += ipc in seen  # a pooled region serving again (same IPC handle, same memory)
             seen.add(ipc)
             ins = [O.synth(length, SEED + 1000 * cyc, r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, case.get("wire", "f16"))

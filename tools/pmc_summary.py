@@ -46,6 +46,8 @@ def main() -> int:
     ap.add_argument("--match", nargs="*", default=["ScaleZeroOp", "SumScaleOp", "AccOp", "AddEncodeZeroOp",
                                                   "DecodeScaleOp", "OptOp", "DirectOp<8,"])
     ap.add_argument("--algo-bytes-per-elem", type=float, default=12.0)
+    ap.add_argument("--commit", default="unknown", help="git commit of the code the passes ran")
+    ap.add_argument("--session", default="", help="which session / box recorded the passes")
     ap.add_argument("--local-elems", type=int, default=16 << 20,
                     help="bucket length of bench.py's local_reduce (SumScaleOp<k> kernels: (k+1) x 4 B/elem)")
     a = ap.parse_args()
@@ -82,7 +84,7 @@ def main() -> int:
             "traffic_over_algorithmic": (rd + wr) / algo,
         })
     doc = {"note": "median over launches; read = 2 x FETCH_SIZE x 1 KiB (gfx950 half-count), write = WRITE_SIZE x 1 KiB",
-           "kernels": kernels}
+           "commit": a.commit, "session": a.session, "kernels": kernels}
     with open(a.out, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc, indent=1))
