@@ -290,9 +290,9 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
     set exceeds the 256 MiB Infinity Cache by > 4x)."""
     n = 16 << 20
     out = {}
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a stream of its own (the ring's reductions run on the caller's)
     for k in (2, 4, 8):
-        nsets = max(3, -(-1024 // ((k + 1) * 64)) + 1)
+        nsets = 1536 // ((k + 1) * 64) + 2  # > 1.5 GiB per rotation: every launch reads HBM
         sets = []
         for si in range(nsets):
             ins = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(k)]
@@ -301,13 +301,13 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
             sets.append((ins, torch.empty(n, dtype=torch.float32, device="cuda")))
         for i in range(warmup):
             ins, dst = sets[i % nsets]
-            ono_amd.kernels.sum_scale(dst, ins, float(k))
+            ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         a.record(stream)
         for i in range(steps):
             ins, dst = sets[(warmup + i) % nsets]
-            ono_amd.kernels.sum_scale(dst, ins, float(k))
+            ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
         b.record(stream)
         torch.cuda.synchronize()
         ms = a.elapsed_time(b) / steps

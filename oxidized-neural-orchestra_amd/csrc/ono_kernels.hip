@@ -137,6 +137,10 @@ template <class Op> struct HasFinish<Op, std::void_t<decltype(std::declval<const
 template <class Op> __device__ __forceinline__ void finish_wave(const Op &op) {
     if constexpr (HasFinish<Op>::value) op.finish();
 }
+// Ops that cap how many of their one-wave workgroups share a CU declare the
+// dynamic LDS each workgroup reserves (kLds bytes; 160 KiB per CU).
+template <class Op, class = void> struct DynLds { static constexpr unsigned value = 0; };
+template <class Op> struct DynLds<Op, std::void_t<decltype(Op::kLds)>> { static constexpr unsigned value = Op::kLds; };
 
 // LOOP = false: the grid covers every vector (the one-shot grid), so no loop
 // at all — one guarded vector per lane (dec 2.5 %, sum8 1 % faster than the
@@ -209,7 +213,7 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     if (!same) {
         size_t blocks = (n + kBlock - 1) / kBlock;
         if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), 0, s, op, n);
+        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), DynLds<Op>::value, s, op, n);
         return hipGetLastError();
     }
     size_t head = (4 - ph) & 3u;
@@ -219,10 +223,12 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     size_t blocks = (work + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     if (blocks > cap) {
-        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(kBlock), 0, s, op, head, nvec, n);
+        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(kBlock), DynLds<Op>::value, s, op, head,
+                           nvec, n);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(kBlock), 0, s, op, head, nvec, n);
+    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(kBlock), DynLds<Op>::value, s, op, head,
+                       nvec, n);
     return hipGetLastError();
 }
 
@@ -237,19 +243,27 @@ hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> pha
 // in round 3 (tools/sum_variants.hip, profiles/r03_sum_variants.txt; same box,
 // medians of 3-5 passes):
 //   K >= 4: ONE load in flight per wave (each input's vector requested once
-//           the previous one has returned): K = 8 99.9 -> 94.9 us (0.755 ->
-//           0.796 of 8 TB/s), K = 4 56.4 -> 53.7 us (0.743 -> 0.782).  All K
-//           loads issued at once — what the compiler does by itself — is the
-//           slowest form; two or three in flight measured like all of them.
-//           (Found through a load-order rotation that happened to serialize
-//           its loads through one register set.)
+//           the previous one has returned) and at most 28 of these one-wave
+//           workgroups per CU (5.6 KiB of dynamic LDS each, unused): K = 8
+//           99.9 -> 91.7 us (0.756 -> 0.823 of 8 TB/s), K = 4 55.9 -> 52.9 us
+//           (0.750 -> 0.794).  All K loads issued at once — what the compiler
+//           does by itself — is the slowest form; two or three in flight
+//           measured like all of them; the cap alone (26-30 per CU) adds 1-2 %
+//           to one load in flight, and costs every other shape.  (Found through
+//           a load-order rotation that happened to serialize its loads through
+//           one register set.)
 //   K == 2: the two inputs land in LDS by LDS-DMA (global_load_lds_dwordx4
 //           nt, no VGPR round trip) and are added from there: 32.3 -> 32.0 us
 //           (0.778 -> 0.787); one load in flight measured no different there.
 struct Ptrs {
     const float *p[ONO_MAX_INPUTS];
 };
-template <int K, int M, bool NTL> struct SumScaleOp {
+// SER: the serialized form (K >= 4, buckets of at least kSerialElems, where
+// bandwidth, not one wave's latency, decides; smaller buckets keep every load
+// in flight).
+constexpr size_t kSerialElems = size_t(4) << 20;
+template <int K, int M, bool NTL, bool SER = false> struct SumScaleOp {
+    static constexpr unsigned kLds = SER ? 160u * 1024u * 2u / 57u : 0u;  // <= 28 workgroups per CU
     Ptrs in;
     float *out;
     float v;
@@ -273,7 +287,8 @@ template <int K, int M, bool NTL> struct SumScaleOp {
                                                  (__attribute__((address_space(3))) void *)&lds[j][0], 16, 0, 2);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             return lds[0][threadIdx.x] + lds[1][threadIdx.x];
-        } else if constexpr (NTL && K >= 4) {
+        } else if constexpr (SER) {
+            static_assert(NTL && K >= 4, "the serialized form reads K >= 4 read-once inputs");
             // one load in flight per wave: each input's vector is requested
             // once the previous one has returned (fold in input order)
             f4 a = get(0, i);
@@ -665,6 +680,15 @@ hipError_t sum_scale_k(float *out, const Ptrs &p, size_t n, const Scale &sc, hip
         case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE, false>{p, out, sc.v}, n, ph, s);
         case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP, false>{p, out, sc.v}, n, ph, s);
         default: return launch_ew(SumScaleOp<K, SCALE_DIV, false>{p, out, sc.v}, n, ph, s);
+        }
+    }
+    if constexpr (K >= 4) {
+        if (n >= kSerialElems) {
+            switch (sc.mode) {
+            case SCALE_NONE: return launch_ew(SumScaleOp<K, SCALE_NONE, true, true>{p, out, sc.v}, n, ph, s);
+            case SCALE_RECIP: return launch_ew(SumScaleOp<K, SCALE_RECIP, true, true>{p, out, sc.v}, n, ph, s);
+            default: return launch_ew(SumScaleOp<K, SCALE_DIV, true, true>{p, out, sc.v}, n, ph, s);
+            }
         }
     }
     switch (sc.mode) {

@@ -163,9 +163,10 @@ def test_optimizer_and_sum_scale_stream_non_temporal(kernels):
 
 def test_sum_scale_load_forms(kernels):
     """Round 3: K = 2 reads its inputs by LDS-DMA (two
-    global_load_lds_dwordx4 nt, no VGPR loads); K >= 4 keeps ONE vector load
-    in flight per wave: its K nt loads are each followed by vmcnt(0) before the
-    next is issued."""
+    global_load_lds_dwordx4 nt, no VGPR loads); the serialized form for large
+    buckets (SER, K >= 4) keeps ONE vector load in flight per wave: its K nt
+    loads are each followed by vmcnt(0) before the next is issued; the
+    small-bucket form keeps all K in flight."""
     ks = {k: v for k, v in _one_shot(kernels, "SumScaleOp").items() if re.search(r"SumScaleOpILi\d+ELi\dELb1E", k)}
     assert ks
     for k, code in ks.items():
@@ -176,5 +177,7 @@ def test_sum_scale_load_forms(kernels):
             assert len(glds) == 2 and not vec, f"{k}: {glds} {vec}"
         elif K >= 4:
             assert len(vec) == K and not glds, f"{k}: {len(vec)} vector loads"
-            for a_, b_ in zip(vec, vec[1:]):
-                assert any(code[j] == "s_waitcnt vmcnt(0)" for j in range(a_ + 1, b_)), f"{k}: two loads in flight"
+            ser = re.search(r"SumScaleOpILi\d+ELi\dELb1ELb1E", k) is not None
+            waits = [any(code[j] == "s_waitcnt vmcnt(0)" for j in range(a_ + 1, b_)) for a_, b_ in zip(vec, vec[1:])]
+            assert all(waits) if ser else not any(waits), f"{k}: serialized={ser}, waits between loads {waits}"
+    assert any(re.search(r"SumScaleOpILi8ELi\dELb1ELb1E", k) for k in ks), "no serialized K = 8 instance"

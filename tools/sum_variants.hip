@@ -24,7 +24,10 @@
 //         (by position within the XCD, by 3 x wave, half the waves by k/2;
 //         with LDS-DMA; 256-thread workgroups)
 //
-//   hipcc --offload-arch=gfx950 -O3 -o sum_variants sum_variants.hip
+//   LIB   the product's ono_sum_scale_f32 (libono_reduce.so) on the same buffers
+//
+//   hipcc --offload-arch=gfx950 -O3 -I../include -o sum_variants sum_variants.hip \
+//         -L../oxidized-neural-orchestra_amd/ono_amd -lono_reduce -Wl,-rpath,...
 //   ./sum_variants [MiB=64] [passes=3]
 #include <hip/hip_runtime.h>
 
@@ -33,6 +36,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include "ono_reduce.h"  // LIB: the product's ono_sum_scale_f32 on the same buffers
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -223,6 +228,30 @@ __global__ __launch_bounds__(64) void k_sum_glds(Args a) {
     if (v < a.nvec) stn(a.out + v, s * 0.5f);
 }
 
+// LDS-DMA, U vectors per lane (one wave apart)
+template <int K, int U>
+__global__ __launch_bounds__(64) void k_sum_glds_u(Args a) {
+    __shared__ f4 lds[U][K][64];
+    const size_t base = (size_t)blockIdx.x * 64 * U + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t v = base + 64 * u, vv = v < a.nvec ? v : a.nvec - 1;
+#pragma unroll
+        for (int j = 0; j < K; j++)
+            __builtin_amdgcn_global_load_lds((const void *)(a.in[j] + vv),
+                                             (__attribute__((address_space(3))) void *)&lds[u][j][0], 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t v = base + 64 * u;
+        f4 s = lds[u][0][threadIdx.x];
+#pragma unroll
+        for (int j = 1; j < K; j++) s += lds[u][j][threadIdx.x];
+        if (v < a.nvec) stn(a.out + v, s * 0.5f);
+    }
+}
+
 __global__ void k_fill(f4 *p, size_t n, unsigned seed) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -231,11 +260,16 @@ __global__ void k_fill(f4 *p, size_t n, unsigned seed) {
 }
 
 static std::vector<f4 *> g_bufs;
+static bool g_synth = false;  // argv[3] == "synth": the bench's data (ono_synth_f32, SURVEY §8(d) distribution)
 static f4 *buf(int i, hipStream_t s) {
     while ((int)g_bufs.size() <= i) {
         f4 *p;
         CK(hipMalloc(&p, N * sizeof(float)));
-        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, p, N / 4, 17u + (unsigned)g_bufs.size());
+        if (g_synth) {
+            if (ono_synth_f32((float *)p, N, 0x0402026 + g_bufs.size(), g_bufs.size() % 9, 0, s) != 0) exit(1);
+        } else {
+            hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, s, p, N / 4, 17u + (unsigned)g_bufs.size());
+        }
         g_bufs.push_back(p);
     }
     return g_bufs[i];
@@ -289,24 +323,31 @@ template <int K>
 static void sweep(hipStream_t s) {
     const unsigned g64 = (unsigned)((N / 4 + 63) / 64), g128 = (unsigned)((N / 4 + 127) / 128);
     variant<K>("P", s, [&](Args a) { hipLaunchKernelGGL((k_sum<K, 64, P>), dim3(g64), dim3(64), 0, s, a); });
-    variant<K>("BUF", s, [&](Args a) { hipLaunchKernelGGL((k_sum_buf<K>), dim3(g64), dim3(64), 0, s, a); });
     variant<K>("GLDS", s, [&](Args a) { hipLaunchKernelGGL((k_sum_glds<K>), dim3(g64), dim3(64), 0, s, a); });
-    variant<K>("ROT", s, [&](Args a) { hipLaunchKernelGGL((k_sum<K, 64, ROT>), dim3(g64), dim3(64), 0, s, a); });
     variant<K>("EMPTY", s, [&](Args a) { hipLaunchKernelGGL((k_sum<K, 64, EMPTY>), dim3(g64), dim3(64), 0, s, a); });
     variant<K>("SER1", s, [&](Args a) { hipLaunchKernelGGL((k_sum_ser<K, 1>), dim3(g64), dim3(64), 0, s, a); });
-    variant<K>("SER2", s, [&](Args a) { hipLaunchKernelGGL((k_sum_ser<K, 2>), dim3(g64), dim3(64), 0, s, a); });
-    variant<K>("SERU1B128", s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 128, 1>), dim3((unsigned)((N / 4 + 127) / 128)), dim3(128), 0, s, a); });
-    variant<K>("SERU1B256", s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 256, 1>), dim3((unsigned)((N / 4 + 255) / 256)), dim3(256), 0, s, a); });
-    variant<K>("SERU2", s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 64, 2>), dim3((unsigned)((N / 4 + 127) / 128)), dim3(64), 0, s, a); });
-    variant<K>("SERU4", s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 64, 4>), dim3((unsigned)((N / 4 + 255) / 256)), dim3(64), 0, s, a); });
-    variant<K>("SERU2B256", s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 256, 2>), dim3((unsigned)((N / 4 + 511) / 512)), dim3(256), 0, s, a); });
+    variant<K>("LIB", s, [&](Args a) {
+        const float *ins[8];
+        for (int j = 0; j < K; j++) ins[j] = (const float *)a.in[j];
+        if (ono_sum_scale_f32((float *)a.out, ins, K, N, 2.0f, s) != 0) { fprintf(stderr, "%s\n", ono_last_error()); exit(1); }
+    });
+    // occupancy limited by dynamic LDS per one-wave workgroup: at most N per CU
+    auto lds_for = [](int n) { return (unsigned)(160 * 1024 * 2 / (2 * n + 1)); };
+    static char names[256][24];
+    static int nn = 0;
+    auto name = [&](const char *f, int occ) { char *nm = names[nn++ % 256]; snprintf(nm, 24, f, occ); return (const char *)nm; };
+    for (int occ : {28}) {
+        const unsigned l = lds_for(occ);
+        variant<K>(name("SER1_occ%d", occ), s, [&](Args a) { hipLaunchKernelGGL((k_sum_ser<K, 1>), dim3(g64), dim3(64), l, s, a); });
+    }
 }
 
 int main(int argc, char **argv) {
     if (argc > 1) N = (size_t)atol(argv[1]) << 18;
     const int passes = argc > 2 ? atoi(argv[2]) : 3;
-    hipStream_t s;
-    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g_synth = argc > 3 && !strcmp(argv[3], "synth");
+    hipStream_t s = nullptr;  // argv[4] == "null": the legacy default stream
+    if (!(argc > 4 && !strcmp(argv[4], "null"))) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     printf("# %s, %d CUs, %zu elements (%zu MiB) per buffer, %d passes, median us per launch\n", p.gcnArchName,
