@@ -137,10 +137,30 @@ template <class Op> struct HasFinish<Op, std::void_t<decltype(std::declval<const
 template <class Op> __device__ __forceinline__ void finish_wave(const Op &op) {
     if constexpr (HasFinish<Op>::value) op.finish();
 }
-// Ops that cap how many of their one-wave workgroups share a CU declare the
-// dynamic LDS each workgroup reserves (kLds bytes; 160 KiB per CU).
-template <class Op, class = void> struct DynLds { static constexpr unsigned value = 0; };
-template <class Op> struct DynLds<Op, std::void_t<decltype(Op::kLds)>> { static constexpr unsigned value = Op::kLds; };
+// Ops that cap how many of their one-wave workgroups share a CU say so with
+// occ() (0 = no cap); the launch then reserves enough dynamic LDS per
+// workgroup (unused; 160 KiB per CU) that no more than occ() fit.  Applied to
+// buckets of at least kOccElems; ONO_EW_OCC=<cap> overrides every op's cap
+// (32 = none) for measurement (tools/occ_sweep.sh).
+template <class Op, class = void> struct HasOcc : std::false_type {};
+template <class Op> struct HasOcc<Op, std::void_t<decltype(std::declval<const Op &>().occ())>> : std::true_type {};
+constexpr size_t kOccElems = size_t(4) << 20;
+inline unsigned lds_for_occ(int occ) {
+    return occ <= 0 || occ >= 32 ? 0u : (unsigned)(160u * 1024u * 2u / (2u * (unsigned)occ + 1u));
+}
+int occ_override() {
+    static int v = [] {
+        const char *e = getenv("ONO_EW_OCC");
+        int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 0;
+    }();
+    return v;
+}
+template <class Op> unsigned ew_lds(const Op &op, size_t n) {
+    if (const int o = occ_override()) return lds_for_occ(o);
+    if constexpr (HasOcc<Op>::value) return n >= kOccElems ? lds_for_occ(op.occ()) : 0u;
+    return 0u;
+}
 
 // LOOP = false: the grid covers every vector (the one-shot grid), so no loop
 // at all — one guarded vector per lane (dec 2.5 %, sum8 1 % faster than the
@@ -210,10 +230,11 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     for (int i = 0; i < nph; i++) same &= (phases[i] == ph);
     const int bpc = blocks_per_cu();
     const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc : (size_t)0x7FFFFFFF;
+    const unsigned lds = ew_lds(op, n);
     if (!same) {
         size_t blocks = (n + kBlock - 1) / kBlock;
         if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), DynLds<Op>::value, s, op, n);
+        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), lds, s, op, n);
         return hipGetLastError();
     }
     size_t head = (4 - ph) & 3u;
@@ -223,11 +244,11 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     size_t blocks = (work + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     if (blocks > cap) {
-        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(kBlock), DynLds<Op>::value, s, op, head,
+        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(kBlock), lds, s, op, head,
                            nvec, n);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(kBlock), DynLds<Op>::value, s, op, head,
+    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(kBlock), lds, s, op, head,
                        nvec, n);
     return hipGetLastError();
 }
@@ -261,9 +282,9 @@ struct Ptrs {
 // SER: the serialized form (K >= 4, buckets of at least kSerialElems, where
 // bandwidth, not one wave's latency, decides; smaller buckets keep every load
 // in flight).
-constexpr size_t kSerialElems = size_t(4) << 20;
+constexpr size_t kSerialElems = kOccElems;
 template <int K, int M, bool NTL, bool SER = false> struct SumScaleOp {
-    static constexpr unsigned kLds = SER ? 160u * 1024u * 2u / 57u : 0u;  // <= 28 workgroups per CU
+    __host__ int occ() const { return SER ? 28 : 0; }  // one-wave workgroups per CU
     Ptrs in;
     float *out;
     float v;
@@ -422,6 +443,7 @@ template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
     const float *src;
     float *zero;
     float v;
+    __host__ int occ() const { return zero ? 24 : 0; }
     typedef f4 R;
     __device__ __forceinline__ void scalar(size_t i) const {
         float x = src[i];
@@ -462,6 +484,7 @@ template <class W> struct EncodeZeroOp {
     typedef typename Wire<W>::V WV;
     W *out;
     float *chunk;
+    __host__ int occ() const { return 24; }
     typedef f4 R;
     __device__ __forceinline__ void scalar(size_t i) const {
         out[i] = Wire<W>::enc(chunk[i]);
@@ -491,6 +514,7 @@ template <class W> struct AddEncodeZeroOp {
     W *out;
     float *acc;
     const W *in;
+    __host__ int occ() const { return 24; }
     struct R { f4 a; WV h; };
     __device__ __forceinline__ void scalar(size_t i) const {
         float x = acc[i] + Wire<W>::dec(in[i]);
@@ -514,6 +538,7 @@ template <class W, int M> struct AddFinishOp {
     float *acc;
     const W *in;
     float v;
+    __host__ int occ() const { return 16; }
     struct R { f4 a; WV h; };
     __device__ __forceinline__ void scalar(size_t i) const {
         float x = acc[i] + Wire<W>::dec(in[i]);
@@ -580,6 +605,7 @@ template <int KIND, int M, bool ZERO, bool PZ> struct OptOp {
     float lr, mu, b1, omb1, b2, omb2, eps, step, nw;
     int fence;  // w2 is read by other ranks after the next flag barrier (xGMI PS)
     struct R { f4 g, w, v, s; };
+    __host__ int occ() const { return KIND == ONO_OPT_GD ? 16 : KIND == ONO_OPT_MOMENTUM || KIND == ONO_OPT_ADAM ? 10 : 0; }
     __device__ __forceinline__ void finish() const {
         if (fence) peer_stores_done();
     }
