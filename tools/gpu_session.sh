@@ -19,5 +19,5 @@ timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench_%pid% -- python3 bench.py --no-cpu-baseline --no-host-fed --no-tcp-edge --sweep-mib "" > gpurun_out/prof.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-fed --no-tcp-edge --xgmi-coresident 0 > gpurun_out/pmc_fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-fed --no-tcp-edge --xgmi-coresident 0 > gpurun_out/pmc_write.log 2>&1 || exit $?
-python3 tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --elems 67108864 --out gpurun_out/pmc_n1.json > gpurun_out/pmc_summary.log 2>&1
+python3 tools/pmc_summary.py --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --elems 67108864 --commit "${ONO_COMMIT:-unknown}" --session "${ONO_SESSION:-gpu_session.sh}" --out gpurun_out/pmc_n1.json > gpurun_out/pmc_summary.log 2>&1
 exit $rc
