@@ -148,14 +148,22 @@ int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *bu
                     void *stream);
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame
  * received into device memory); same results and errors as ono_sparse_lift.
- * Both parse on the device: speculative record starts per 128-B segment,
- * verified walks that note every record, one lane per record placing its
- * run; the reference's sequential host parse runs only when the speculation
- * is refuted or the stream is malformed.  g[total, cap) is left untouched.  */
+ * Both parse on the device, in up to three tiers, each exact or refuted:
+ * (1) the pattern path — in drop output with gaps and runs below 2^16 values
+ * a record starts exactly where units k+1 and k+3 are zero; the candidates are
+ * checked to be the sequential parse (head, every successor, the sum) in
+ * parallel; (2) the walk path — speculative record starts per 128-B segment
+ * and verified walks; (3) the reference's sequential host parse, when the walk
+ * is refuted or the stream is malformed (and the source of its error
+ * messages).  g[total, cap) is left untouched.                             */
 int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
                         void *stream);
 /* lifts so far (this process) that took the sequential host parse        */
 size_t ono_sparse_lift_fallbacks(void);
+/* lifts so far (this process) that the pattern path handed to the walk path */
+size_t ono_sparse_lift_pattern_misses(void);
+/* diagnostics: 0 (default) pattern path first; 1 walk path only            */
+int ono_sparse_lift_set_mode(int mode);
 int ono_sparse_mask(float *g_dev, size_t n, float threshold, int zero_kept, void *stream);
 
 /* synthetic gradient bucket (SURVEY.md §8(d) distribution), bit-identical to

@@ -117,12 +117,7 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
                                             uint32_t &tb) {
     __shared__ uint32_t wa[NT / 64], wb[NT / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t ia = a, ib = b;  // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t ya = __shfl_up(ia, d, 64), yb = __shfl_up(ib, d, 64);
-        if (lane >= d) { ia += ya; ib += yb; }
-    }
+    const uint32_t ia = wave_incl_sum_dpp(a), ib = wave_incl_sum_dpp(b);  // inclusive wave scans (DPP)
     if (lane == 63) { wa[wave] = ia; wb[wave] = ib; }
     __syncthreads();
     uint32_t pa = 0, pb = 0;
@@ -818,6 +813,21 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v) {
     return t;
 }
 
+// Block-wide max of a u64 (the same value in every thread).
+template <int NT>
+__device__ __forceinline__ uint64_t block_max64(uint64_t v) {
+    __shared__ uint64_t wm[NT / 64];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, d, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t m = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) m = max(m, wm[w]);
+    __syncthreads();
+    return m;
+}
+
 // Per segment s (sl_index): p0 (its speculative start or kNone), gpre (the
 // element index its records start from, within its window), the stamps of the
 // starts its walk landed on (reached = this call's epoch), and its records:
@@ -932,9 +942,13 @@ __global__ __launch_bounds__(kLW) void sl_index(const uint8_t *b, size_t nbytes,
 // A span of g for sl_long as chunks of kLongChunk: zeros (kind 1) or the f16
 // values from stream byte vp on (kind 0).  Reserved with one atomic (rare:
 // long runs, and the gaps of groups spanning more than kZeroMax values).
+// qflag (pattern path): a host-mapped word set to the epoch, so the host
+// launches sl_long only when something was queued.
 __device__ __forceinline__ void queue_span(size_t dst, size_t vp, size_t n, uint32_t kind, uint4 *queue,
-                                           uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint32_t epoch) {
+                                           uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint32_t epoch,
+                                           uint64_t *qflag = nullptr) {
     if (n == 0) return;
+    if (qflag) *(volatile uint64_t *)qflag = epoch;
     const uint32_t nc = (uint32_t)((n + kLongChunk - 1) / kLongChunk);
     const uint32_t k = atomicAdd(qcount, nc);
     if (k + nc > qcap || k + nc < k) { raise_bad(host_word, epoch); return; }  // only a refuted stream overfills it
@@ -1174,6 +1188,438 @@ __global__ __launch_bounds__(kSB) void sl_long(float *g, const uint8_t *b, const
     }
 }
 
+// ------------------------------------------------- lift: pattern path ----
+// The common stream parses with no speculation and no walks (round 3).  In
+// grad_drop_into's output (protocol.rs:57-86) every run length is >= 1, every
+// offset after the first >= 1 (runs are maximal), and every kept value is a
+// nonzero f16 (|g| >= t >= f16::MIN_POSITIVE, protocol.rs:48).  When the gaps
+// and runs are also shorter than 2^16 values, the only zero u16s of the stream
+// are the high halves of the headers' two fields, so unit k (byte 8 + 2k)
+// starts a record iff units k + 1 and k + 3 are zero: offset = unit k, length
+// = unit k + 2.  (Another k with both zeros would need a header high half at
+// k + 3 with k not a header: k = h + 2 puts a zero at h + 5, i.e. another
+// header at h + 4 — a zero-length run.)  The candidates are then CHECKED to be
+// the sequential parse, exactly and in parallel: the first is unit 0, each
+// candidate's successor k + 4 + length is the next candidate or the end of the
+// stream, and the offsets and lengths sum to at most total.  By induction from
+// the head the reference's loop (protocol.rs:109-141) visits exactly these
+// records, in order, with the same bounds checks passing.  A stream outside the
+// shape (long gaps or runs, zero-length runs, zero payloads, malformed input)
+// fails a check and the walk path below parses it, rewriting [0, total).
+// Three launches: pl_index (per 8 KiB tile: candidates, in-tile successor
+// checks, {count, sum of offset + length, first, exit}), pl_scan (one
+// workgroup: the tiles' element prefixes and the cross-tile links), pl_place
+// (per tile: its range of g — the gap before each record, the records' runs,
+// the tail after the last — built in LDS from the staged tile and stored once).
+constexpr int kPatU = 2048;                           // stream units (u16) per tile: 4 KiB
+constexpr int kPatT = 256, kPatPer = kPatU / kPatT;   // 8 units per thread
+constexpr int kPatImg = 6144;                         // pl_place's LDS image, floats (a tile's range is
+                                                      // ~4.5 K values at 10 % kept)
+constexpr int kPatHalo = 40;                          // staged past the tile: the last header's fields and
+                                                      // every short run that starts in the tile
+constexpr int kPatScanT = 1024;                       // pl_scan's one workgroup
+constexpr uint32_t kPatNone = 0xFFFFFFFFu;
+static_assert(kPatPer == 8, "a thread's 8 units and the 4 after them are one 16-B and one 8-B LDS read");
+static_assert(kPatHalo >= 4 + kShortP, "short runs of the tile's records are staged whole");
+
+// A thread's units and the 4 after them from the staged tile.
+struct Units12 {
+    uint32_t w[6];
+    __device__ __forceinline__ uint32_t u(int i) const { return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu; }
+};
+__device__ __forceinline__ Units12 units12(const uint4 *lw4) {
+    Units12 r;
+    const uint4 a = lw4[threadIdx.x];
+    const uint2 c = ((const uint2 *)lw4)[2 * threadIdx.x + 2];
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
+    r.w[4] = c.x; r.w[5] = c.y;
+    return r;
+}
+// Candidate mask of the thread's units (k = base + 8 t + j, a header needs k + 4 <= M) and the sum of
+// their offsets and lengths.
+__device__ __forceinline__ uint32_t pat_mask(const Units12 &U, size_t k0, size_t M, uint32_t &sum) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < kPatPer; j++) m |= (U.u(j + 1) == 0u && U.u(j + 3) == 0u) ? 1u << j : 0u;
+    if (k0 + 4 > M) m = 0;
+    else if (M - k0 - 4 < (size_t)kPatPer - 1) m &= (2u << (M - k0 - 4)) - 1u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kPatPer; j++) s += (m >> j & 1u) ? U.u(j) + U.u(j + 2) : 0u;
+    sum = s;
+    return m;
+}
+constexpr int kPatStage = kPatU + kPatHalo;  // units staged per tile
+// the tile's units [base, base + kPatStage) of the stream's M (after the 8-byte total) into LDS
+__device__ __forceinline__ size_t pat_stage(uint4 *lw4, const uint8_t *b, size_t base, size_t M) {
+    const size_t n16 = min(M - base, (size_t)kPatStage);
+    stage_bytes<kPatT, 2 * kPatStage>((uint16_t *)lw4, b, 8 + 2 * base, n16);
+    return n16;
+}
+
+// rec[4 t ..]: candidates, sum of offset + length, first candidate, exit (the
+// last candidate's successor: the next tile's first record or M).
+__global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, uint32_t *rec, uint32_t *tsum,
+                                                  uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
+                                                  uint32_t epoch, int dbg) {
+    __shared__ uint4 lw4[kPatStage / 8 + 1];
+    __shared__ uint16_t lmask[kPatT], lpre[kPatT];  // (masks of kPatPer bits)
+    const size_t t = blockIdx.x, base = t * kPatU;
+    const uint16_t *lwu = (const uint16_t *)lw4;
+    if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, empty queues
+        host_word[1] = stream_total(b);
+        *qcount = 0;
+        *wide = 0;
+    }
+    pat_stage(lw4, b, base, M);
+    __syncthreads();
+    if (dbg == 1) return;
+    const Units12 U = units12(lw4);
+    const uint32_t j0 = kPatPer * threadIdx.x;
+    uint32_t sum;
+    const uint32_t m = pat_mask(U, base + j0, M, sum);
+    uint32_t ec, es, tc, ts;
+    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
+    if (dbg == 2) { if (m == 12345) rec[0] = es; return; }
+    lmask[threadIdx.x] = (uint16_t)m;
+    lpre[threadIdx.x] = (uint16_t)ec;
+    __syncthreads();
+    bool bad = false;
+    uint32_t rank = ec;
+    for (uint32_t mm = m; mm; mm &= mm - 1, rank++) {
+        const uint32_t j = (uint32_t)__builtin_ctz(mm), k = j0 + j;
+        const uint32_t nx = k + 4 + lwu[k + 2];  // tile-local successor (units read back from LDS: a
+                                                  // register array indexed at run time would be moved to
+                                                  // LDS by the compiler, addressed through the dispatch packet)
+        if (base + nx > M) { bad = true; break; }  // the run overruns the stream
+        if (nx < (uint32_t)kPatU && base + nx < M) {
+            const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
+            const uint32_t p2 = lpre[nx / kPatPer] + (uint32_t)__builtin_popcount(m2 & ((1u << b2) - 1u));
+            if (!(m2 >> b2 & 1u) || p2 != rank + 1) { bad = true; break; }
+        } else {  // the end of the stream or another tile: only the tile's last candidate goes there
+            if (rank + 1 != tc) { bad = true; break; }
+            rec[4 * t + 3] = (uint32_t)(base + nx);
+        }
+    }
+    if (bad) raise_bad(host_word + 2, epoch);
+    if (m && ec == 0) rec[4 * t + 2] = (uint32_t)(base + j0 + __builtin_ctz(m));
+    if (threadIdx.x == 0) {
+        rec[4 * t] = tc;
+        rec[4 * t + 1] = ts;
+        tsum[t] = ts;  // (again, contiguous: pl_place sums the earlier tiles' from here)
+        if (tc == 0) { rec[4 * t + 2] = kPatNone; rec[4 * t + 3] = kPatNone; }
+    }
+}
+
+// E[t] = the element index tile t's range starts at: one workgroup scans the
+// tiles' sums, 4 per thread, kPatScanT x 4 tiles per step (DPP wave scans; the
+// u32 partial sums are exact when the u64 total is at most total < 2^32, which
+// is checked).  E[T] = where the last run ends.
+constexpr int kPatScanPer = 4;
+__global__ __launch_bounds__(kPatScanT) void pl_scan(const uint8_t *b, const uint32_t *rec, size_t T, uint64_t *E,
+                                                     uint64_t *host_word, uint32_t epoch) {
+    __shared__ uint32_t wtot[kPatScanT / 64];
+    const uint64_t total = stream_total(b);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t carry = 0;
+    for (size_t c0 = 0; c0 < T; c0 += (size_t)kPatScanT * kPatScanPer) {
+        const size_t i0 = c0 + (size_t)kPatScanPer * threadIdx.x;
+        uint32_t v[kPatScanPer];
+#pragma unroll
+        for (int q = 0; q < kPatScanPer; q++) v[q] = i0 + q < T ? ((const uint4 *)rec)[i0 + q].y : 0u;
+        uint32_t own = 0;
+#pragma unroll
+        for (int q = 0; q < kPatScanPer; q++) own += v[q];
+        const uint32_t inc = wave_incl_sum_dpp(own);
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0;
+        uint64_t all = 0;
+#pragma unroll
+        for (int w = 0; w < kPatScanT / 64; w++) {
+            before += w < wave ? wtot[w] : 0u;
+            all += wtot[w];
+        }
+        __syncthreads();
+        uint64_t e = carry + before + (inc - own);
+#pragma unroll
+        for (int q = 0; q < kPatScanPer; q++) {
+            if (i0 + q < T) E[i0 + q] = e;
+            e += v[q];
+        }
+        carry += all;
+    }
+    if (threadIdx.x == 0) {
+        E[T] = carry;
+        if (carry > total) raise_bad(host_word + 2, epoch);
+    }
+}
+
+// The non-empty tile before tile `from` (exclusive), or -1: the workgroup
+// tests 256 tiles at a time, nearest first (a run spanning many tiles).
+__device__ int64_t prev_nonempty(const uint32_t *rec, size_t from) {
+    __shared__ int64_t best[kPatT / 64];
+    size_t hi = from;  // candidates [0, hi)
+    while (hi > 0) {
+        const size_t i = hi - 1 - threadIdx.x;
+        int64_t v = threadIdx.x < hi && rec[4 * i] > 0 ? (int64_t)i : -1;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, d, 64));
+        if ((threadIdx.x & 63) == 0) best[threadIdx.x >> 6] = v;
+        __syncthreads();
+        int64_t r = -1;
+#pragma unroll
+        for (int w = 0; w < kPatT / 64; w++) r = max(r, best[w]);
+        __syncthreads();
+        if (r >= 0) return r;
+        hi = hi > (size_t)kPatT ? hi - kPatT : 0;
+    }
+    return -1;
+}
+
+// Tile t's range of g: [E_t, E_t+1) — [E_T-1, total) for the last tile, which
+// also holds the tail — with its zeros and values, and the cross-tile links:
+// the tile's first record is the exit of the nearest non-empty tile before it
+// (or the head, unit 0); the last tile's (or the last non-empty one's) exit is M.
+// A range of up to kPatImg values (every tile of a 10 %-kept stream) is built in
+// LDS in one pass — zeros, each record's run placed by the lane that holds it
+// (short runs from the staged units, long ones by the workgroup) — and stored
+// as whole 16-B vectors.  A wider range (sparse streams) is listed for pl_wide.
+constexpr size_t kPatDirect = 4096;  // up to this many tiles pl_place sums the earlier tiles itself
+__global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
+                                                  uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
+                                                  uint32_t *wide, uint64_t *host_word, uint32_t epoch, int dbg) {
+    __shared__ f4s img4[kPatImg / 4];
+    __shared__ uint4 lw4[kPatStage / 8 + 1];
+    __shared__ uint32_t lq[3 * kLQ], lqn;
+    float *img = (float *)img4;
+    const uint16_t *lw = (const uint16_t *)lw4;
+    const size_t t = blockIdx.x, base = t * kPatU;
+    const bool direct = T <= kPatDirect;  // (uniform) else E[] from pl_scan
+    // the prologue's loads issued together: the tile's record, its range (E from pl_scan, or the earlier
+    // tiles' sums), the record of each of the 256 tiles before it (the nearest non-empty one's exit is
+    // the link into this tile)
+    const uint4 me = ((const uint4 *)rec)[t];
+    constexpr int kSumPer = (int)(kPatDirect / kPatT);
+    uint32_t sums[kSumPer];
+    uint64_t E0 = 0, E1 = 0;
+    if (direct) {
+#pragma unroll
+        for (int q = 0; q < kSumPer; q++) {
+            const size_t i = threadIdx.x + (size_t)q * kPatT;
+            sums[q] = i < t ? tsum[i] : 0u;
+        }
+    } else {
+        E0 = E[t];
+        E1 = E[t + 1];
+    }
+    const uint4 near = threadIdx.x < t ? ((const uint4 *)rec)[t - 1 - threadIdx.x] : make_uint4(0, 0, 0, 0);
+    const uint64_t total = stream_total(b);
+    pat_stage(lw4, b, base, M);
+    if (total > cap) return;  // ONO_E_SIZE: nothing is written
+    {
+        uint64_t key = threadIdx.x < t && near.x > 0 ? (uint64_t)(t - threadIdx.x) << 32 | near.w : 0;
+        key = block_max64<kPatT>(key);  // (index + 1) << 32 | exit of the nearest non-empty tile
+        uint32_t pexit = (uint32_t)key;
+        bool found = key != 0;
+        if (!found && t > (size_t)kPatT) {  // none among those 256
+            const int64_t q = prev_nonempty(rec, t - kPatT);
+            found = q >= 0;
+            if (found) pexit = rec[4 * q + 3];
+        }
+        bool bad = me.x > 0 && (found ? pexit != me.z : me.z != 0u);
+        if (t + 1 == T) bad |= me.x > 0 ? me.w != (uint32_t)M : !found || pexit != (uint32_t)M;
+        if (direct) {
+            uint64_t part = 0;
+#pragma unroll
+            for (int q = 0; q < kSumPer; q++) part += sums[q];
+            E0 = block_sum64<kPatT>(part);
+            E1 = E0 + me.y;
+            if (t + 1 == T) bad |= E1 > total;  // the offsets and lengths sum to at most total
+        }
+        if (bad && threadIdx.x == 0) raise_bad(host_word + 2, epoch);
+    }
+    const uint64_t ea = min(E0, total);
+    uint64_t eb = t + 1 == T ? total : min(E1, total);
+    eb = max(eb, ea);
+    if (eb == ea) return;  // (uniform) an empty tile inside a run
+    const uint64_t ia = vec ? ea & ~3ull : ea;
+    const uint32_t n = (uint32_t)min(eb - ia, (uint64_t)kPatImg + 1);
+    if (n > (uint32_t)kPatImg) {  // (uniform) a wide range: pl_wide places it
+        if (threadIdx.x == 0) {
+            if (direct) E[t] = E0;
+            wide[1 + atomicAdd(wide, 1u)] = (uint32_t)t;
+            *(volatile uint64_t *)(host_word + 4) = epoch;
+        }
+        return;
+    }
+    {
+        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img4[i] = z;
+    }
+    if (threadIdx.x == 0) lqn = 0;
+    __syncthreads();  // the staged units, the zeros
+    if (dbg == 1) return;
+    const Units12 U = units12(lw4);
+    const uint32_t j0 = kPatPer * threadIdx.x;
+    uint32_t sum;
+    const uint32_t m = pat_mask(U, base + j0, M, sum);
+    uint32_t ec, es, tc, ts;
+    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
+    if (dbg == 3) { if (m == 77777) g[0] = es; return; }
+    uint64_t cur = E0 + es;  // where the run before the thread's first record ended
+    for (uint32_t mm = m; mm; mm &= mm - 1) {
+        const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+        const uint64_t gi = cur + off;
+        if (gi < ea || gi + len > eb || base + k + 4 + len > M) {  // only a refuted stream
+            raise_bad(host_word + 2, epoch);
+            break;
+        }
+        float *d = img + (gi - ia);
+        if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
+            for (uint32_t i = 0; i < len; i++) d[i] = from_f16_sp(lw[k + 4 + i]);
+        } else {
+            const uint32_t q = atomicAdd(&lqn, 1u);
+            const uint32_t vp = (uint32_t)(8 + 2 * (base + k + 4));
+            if (q < (uint32_t)kLQ) {
+                lq[3 * q] = (uint32_t)(gi - ia);
+                lq[3 * q + 1] = vp;
+                lq[3 * q + 2] = len;
+            } else {
+                for (uint32_t i = 0; i < len; i++) d[i] = from_f16_sp(((glb_u16 *)(b + vp))[i]);
+            }
+        }
+        cur = gi + len;
+    }
+    __syncthreads();  // the short runs and the long-run queue
+    const uint32_t nl = min(lqn, (uint32_t)kLQ);
+    if (nl) {  // (uniform) long runs: the whole workgroup copies each
+        for (uint32_t q = 0; q < nl; q++) {
+            const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
+            glb_u16 *src = (glb_u16 *)(b + vp);
+            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
+        }
+        __syncthreads();
+    }
+    if (dbg == 2) return;
+    // the range out: whole 16-B vectors inside [ea, eb), then the partial first and last vectors
+    const uint32_t skip = (uint32_t)(ea - ia);
+    if (vec) {
+        const uint32_t v0 = skip ? 1u : 0u, v1 = n / 4;  // whole vectors [v0, v1)
+        for (uint32_t i = v0 + threadIdx.x; i < v1; i += kPatT)
+            __builtin_nontemporal_store(img4[i], (f4s *)(g + ia) + i);
+        if (threadIdx.x < 4) {
+            const uint32_t e = threadIdx.x;
+            if (skip && e >= skip && e < n) g[ia + e] = img[e];  // the first vector's part in range
+            const uint32_t l = 4 * v1 + e;
+            if (l < n && l >= 4 * v0) g[ia + l] = img[l];        // the last vector's part
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < n; i += kPatT) g[ia + i] = img[i];
+    }
+}
+
+// The tiles pl_place listed (ranges above kPatImg: sparse streams), one
+// workgroup each, grid-stride: up to kPatPasses windows of kPatImg values built
+// in LDS one after another; wider still (few tiles hold all of g), the gaps and
+// the tail queued as zero chunks for sl_long's full grid and the values
+// scattered (long runs queued).
+constexpr int kPatPasses = 8;
+__global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, size_t M, size_t T, int vec,
+                                                 const uint64_t *E, const uint32_t *tsum, const uint32_t *wide,
+                                                 uint4 *queue,
+                                                 uint32_t *qcount, uint32_t qcap, uint64_t *host_word,
+                                                 uint32_t epoch) {
+    __shared__ f4s img4[kPatImg / 4];
+    __shared__ uint4 lw4[kPatStage / 8 + 1];
+    __shared__ uint32_t lq[3 * kLQ], lqn;
+    float *img = (float *)img4;
+    const uint16_t *lw = (const uint16_t *)lw4;
+    const uint64_t total = stream_total(b);
+    const uint32_t nw = wide[0];
+    for (uint32_t wi = blockIdx.x; wi < nw; wi += gridDim.x) {
+        const size_t t = wide[1 + wi], base = t * kPatU;
+        const uint64_t E0 = E[t];
+        const uint64_t ea = min(E0, total);
+        uint64_t eb = t + 1 == T ? total : min(E0 + tsum[t], total);
+        eb = max(eb, ea);
+        __syncthreads();  // the previous tile's reads of the staged units
+        pat_stage(lw4, b, base, M);
+        __syncthreads();
+        const Units12 U = units12(lw4);
+        const uint32_t j0 = kPatPer * threadIdx.x;
+        uint32_t sum;
+        const uint32_t m = pat_mask(U, base + j0, M, sum);
+        uint32_t ec, es, tc, ts;
+        block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
+        const uint64_t ia = vec ? ea & ~3ull : ea, span = eb - ia;
+        const uint64_t npass = (span + kPatImg - 1) / kPatImg;
+        if (npass > (uint64_t)kPatPasses) {
+            uint64_t cur = E0 + es;
+            for (uint32_t mm = m; mm; mm &= mm - 1) {
+                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+                const uint64_t gi = cur + off;
+                if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(host_word + 2, epoch); break; }
+                queue_span(cur, 0, off, 1u, queue, qcount, qcap, host_word, epoch, host_word + 3);
+                if (len <= (uint32_t)kShortP)
+                    for (uint32_t i = 0; i < len; i++) g[gi + i] = from_f16_sp(lw[k + 4 + i]);
+                else
+                    queue_span(gi, 8 + 2 * (base + k + 4), len, 0u, queue, qcount, qcap, host_word, epoch,
+                               host_word + 3);
+                cur = gi + len;
+            }
+            const bool holds_last = m != 0 && ec + (uint32_t)__builtin_popcount(m) == tc;
+            if (t + 1 == T && (holds_last || (tc == 0 && threadIdx.x == 0)))
+                queue_span(E0 + ts, 0, total > E0 + ts ? total - (E0 + ts) : 0, 1u, queue, qcount, qcap, host_word,
+                           epoch, host_word + 3);
+            continue;
+        }
+        const uint32_t skip = (uint32_t)(ea - ia);
+        for (uint32_t p = 0; p < (uint32_t)npass; p++) {
+            const uint32_t w0 = p * kPatImg, w1 = (uint32_t)min((uint64_t)w0 + kPatImg, span), wn = w1 - w0;
+            const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (uint32_t i = threadIdx.x; i < (wn + 3) / 4; i += kPatT) img4[i] = z;
+            if (threadIdx.x == 0) lqn = 0;
+            __syncthreads();
+            uint64_t cur = E0 + es;
+            for (uint32_t mm = m; mm; mm &= mm - 1) {
+                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+                const uint64_t gi = cur + off;
+                cur = gi + len;
+                if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(host_word + 2, epoch); break; }
+                const uint32_t r0 = (uint32_t)(gi - ia), a = max(r0, w0), e = min(r0 + len, w1);
+                if (a >= e) continue;
+                const uint32_t c = e - a, u0 = k + 4 + (a - r0);
+                if (len <= (uint32_t)kShortP) {
+                    for (uint32_t i = 0; i < c; i++) img[a - w0 + i] = from_f16_sp(lw[u0 + i]);
+                } else {
+                    const uint32_t q = atomicAdd(&lqn, 1u);
+                    if (q < (uint32_t)kLQ) {
+                        lq[3 * q] = a - w0;
+                        lq[3 * q + 1] = (uint32_t)(8 + 2 * (base + u0));
+                        lq[3 * q + 2] = c;
+                    } else {
+                        for (uint32_t i = 0; i < c; i++)
+                            img[a - w0 + i] = from_f16_sp(((glb_u16 *)(b + 8 + 2 * (base + u0)))[i]);
+                    }
+                }
+            }
+            __syncthreads();
+            const uint32_t nl = min(lqn, (uint32_t)kLQ);
+            for (uint32_t q = 0; q < nl; q++) {
+                const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
+                glb_u16 *src = (glb_u16 *)(b + vp);
+                for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
+            }
+            __syncthreads();
+            float *dst = g + ia + w0;
+            for (uint32_t i = threadIdx.x; i < wn; i += kPatT)
+                if (w0 + i >= skip) dst[i] = img[i];
+            __syncthreads();
+        }
+    }
+}
+
 // the totals into the host-mapped words (the exact-size path of a small buffer), one wave
 __global__ void sp_totals_out(const uint4 *agg, uint32_t G, uint64_t *host_tot) {
     const uint2 t = chunk_totals(agg, G);
@@ -1232,10 +1678,18 @@ struct LiftScratch {
     uint4 *queue = nullptr;    // q_cap chunks of long runs
     uint32_t epoch = 0;
     uint8_t *buf = nullptr;
-    uint64_t *host_word = nullptr, *host_word_dev = nullptr;  // [0] bad (= epoch), [1] total
+    size_t pt_cap = 0;
+    uint32_t *prec = nullptr;  // pattern path: 4 x pt_cap tile records, then pt_cap tile sums
+    uint64_t *pE = nullptr;    // pattern path: pt_cap + 1 element prefixes
+    uint32_t *pwide = nullptr; // pattern path: [0] count, then the tiles of wide ranges
+    // [0] walk refuted / malformed (= epoch), [1] total, [2] pattern refuted (= epoch), [3] pattern queued a
+    // chunk, [4] pattern listed a wide tile
+    uint64_t *host_word = nullptr, *host_word_dev = nullptr;
 };
 LiftScratch g_lift[64];
-std::atomic<size_t> g_lift_fallbacks{0};
+std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
+std::atomic<size_t> g_lift_pattern_misses{0}; // lifts the pattern path handed to the walk path
+std::atomic<int> g_lift_mode{0};              // 0: pattern, then walk, then host; 1: walk, then host
 
 template <class T> int grow(T **p, size_t &cap, size_t want) {
     if (want <= cap) return ONO_OK;
@@ -1329,7 +1783,7 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     LiftScratch &L = g_lift[dev];
     const size_t S = (nbytes - 8 + kSeg - 1) / kSeg, W = (S + kLW - 1) / kLW;
     if (!L.host_word) {
-        ONO_HIP(hipHostMalloc((void **)&L.host_word, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostMalloc((void **)&L.host_word, 8 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&L.host_word_dev, L.host_word, 0));
     }
     bool restamp = false;
@@ -1361,10 +1815,61 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     if (restamp) ONO_HIP(hipMemsetAsync(reached, 0, C * sizeof(uint32_t), s));
     uint32_t *wsum = L.win, *qcount = L.win + Wg;
     volatile uint64_t *word = L.host_word;
-    word[0] = 0;
-    word[1] = 0;
     const uint32_t epoch = L.epoch;
     const int vec = ((uintptr_t)g & 15) == 0;
+    // the pattern path first (streams of an even length with at least one unit)
+    const size_t M = (nbytes - 8) / 2;
+    if (g_lift_mode.load() == 0 && M > 0 && (nbytes & 1) == 0) {
+        const size_t T = (M + kPatU - 1) / kPatU;
+        if (T > L.pt_cap) {
+            (void)hipFree(L.prec);
+            (void)hipFree(L.pE);
+            (void)hipFree(L.pwide);
+            L.prec = nullptr;
+            L.pE = nullptr;
+            L.pwide = nullptr;
+            L.pt_cap = 0;
+            ONO_HIP(hipMalloc((void **)&L.prec, 5 * T * sizeof(uint32_t)));  // records, then the sums again
+            ONO_HIP(hipMalloc((void **)&L.pE, (T + 1) * sizeof(uint64_t)));
+            ONO_HIP(hipMalloc((void **)&L.pwide, (T + 1) * sizeof(uint32_t)));
+            L.pt_cap = T;
+        }
+        word[1] = word[2] = word[3] = word[4] = 0;
+        static const int dbg = [] { const char *e = getenv("ONO_PL_DBG"); return e ? atoi(e) : 0; }();
+        uint32_t *tsum = L.prec + 4 * L.pt_cap;
+        hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, dbuf, M, L.prec, tsum, qcount, L.pwide,
+                           L.host_word_dev, epoch, dbg >> 4);
+        if (T > kPatDirect)
+            hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev, epoch);
+        hipLaunchKernelGGL(pl_place, dim3((unsigned)T), dim3(kPatT), 0, s, g, dbuf, M, T, cap, vec, L.pE, L.prec, tsum,
+                           L.pwide, L.host_word_dev, epoch, dbg & 15);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
+        const uint64_t total = word[1];
+        if (total > cap) return size_error(total);
+        if (word[2] != epoch && word[4] == epoch) {  // tiles with wide ranges (a sparse stream)
+            hipLaunchKernelGGL(pl_wide, dim3((unsigned)std::min<size_t>(T, 2048)), dim3(kPatT), 0, s, g, dbuf, M, T,
+                               vec, L.pE, tsum, L.pwide, L.queue, qcount, (uint32_t)qcap, L.host_word_dev, epoch);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
+        }
+        if (word[2] != epoch) {
+            if (word[3] == epoch) {  // long runs or wide gaps were queued
+                hipLaunchKernelGGL(sl_long, dim3((unsigned)std::min<size_t>(2048, qcap)), dim3(kSB), 0, s, g, dbuf,
+                                   L.queue, qcount, (uint32_t)qcap);
+                e = hipGetLastError();
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
+            }
+            *out_len = total;
+            return ONO_OK;
+        }
+        g_lift_pattern_misses.fetch_add(1);  // not the pattern: the walk path parses it
+    }
+    word[0] = 0;
+    word[1] = 0;
     hipLaunchKernelGGL(sl_index, dim3((unsigned)Wg), dim3(kLW), 0, s, dbuf, nbytes, S, epoch, p0, gpre, rcnt, L.ent,
                        reached, wsum, qcount, L.host_word_dev);
     hipLaunchKernelGGL(sl_place, dim3((unsigned)std::max<size_t>(1, (S + kPSeg - 1) / kPSeg)), dim3(kPT), 0, s, g,
@@ -1588,6 +2093,12 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
 }
 
 size_t ono_sparse_lift_fallbacks(void) { return g_lift_fallbacks.load(); }
+size_t ono_sparse_lift_pattern_misses(void) { return g_lift_pattern_misses.load(); }
+int ono_sparse_lift_set_mode(int mode) {
+    if (mode != 0 && mode != 1) return set_error(ONO_E_ARG, "lift mode %d (0: pattern path first, 1: walk path)", mode);
+    g_lift_mode.store(mode);
+    return ONO_OK;
+}
 
 int ono_sparse_lift_dev(float *g, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
                         void *stream) {

@@ -20,6 +20,16 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
 
 
+@pytest.fixture(params=[0, 1], ids=["pattern_first", "walk_only"])
+def lift_mode(request):
+    """Each device-lift test runs with the pattern path first (the default) and
+    with the walk path alone, so both parsers meet every case."""
+    L = ono_amd.lib()
+    assert L.ono_sparse_lift_set_mode(request.param) == 0
+    yield request.param
+    assert L.ono_sparse_lift_set_mode(0) == 0
+
+
 def test_grad_drop_kat():  # protocol.rs:150-170
     assert SP.grad_drop(dev([1.0, -1.0, 0.0, 2.0]), 1.0) == KAT_BUF
 
@@ -149,6 +159,7 @@ def random_stream(rng, nrec: int, max_off: int, max_len: int, payload: str, min_
     return b"".join(parts)
 
 
+@pytest.mark.usefixtures("lift_mode")
 def test_lift_dev_kats():
     assert SP.grad_lift(to_dev(KAT_BUF)).cpu().tolist() == [1.0, -1.0, 0.0, 2.0]
     short = bytes([3, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 2, 0, 0, 0, 0, 60, 0, 188])
@@ -156,6 +167,7 @@ def test_lift_dev_kats():
     assert SP.grad_lift(to_dev(bytes(8))).numel() == 0
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("n", [2049, 65536 + 17, (1 << 20) + 5, 1 << 24])
 @pytest.mark.parametrize("r", [0.0, 0.5, 0.9, 0.999])
 def test_drop_lift_device_resident(n, r):
@@ -171,6 +183,7 @@ def test_drop_lift_device_resident(n, r):
     assert_bitexact(SP.grad_lift(host_bytes, cap=n).cpu().numpy(), want)
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("payload", ["random", "small", "zeros"])
 @pytest.mark.parametrize("nrec,max_off,max_len", [(1, 3, 5), (37, 2, 3), (5000, 4, 40), (200000, 1, 6),
                                                   (3000, 0, 2000)])
@@ -205,6 +218,7 @@ def test_lift_dev_typical_stream_takes_the_parallel_parse():
     assert torch.equal(back.view(torch.int32), ref.view(torch.int32))
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("buf,msg", [
     (bytes([4, 0, 0, 0, 0, 0, 0, 0, 0, 0]), "Missing index bytes"),
     (bytes([4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 0]), "Missing chunk length bytes"),
@@ -216,6 +230,7 @@ def test_lift_dev_errors(buf, msg):
         SP.grad_lift_dev(to_dev(buf), 16)
 
 
+@pytest.mark.usefixtures("lift_mode")
 def test_lift_dev_error_deep_in_a_long_stream():
     """A bounds error in record 150000 of a valid-looking stream: the parallel
     parse refutes itself and the sequential parse reports the reference's error."""
@@ -227,6 +242,7 @@ def test_lift_dev_error_deep_in_a_long_stream():
         SP.grad_lift_dev(to_dev(bytes(b)), total)
 
 
+@pytest.mark.usefixtures("lift_mode")
 def test_lift_dev_size_error_and_short_cap():
     """total > cap: ONO_E_SIZE from the device-side check, nothing written."""
     import ctypes as C
@@ -244,6 +260,7 @@ def test_lift_dev_size_error_and_short_cap():
     assert_bitexact(back.cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=64))
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("offset", [0, 1, 2])
 def test_lift_dev_into_unaligned_gradient(offset):
     """g at a 4-B (not 16-B) boundary: the device zero-fill's scalar form."""
@@ -397,6 +414,7 @@ def _lift_into(buf_dev: torch.Tensor, out: torch.Tensor, cap: int) -> int:
     return ln.value
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("n,r", [(70001, 0.9), (1 << 20, 0.5), (4099, 0.0)])
 def test_lift_dev_leaves_values_past_total_untouched(n, r):
     """cap > total: g[0, total) is the lift (zeros between the runs), g[total, cap) keeps what it held
@@ -411,6 +429,7 @@ def test_lift_dev_leaves_values_past_total_untouched(n, r):
     assert torch.all(out[n:] == 9.0)
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("lens", [[4096], [4097], [8192 + 33], [33, 32, 31, 4096 * 3 + 1], [1, 2, 3] * 50])
 def test_lift_dev_long_runs_across_chunks(lens):
     """Runs longer than one lane's share (> 32 values) go through the chunk queue, including runs that
@@ -453,6 +472,7 @@ def test_lift_dev_walks_longer_than_the_noted_records():
     assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
 
 
+@pytest.mark.usefixtures("lift_mode")
 @pytest.mark.parametrize("offs,lens,tail", [
     ([], [], 3_000_000),                                   # no records: g is all tail (queued zero chunks)
     ([1_500_000, 2_000_000, 10], [5, 40, 1], 2_500_000),  # gaps wider than a workgroup zeroes itself

@@ -1,0 +1,175 @@
+"""The device lift's pattern path (round 3): drop-shaped streams parse with no
+speculation and no walks, checked to be the reference's sequential parse
+(comms/src/sparse/protocol.rs:96-144); every other stream is refuted by those
+checks and parsed by the walk path or the host, never mis-parsed."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import ono_amd
+from ono_amd import sparse as SP
+from conftest import SEED, assert_bitexact
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def to_dev(b: bytes) -> torch.Tensor:
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+
+
+def lift_into(buf_dev: torch.Tensor, out: torch.Tensor, cap: int) -> int:
+    ln = C.c_size_t(0)
+    rc = ono_amd.lib().ono_sparse_lift_dev(out.data_ptr(), cap, C.byref(ln), buf_dev.data_ptr(), buf_dev.numel(),
+                                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rc == 0, ono_amd.lib().ono_last_error()
+    return ln.value
+
+
+def counters():
+    L = ono_amd.lib()
+    return L.ono_sparse_lift_pattern_misses(), L.ono_sparse_lift_fallbacks()
+
+
+def pattern_stream(rng, nrec, off_range, len_range, pad=3):
+    """A drop-shaped stream: offsets in off_range (>= 1 after the first), lengths >= 1, both < 2^16,
+    nonzero finite f16 payloads of either sign."""
+    offs = rng.integers(off_range[0], off_range[1] + 1, nrec).astype(np.int64)
+    lens = rng.integers(len_range[0], len_range[1] + 1, nrec).astype(np.int64)
+    total = int(offs.sum() + lens.sum()) + pad
+    units = 4 + lens
+    starts = np.concatenate([[0], np.cumsum(units)[:-1]])
+    u = rng.integers(1, 0x7C00, int(units.sum())).astype(np.uint16)
+    u |= rng.integers(0, 2, u.size).astype(np.uint16) << 15
+    u[starts], u[starts + 1] = offs & 0xFFFF, offs >> 16
+    u[starts + 2], u[starts + 3] = lens & 0xFFFF, lens >> 16
+    return np.uint64(total).tobytes() + u.tobytes(), total
+
+
+def header_positions(b: bytes, upto: int) -> list[int]:
+    pos, out = 8, []
+    while pos < len(b) and len(out) < upto:
+        out.append(pos)
+        pos += 8 + 2 * int.from_bytes(b[pos + 4:pos + 8], "little")
+    return out
+
+
+@pytest.mark.parametrize("n,r", [(1 << 24, 0.9), ((1 << 20) + 5, 0.5), (65536 + 17, 0.99), (4099, 0.1),
+                                 (1 << 22, 0.999)])
+def test_pattern_path_takes_drop_output(n, r):
+    """grad_drop's output is parsed by the pattern path: no hand-over to the walk path, no host parse,
+    bit-exact with the oracle's lift."""
+    g = O.synth(n, SEED + 51, 5)
+    t = max(float(np.quantile(np.abs(g), r)), 6.103515625e-05)
+    wire = SP.grad_drop_dev(dev(g), t)
+    before = counters()
+    out = SP.grad_lift_dev(wire, n)
+    assert counters() == before
+    assert_bitexact(out.cpu().numpy(), O.grad_lift(bytes(wire.cpu().numpy()), cap=n))
+
+
+@pytest.mark.parametrize("nrec,off_range,len_range", [
+    (1, (0, 0), (1, 1)),                 # one record at offset 0
+    (3, (1, 5), (1, 3)),
+    (20000, (1, 30), (1, 12)),           # many tiles, short runs (one lane each)
+    (3000, (1, 40), (33, 700)),          # long runs: the workgroup copies them
+    (40, (1, 9), (20000, 65535)),        # runs longer than a tile: payloads read past the staged tile
+    (2000, (50, 200), (1, 3)),           # tile ranges above the LDS image: zeroed in g, then scattered
+    (1200, (60000, 65535), (1, 2)),      # wide tile ranges: zero chunks queued for sl_long's grid
+    (3_600_000, (1, 9), (1, 2)),         # more than 4096 tiles: the element prefixes from pl_scan
+])
+def test_pattern_path_range_shapes(nrec, off_range, len_range):
+    """Drop-shaped streams of every range shape stay on the pattern path, are exact, and leave
+    g[total, cap) untouched."""
+    rng = np.random.default_rng(nrec + off_range[1] + len_range[1])
+    b, total = pattern_stream(rng, nrec, off_range, len_range)
+    before = counters()
+    out = torch.full((total + 16,), 4.0, dtype=torch.float32, device="cuda")
+    assert lift_into(to_dev(b), out, total + 16) == total
+    assert counters() == before
+    assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
+    assert torch.all(out[total:] == 4.0)
+
+
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_pattern_path_into_unaligned_gradient(offset):
+    """g at a 4-B (not 16-B) boundary: the image's scalar store form."""
+    rng = np.random.default_rng(offset)
+    b, total = pattern_stream(rng, 9000, (1, 12), (1, 5))
+    base = torch.full((total + 8,), 5.0, dtype=torch.float32, device="cuda")
+    view = base[offset:offset + total]
+    before = counters()
+    assert lift_into(to_dev(b), view, total) == total
+    assert counters() == before
+    assert_bitexact(view.cpu().numpy(), O.grad_lift(b, cap=total))
+    assert torch.all(base[:offset] == 5.0) and torch.all(base[offset + total:] == 5.0)
+
+
+@pytest.mark.parametrize("case", ["zero_payload", "zero_length_run", "gap_2_16", "run_2_16", "header_like",
+                                  "odd_tail", "total_too_small", "truncated"])
+def test_pattern_refuted_streams_are_never_misparsed(case):
+    """Streams outside the pattern's shape fail its checks (never a wrong parse): the walk path or the
+    host parse gives the oracle's result or the reference's error."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    b, total = pattern_stream(rng, 5000, (1, 20), (1, 6))
+    b = bytearray(b)
+    rec = header_positions(bytes(b), 2001)[2000]  # a header deep in the stream (tile 2 or so)
+    ln = int.from_bytes(b[rec + 4:rec + 8], "little")
+    if case == "zero_payload":  # 0x0000 values: false candidates where a header follows a 1-value run
+        for p in header_positions(bytes(b), 5000)[::7]:
+            b[p + 8:p + 10] = b"\x00\x00"
+    elif case == "zero_length_run":  # a record with no values (the reference lifts it)
+        b[rec + 8 + 2 * ln:rec + 8 + 2 * ln] = np.array([3, 0], np.uint32).tobytes()
+        total += 3
+    elif case == "gap_2_16":  # an offset of 2^16 or more: its header's high half is not zero
+        off = int.from_bytes(b[rec:rec + 4], "little") + 70000
+        b[rec:rec + 4] = np.uint32(off).tobytes()
+        total += 70000
+    elif case == "run_2_16":
+        b[rec + 4:rec + 8] = np.uint32(ln + 70000).tobytes()
+        b[rec + 8 + 2 * ln:rec + 8 + 2 * ln] = rng.integers(1, 0x7C00, 70000).astype(np.uint16).tobytes()
+        total += 70000
+    elif case == "header_like":  # payload values that read as a plausible header pair
+        b[rec + 8:rec + 8] = np.array([2, 0, 1, 0], np.uint16).tobytes()
+        b[rec + 4:rec + 8] = np.uint32(ln + 4).tobytes()
+        total += 4
+    elif case == "odd_tail":
+        b += b"\x01"
+    elif case == "total_too_small":
+        total -= 10
+    elif case == "truncated":  # the last run's length points past the stream
+        last = header_positions(bytes(b), 5000)[-1]
+        b[last + 4:last + 8] = np.uint32(int.from_bytes(b[last + 4:last + 8], "little") + 2).tobytes()
+    b[:8] = np.uint64(total).tobytes()
+    b = bytes(b)
+    m0, _ = counters()
+    errors = {"odd_tail": "Missing index bytes", "total_too_small": "exceeds target vector bounds",
+              "truncated": "Truncated float data"}
+    if case in errors:
+        with pytest.raises(ono_amd.InvalidWorkerEvent, match=errors[case]):
+            SP.grad_lift_dev(to_dev(b), total + 16)
+        assert counters()[0] == m0 + (0 if case == "odd_tail" else 1)
+        return
+    out = SP.grad_lift_dev(to_dev(b), total)
+    if case != "zero_payload":
+        assert counters()[0] == m0 + 1
+    assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+def test_pattern_path_many_lifts_reuse_scratch():
+    """Lifts of growing and shrinking streams back to back (scratch regrown, epochs advancing): each
+    exact, none handed over."""
+    rng = np.random.default_rng(77)
+    before = counters()
+    for nrec in (10, 40000, 500, 120000, 1):
+        b, total = pattern_stream(rng, nrec, (1, 15), (1, 4))
+        out = SP.grad_lift_dev(to_dev(b), total)
+        assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+    assert counters() == before
