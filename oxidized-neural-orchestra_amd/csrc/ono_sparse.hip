@@ -1261,26 +1261,23 @@ __device__ __forceinline__ size_t pat_stage(uint4 *lw4, const uint8_t *b, size_t
 // last candidate's successor: the next tile's first record or M).
 __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, uint32_t *rec, uint32_t *tsum,
                                                   uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
-                                                  uint32_t epoch, int dbg) {
+                                                  uint32_t epoch) {
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint16_t lmask[kPatT], lpre[kPatT];  // (masks of kPatPer bits)
     const size_t t = blockIdx.x, base = t * kPatU;
     const uint16_t *lwu = (const uint16_t *)lw4;
-    if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, empty queues
+    if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
         host_word[1] = stream_total(b);
         *qcount = 0;
-        *wide = 0;
     }
     pat_stage(lw4, b, base, M);
     __syncthreads();
-    if (dbg == 1) return;
     const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
     uint32_t sum;
     const uint32_t m = pat_mask(U, base + j0, M, sum);
     uint32_t ec, es, tc, ts;
     block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
-    if (dbg == 2) { if (m == 12345) rec[0] = es; return; }
     lmask[threadIdx.x] = (uint16_t)m;
     lpre[threadIdx.x] = (uint16_t)ec;
     __syncthreads();
@@ -1384,11 +1381,11 @@ __device__ int64_t prev_nonempty(const uint32_t *rec, size_t from) {
 // A range of up to kPatImg values (every tile of a 10 %-kept stream) is built in
 // LDS in one pass — zeros, each record's run placed by the lane that holds it
 // (short runs from the staged units, long ones by the workgroup) — and stored
-// as whole 16-B vectors.  A wider range (sparse streams) is listed for pl_wide.
+// as whole 16-B vectors.  A wider range (sparse streams) is flagged for pl_wide.
 constexpr size_t kPatDirect = 4096;  // up to this many tiles pl_place sums the earlier tiles itself
 __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
-                                                  uint32_t *wide, uint64_t *host_word, uint32_t epoch, int dbg) {
+                                                  uint32_t *wide, uint64_t *host_word, uint32_t epoch) {
     __shared__ f4s img4[kPatImg / 4];
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -1442,31 +1439,29 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const uint64_t ea = min(E0, total);
     uint64_t eb = t + 1 == T ? total : min(E1, total);
     eb = max(eb, ea);
-    if (eb == ea) return;  // (uniform) an empty tile inside a run
     const uint64_t ia = vec ? ea & ~3ull : ea;
     const uint32_t n = (uint32_t)min(eb - ia, (uint64_t)kPatImg + 1);
-    if (n > (uint32_t)kPatImg) {  // (uniform) a wide range: pl_wide places it
-        if (threadIdx.x == 0) {
+    const bool is_wide = eb > ea && n > (uint32_t)kPatImg;
+    if (threadIdx.x == 0) {
+        wide[t] = is_wide;  // (every tile writes its flag: nothing to reset between lifts)
+        if (is_wide) {
             if (direct) E[t] = E0;
-            wide[1 + atomicAdd(wide, 1u)] = (uint32_t)t;
             *(volatile uint64_t *)(host_word + 4) = epoch;
         }
-        return;
     }
+    if (eb == ea || is_wide) return;  // (uniform) an empty tile inside a run; a wide range: pl_wide places it
     {
         const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
         for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img4[i] = z;
     }
     if (threadIdx.x == 0) lqn = 0;
     __syncthreads();  // the staged units, the zeros
-    if (dbg == 1) return;
     const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
     uint32_t sum;
     const uint32_t m = pat_mask(U, base + j0, M, sum);
     uint32_t ec, es, tc, ts;
     block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
-    if (dbg == 3) { if (m == 77777) g[0] = es; return; }
     uint64_t cur = E0 + es;  // where the run before the thread's first record ended
     for (uint32_t mm = m; mm; mm &= mm - 1) {
         const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
@@ -1501,7 +1496,6 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
         __syncthreads();
     }
-    if (dbg == 2) return;
     // the range out: whole 16-B vectors inside [ea, eb), then the partial first and last vectors
     const uint32_t skip = (uint32_t)(ea - ia);
     if (vec) {
@@ -1519,8 +1513,8 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     }
 }
 
-// The tiles pl_place listed (ranges above kPatImg: sparse streams), one
-// workgroup each, grid-stride: up to kPatPasses windows of kPatImg values built
+// The tiles pl_place flagged (ranges above kPatImg: sparse
+// streams), one workgroup each, grid-stride over the tiles: up to kPatPasses windows of kPatImg values built
 // in LDS one after another; wider still (few tiles hold all of g), the gaps and
 // the tail queued as zero chunks for sl_long's full grid and the values
 // scattered (long runs queued).
@@ -1536,9 +1530,9 @@ __global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, siz
     float *img = (float *)img4;
     const uint16_t *lw = (const uint16_t *)lw4;
     const uint64_t total = stream_total(b);
-    const uint32_t nw = wide[0];
-    for (uint32_t wi = blockIdx.x; wi < nw; wi += gridDim.x) {
-        const size_t t = wide[1 + wi], base = t * kPatU;
+    for (size_t t = blockIdx.x; t < T; t += gridDim.x) {
+        if (!wide[t]) continue;  // (uniform)
+        const size_t base = t * kPatU;
         const uint64_t E0 = E[t];
         const uint64_t ea = min(E0, total);
         uint64_t eb = t + 1 == T ? total : min(E0 + tsum[t], total);
@@ -1681,7 +1675,7 @@ struct LiftScratch {
     size_t pt_cap = 0;
     uint32_t *prec = nullptr;  // pattern path: 4 x pt_cap tile records, then pt_cap tile sums
     uint64_t *pE = nullptr;    // pattern path: pt_cap + 1 element prefixes
-    uint32_t *pwide = nullptr; // pattern path: [0] count, then the tiles of wide ranges
+    uint32_t *pwide = nullptr; // pattern path: per tile, 1 = a wide range (for pl_wide)
     // [0] walk refuted / malformed (= epoch), [1] total, [2] pattern refuted (= epoch), [3] pattern queued a
     // chunk, [4] pattern listed a wide tile
     uint64_t *host_word = nullptr, *host_word_dev = nullptr;
@@ -1831,18 +1825,17 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
             L.pt_cap = 0;
             ONO_HIP(hipMalloc((void **)&L.prec, 5 * T * sizeof(uint32_t)));  // records, then the sums again
             ONO_HIP(hipMalloc((void **)&L.pE, (T + 1) * sizeof(uint64_t)));
-            ONO_HIP(hipMalloc((void **)&L.pwide, (T + 1) * sizeof(uint32_t)));
+            ONO_HIP(hipMalloc((void **)&L.pwide, T * sizeof(uint32_t)));
             L.pt_cap = T;
         }
         word[1] = word[2] = word[3] = word[4] = 0;
-        static const int dbg = [] { const char *e = getenv("ONO_PL_DBG"); return e ? atoi(e) : 0; }();
         uint32_t *tsum = L.prec + 4 * L.pt_cap;
         hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, dbuf, M, L.prec, tsum, qcount, L.pwide,
-                           L.host_word_dev, epoch, dbg >> 4);
+                           L.host_word_dev, epoch);
         if (T > kPatDirect)
             hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev, epoch);
         hipLaunchKernelGGL(pl_place, dim3((unsigned)T), dim3(kPatT), 0, s, g, dbuf, M, T, cap, vec, L.pE, L.prec, tsum,
-                           L.pwide, L.host_word_dev, epoch, dbg & 15);
+                           L.pwide, L.host_word_dev, epoch);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);

@@ -15,13 +15,13 @@ for v in default $SP_VARIANTS; do
   else
     env $v timeout -k 10 120 python -u tools/sparse_codec_run.py 20 > gpurun_out/sp_run_$v.log 2>&1 || { cat gpurun_out/sp_run_$v.log; exit 1; }
   fi
-  grep drop gpurun_out/sp_run_$v.log
+  grep -E "drop|lift" gpurun_out/sp_run_$v.log
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sp_prof -o sp -- python3 tools/sparse_codec_run.py 20 > gpurun_out/sp_prof.log 2>&1 || exit 1
 python3 - <<'PY'
 import csv, glob
 for f in glob.glob('gpurun_out/sp_prof/*kernel_stats.csv'):
     for r in csv.DictReader(open(f)):
-        if 'sp_' in r['Name'] or 'sl_' in r['Name']:
+        if any(k in r['Name'] for k in ('sp_', 'sl_', 'pl_')):
             print(r['Name'].replace('(anonymous namespace)::', '').split('(')[0][-40:], r['Calls'], round(float(r['AverageNs'])/1000, 2), round(float(r['MinNs'])/1000, 2), round(float(r['MaxNs'])/1000, 2))
 PY
