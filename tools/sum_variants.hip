@@ -336,9 +336,17 @@ static void sweep(hipStream_t s) {
     static char names[256][24];
     static int nn = 0;
     auto name = [&](const char *f, int occ) { char *nm = names[nn++ % 256]; snprintf(nm, 24, f, occ); return (const char *)nm; };
-    for (int occ : {28}) {
+    for (int occ : {20, 24, 28}) {
         const unsigned l = lds_for(occ);
         variant<K>(name("SER1_occ%d", occ), s, [&](Args a) { hipLaunchKernelGGL((k_sum_ser<K, 1>), dim3(g64), dim3(64), l, s, a); });
+        variant<K>(name("GLDS_occ%d", occ), s, [&](Args a) { hipLaunchKernelGGL((k_sum_glds<K>), dim3(g64), dim3(64), l, s, a); });
+    }
+    // U vectors per lane, serialized by input (round 3, session 2): fewer waves, more bytes per load burst
+    const unsigned g64u2 = (unsigned)((N / 4 + 127) / 128), g64u4 = (unsigned)((N / 4 + 255) / 256);
+    for (int occ : {0, 16, 24}) {
+        const unsigned l = occ ? lds_for(occ) : 0u;
+        variant<K>(name("SERU2_occ%d", occ), s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 64, 2>), dim3(g64u2), dim3(64), l, s, a); });
+        variant<K>(name("SERU4_occ%d", occ), s, [&](Args a) { hipLaunchKernelGGL((k_sum_seru<K, 64, 4>), dim3(g64u4), dim3(64), l, s, a); });
     }
 }
 
