@@ -1260,23 +1260,53 @@ __device__ __forceinline__ size_t pat_stage(uint4 *lw4, const uint8_t *b, size_t
 
 // rec[4 t ..]: candidates, sum of offset + length, first candidate, exit (the
 // last candidate's successor: the next tile's first record or M).
+// A thread's 12 units straight from the stream (one 16-B and one 8-B load; the
+// 8-byte total keeps them 8-B aligned), element by element at the stream's end.
+__device__ __forceinline__ Units12 units12_global(const uint8_t *b, size_t k0, size_t M) {
+    Units12 r;
+    const uint8_t *p = b + 8 + 2 * k0;
+    if (k0 + 12 <= M) {
+        const uint4 a = *(const uint4 *)p;
+        const uint2 c = *(const uint2 *)(p + 16);
+        r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
+        r.w[4] = c.x; r.w[5] = c.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const uint32_t lo = k0 + 2 * i < M ? ((const uint16_t *)p)[2 * i] : 0u;
+            const uint32_t hi = k0 + 2 * i + 1 < M ? ((const uint16_t *)p)[2 * i + 1] : 0u;
+            r.w[i] = lo | hi << 16;
+        }
+    }
+    return r;
+}
+// unit j + 2 of the thread's units for a run-time j < kPatPer (a select chain: a register array
+// indexed at run time would be moved to LDS and addressed through the dispatch packet)
+__device__ __forceinline__ uint32_t unit_plus2(const Units12 &U, uint32_t j) {
+    uint32_t v = U.u(2);
+#pragma unroll
+    for (int q = 1; q < kPatPer; q++) v = j == (uint32_t)q ? U.u(q + 2) : v;
+    return v;
+}
+
+// rec[4 t ..]: candidates, sum of offset + length, first candidate, exit (the
+// last candidate's successor: the next tile's first record or M).  The units
+// come straight from HBM into registers (no LDS staging); the masks and their
+// prefixes go through LDS for the successor checks.
 __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, uint32_t *rec, uint32_t *tsum,
                                                   uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
                                                   uint32_t epoch) {
-    __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint16_t lmask[kPatT], lpre[kPatT];  // (masks of kPatPer bits)
     const size_t t = blockIdx.x, base = t * kPatU;
-    const uint16_t *lwu = (const uint16_t *)lw4;
     if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
         host_word[1] = stream_total(b);
         *qcount = 0;
     }
-    pat_stage(lw4, b, base, M);
-    __syncthreads();
-    const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
-    uint32_t sum;
-    const uint32_t m = pat_mask(U, base + j0, M, sum);
+    const bool any = base + j0 < M;
+    const Units12 U = any ? units12_global(b, base + j0, M) : Units12{};
+    uint32_t sum = 0;
+    const uint32_t m = any ? pat_mask(U, base + j0, M, sum) : 0u;
     uint32_t ec, es, tc, ts;
     block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
     lmask[threadIdx.x] = (uint16_t)m;
@@ -1286,9 +1316,7 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, ui
     uint32_t rank = ec;
     for (uint32_t mm = m; mm; mm &= mm - 1, rank++) {
         const uint32_t j = (uint32_t)__builtin_ctz(mm), k = j0 + j;
-        const uint32_t nx = k + 4 + lwu[k + 2];  // tile-local successor (units read back from LDS: a
-                                                  // register array indexed at run time would be moved to
-                                                  // LDS by the compiler, addressed through the dispatch packet)
+        const uint32_t nx = k + 4 + unit_plus2(U, j);  // tile-local successor
         if (base + nx > M) { bad = true; break; }  // the run overruns the stream
         if (nx < (uint32_t)kPatU && base + nx < M) {
             const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
