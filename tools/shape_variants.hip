@@ -74,6 +74,34 @@ __global__ __launch_bounds__(64) void k_dec(Args a) {
     stn(a.b[1] + v, x * 0.125f);
 }
 
+// the decode with B threads per workgroup and U vectors per lane (one wave apart: each
+// instruction 512 B in, 1 KiB out, contiguous): fewer workgroups for the dispatcher (round 3)
+template <int B, int U>
+__global__ __launch_bounds__(B) void k_dec_bu(Args a) {
+    const size_t base = ((size_t)blockIdx.x * (B / 64) + threadIdx.x / 64) * 64 * U + threadIdx.x % 64;
+    h4 h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t v = base + 64 * u;
+        if (v < a.nvec) h[u] = ldn((const h4 *)a.b[0] + v);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t v = base + 64 * u;
+        if (v < a.nvec) {
+            f4 x = {(float)__builtin_bit_cast(_Float16, h[u].x), (float)__builtin_bit_cast(_Float16, h[u].y),
+                    (float)__builtin_bit_cast(_Float16, h[u].z), (float)__builtin_bit_cast(_Float16, h[u].w)};
+            stn(a.b[1] + v, x * 0.125f);
+        }
+    }
+}
+// the same grid doing nothing but its guard
+template <int B, int U>
+__global__ __launch_bounds__(B) void k_empty_bu(Args a) {
+    const size_t base = ((size_t)blockIdx.x * (B / 64) + threadIdx.x / 64) * 64 * U + threadIdx.x % 64;
+    if (base == (size_t)-1) a.b[1][0] = f4{0, 0, 0, 0};
+}
+
 __global__ void k_fill(f4 *p, size_t n, unsigned seed) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -147,6 +175,23 @@ static void shape(const char *tag, hipStream_t s) {
     }
 }
 
+template <int B, int U>
+static void dec_bu(hipStream_t s, bool empty) {
+    const int nsets = 1536 / (6 * 64 / 4 * 4 / 4) + 2;
+    const unsigned g = (unsigned)((N / 4 + 64 * U * (B / 64) - 1) / (64 * U * (B / 64)));
+    const double us = timeit(nsets, s, [&](int set) {
+        Args a{};
+        a.b[0] = buf(set * 2, s);
+        a.b[1] = buf(set * 2 + 1, s);
+        a.nvec = N / 4;
+        if (empty) hipLaunchKernelGGL((k_empty_bu<B, U>), dim3(g), dim3(B), 0, s, a);
+        else hipLaunchKernelGGL((k_dec_bu<B, U>), dim3(g), dim3(B), 0, s, a);
+    });
+    char nm[64];
+    snprintf(nm, sizeof nm, "%s B%d U%d", empty ? "empty" : "dec", B, U);
+    record(nm, 6.0 * N, us);
+}
+
 static void dec(hipStream_t s) {
     const int nsets = 1536 / (6 * 64 / 4 * 4 / 4) + 2;  // 6 B per element
     const unsigned g = (unsigned)((N / 4 + 63) / 64);
@@ -175,14 +220,26 @@ int main(int argc, char **argv) {
            p.multiProcessorCount, N, passes);
     fflush(stdout);
     for (int pass = 0; pass < passes; pass++) {
-        shape<1, 2>("1R2W", s);
-        shape<2, 1>("2R1W", s);
-        shape<2, 2>("2R2W", s);
-        shape<2, 3>("2R3W", s);
-        shape<3, 4>("3R4W", s);
-        shape<4, 5>("4R5W", s);
-        shape<8, 3>("8R3W", s);
+        if (!getenv("DEC_BU")) {
+            shape<1, 2>("1R2W", s);
+            shape<2, 1>("2R1W", s);
+            shape<2, 2>("2R2W", s);
+            shape<2, 3>("2R3W", s);
+            shape<3, 4>("3R4W", s);
+            shape<4, 5>("4R5W", s);
+            shape<8, 3>("8R3W", s);
+        }
         dec(s);
+        if (getenv("DEC_BU")) {
+            for (bool e : {false, true}) {
+                dec_bu<64, 1>(s, e);
+                dec_bu<64, 2>(s, e);
+                dec_bu<64, 4>(s, e);
+                dec_bu<256, 1>(s, e);
+                dec_bu<256, 2>(s, e);
+                dec_bu<1024, 1>(s, e);
+            }
+        }
         fprintf(stderr, "pass %d done\n", pass);
     }
     for (auto &r : g_rows) {
