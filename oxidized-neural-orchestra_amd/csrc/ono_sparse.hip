@@ -1260,12 +1260,13 @@ __device__ __forceinline__ size_t pat_stage(uint4 *lw4, const uint8_t *b, size_t
 
 // rec[4 t ..]: candidates, sum of offset + length, first candidate, exit (the
 // last candidate's successor: the next tile's first record or M).
-// A thread's 12 units straight from the stream (one 16-B and one 8-B load; the
-// 8-byte total keeps them 8-B aligned), element by element at the stream's end.
+// A thread's 12 units straight from the stream (one 16-B and one 8-B load when
+// the stream is 8-B aligned: the 8-byte total keeps them so), unit by unit at
+// the stream's end or for a stream at a 2-B boundary.
 __device__ __forceinline__ Units12 units12_global(const uint8_t *b, size_t k0, size_t M) {
     Units12 r;
     const uint8_t *p = b + 8 + 2 * k0;
-    if (k0 + 12 <= M) {
+    if (k0 + 12 <= M && ((uintptr_t)b & 7) == 0) {
         const uint4 a = *(const uint4 *)p;
         const uint2 c = *(const uint2 *)(p + 16);
         r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;

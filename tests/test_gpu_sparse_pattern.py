@@ -173,3 +173,20 @@ def test_pattern_path_many_lifts_reuse_scratch():
         out = SP.grad_lift_dev(to_dev(b), total)
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
     assert counters() == before
+
+
+@pytest.mark.parametrize("shift", [2, 4, 6])
+def test_pattern_path_stream_at_a_2_byte_boundary(shift):
+    """The stream itself at 2 / 4 / 6 bytes past an 8-byte boundary (a frame inside a larger receive
+    buffer): the unit loads take their 2-byte form; exact, no hand-over."""
+    rng = np.random.default_rng(shift)
+    b, total = pattern_stream(rng, 7000, (1, 12), (1, 5))
+    raw = torch.zeros(len(b) + 16, dtype=torch.uint8, device="cuda")
+    raw[shift:shift + len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    view = raw[shift:shift + len(b)]
+    assert view.data_ptr() % 8 == shift
+    before = counters()
+    out = torch.empty(total, dtype=torch.float32, device="cuda")
+    assert lift_into(view, out, total) == total
+    assert counters() == before
+    assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
