@@ -1413,6 +1413,31 @@ __device__ int64_t prev_nonempty(const uint32_t *rec, size_t from) {
 // (short runs from the staged units, long ones by the workgroup) — and stored
 // as whole 16-B vectors.  A wider range (sparse streams) is flagged for pl_wide.
 constexpr size_t kPatDirect = 4096;  // up to this many tiles pl_place sums the earlier tiles itself
+// One block-wide reduction of a u64 sum and a u64 max (one LDS exchange).
+template <int NT>
+__device__ __forceinline__ void block_sum_max64(uint64_t s, uint64_t x, uint64_t &S, uint64_t &X) {
+    __shared__ uint64_t ws[NT / 64], wx[NT / 64];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        s += (uint64_t)__shfl_xor((unsigned long long)s, d, 64);
+        x = max(x, (uint64_t)__shfl_xor((unsigned long long)x, d, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        ws[threadIdx.x >> 6] = s;
+        wx[threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    S = 0;
+    X = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        S += ws[w];
+        X = max(X, wx[w]);
+    }
+}
+
+// (32-bit element and unit arithmetic: total <= cap < 2^32 and M < 2^31 on the device path; the one
+// sum that could wrap in a malformed stream, the last tile's, is checked in 64 bits)
 __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
                                                   uint32_t *wide, uint64_t *host_word, uint32_t epoch) {
@@ -1421,7 +1446,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     __shared__ uint32_t lq[3 * kLQ], lqn;
     float *img = (float *)img4;
     const uint16_t *lw = (const uint16_t *)lw4;
-    const size_t t = blockIdx.x, base = t * kPatU;
+    const uint32_t t = blockIdx.x, base = t * (uint32_t)kPatU, M32 = (uint32_t)M, T32 = (uint32_t)T;
     const bool direct = T <= kPatDirect;  // (uniform) else E[] from pl_scan
     // the prologue's loads issued together: the tile's record, its range (E from pl_scan, or the earlier
     // tiles' sums), the record of each of the 256 tiles before it (the nearest non-empty one's exit is
@@ -1433,7 +1458,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     if (direct) {
 #pragma unroll
         for (int q = 0; q < kSumPer; q++) {
-            const size_t i = threadIdx.x + (size_t)q * kPatT;
+            const uint32_t i = threadIdx.x + (uint32_t)q * kPatT;
             sums[q] = i < t ? tsum[i] : 0u;
         }
     } else {
@@ -1444,33 +1469,38 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const uint64_t total = stream_total(b);
     pat_stage(lw4, b, base, M);
     if (total > cap) return;  // ONO_E_SIZE: nothing is written
+    if (threadIdx.x == 0) lqn = 0;
     {
-        uint64_t key = threadIdx.x < t && near.x > 0 ? (uint64_t)(t - threadIdx.x) << 32 | near.w : 0;
-        key = block_max64<kPatT>(key);  // (index + 1) << 32 | exit of the nearest non-empty tile
+        uint64_t part = 0;
+        if (direct) {
+#pragma unroll
+            for (int q = 0; q < kSumPer; q++) part += sums[q];
+        }
+        // (index + 1) << 32 | exit of the nearest non-empty tile among the 256 before t
+        const uint64_t key0 = threadIdx.x < t && near.x > 0 ? (uint64_t)(t - threadIdx.x) << 32 | near.w : 0;
+        uint64_t S, key;
+        block_sum_max64<kPatT>(part, key0, S, key);  // (its sync also covers the staged units)
         uint32_t pexit = (uint32_t)key;
         bool found = key != 0;
-        if (!found && t > (size_t)kPatT) {  // none among those 256
+        if (!found && t > (uint32_t)kPatT) {  // none among those 256
             const int64_t q = prev_nonempty(rec, t - kPatT);
             found = q >= 0;
             if (found) pexit = rec[4 * q + 3];
         }
         bool bad = me.x > 0 && (found ? pexit != me.z : me.z != 0u);
-        if (t + 1 == T) bad |= me.x > 0 ? me.w != (uint32_t)M : !found || pexit != (uint32_t)M;
+        if (t + 1 == T32) bad |= me.x > 0 ? me.w != M32 : !found || pexit != M32;
         if (direct) {
-            uint64_t part = 0;
-#pragma unroll
-            for (int q = 0; q < kSumPer; q++) part += sums[q];
-            E0 = block_sum64<kPatT>(part);
+            E0 = S;
             E1 = E0 + me.y;
-            if (t + 1 == T) bad |= E1 > total;  // the offsets and lengths sum to at most total
+            if (t + 1 == T32) bad |= E1 > total;  // the offsets and lengths sum to at most total
         }
         if (bad && threadIdx.x == 0) raise_bad(host_word + 2, epoch);
     }
-    const uint64_t ea = min(E0, total);
-    uint64_t eb = t + 1 == T ? total : min(E1, total);
-    eb = max(eb, ea);
-    const uint64_t ia = vec ? ea & ~3ull : ea;
-    const uint32_t n = (uint32_t)min(eb - ia, (uint64_t)kPatImg + 1);
+    const uint32_t total32 = (uint32_t)total;
+    const uint32_t ea = (uint32_t)min(E0, total);
+    const uint32_t eb = max(t + 1 == T32 ? total32 : (uint32_t)min(E1, total), ea);
+    const uint32_t ia = vec ? ea & ~3u : ea;
+    const uint32_t n = min(eb - ia, (uint32_t)kPatImg + 1);
     const bool is_wide = eb > ea && n > (uint32_t)kPatImg;
     if (threadIdx.x == 0) {
         wide[t] = is_wide;  // (every tile writes its flag: nothing to reset between lifts)
@@ -1484,20 +1514,19 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
         for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img4[i] = z;
     }
-    if (threadIdx.x == 0) lqn = 0;
-    __syncthreads();  // the staged units, the zeros
     const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
     uint32_t sum;
     const uint32_t m = pat_mask(U, base + j0, M, sum);
     uint32_t ec, es, tc, ts;
-    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
-    uint64_t cur = E0 + es;  // where the run before the thread's first record ended
+    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);  // (its sync: the zeros)
+    uint32_t cur = (uint32_t)E0 + es;  // where the run before the thread's first record ended
     for (uint32_t mm = m; mm; mm &= mm - 1) {
         const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
-        const uint64_t gi = cur + off;
-        if (gi < ea || gi + len > eb || base + k + 4 + len > M) {  // only a refuted stream
-            raise_bad(host_word + 2, epoch);
+        const uint32_t gi = cur + off;
+        // (overflow-free: in a refuted stream cur + off may wrap; then gi < ea or it lies past eb)
+        if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
+            raise_bad(host_word + 2, epoch);  // only a refuted stream
             break;
         }
         float *d = img + (gi - ia);
@@ -1505,9 +1534,9 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
             for (uint32_t i = 0; i < len; i++) d[i] = from_f16_sp(lw[k + 4 + i]);
         } else {
             const uint32_t q = atomicAdd(&lqn, 1u);
-            const uint32_t vp = (uint32_t)(8 + 2 * (base + k + 4));
+            const uint32_t vp = 8 + 2 * (base + k + 4);
             if (q < (uint32_t)kLQ) {
-                lq[3 * q] = (uint32_t)(gi - ia);
+                lq[3 * q] = gi - ia;
                 lq[3 * q + 1] = vp;
                 lq[3 * q + 2] = len;
             } else {
@@ -1527,19 +1556,20 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         __syncthreads();
     }
     // the range out: whole 16-B vectors inside [ea, eb), then the partial first and last vectors
-    const uint32_t skip = (uint32_t)(ea - ia);
+    const uint32_t skip = ea - ia;
+    float *gi0 = g + ia;
     if (vec) {
         const uint32_t v0 = skip ? 1u : 0u, v1 = n / 4;  // whole vectors [v0, v1)
         for (uint32_t i = v0 + threadIdx.x; i < v1; i += kPatT)
-            __builtin_nontemporal_store(img4[i], (f4s *)(g + ia) + i);
+            __builtin_nontemporal_store(img4[i], (f4s *)gi0 + i);
         if (threadIdx.x < 4) {
             const uint32_t e = threadIdx.x;
-            if (skip && e >= skip && e < n) g[ia + e] = img[e];  // the first vector's part in range
+            if (skip && e >= skip && e < n) gi0[e] = img[e];  // the first vector's part in range
             const uint32_t l = 4 * v1 + e;
-            if (l < n && l >= 4 * v0) g[ia + l] = img[l];        // the last vector's part
+            if (l < n && l >= 4 * v0) gi0[l] = img[l];        // the last vector's part
         }
     } else {
-        for (uint32_t i = threadIdx.x; i < n; i += kPatT) g[ia + i] = img[i];
+        for (uint32_t i = threadIdx.x; i < n; i += kPatT) gi0[i] = img[i];
     }
 }
 
