@@ -158,6 +158,16 @@ int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *bu
  * messages).  g[total, cap) is left untouched.                             */
 int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_dev, size_t nbytes,
                         void *stream);
+/* The stream-ordered lift (ono_sparse_drop_async's counterpart): the pattern
+ * path alone, nothing waits on the host.  *ticket receives a nonzero value;
+ * once the stream has passed the call, *status (device or host-mapped u64, one
+ * per stream) equals *ticket iff the lift was refused — a stream outside the
+ * pattern's shape, a malformed one, or total > cap — and g is then
+ * unspecified: call ono_sparse_lift_dev (blocking), which parses any stream and
+ * returns the reference's errors and ONO_E_SIZE.  Otherwise g[0, total) holds
+ * the lift (total: the stream's first 8 bytes).  Scratch is per stream.     */
+int ono_sparse_lift_dev_async(float *g_dev, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
+                              uint64_t *ticket, void *stream);
 /* lifts so far (this process) that took the sequential host parse        */
 size_t ono_sparse_lift_fallbacks(void);
 /* lifts so far (this process) that the pattern path handed to the walk path */

@@ -1296,7 +1296,7 @@ __device__ __forceinline__ uint32_t unit_plus2(const Units12 &U, uint32_t j) {
 // prefixes go through LDS for the successor checks.
 __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, uint32_t *rec, uint32_t *tsum,
                                                   uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
-                                                  uint32_t epoch) {
+                                                  uint64_t *badw, uint32_t epoch) {
     __shared__ uint16_t lmask[kPatT], lpre[kPatT];  // (masks of kPatPer bits)
     const size_t t = blockIdx.x, base = t * kPatU;
     if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, ui
             rec[4 * t + 3] = (uint32_t)(base + nx);
         }
     }
-    if (bad) raise_bad(host_word + 2, epoch);
+    if (bad) raise_bad(badw, epoch);
     if (m && ec == 0) rec[4 * t + 2] = (uint32_t)(base + j0 + __builtin_ctz(m));
     if (threadIdx.x == 0) {
         rec[4 * t] = tc;
@@ -1344,7 +1344,7 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, ui
 // is checked).  E[T] = where the last run ends.
 constexpr int kPatScanPer = 4;
 __global__ __launch_bounds__(kPatScanT) void pl_scan(const uint8_t *b, const uint32_t *rec, size_t T, uint64_t *E,
-                                                     uint64_t *host_word, uint32_t epoch) {
+                                                     uint64_t *badw, uint32_t epoch) {
     __shared__ uint32_t wtot[kPatScanT / 64];
     const uint64_t total = stream_total(b);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(kPatScanT) void pl_scan(const uint8_t *b, const uin
     }
     if (threadIdx.x == 0) {
         E[T] = carry;
-        if (carry > total) raise_bad(host_word + 2, epoch);
+        if (carry > total) raise_bad(badw, epoch);
     }
 }
 
@@ -1413,6 +1413,101 @@ __device__ int64_t prev_nonempty(const uint32_t *rec, size_t from) {
 // (short runs from the staged units, long ones by the workgroup) — and stored
 // as whole 16-B vectors.  A wider range (sparse streams) is flagged for pl_wide.
 constexpr size_t kPatDirect = 4096;  // up to this many tiles pl_place sums the earlier tiles itself
+// One tile with a wide range (above kPatImg: sparse streams), placed by one
+// workgroup: up to kPatPasses windows of kPatImg values built in LDS one after
+// another; wider still (few tiles hold all of g) and allow_queue, the gaps and
+// the tail queued as zero chunks for sl_long's full grid and the values
+// scattered (long runs queued); without allow_queue (the stream-ordered lift,
+// which launches nothing after it) every window in turn, however many.
+constexpr int kPatPasses = 8;
+__device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, size_t T, int vec, size_t t,
+                                          uint64_t E0, uint32_t sum_t, uint64_t total, bool allow_queue,
+                                          f4s *img4, uint4 *lw4, uint32_t *lq, uint32_t *lqn, uint4 *queue,
+                                          uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint64_t *badw,
+                                          uint32_t epoch) {
+    float *img = (float *)img4;
+    const uint16_t *lw = (const uint16_t *)lw4;
+    const size_t base = t * kPatU;
+    const uint64_t ea = min(E0, total);
+    uint64_t eb = t + 1 == T ? total : min(E0 + sum_t, total);
+    eb = max(eb, ea);
+    __syncthreads();  // earlier reads of the staged units
+    pat_stage(lw4, b, base, M);
+    __syncthreads();
+    const Units12 U = units12(lw4);
+    const uint32_t j0 = kPatPer * threadIdx.x;
+    uint32_t sum;
+    const uint32_t m = pat_mask(U, base + j0, M, sum);
+    uint32_t ec, es, tc, ts;
+    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
+    const uint64_t ia = vec ? ea & ~3ull : ea, span = eb - ia;
+    const uint64_t npass = (span + kPatImg - 1) / kPatImg;
+    if (allow_queue && npass > (uint64_t)kPatPasses) {
+        uint64_t cur = E0 + es;
+        for (uint32_t mm = m; mm; mm &= mm - 1) {
+            const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+            const uint64_t gi = cur + off;
+            if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(badw, epoch); break; }
+            queue_span(cur, 0, off, 1u, queue, qcount, qcap, host_word, epoch, host_word + 3);
+            if (len <= (uint32_t)kShortP)
+                for (uint32_t i = 0; i < len; i++) g[gi + i] = from_f16_sp(lw[k + 4 + i]);
+            else
+                queue_span(gi, 8 + 2 * (base + k + 4), len, 0u, queue, qcount, qcap, host_word, epoch,
+                           host_word + 3);
+            cur = gi + len;
+        }
+        const bool holds_last = m != 0 && ec + (uint32_t)__builtin_popcount(m) == tc;
+        if (t + 1 == T && (holds_last || (tc == 0 && threadIdx.x == 0)))
+            queue_span(E0 + ts, 0, total > E0 + ts ? total - (E0 + ts) : 0, 1u, queue, qcount, qcap, host_word,
+                       epoch, host_word + 3);
+        return;
+    }
+    const uint64_t skip = ea - ia;
+    for (uint64_t p = 0; p < npass; p++) {
+        const uint64_t w0 = p * kPatImg, w1 = min(w0 + kPatImg, span);
+        const uint32_t wn = (uint32_t)(w1 - w0);
+        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t i = threadIdx.x; i < (wn + 3) / 4; i += kPatT) img4[i] = z;
+        if (threadIdx.x == 0) *lqn = 0;
+        __syncthreads();
+        uint64_t cur = E0 + es;
+        for (uint32_t mm = m; mm; mm &= mm - 1) {
+            const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+            const uint64_t gi = cur + off;
+            cur = gi + len;
+            if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(badw, epoch); break; }
+            const uint64_t r0 = gi - ia, a = max(r0, w0), e = min(r0 + len, w1);
+            if (a >= e) continue;
+            const uint32_t c = (uint32_t)(e - a), u0 = k + 4 + (uint32_t)(a - r0), ai = (uint32_t)(a - w0);
+            if (len <= (uint32_t)kShortP) {
+                for (uint32_t i = 0; i < c; i++) img[ai + i] = from_f16_sp(lw[u0 + i]);
+            } else {
+                const uint32_t q = atomicAdd(lqn, 1u);
+                if (q < (uint32_t)kLQ) {
+                    lq[3 * q] = ai;
+                    lq[3 * q + 1] = (uint32_t)(8 + 2 * (base + u0));
+                    lq[3 * q + 2] = c;
+                } else {
+                    for (uint32_t i = 0; i < c; i++)
+                        img[ai + i] = from_f16_sp(((glb_u16 *)(b + 8 + 2 * (base + u0)))[i]);
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nl = min(*lqn, (uint32_t)kLQ);
+        for (uint32_t q = 0; q < nl; q++) {
+            const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
+            glb_u16 *src = (glb_u16 *)(b + vp);
+            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
+        }
+        __syncthreads();
+        float *dst = g + ia + w0;
+        for (uint32_t i = threadIdx.x; i < wn; i += kPatT)
+            if (w0 + i >= skip) dst[i] = img[i];
+        __syncthreads();
+    }
+}
+
 // One block-wide reduction of a u64 sum and a u64 max (one LDS exchange).
 template <int NT>
 __device__ __forceinline__ void block_sum_max64(uint64_t s, uint64_t x, uint64_t &S, uint64_t &X) {
@@ -1438,9 +1533,13 @@ __device__ __forceinline__ void block_sum_max64(uint64_t s, uint64_t x, uint64_t
 
 // (32-bit element and unit arithmetic: total <= cap < 2^32 and M < 2^31 on the device path; the one
 // sum that could wrap in a malformed stream, the last tile's, is checked in 64 bits)
+// ASYNC (the stream-ordered lift): nothing is launched after it, so a wide range is placed here
+// (wide_tile without the queue) and total > cap refutes the call instead of being read by the host.
+template <bool ASYNC>
 __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
-                                                  uint32_t *wide, uint64_t *host_word, uint32_t epoch) {
+                                                  uint32_t *wide, uint64_t *host_word, uint64_t *badw,
+                                                  uint32_t epoch) {
     __shared__ f4s img4[kPatImg / 4];
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -1468,7 +1567,10 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const uint4 near = threadIdx.x < t ? ((const uint4 *)rec)[t - 1 - threadIdx.x] : make_uint4(0, 0, 0, 0);
     const uint64_t total = stream_total(b);
     pat_stage(lw4, b, base, M);
-    if (total > cap) return;  // ONO_E_SIZE: nothing is written
+    if (total > cap) {  // ONO_E_SIZE: nothing is written
+        if (ASYNC && t == 0 && threadIdx.x == 0) raise_bad(badw, epoch);
+        return;
+    }
     if (threadIdx.x == 0) lqn = 0;
     {
         uint64_t part = 0;
@@ -1494,7 +1596,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
             E1 = E0 + me.y;
             if (t + 1 == T32) bad |= E1 > total;  // the offsets and lengths sum to at most total
         }
-        if (bad && threadIdx.x == 0) raise_bad(host_word + 2, epoch);
+        if (bad && threadIdx.x == 0) raise_bad(badw, epoch);
     }
     const uint32_t total32 = (uint32_t)total;
     const uint32_t ea = (uint32_t)min(E0, total);
@@ -1502,7 +1604,13 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const uint32_t ia = vec ? ea & ~3u : ea;
     const uint32_t n = min(eb - ia, (uint32_t)kPatImg + 1);
     const bool is_wide = eb > ea && n > (uint32_t)kPatImg;
-    if (threadIdx.x == 0) {
+    if constexpr (ASYNC) {
+        if (is_wide) {  // (uniform)
+            wide_tile(g, b, M, T, vec, t, E0, me.y, total, false, img4, lw4, lq, &lqn, nullptr, nullptr, 0,
+                      host_word, badw, epoch);
+            return;
+        }
+    } else if (threadIdx.x == 0) {
         wide[t] = is_wide;  // (every tile writes its flag: nothing to reset between lifts)
         if (is_wide) {
             if (direct) E[t] = E0;
@@ -1526,7 +1634,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         const uint32_t gi = cur + off;
         // (overflow-free: in a refuted stream cur + off may wrap; then gi < ea or it lies past eb)
         if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
-            raise_bad(host_word + 2, epoch);  // only a refuted stream
+            raise_bad(badw, epoch);  // only a refuted stream
             break;
         }
         float *d = img + (gi - ia);
@@ -1573,104 +1681,19 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     }
 }
 
-// The tiles pl_place flagged (ranges above kPatImg: sparse
-// streams), one workgroup each, grid-stride over the tiles: up to kPatPasses windows of kPatImg values built
-// in LDS one after another; wider still (few tiles hold all of g), the gaps and
-// the tail queued as zero chunks for sl_long's full grid and the values
-// scattered (long runs queued).
-constexpr int kPatPasses = 8;
+// The tiles pl_place flagged, one workgroup each, grid-stride over the tiles.
 __global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, size_t M, size_t T, int vec,
                                                  const uint64_t *E, const uint32_t *tsum, const uint32_t *wide,
-                                                 uint4 *queue,
-                                                 uint32_t *qcount, uint32_t qcap, uint64_t *host_word,
-                                                 uint32_t epoch) {
+                                                 uint4 *queue, uint32_t *qcount, uint32_t qcap, uint64_t *host_word,
+                                                 uint64_t *badw, uint32_t epoch) {
     __shared__ f4s img4[kPatImg / 4];
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
-    float *img = (float *)img4;
-    const uint16_t *lw = (const uint16_t *)lw4;
     const uint64_t total = stream_total(b);
     for (size_t t = blockIdx.x; t < T; t += gridDim.x) {
         if (!wide[t]) continue;  // (uniform)
-        const size_t base = t * kPatU;
-        const uint64_t E0 = E[t];
-        const uint64_t ea = min(E0, total);
-        uint64_t eb = t + 1 == T ? total : min(E0 + tsum[t], total);
-        eb = max(eb, ea);
-        __syncthreads();  // the previous tile's reads of the staged units
-        pat_stage(lw4, b, base, M);
-        __syncthreads();
-        const Units12 U = units12(lw4);
-        const uint32_t j0 = kPatPer * threadIdx.x;
-        uint32_t sum;
-        const uint32_t m = pat_mask(U, base + j0, M, sum);
-        uint32_t ec, es, tc, ts;
-        block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
-        const uint64_t ia = vec ? ea & ~3ull : ea, span = eb - ia;
-        const uint64_t npass = (span + kPatImg - 1) / kPatImg;
-        if (npass > (uint64_t)kPatPasses) {
-            uint64_t cur = E0 + es;
-            for (uint32_t mm = m; mm; mm &= mm - 1) {
-                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
-                const uint64_t gi = cur + off;
-                if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(host_word + 2, epoch); break; }
-                queue_span(cur, 0, off, 1u, queue, qcount, qcap, host_word, epoch, host_word + 3);
-                if (len <= (uint32_t)kShortP)
-                    for (uint32_t i = 0; i < len; i++) g[gi + i] = from_f16_sp(lw[k + 4 + i]);
-                else
-                    queue_span(gi, 8 + 2 * (base + k + 4), len, 0u, queue, qcount, qcap, host_word, epoch,
-                               host_word + 3);
-                cur = gi + len;
-            }
-            const bool holds_last = m != 0 && ec + (uint32_t)__builtin_popcount(m) == tc;
-            if (t + 1 == T && (holds_last || (tc == 0 && threadIdx.x == 0)))
-                queue_span(E0 + ts, 0, total > E0 + ts ? total - (E0 + ts) : 0, 1u, queue, qcount, qcap, host_word,
-                           epoch, host_word + 3);
-            continue;
-        }
-        const uint32_t skip = (uint32_t)(ea - ia);
-        for (uint32_t p = 0; p < (uint32_t)npass; p++) {
-            const uint32_t w0 = p * kPatImg, w1 = (uint32_t)min((uint64_t)w0 + kPatImg, span), wn = w1 - w0;
-            const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (uint32_t i = threadIdx.x; i < (wn + 3) / 4; i += kPatT) img4[i] = z;
-            if (threadIdx.x == 0) lqn = 0;
-            __syncthreads();
-            uint64_t cur = E0 + es;
-            for (uint32_t mm = m; mm; mm &= mm - 1) {
-                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
-                const uint64_t gi = cur + off;
-                cur = gi + len;
-                if (gi < ea || gi + len > eb || base + k + 4 + len > M) { raise_bad(host_word + 2, epoch); break; }
-                const uint32_t r0 = (uint32_t)(gi - ia), a = max(r0, w0), e = min(r0 + len, w1);
-                if (a >= e) continue;
-                const uint32_t c = e - a, u0 = k + 4 + (a - r0);
-                if (len <= (uint32_t)kShortP) {
-                    for (uint32_t i = 0; i < c; i++) img[a - w0 + i] = from_f16_sp(lw[u0 + i]);
-                } else {
-                    const uint32_t q = atomicAdd(&lqn, 1u);
-                    if (q < (uint32_t)kLQ) {
-                        lq[3 * q] = a - w0;
-                        lq[3 * q + 1] = (uint32_t)(8 + 2 * (base + u0));
-                        lq[3 * q + 2] = c;
-                    } else {
-                        for (uint32_t i = 0; i < c; i++)
-                            img[a - w0 + i] = from_f16_sp(((glb_u16 *)(b + 8 + 2 * (base + u0)))[i]);
-                    }
-                }
-            }
-            __syncthreads();
-            const uint32_t nl = min(lqn, (uint32_t)kLQ);
-            for (uint32_t q = 0; q < nl; q++) {
-                const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
-                glb_u16 *src = (glb_u16 *)(b + vp);
-                for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
-            }
-            __syncthreads();
-            float *dst = g + ia + w0;
-            for (uint32_t i = threadIdx.x; i < wn; i += kPatT)
-                if (w0 + i >= skip) dst[i] = img[i];
-            __syncthreads();
-        }
+        wide_tile(g, b, M, T, vec, t, E[t], tsum[t], total, true, img4, lw4, lq, &lqn, queue, qcount, qcap,
+                  host_word, badw, epoch);
     }
 }
 
@@ -1749,6 +1772,17 @@ struct LiftScratch {
     uint64_t *host_word = nullptr, *host_word_dev = nullptr;
 };
 LiftScratch g_lift[64];
+// The stream-ordered lift's scratch, per (device, stream): calls on one stream are ordered, calls on
+// different streams never share it.
+struct PatScratch {
+    size_t cap = 0;
+    uint32_t *prec = nullptr;  // 4 x cap tile records, then cap tile sums
+    uint64_t *pE = nullptr;    // cap + 1 element prefixes (pl_scan, wide tiles)
+    uint32_t *pwide = nullptr; // (unused flags: pl_place<true> places wide tiles itself)
+    uint64_t *aw = nullptr;    // 8 device words standing in for the blocking lift's host words
+    uint32_t epoch = 0;
+};
+std::map<std::pair<int, hipStream_t>, PatScratch> g_pat;
 std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
 std::atomic<size_t> g_lift_pattern_misses{0}; // lifts the pattern path handed to the walk path
 std::atomic<int> g_lift_mode{0};              // 0: pattern, then walk, then host; 1: walk, then host
@@ -1917,11 +1951,11 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
         word[1] = word[2] = word[3] = word[4] = 0;
         uint32_t *tsum = L.prec + 4 * L.pt_cap;
         hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, dbuf, M, L.prec, tsum, qcount, L.pwide,
-                           L.host_word_dev, epoch);
+                           L.host_word_dev, L.host_word_dev + 2, epoch);
         if (T > kPatDirect)
-            hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev, epoch);
-        hipLaunchKernelGGL(pl_place, dim3((unsigned)T), dim3(kPatT), 0, s, g, dbuf, M, T, cap, vec, L.pE, L.prec, tsum,
-                           L.pwide, L.host_word_dev, epoch);
+            hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev + 2, epoch);
+        hipLaunchKernelGGL(pl_place<false>, dim3((unsigned)T), dim3(kPatT), 0, s, g, dbuf, M, T, cap, vec, L.pE, L.prec, tsum,
+                           L.pwide, L.host_word_dev, L.host_word_dev + 2, epoch);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = host_wait(s, L.host_word + 5, L.host_word_dev + 5, epoch);
         if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
@@ -1929,7 +1963,8 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
         if (total > cap) return size_error(total);
         if (word[2] != epoch && word[4] == epoch) {  // tiles with wide ranges (a sparse stream)
             hipLaunchKernelGGL(pl_wide, dim3((unsigned)std::min<size_t>(T, 2048)), dim3(kPatT), 0, s, g, dbuf, M, T,
-                               vec, L.pE, tsum, L.pwide, L.queue, qcount, (uint32_t)qcap, L.host_word_dev, epoch);
+                               vec, L.pE, tsum, L.pwide, L.queue, qcount, (uint32_t)qcap, L.host_word_dev,
+                               L.host_word_dev + 2, epoch);
             e = hipGetLastError();
             if (e == hipSuccess) e = host_wait(s, L.host_word + 5, L.host_word_dev + 5, epoch);
             if (e != hipSuccess) return hip_error(e, "sparse lift", __FILE__, __LINE__);
@@ -2169,6 +2204,56 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
     ONO_HIP(hipGetLastError());
     ONO_HIP(hipStreamSynchronize(s));
     *t_out = *(volatile float *)T.t_host;
+    return ONO_OK;
+}
+
+int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
+                              uint64_t *ticket, void *stream) {
+    if (!status || !ticket || (!buf_dev && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
+    if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
+    PatScratch &P = g_pat[{dev, s}];
+    if (!P.aw) {
+        ONO_HIP(hipMalloc((void **)&P.aw, 8 * sizeof(uint64_t)));
+        ONO_HIP(hipMemsetAsync(P.aw, 0, 8 * sizeof(uint64_t), s));
+    }
+    if (++P.epoch == 0) P.epoch = 1;
+    const uint32_t epoch = P.epoch;
+    *ticket = epoch;
+    const size_t M = (nbytes - 8) / 2;
+    // the pattern path's domain (as lift_device's); any other stream is refused at once
+    if (M == 0 || (nbytes & 1) || nbytes >= 0xFFFFFFF0ull || cap >= 0xFFFFFFFFull || ((uintptr_t)buf_dev & 1)) {
+        hipLaunchKernelGGL(sp_signal, dim3(1), dim3(64), 0, s, status, epoch);
+        ONO_HIP(hipGetLastError());
+        return ONO_OK;
+    }
+    const size_t T = (M + kPatU - 1) / kPatU;
+    if (T > P.cap) {  // (hipFree waits for the work that still uses the old arrays)
+        (void)hipFree(P.prec);
+        (void)hipFree(P.pE);
+        (void)hipFree(P.pwide);
+        P.prec = nullptr;
+        P.pE = nullptr;
+        P.pwide = nullptr;
+        P.cap = 0;
+        ONO_HIP(hipMalloc((void **)&P.prec, 5 * T * sizeof(uint32_t)));
+        ONO_HIP(hipMalloc((void **)&P.pE, (T + 1) * sizeof(uint64_t)));
+        ONO_HIP(hipMalloc((void **)&P.pwide, T * sizeof(uint32_t)));
+        P.cap = T;
+    }
+    uint32_t *tsum = P.prec + 4 * P.cap, *qcount = (uint32_t *)(P.aw + 6);
+    const int vec = ((uintptr_t)g & 15) == 0;
+    hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, buf_dev, M, P.prec, tsum, qcount, P.pwide, P.aw,
+                       status, epoch);
+    if (T > kPatDirect)
+        hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, buf_dev, P.prec, T, P.pE, status, epoch);
+    hipLaunchKernelGGL(pl_place<true>, dim3((unsigned)T), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.pE, P.prec,
+                       tsum, P.pwide, P.aw, status, epoch);
+    ONO_HIP(hipGetLastError());
     return ONO_OK;
 }
 

@@ -117,6 +117,19 @@ def grad_lift_dev(buf: torch.Tensor, cap: int | None = None, stream=None) -> tor
     return out[: ln.value]
 
 
+def grad_lift_dev_async(buf: torch.Tensor, out: torch.Tensor, status: torch.Tensor, stream=None) -> int:
+    """Stream-ordered grad_lift (ono_sparse_lift_dev_async) of wire bytes in HBM
+    into out[0, total): returns the ticket; once the stream has passed the call,
+    status (one int64 on the device) equals it iff the lift was refused (then
+    use grad_lift_dev)."""
+    assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+    assert status.is_cuda and status.dtype == torch.int64 and out.is_cuda and out.dtype == torch.float32
+    ticket = C.c_uint64(0)
+    call("ono_sparse_lift_dev_async", kernels.f32_ptr(out), out.numel(), buf.data_ptr(), buf.numel(),
+         status.data_ptr(), C.byref(ticket), kernels.stream_handle(stream))
+    return ticket.value
+
+
 def mask_sent(g: torch.Tensor, threshold: float, stream=None) -> torch.Tensor:
     """Scatter side: the values just sent (|g| >= t) leave the residual."""
     call("ono_sparse_mask", kernels.f32_ptr(g), g.numel(), float(threshold), 1, kernels.stream_handle(stream))

@@ -190,3 +190,108 @@ def test_pattern_path_stream_at_a_2_byte_boundary(shift):
     assert lift_into(view, out, total) == total
     assert counters() == before
     assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+# ---- the stream-ordered lift (ono_sparse_lift_dev_async)
+
+def lift_async(b: bytes, cap: int, status: torch.Tensor, fill: float = 6.0):
+    buf = to_dev(b)
+    out = torch.full((cap + 8,), fill, dtype=torch.float32, device="cuda")
+    ticket = SP.grad_lift_dev_async(buf, out[:cap], status)
+    torch.cuda.synchronize()
+    return out, ticket, int(status.item()) == ticket
+
+
+@pytest.mark.parametrize("n,r", [(1 << 24, 0.9), ((1 << 20) + 5, 0.5), (4099, 0.1)])
+def test_async_lift_of_drop_output(n, r):
+    """Stream-ordered, drop output: not refused, bit-exact, g[total, cap) untouched."""
+    g = O.synth(n, SEED + 61, 6)
+    t = max(float(np.quantile(np.abs(g), r)), 6.103515625e-05)
+    b = bytes(SP.grad_drop_dev(dev(g), t).cpu().numpy())
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out, ticket, refused = lift_async(b, n + 5, status)
+    assert ticket != 0 and not refused
+    assert_bitexact(out[:n].cpu().numpy(), O.grad_lift(b, cap=n))
+    assert torch.all(out[n:] == 6.0)
+
+
+@pytest.mark.parametrize("nrec,off_range,len_range", [
+    (2000, (50, 200), (1, 3)),          # wide tile ranges: placed in windows by pl_place itself
+    (1200, (60000, 65535), (1, 2)),     # very wide: every window in turn (no queue in this form)
+    (3000, (1, 40), (33, 700)),         # long runs
+    (3_600_000, (1, 9), (1, 2)),        # more than 4096 tiles: pl_scan
+])
+def test_async_lift_range_shapes(nrec, off_range, len_range):
+    rng = np.random.default_rng(nrec + 17)
+    b, total = pattern_stream(rng, nrec, off_range, len_range)
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out, ticket, refused = lift_async(b, total, status)
+    assert not refused
+    assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+@pytest.mark.parametrize("case", ["zero_length_run", "gap_2_16", "odd_tail", "empty", "total_over_cap",
+                                  "truncated"])
+def test_async_lift_refuses_what_the_pattern_cannot_take(case):
+    """Refused calls say so through the status word (the blocking lift then parses them or reports the
+    reference's error); total > cap writes nothing."""
+    rng = np.random.default_rng(5)
+    b, total = pattern_stream(rng, 3000, (1, 20), (1, 6))
+    b = bytearray(b)
+    rec = header_positions(bytes(b), 1001)[1000]
+    ln = int.from_bytes(b[rec + 4:rec + 8], "little")
+    cap = total
+    if case == "zero_length_run":
+        b[rec + 8 + 2 * ln:rec + 8 + 2 * ln] = np.array([3, 0], np.uint32).tobytes()
+        total += 3
+        cap = total
+    elif case == "gap_2_16":
+        b[rec:rec + 4] = np.uint32(int.from_bytes(b[rec:rec + 4], "little") + 70000).tobytes()
+        total += 70000
+        cap = total
+    elif case == "odd_tail":
+        b += b"\x01"
+    elif case == "empty":
+        b = bytearray(np.uint64(17).tobytes())
+        total = cap = 17
+    elif case == "total_over_cap":
+        cap = total - 1
+    elif case == "truncated":
+        last = header_positions(bytes(b), 3000)[-1]
+        b[last + 4:last + 8] = np.uint32(int.from_bytes(b[last + 4:last + 8], "little") + 2).tobytes()
+    b[:8] = np.uint64(total).tobytes()
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out, ticket, refused = lift_async(bytes(b), cap, status, fill=2.0)
+    assert refused
+    if case == "total_over_cap":
+        assert torch.all(out == 2.0)
+
+
+def test_async_lifts_back_to_back_on_one_stream():
+    """Several stream-ordered lifts queued without a wait, one status word per call: each call's ticket
+    is new, the refused one (a zero-length run) is the only one flagged, the others exact."""
+    rng = np.random.default_rng(9)
+    streams, outs, statuses, tickets = [], [], [], []
+    for i in range(4):
+        b, total = pattern_stream(rng, 5000 + 1000 * i, (1, 15), (1, 4))
+        if i == 2:
+            bb = bytearray(b)
+            rec = header_positions(b, 11)[10]
+            ln = int.from_bytes(bb[rec + 4:rec + 8], "little")
+            bb[rec + 8 + 2 * ln:rec + 8 + 2 * ln] = np.array([1, 0], np.uint32).tobytes()
+            total += 1
+            bb[:8] = np.uint64(total).tobytes()
+            b = bytes(bb)
+        buf = to_dev(b)
+        out = torch.empty(total, dtype=torch.float32, device="cuda")
+        st = torch.zeros(1, dtype=torch.int64, device="cuda")
+        tickets.append(SP.grad_lift_dev_async(buf, out, st))
+        streams.append((b, buf, total))
+        outs.append(out)
+        statuses.append(st)
+    torch.cuda.synchronize()
+    assert len(set(tickets)) == 4
+    for i, ((b, _, total), out, st, tk) in enumerate(zip(streams, outs, statuses, tickets)):
+        assert (int(st.item()) == tk) == (i == 2)
+        if i != 2:
+            assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))

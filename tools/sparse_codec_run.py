@@ -68,4 +68,15 @@ if KL:
           f"{ev0.elapsed_time(ev1) / KL * 1e3:.1f} us between events")
     ref = ono_amd.sparse.grad_lift(bytes(wire.cpu().numpy()), n)
     print("lift_dev equals the host-stream lift:", bool(torch.equal(out.view(torch.int32), ref.view(torch.int32))))
+if KL:  # stream-ordered lifts back to back (ono_sparse_lift_dev_async): the device's own time per lift
+    st = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        ono_amd.sparse.grad_lift_dev_async(wire, out, st)
+    torch.cuda.synchronize()
+    ev0.record()
+    tks = [ono_amd.sparse.grad_lift_dev_async(wire, out, st) for _ in range(KL)]
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"lift_dev {ev0.elapsed_time(ev1) / KL * 1e3:.1f} us per stream-ordered lift, back to back "
+          f"(refused: {int(st.item()) in tks})")
 print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
