@@ -295,3 +295,24 @@ def test_async_lifts_back_to_back_on_one_stream():
         assert (int(st.item()) == tk) == (i == 2)
         if i != 2:
             assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+def test_async_lifts_on_two_streams_concurrently():
+    """Per-stream scratch: stream-ordered lifts queued on two streams at once (no wait between them) are
+    each exact and not refused."""
+    rng = np.random.default_rng(21)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    prep = []
+    for k in range(6):
+        b, total = pattern_stream(rng, 20000 + 3000 * k, (1, 15), (1, 4))
+        prep.append((b, total, to_dev(b), torch.empty(total, dtype=torch.float32, device="cuda"),
+                     torch.zeros(1, dtype=torch.int64, device="cuda")))
+    torch.cuda.synchronize()  # inputs in place; then every lift queued with no wait in between
+    jobs = []
+    for k, (b, total, buf, out, st) in enumerate(prep):
+        s = s1 if k % 2 == 0 else s2
+        jobs.append((b, total, out, st, SP.grad_lift_dev_async(buf, out, st, s)))
+    torch.cuda.synchronize()
+    for b, total, out, st, tk in jobs:
+        assert int(st.item()) != tk
+        assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
