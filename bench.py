@@ -329,6 +329,47 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
             **out}
 
 
+def copy_ceiling(torch, steps: int, warmup: int) -> dict:
+    """SURVEY §8(d) "also record a measured copy-kernel ceiling": the runtime's
+    own device-to-device copy (torch `copy_` -> the HIP blit kernel, 1 read +
+    1 write, 8 B/elem) and fill (`zero_` -> memset, 4 B/elem) at the headline
+    bucket (256 MiB) and the config-2 size (64 MiB), timed like the path's
+    kernels (one event pair around K back-to-back launches over rotating sets
+    larger than the Infinity Cache).  Not our code: the yardstick our 1R2W /
+    kR1W streams are read against (`frac_of_copy_ceiling` in the roofline)."""
+    out = {}
+    stream = torch.cuda.current_stream()
+    for mib in (256, 64):
+        n = mib << 18
+        nsets = max(2, 1536 // (2 * mib) + 1)
+        sets = [(torch.empty(n, dtype=torch.float32, device="cuda"),
+                 torch.empty(n, dtype=torch.float32, device="cuda")) for _ in range(nsets)]
+        for src, dst in sets:
+            src.fill_(1.0)
+            dst.zero_()
+        for name, per, fn in (("copy", 8, lambda st: st[1].copy_(st[0])), ("fill", 4, lambda st: st[1].zero_())):
+            warm = max(warmup, nsets)
+            for i in range(warm):
+                fn(sets[i % nsets])
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record(stream)
+            for i in range(steps):
+                fn(sets[(warm + i) % nsets])
+            b.record(stream)
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) / steps * 1e3
+            gbs = per * n / (us * 1e-6) / 1e9
+            out[f"{name}_{mib}MiB"] = {"bytes_per_launch": per * n, "us_per_launch": round(us, 2),
+                                       "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                                       "rotating_sets": nsets}
+        del sets
+        torch.cuda.empty_cache()
+    return {"workload": "HIP runtime D2D copy (torch copy_) and fill (zero_), f32, device-resident",
+            "hbm_peak_gbs": HBM_PEAK_GBS,
+            "timing": "one HIP event pair around K back-to-back launches over rotating sets", **out}
+
+
 def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
     """SURVEY §8(f) rows 1, 2 and 4 at the measurement bar: the remaining
     kernels of the path, each timed as one HIP event pair around K
@@ -958,6 +999,11 @@ def main(argv=None) -> int:
             leg("local_reduce", lambda: local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
             leg("path_kernels", lambda: path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
             leg("sparse_codec", lambda: sparse_codec(torch, ono_amd))
+            leg("copy_ceiling", lambda: copy_ceiling(torch, max(args.steps, 10), max(args.warmup, 2)))
+            cc = extra.get("copy_ceiling", {}).get("copy_256MiB")
+            if isinstance(cc, dict) and extra["roofline"].get("achieved"):
+                extra["roofline"]["copy_ceiling_gbs"] = cc["achieved_gbs"]
+                extra["roofline"]["frac_of_copy_ceiling"] = round(extra["roofline"]["achieved"] / cc["achieved_gbs"], 4)
         if not args.no_cpu_baseline:
             leg("cpu_baseline", lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
         lr = extra.get("local_reduce", {})
