@@ -83,6 +83,15 @@ int ono_acc_f32(float *acc, const float *in, size_t n, void *stream);
 int ono_scale_zero_f32(float *dst, const float *src, size_t n, float divisor, float *zero,
                        void *stream);
 
+/* dst[i] = src[i] and dst[i] = value: the library's own pure streams (the
+ * kernels above minus the arithmetic).  The owner's `grad[own] =
+ * residual[own]` copy and the residual reset of the gather (worker_ring.rs:
+ * 166-171, 191-193) when they run alone, the plan interpreter's device copies
+ * and zero fills, and the measured copy ceiling the path's kernels are read
+ * against (bench.py copy_ceiling).  dst and src must not overlap.           */
+int ono_copy_f32(float *dst, const float *src, size_t n, void *stream);
+int ono_fill_f32(float *dst, float value, size_t n, void *stream);
+
 /* f16 wire codec (crate half 2.7.1: RNE, overflow -> inf, subnormals kept,
  * NaN keeps payload + quiet bit).  compressor.rs:116 / handles/worker.rs:94  */
 int ono_f16_encode(uint16_t *out, const float *in, size_t n, void *stream);
@@ -302,17 +311,29 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
 /* A ring with no collective library at all (ONO_ALGO_XGMI only): create,
  * export this rank's handle, pass every rank's handle (nranks x
  * ONO_XGMI_HANDLE_BYTES, rank order) to connect.  The handles travel out of
- * band, like the RCCL id.  A handle is the region's IPC handle (64 bytes), the
- * region's random 64-bit ring id and its size; connect maps every peer region,
- * checks that every page of each mapping shows that peer's ring id (a stale
- * import -> ONO_E_IO), and returns once every rank has connected (a device
- * barrier).  Destroy is collective: each rank marks every peer region it is
- * done with, closes its imports, and frees its own region once all peers have
- * marked it (or the timeout passed).                                          */
-#define ONO_XGMI_HANDLE_BYTES 128 /* hipIpcMemHandle_t + ring id + region bytes + zero */
+ * band, like the RCCL id.  A handle is [IPC handle, 64 B][u64 ring id][u64
+ * layout bytes][u64 region uid][u64 region alloc bytes], zero-padded to
+ * ONO_XGMI_HANDLE_BYTES; connect maps every peer region, checks that every
+ * page of each mapping shows that peer's ring id (a stale import -> ONO_E_IO),
+ * and returns once every rank has connected (a device barrier).  Destroy is
+ * collective: each rank marks every peer region it is done with; a region goes
+ * back to the process's pool once all peers have marked it, and is
+ * quarantined (never reused) when the timeout passed or the ring was aborted.
+ * RETENTION: pooled regions and peer imports are kept for the life of the
+ * process (a later ring reuses them; re-importing a freed region's successor
+ * handed out partly stale mappings on this ROCm) until ono_xgmi_pool_release. */
+#define ONO_XGMI_HANDLE_BYTES 128
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
 int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
+/* Frees every idle pooled exchange region and closes every peer import of
+ * this process; ONO_E_ARG while an xGMI ring of the process is alive.  Call it
+ * on every rank once all rings are destroyed (an import pins the exporter's
+ * HBM until the importer closes it).  Quarantined regions stay.  Rings created
+ * afterwards export and import fresh regions (verified at connect as always). */
+int ono_xgmi_pool_release(size_t *freed_bytes, size_t *closed_imports);
+/* regions pooled (and their bytes, of which quarantined), peer imports held */
+int ono_xgmi_pool_stats(size_t *regions, size_t *region_bytes, size_t *quarantined, size_t *imports);
 /* How long an xGMI barrier waits for a peer (seconds, > 0) before the round
  * fails with ONO_E_IO; 0 = env ONO_XGMI_TIMEOUT_S, else 600 s.  The reference
  * ring blocks while a peer is slow: set this above the longest time ranks may
@@ -446,7 +467,8 @@ int ono_barrier_acquire(ono_barrier *b);
 /* ===================================================================== */
 /* Multi-GPU parameter-server mode (BASELINE config 5): the sharded        */
 /* synchronizer as reduce-scatter + fused (÷nworkers + optimizer) + all-gather */
-/* over the ring's communicator.  Rank r owns shard r of split_chunks(n, nranks). */
+/* over the ring's communicator.  Shards of ceil(n / nranks) parameters, the   */
+/* last one zero-padded; rank r owns shard r (ono_plan_ps_step).            */
 /* ===================================================================== */
 typedef struct ono_ps ono_ps;
 int ono_ps_create(ono_ps **out, ono_ring *ring, const float *init_params_host, size_t nparams,

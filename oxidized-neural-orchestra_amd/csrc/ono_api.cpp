@@ -71,6 +71,16 @@ int ono_scale_zero_f32(float *dst, const float *src, size_t n, float divisor, fl
     ONO_LAUNCH(launch_scale_zero(dst, src, n, divisor, zero, S(stream)));
 }
 
+int ono_copy_f32(float *dst, const float *src, size_t n, void *stream) {
+    if (n && (!dst || !src)) return set_error(ONO_E_ARG, "NULL pointer");
+    ONO_LAUNCH(launch_copy<float>(dst, src, n, S(stream)));
+}
+
+int ono_fill_f32(float *dst, float value, size_t n, void *stream) {
+    if (n && !dst) return set_error(ONO_E_ARG, "NULL pointer");
+    ONO_LAUNCH(launch_fill<float>(dst, value, n, S(stream)));
+}
+
 int ono_f16_encode(uint16_t *out, const float *in, size_t n, void *stream) {
     if (n && (!out || !in)) return set_error(ONO_E_ARG, "NULL pointer");
     ONO_LAUNCH(launch_encode<uint16_t>(out, in, n, S(stream)));

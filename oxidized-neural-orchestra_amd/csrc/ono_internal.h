@@ -64,6 +64,9 @@ hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divis
                              hipStream_t s);
 hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
                         hipStream_t s);
+// the library's own pure streams (T = float or uint16_t): dst = src, dst = value
+template <class T> hipError_t launch_copy(T *dst, const T *src, size_t n, hipStream_t s);
+template <class T> hipError_t launch_fill(T *dst, T value, size_t n, hipStream_t s);
 
 // wire-templated hop kernels: W = uint16_t (f16 wire) or float (f32 wire)
 template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, hipStream_t s);

@@ -457,6 +457,34 @@ template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
     }
 };
 
+// dst = src (1R1W) and dst = value (0R1W): the library's own pure streams on
+// the same skeleton — the copy ceiling the path's kernels are read against
+// (bench.py copy_ceiling) and the plan interpreter's device copies / zero
+// fills (ONO_PLAN_COPY / ONO_PLAN_MEMSET), in place of the runtime's blit
+// kernels.  Read-once source: nt loads; write-once output: nt stores.
+template <class T> struct CopyOp {
+    typedef typename Wire<T>::V V;
+    T *dst;
+    const T *src;
+    typedef V R;
+    __device__ __forceinline__ void scalar(size_t i) const { dst[i] = src[i]; }
+    __device__ __forceinline__ R load(size_t i) const { return ldn((const V *)(src + i)); }
+    __device__ __forceinline__ void store(size_t i, R x) const { st_nt((V *)(dst + i), x); }
+};
+template <class T> struct FillOp {
+    typedef typename Wire<T>::V V;
+    T *dst;
+    T value;
+    typedef int R;
+    __device__ __forceinline__ void scalar(size_t i) const { dst[i] = value; }
+    __device__ __forceinline__ R load(size_t) const { return 0; }
+    __device__ __forceinline__ void store(size_t i, R) const {
+        V x;
+        x.x = value; x.y = value; x.z = value; x.w = value;
+        st_nt((V *)(dst + i), x);
+    }
+};
+
 template <class W> struct EncodeOp {
     typedef typename Wire<W>::V WV;
     W *out;
@@ -861,6 +889,17 @@ hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divis
     default: return launch_ew(ScaleZeroOp<SCALE_DIV>{dst, src, zero, sc.v}, n, ph, s);
     }
 }
+
+template <class T> hipError_t launch_copy(T *dst, const T *src, size_t n, hipStream_t s) {
+    return launch_ew(CopyOp<T>{dst, src}, n, {wph(dst), wph(src)}, s);
+}
+template <class T> hipError_t launch_fill(T *dst, T value, size_t n, hipStream_t s) {
+    return launch_ew(FillOp<T>{dst, value}, n, {wph(dst)}, s);
+}
+template hipError_t launch_copy<float>(float *, const float *, size_t, hipStream_t);
+template hipError_t launch_copy<uint16_t>(uint16_t *, const uint16_t *, size_t, hipStream_t);
+template hipError_t launch_fill<float>(float *, float, size_t, hipStream_t);
+template hipError_t launch_fill<uint16_t>(uint16_t *, uint16_t, size_t, hipStream_t);
 
 hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
                         hipStream_t s) {

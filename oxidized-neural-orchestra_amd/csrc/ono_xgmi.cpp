@@ -28,8 +28,9 @@
 // links at once.  No stream synchronisation or host round trip per round: the
 // barriers are device-side flag exchanges with a timeout.
 //
-// Connect is verified, teardown is ordered, and no exchange region is ever
-// freed or unmapped while the process lives (round 3).  Every region carries a
+// Connect is verified, teardown is ordered, and no exchange region is freed
+// or unmapped while a ring of the process is alive (round 3; round 4 adds the
+// explicit ono_xgmi_pool_release for when none is).  Every region carries a
 // random 64-bit ring id, stamped at the start of every 4 KiB page before its
 // handle leaves the process; the handle blob (ONO_XGMI_HANDLE_BYTES) holds the
 // IPC handle, the ring id, the layout's size and a per-region uid.  An
@@ -46,7 +47,13 @@
 // destroyed ring's region (flags reset, re-stamped) serves the next ring that
 // fits in it, a new one is allocated only when none fits, and importers keep
 // every peer region they mapped (keyed by its uid) for reuse instead of
-// closing it — no handle, virtual address or mapping is ever recycled.
+// closing it — no handle, virtual address or mapping is recycled while rings
+// come and go.  A region whose teardown ended without every peer's marker
+// (timeout, abort) is quarantined: never reset for another ring, never freed.
+// ono_xgmi_pool_release frees the idle regions and closes every import once no
+// ring of the process is alive (collectively, on every rank, so that the
+// peers' imports stop pinning the freed HBM); a ring created after it exports
+// and imports fresh regions, which the page check verifies as always.
 // Destroy stays collective: each rank, once its own work is done, stores the
 // owner's id into a teardown slot of every peer region it mapped; an owner
 // returns its region to the pool only when every peer's marker is there (or
@@ -81,7 +88,8 @@ constexpr size_t kFlagBytes = 4096;  // flag page: barrier slots (n x u64) at of
 constexpr size_t kDoneOff = 1024;    //   teardown markers (n x u64),
 constexpr size_t kIdOff = 2048;      //   the region's ring id
 constexpr size_t kPage = 4096;       // every later page starts with the id until the first round
-// the handle blob: [hipIpcMemHandle_t][u64 ring id][u64 region bytes][zero]
+// the handle blob: [hipIpcMemHandle_t (64 B)][u64 ring id][u64 layout bytes][u64 region uid][u64 region
+// alloc bytes][zero to ONO_XGMI_HANDLE_BYTES]
 constexpr size_t kBlobId = sizeof(hipIpcMemHandle_t), kBlobBytes = kBlobId + 8, kBlobUid = kBlobBytes + 8,
                  kBlobAlloc = kBlobUid + 8;
 static_assert(kBlobAlloc + 8 <= ONO_XGMI_HANDLE_BYTES, "handle blob layout");
@@ -95,6 +103,10 @@ struct PooledRegion {
     uint64_t uid;
     hipIpcMemHandle_t handle;
     bool busy;
+    // a ring's teardown ended without every peer's done marker (timeout, abort,
+    // a failed signal): a slow peer may still write into the region, so it is
+    // never reset for another ring and never freed by ono_xgmi_pool_release
+    bool quarantined;
 };
 struct MappedPeer {
     int device;
@@ -105,6 +117,7 @@ struct MappedPeer {
 std::mutex g_pool_mu;
 std::vector<PooledRegion> g_regions;
 std::vector<MappedPeer> g_mapped;
+int g_live = 0;  // xGMI states (rings holding a region) alive in this process
 
 struct XgmiState {
     uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
@@ -125,6 +138,7 @@ struct XgmiState {
     size_t alloc = 0;                 // the pooled region's size (>= bytes)
     uint64_t uid = 0;                 // the pooled region's uid
     hipIpcMemHandle_t handle{};       // its IPC handle
+    bool exported = false;            // the handle left this process (a peer may have mapped the region)
     std::vector<uint64_t> peer_id;    // every peer region's id, from its blob
 };
 
@@ -184,6 +198,7 @@ int xgmi_alloc(ono_ring *r) {
             best = &g_regions.back();
         }
         best->busy = true;
+        g_live++;
         x->xbuf = best->ptr;
         x->alloc = best->bytes;
         x->uid = best->uid;
@@ -343,6 +358,7 @@ int xgmi_connect_over_rccl(ono_ring *r, hipStream_t s) {
     const size_t H = ONO_XGMI_HANDLE_BYTES;
     std::vector<uint8_t> all((size_t)r->n * H);
     make_blob(r->xgmi, all.data() + (size_t)r->pos * H);
+    r->xgmi->exported = true;
     uint8_t *d = nullptr;
     ONO_HIP(hipMalloc((void **)&d, all.size()));
     hipError_t e = hipMemcpyAsync(d + (size_t)r->pos * H, all.data() + (size_t)r->pos * H, H, hipMemcpyHostToDevice, s);
@@ -646,6 +662,9 @@ void xgmi_free(ono_ring *r) {
         ok = ok && launch_xgmi_signal(sig, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
         wait &= ok;
     }
+    // a region that never left this process is nobody else's; one whose
+    // peers all marked it is free again; anything else is quarantined
+    bool released = !x->exported;
     if (wait) {  // every peer's marker in this region (uncached: a D2H copy reads what landed)
         const auto t0 = std::chrono::steady_clock::now();
         std::vector<uint64_t> done(r->n);
@@ -655,16 +674,21 @@ void xgmi_free(ono_ring *r) {
                 break;
             bool all = true;
             for (int q = 0; q < r->n; q++) all &= q == r->pos || done[q] == x->id;
+            if (all) released = true;
             if (all || r->aborted.load()) break;
             if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > x->timeout_s) break;
             std::this_thread::sleep_for(std::chrono::microseconds(200));
         }
     }
     for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
-    {  // the region goes back to the pool; peer mappings stay in the process's table
+    {  // the region goes back to the pool (or into quarantine); peer mappings stay in the process's table
         std::lock_guard<std::mutex> lk(g_pool_mu);
         for (auto &pr : g_regions)
-            if (pr.ptr == x->xbuf) pr.busy = false;
+            if (pr.ptr == x->xbuf) {
+                if (released) pr.busy = false;
+                else pr.quarantined = true;  // stays busy: never handed to another ring
+            }
+        g_live--;
     }
     if (x->err) (void)hipHostFree(x->err);
     delete x;
@@ -706,6 +730,55 @@ int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
     int rc = xgmi_alloc(r);
     if (rc) return rc;
     make_blob(r->xgmi, handle);
+    r->xgmi->exported = true;
+    return ONO_OK;
+}
+
+int ono_xgmi_pool_release(size_t *freed_bytes, size_t *closed_imports) {
+    if (freed_bytes) *freed_bytes = 0;
+    if (closed_imports) *closed_imports = 0;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_live > 0) return set_error(ONO_E_ARG, "%d xGMI ring(s) of this process are alive", g_live);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    size_t freed = 0, closed = 0;
+    int rc = ONO_OK;
+    std::vector<PooledRegion> keep;
+    for (auto &pr : g_regions) {
+        if (pr.busy) {  // quarantined: a peer's teardown never confirmed
+            keep.push_back(pr);
+            continue;
+        }
+        hipError_t e = hipSetDevice(pr.device);
+        if (e == hipSuccess) e = hipFree(pr.ptr);
+        if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "hipFree (pooled exchange region)", __FILE__, __LINE__);
+        freed += pr.bytes;
+    }
+    g_regions.swap(keep);
+    for (auto &m : g_mapped) {
+        hipError_t e = hipSetDevice(m.device);
+        if (e == hipSuccess) e = hipIpcCloseMemHandle(m.ptr);
+        if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "hipIpcCloseMemHandle (peer region)", __FILE__, __LINE__);
+        closed++;
+    }
+    g_mapped.clear();
+    (void)hipSetDevice(cur);
+    if (freed_bytes) *freed_bytes = freed;
+    if (closed_imports) *closed_imports = closed;
+    return rc;
+}
+
+int ono_xgmi_pool_stats(size_t *regions, size_t *region_bytes, size_t *quarantined, size_t *imports) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    size_t b = 0, q = 0;
+    for (const auto &pr : g_regions) {
+        b += pr.bytes;
+        q += pr.quarantined ? 1 : 0;
+    }
+    if (regions) *regions = g_regions.size();
+    if (region_bytes) *region_bytes = b;
+    if (quarantined) *quarantined = q;
+    if (imports) *imports = g_mapped.size();
     return ONO_OK;
 }
 

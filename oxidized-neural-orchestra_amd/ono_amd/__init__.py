@@ -14,7 +14,8 @@ import torch  # noqa: F401  (must precede the library load; see above)
 from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, IoError, OnoError,
                    RcclError, SizeMismatch, header_functions, lib, worker_event_check)
 from . import kernels, plan, sparse
-from .ring import DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id
+from .ring import (DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id,
+                   xgmi_pool_release, xgmi_pool_stats)
 from .store import (Adam, AddOptimizer, BarrierSync, BlockingStore, DynBarrier, GradientDescent,
                     GradientDescentWithMomentum, NoBlockingSync, WildStore, shard_size_for)
 from .ps import ShardedParamServer
@@ -26,5 +27,5 @@ __all__ = [
     "SizeMismatch", "header_functions", "lib", "kernels", "DeviceOptimizer", "ParamManager", "WorkerRingManager",
     "local_ring_pull_grads", "unique_id", "Adam", "AddOptimizer", "BarrierSync", "BlockingStore",
     "DynBarrier", "GradientDescent", "GradientDescentWithMomentum", "NoBlockingSync", "WildStore",
-    "shard_size_for", "ShardedParamServer", "worker_event_check",
+    "shard_size_for", "ShardedParamServer", "worker_event_check", "xgmi_pool_release", "xgmi_pool_stats",
 ]

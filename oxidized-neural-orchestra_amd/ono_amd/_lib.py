@@ -97,6 +97,8 @@ _SIGS = {
     "ono_sum_scale_f32": (_i, [_fp, C.POINTER(C.c_void_p), _i, _sz, C.c_float, _vp]),
     "ono_acc_f32": (_i, [_fp, _fp, _sz, _vp]),
     "ono_scale_zero_f32": (_i, [_fp, _fp, _sz, C.c_float, _fp, _vp]),
+    "ono_copy_f32": (_i, [_fp, _fp, _sz, _vp]),
+    "ono_fill_f32": (_i, [_fp, C.c_float, _sz, _vp]),
     "ono_f16_encode": (_i, [_vp, _fp, _sz, _vp]),
     "ono_f16_decode": (_i, [_fp, _vp, _sz, _vp]),
     "ono_f16_encode_zero": (_i, [_vp, _fp, _sz, _vp]),
@@ -127,6 +129,8 @@ _SIGS = {
     "ono_ring_xgmi_handle": (_i, [_vp, C.c_char_p]),
     "ono_ring_xgmi_connect": (_i, [_vp, C.c_char_p]),
     "ono_ring_set_xgmi_timeout": (_i, [_vp, C.c_double]),
+    "ono_xgmi_pool_release": (_i, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "ono_xgmi_pool_stats": (_i, [C.POINTER(C.c_size_t)] * 4),
     "ono_ring_check": (_i, [_vp]),
     "ono_ring_destroy": (_i, [_vp]),
     "ono_ring_set_pipeline": (_i, [_vp, _i]),

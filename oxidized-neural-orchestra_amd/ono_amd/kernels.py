@@ -84,6 +84,20 @@ def scale_zero(dst: torch.Tensor, src: torch.Tensor, divisor: float, zero: torch
     return dst
 
 
+def copy(dst: torch.Tensor, src: torch.Tensor, stream=None) -> torch.Tensor:
+    """dst = src — the library's own 1R1W stream (no overlap)."""
+    if src.numel() != dst.numel():
+        raise ValueError("length mismatch")
+    call("ono_copy_f32", f32_ptr(dst), f32_ptr(src), dst.numel(), stream_handle(stream))
+    return dst
+
+
+def fill(dst: torch.Tensor, value: float = 0.0, stream=None) -> torch.Tensor:
+    """dst[:] = value — the library's own write-only stream."""
+    call("ono_fill_f32", f32_ptr(dst), float(value), dst.numel(), stream_handle(stream))
+    return dst
+
+
 def f16_encode(out: torch.Tensor, x: torch.Tensor, stream=None) -> torch.Tensor:
     call("ono_f16_encode", u16_ptr(out), f32_ptr(x), x.numel(), stream_handle(stream))
     return out

@@ -273,6 +273,21 @@ class WorkerRingManager:
             pass
 
 
+def xgmi_pool_release() -> dict:
+    """Free this process's idle xGMI exchange regions and close its peer imports
+    (ono_xgmi_pool_release): only when no xGMI ring of the process is alive;
+    call it on every rank."""
+    freed, closed = C.c_size_t(0), C.c_size_t(0)
+    call("ono_xgmi_pool_release", C.byref(freed), C.byref(closed))
+    return {"freed_bytes": freed.value, "closed_imports": closed.value}
+
+
+def xgmi_pool_stats() -> dict:
+    v = [C.c_size_t(0) for _ in range(4)]
+    call("ono_xgmi_pool_stats", *[C.byref(x) for x in v])
+    return dict(zip(("regions", "region_bytes", "quarantined", "imports"), (x.value for x in v)))
+
+
 def local_ring_pull_grads(residuals: list[torch.Tensor], grads: list[torch.Tensor], wire: str = "f16",
                           stream=None, algo: str = "hops") -> None:
     """Every rank of one pull_grads round, co-resident on one device (the

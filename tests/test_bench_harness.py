@@ -130,3 +130,52 @@ def test_xgmi_children_under_torchrun_rendezvous_and_report():
     assert r1 == {}
     err = r0["xgmi"]["error"]
     assert "killed after" not in err and "exited" not in err, err  # the children rendezvoused and reported
+
+
+def test_n1_line_carries_reduce_kernel_and_ceiling_as_flat_keys():
+    """The driver's parser keeps the roofline's scalar keys only (BENCH_r03.json
+    `parsed.roofline` dropped the nested reduce_kernel): the config-2 reduce
+    fractions and the copy ceiling must be there as flat keys."""
+    rl = {"bound": "hbm", "achieved": 6900.0, "frac": 0.8625}
+    lr = {"k2": {"frac_of_hbm_peak": 0.79, "achieved_gbs": 6320.0},
+          "k4": {"frac_of_hbm_peak": 0.785, "achieved_gbs": 6280.0},
+          "k8": {"frac_of_hbm_peak": 0.80, "achieved_gbs": 6400.0}, "timing": "events"}
+    cc = {"ceiling_256MiB": {"shape": "copy_zero", "achieved_gbs": 6950.0},
+          "ceiling_64MiB": {"shape": "copy_zero", "achieved_gbs": 6400.0}}
+    bench.n1_roofline_summary(rl, lr, cc)
+    line = bench.build_line(value=2100.0, n_gpus=1, steps=20, warmup=5, elapsed=0.0024,
+                            bucket_bytes=256 << 20, wire="f32", extra={"roofline": rl})
+    flat = {k: v for k, v in line["roofline"].items() if not isinstance(v, (dict, list))}
+    assert flat["reduce_kernel_frac_min"] == 0.785
+    assert flat["reduce_kernel_frac_k2"] == 0.79 and flat["reduce_kernel_frac_k8"] == 0.80
+    assert flat["copy_ceiling_gbs"] == 6950.0 and flat["copy_ceiling_shape"] == "copy_zero"
+    assert flat["frac_of_copy_ceiling"] == pytest.approx(6900 / 6950, abs=1e-4) and flat["frac_of_copy_ceiling"] <= 1
+    assert flat["reduce_kernel_frac_of_ceiling_min"] == pytest.approx(6280 / 6400, abs=1e-4)
+    json.dumps(line)
+
+
+@pytest.mark.parametrize("algo,wire", [("xgmi", "f32"), ("xgmi", "f16"), ("allreduce", "f32"), ("direct", "f16")])
+def test_nx_line_carries_xgmi_algbw_links_and_phases(algo, wire):
+    """The N > 1 line (driver's 8-GPU run): frac_of_xgmi_algbw, per_link_gbs and
+    phases_ms_per_step, with flat copies of the per-phase and per-link figures."""
+    world, steps, elems = 8, 10, 64 << 20
+    phases = {"kernel": (2.0, 10), "rccl": (0.0, 0), "xgmi_scatter": (3.0, 10), "xgmi_barrier": (0.2, 20),
+              "xgmi_gather": (2.5, 10)} if algo == "xgmi" else {"kernel": (1.0, 10), "rccl": (9.0, 10)}
+    tim = {"kernel_ms": 2.0, "kernels": 10, "collective_ms": 9.0, "collectives": 10, "phases": phases}
+    rl = bench.nx_roofline(tim, elems * 4, elems, world, wire, algo, steps, elapsed=0.012,
+                           link={"gbs": 70.0})
+    line = bench.build_line(value=1.0, n_gpus=world, steps=steps, warmup=2, elapsed=0.012,
+                            bucket_bytes=elems * 4, wire=wire, extra={"roofline": rl})
+    r = line["roofline"]
+    assert r["bound"] == "xgmi" and r["frac_of_xgmi_algbw"] > 0 and r["north_star_target_frac_of_xgmi_algbw"] == 0.7
+    assert r["xgmi_algbw_peak_gbs"] == pytest.approx(world * bench.XGMI_LINK_GBS / 2, abs=0.1)
+    assert isinstance(r["phases_ms_per_step"], dict) and r["phases_ms_per_step"]
+    assert r["frac_of_measured_links"] > 0
+    for ph, ms in r["phases_ms_per_step"].items():
+        assert r[f"phase_ms_{ph}"] == ms
+    if algo == "xgmi":
+        assert set(r["per_link_gbs"]) == {"xgmi_scatter", "xgmi_gather"}
+        assert r["per_link_gbs_xgmi_scatter"] == pytest.approx(4 * elems / world / 0.3e-3 / 1e9, rel=1e-3)
+    else:
+        assert r["per_link_gbs"] is None
+    json.dumps(line)

@@ -1,0 +1,369 @@
+// launch_phases.hip — measurement tool (not part of the product): where the
+// fixed cost of one back-to-back streaming launch goes.
+//
+// Every kernel here is the library's skeleton (64-thread workgroups, one
+// 16-B vector per lane per stream, a one-shot grid) in a STAMP build: lane 0
+// of every workgroup reads the 100 MHz real-time counter at its first
+// instruction and again after its own stores have been acknowledged
+// (s_waitcnt vmcnt(0)), and writes {start, end, XCC id, HW id} with one
+// vector store into a side buffer.  From the stamps of L back-to-back
+// launches over rotating buffer sets (> 1.5 GiB, no Infinity-Cache reuse):
+//   span    first workgroup start -> last workgroup end of one launch
+//   gap     last end of launch i -> first start of launch i+1 (the boundary)
+//   steady  the streaming rate R fitted on the 20-80 % completions, and the
+//           span that rate would take: ideal = bytes / R
+//   ramp    first start -> where the fitted line leaves zero completions
+//   drain   where the fitted line reaches all completions -> last end
+//   xcd     max - min over the 8 XCDs of their last end (drain imbalance)
+// span = ramp + ideal + drain; per launch (events) = span + gap.
+//
+// The same shapes also run un-stamped (HIP events only, what bench.py times)
+// and through the product library (LIB: ono_sum_scale_f32, ono_scale_zero_f32,
+// ono_copy_f32, ono_fill_f32, ono_f16_decode_scale on the same buffers).
+//
+//   ./launch_phases [MiB list, default "64,256"] [launches L = 24]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ono_reduce.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint16_t h4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                                     \
+    do {                                                                                          \
+        hipError_t e = (x);                                                                       \
+        if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } \
+    } while (0)
+#define OK(x)                                                                    \
+    do {                                                                         \
+        if ((x) != 0) { fprintf(stderr, "%s: %s\n", #x, ono_last_error()); exit(1); } \
+    } while (0)
+
+struct Stamp {  // 16 B, one per workgroup
+    uint32_t t0_lo, t0_hi, dt, ids;  // start (64-bit), end - start, XCC id << 16 | (HW id >> 8 & 0xFFFF)
+};
+
+struct Args {
+    const f4 *in[8];
+    f4 *out[2];
+    size_t nvec;
+    Stamp *st;
+};
+
+template <class T> __device__ __forceinline__ T ldn(const T *p) { return __builtin_nontemporal_load(p); }
+template <class T> __device__ __forceinline__ void stn(T *p, T v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_sc1(f4 *p, f4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+
+template <bool STAMP> struct Clock {
+    uint64_t t0 = 0;
+    __device__ __forceinline__ void start() {
+        if constexpr (STAMP) t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ __forceinline__ void stop(Stamp *st) {
+        if constexpr (STAMP) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            unsigned x, h;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+            if (threadIdx.x == 0) {
+                uint4 v = {(unsigned)t0, (unsigned)(t0 >> 32), (unsigned)(t1 - t0), ((x & 0xF) << 16) | ((h >> 8) & 0xFFFF)};
+                *(uint4 *)&st[blockIdx.x] = v;
+            }
+        }
+    }
+};
+
+enum Shape { COPY = 0, COPYZ, FILL, SUM2, SUM4, SUM8, DEC, EMPTY, NSHAPES };
+static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 2R1W", "sum4 4R1W", "sum8 8R1W",
+                              "f16 decode", "empty"};
+static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0}, kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0};
+// algorithmic bytes per f32 element
+static const double kBytes[] = {8, 12, 4, 12, 20, 36, 6, 0};
+
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copy(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) stn(a.out[0] + v, ldn(a.in[0] + v));
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copyz(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) {
+        const f4 x = ldn(a.in[0] + v);
+        st_sc1(a.out[0] + v, x);
+        st_sc1(a.out[1] + v, f4{0, 0, 0, 0});
+    }
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(64) void k_fill(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) stn(a.out[0] + v, f4{0, 0, 0, 0});
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(64) void k_empty(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    c.stop(a.st);
+}
+// the product's K = 2 form: both inputs by LDS-DMA, one wait, add from LDS
+template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    __shared__ f4 lds[2][64];
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) {
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+            __builtin_amdgcn_global_load_lds((const void *)(a.in[j] + v), (__attribute__((address_space(3))) void *)&lds[j][0],
+                                             16, 0, 2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stn(a.out[0] + v, (lds[0][threadIdx.x] + lds[1][threadIdx.x]) * 0.5f);
+    }
+    c.stop(a.st);
+}
+// the product's K >= 4 form: one load in flight per wave (occupancy capped by the launch)
+template <int K, bool STAMP> __global__ __launch_bounds__(64) void k_sumser(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) {
+        f4 s = ldn(a.in[0] + v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 1; j < K; j++) {
+            const f4 x = ldn(a.in[j] + v);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            s += x;
+        }
+        stn(a.out[0] + v, s * (1.0f / K));
+    }
+    c.stop(a.st);
+}
+// gather decode: 8-B f16 load, 16-B f32 store (the f16 input is the first half of in[0])
+template <bool STAMP> __global__ __launch_bounds__(64) void k_dec(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (v < a.nvec) {
+        const h4 h = ldn((const h4 *)a.in[0] + v);
+        f4 r;
+        r.x = (float)__builtin_bit_cast(_Float16, h.x);
+        r.y = (float)__builtin_bit_cast(_Float16, h.y);
+        r.z = (float)__builtin_bit_cast(_Float16, h.z);
+        r.w = (float)__builtin_bit_cast(_Float16, h.w);
+        stn(a.out[0] + v, r * 0.5f);
+    }
+    c.stop(a.st);
+}
+
+__global__ void k_init(f4 *p, size_t n, unsigned seed) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned h = (unsigned)i * 2654435761u ^ seed;
+        p[i] = f4{(float)(h & 1023) * 0.25f, (float)((h >> 10) & 1023), 1.0f, -2.0f};
+    }
+}
+
+static size_t g_max_elems = 64u << 20;  // per pool buffer (256 MiB)
+constexpr int kPool = 27;               // 27 x 256 MiB = 6.75 GiB
+static std::vector<f4 *> g_pool;
+static int L = 24;
+
+static unsigned lds_for_occ(int occ) { return (unsigned)(160 * 1024 * 2 / (2 * occ + 1)); }
+
+// mode: 0 = un-stamped tool kernel, 1 = stamped tool kernel, 2 = LIB
+static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) {
+    const unsigned grid = (unsigned)((a.nvec + 63) / 64);
+    const bool st = mode == 1;
+#define L2(KER) \
+    if (st) hipLaunchKernelGGL(KER<true>, dim3(grid), dim3(64), 0, s, a); \
+    else hipLaunchKernelGGL(KER<false>, dim3(grid), dim3(64), 0, s, a);
+    if (mode == 2) {
+        switch (shape) {
+        case COPY: OK(ono_copy_f32((float *)a.out[0], (const float *)a.in[0], n, s)); return;
+        case COPYZ: OK(ono_scale_zero_f32((float *)a.out[0], (const float *)a.in[0], n, 1.0f, (float *)a.out[1], s)); return;
+        case FILL: OK(ono_fill_f32((float *)a.out[0], 0.0f, n, s)); return;
+        case DEC: OK(ono_f16_decode_scale((float *)a.out[0], (const uint16_t *)a.in[0], n, 2.0f, s)); return;
+        case SUM2: case SUM4: case SUM8: {
+            const int k = shape == SUM2 ? 2 : shape == SUM4 ? 4 : 8;
+            const float *ins[8];
+            for (int j = 0; j < k; j++) ins[j] = (const float *)a.in[j];
+            OK(ono_sum_scale_f32((float *)a.out[0], ins, k, n, (float)k, s));
+            return;
+        }
+        default: return;
+        }
+    }
+    switch (shape) {
+    case COPY: L2(k_copy) break;
+    case COPYZ: L2(k_copyz) break;
+    case FILL: L2(k_fill) break;
+    case SUM2: L2(k_sum2) break;
+    case DEC: L2(k_dec) break;
+    case EMPTY: L2(k_empty) break;
+    case SUM4:
+        if (st) hipLaunchKernelGGL((k_sumser<4, true>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
+        else hipLaunchKernelGGL((k_sumser<4, false>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
+        break;
+    case SUM8:
+        if (st) hipLaunchKernelGGL((k_sumser<8, true>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
+        else hipLaunchKernelGGL((k_sumser<8, false>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
+        break;
+    }
+#undef L2
+    CK(hipGetLastError());
+}
+
+struct Phases {
+    double span, gap, ramp, ideal, drain, xcd, rate_gbs, first_to_last_start, tail;
+};
+
+static double median(std::vector<double> v) {
+    if (v.empty()) return 0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+// stamps of L launches (nwg each), ticks of 10 ns
+static Phases analyse(const std::vector<Stamp> &h, size_t nwg, double bytes) {
+    std::vector<double> span, gap, ramp, ideal, drain, xcd, rate, fls, tail;
+    std::vector<double> first(L), last(L);
+    for (int i = 0; i < L; i++) {
+        const Stamp *s = &h[(size_t)i * nwg];
+        std::vector<double> st(nwg), en(nwg);
+        double xend[16] = {0};
+        for (size_t w = 0; w < nwg; w++) {
+            const uint64_t t0 = ((uint64_t)s[w].t0_hi << 32) | s[w].t0_lo;
+            st[w] = (double)t0 * 10.0;  // ns
+            en[w] = st[w] + (double)s[w].dt * 10.0;
+            const unsigned x = (s[w].ids >> 16) & 0xF;
+            xend[x] = std::max(xend[x], en[w]);
+        }
+        std::sort(st.begin(), st.end());
+        std::sort(en.begin(), en.end());
+        first[i] = st.front();
+        last[i] = en.back();
+        const size_t a = nwg / 5, b = nwg * 4 / 5;
+        const double R = (double)(b - a) / std::max(1.0, en[b] - en[a]);  // workgroups per ns
+        const double t_lo = en[a] - (double)a / R, t_hi = en[b] + (double)(nwg - 1 - b) / R;
+        span.push_back(last[i] - first[i]);
+        ramp.push_back(t_lo - first[i]);
+        ideal.push_back(t_hi - t_lo);
+        drain.push_back(last[i] - t_hi);
+        rate.push_back(bytes / ((double)nwg / R));  // bytes per ns = GB/s
+        fls.push_back(st.back() - st.front());
+        tail.push_back(last[i] - st.back());
+        double lo = 1e300, hi = 0;
+        for (int x = 0; x < 16; x++)
+            if (xend[x] > 0) { lo = std::min(lo, xend[x]); hi = std::max(hi, xend[x]); }
+        xcd.push_back(hi - lo);
+    }
+    for (int i = 0; i + 1 < L; i++) gap.push_back(first[i + 1] - last[i]);
+    return {median(span) / 1e3, median(gap) / 1e3, median(ramp) / 1e3, median(ideal) / 1e3, median(drain) / 1e3,
+            median(xcd) / 1e3, median(rate), median(fls) / 1e3, median(tail) / 1e3};
+}
+
+static void run_size(size_t mib, hipStream_t s) {
+    const size_t n = mib << 18, nvec = n / 4, nwg = (nvec + 63) / 64;
+    Stamp *dst;
+    CK(hipMalloc(&dst, sizeof(Stamp) * nwg * L));
+    printf("\n# %zu MiB per buffer (%zu f32, %zu workgroups), %d back-to-back launches per row, medians\n", mib, n, nwg,
+           L);
+    printf("# %-16s %9s %9s %9s | %8s %7s %7s %7s %7s %7s %7s %7s | %8s %6s\n", "shape", "ev_us", "stamp_us", "lib_us",
+           "span", "gap", "ramp", "ideal", "drain", "xcd", "dstart", "tail", "R_GB/s", "frac");
+    for (int shape = 0; shape < NSHAPES; shape++) {
+        const int per = kReads[shape] + kWrites[shape];
+        const int nsets = per ? kPool / per : 1;
+        auto args = [&](int it) {
+            Args a{};
+            const int set = it % nsets;
+            for (int j = 0; j < kReads[shape]; j++) a.in[j] = g_pool[set * per + j];
+            for (int j = 0; j < kWrites[shape]; j++) a.out[j] = g_pool[set * per + kReads[shape] + j];
+            a.nvec = nvec;
+            a.st = dst + (size_t)(it % L) * nwg;
+            return a;
+        };
+        double us[3] = {0, 0, 0};
+        std::vector<Stamp> h;
+        for (int mode = 0; mode < 3; mode++) {
+            if (mode == 2 && (shape == EMPTY)) continue;
+            for (int it = 0; it < nsets + 2; it++) launch(shape, mode, args(it), n, s);  // whole rotation touched
+            CK(hipStreamSynchronize(s));
+            hipEvent_t e0, e1;
+            CK(hipEventCreate(&e0));
+            CK(hipEventCreate(&e1));
+            CK(hipEventRecord(e0, s));
+            for (int it = 0; it < L; it++) {
+                Args a = args(nsets + 2 + it);
+                a.st = dst + (size_t)it * nwg;
+                launch(shape, mode, a, n, s);
+            }
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            us[mode] = ms * 1e3 / L;
+            CK(hipEventDestroy(e0));
+            CK(hipEventDestroy(e1));
+            if (mode == 1) {
+                h.resize(nwg * L);
+                CK(hipMemcpy(h.data(), dst, sizeof(Stamp) * nwg * L, hipMemcpyDeviceToHost));
+            }
+        }
+        const double bytes = kBytes[shape] * (double)n;
+        const Phases p = analyse(h, nwg, bytes);
+        const double best = us[2] > 0 ? std::min(us[0], us[2]) : us[0];
+        printf("%-18s %9.2f %9.2f %9.2f | %8.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f | %8.0f %6.3f\n", kName[shape],
+               us[0], us[1], us[2], p.span, p.gap, p.ramp, p.ideal, p.drain, p.xcd, p.first_to_last_start, p.tail,
+               p.rate_gbs, bytes ? bytes / (best * 1e3) / 8000.0 : 0.0);
+        fflush(stdout);
+    }
+    CK(hipFree(dst));
+}
+
+int main(int argc, char **argv) {
+    std::vector<size_t> sizes = {64, 256};
+    if (argc > 1) {
+        sizes.clear();
+        for (char *t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) sizes.push_back((size_t)atol(t));
+    }
+    if (argc > 2) L = atoi(argv[2]);
+    size_t mx = 0;
+    for (size_t m : sizes) mx = std::max(mx, m);
+    g_max_elems = mx << 18;
+    hipDeviceProp_t p;
+    CK(hipGetDeviceProperties(&p, 0));
+    printf("# launch_phases: %s, %d CUs; stamps = s_memrealtime (100 MHz) per workgroup, lane 0\n", p.gcnArchName,
+           p.multiProcessorCount);
+    printf("# ev_us: HIP events around L launches (un-stamped tool kernel); stamp_us: the stamped build; lib_us: the\n"
+           "# product library on the same buffers; span/gap/ramp/ideal/drain/xcd/dstart/tail in us from the stamps\n"
+           "# (dstart = first -> last workgroup start, tail = last start -> last end); R = fitted steady rate of\n"
+           "# algorithmic bytes; frac = algorithmic bytes / min(ev_us, lib_us) of 8 TB/s\n");
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (int i = 0; i < kPool; i++) {
+        f4 *q;
+        CK(hipMalloc(&q, g_max_elems * 4));
+        hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, q, g_max_elems / 4, 17u + i);
+        g_pool.push_back(q);
+    }
+    CK(hipStreamSynchronize(s));
+    for (size_t m : sizes) run_size(m, s);
+    for (f4 *q : g_pool) CK(hipFree(q));
+    return 0;
+}
