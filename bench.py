@@ -653,12 +653,18 @@ def host_fed(ono_amd, ring, elems: int, rounds: int) -> dict:
             ring.pull_grads_host(res, grad)
             if r:
                 ts.append(time.perf_counter() - t0)
-        t = sorted(ts)[len(ts) // 2]
-        out[form] = {"ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 2)}
+        ts.sort()
+        t, tmin, tmax = ts[len(ts) // 2], ts[0], ts[-1]
+        out[form] = {"ms": round(t * 1e3, 3), "gib_s": round(elems * 4 / t / GIB, 2),
+                     "ms_min": round(tmin * 1e3, 3), "gib_s_best": round(elems * 4 / tmin / GIB, 2),
+                     "gib_s_worst": round(elems * 4 / tmax / GIB, 2), "rounds": len(ts)}
     ring.unregister_host(res)
     ring.unregister_host(grad)
     return {"workload": "pull_grads_host, 256 MiB host bucket in, 256 MiB host grad out, n = 1 device round trip",
-            "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams", **out}
+            "pipeline": "16 MiB chunks: H2D || reduce || D2H on three HIP streams; pageable: bounce copies on "
+                        "ONO_HOST_THREADS threads bound to the GPU's NUMA node",
+            "stat": "ms / gib_s = median of the rounds, ms_min / gib_s_best = the fastest, gib_s_worst = the slowest",
+            **out}
 
 
 def host_fed_n(ono_amd, ring, elems: int, ctl, world: int, rounds: int = 5) -> dict:

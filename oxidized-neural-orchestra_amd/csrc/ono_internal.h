@@ -64,6 +64,9 @@ hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divis
                              hipStream_t s);
 hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
                         hipStream_t s);
+// a SparseGrad's values [0, min(total, L)) on the host after the reference's
+// sequential parse of the whole stream (ono_sparse.hip); *got = its total
+int sparse_lift_prefix_host(const uint8_t *buf, size_t nbytes, float *out, size_t L, size_t *got);
 // the library's own pure streams (T = float or uint16_t): dst = src, dst = value
 template <class T> hipError_t launch_copy(T *dst, const T *src, size_t n, hipStream_t s);
 template <class T> hipError_t launch_fill(T *dst, T value, size_t n, hipStream_t s);

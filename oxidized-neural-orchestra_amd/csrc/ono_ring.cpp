@@ -16,7 +16,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
 #include <atomic>
 #include <cerrno>
 #include <cmath>
@@ -46,11 +51,62 @@ namespace ono {
 // T = env ONO_HOST_THREADS (default 16, at most the hardware threads).  The
 // registered form does not use it: its only CPU work is zeroing the residual,
 // and a single thread there leaves the host memory bandwidth to the DMA.
+// The pool's threads run on the CPUs of the GPU's NUMA node (the node that
+// /sys reports for its PCI function, intersected with the process's allowed
+// CPUs): the bounce slots are pinned there, and the round-to-round spread of
+// the pageable rate (21-33 GiB/s unbound) came from copies that
+// the scheduler moved across sockets.  ONO_HOST_NUMA=0 leaves them unbound.
+static bool gpu_node_cpus(int device, cpu_set_t *out) {
+    const char *e = getenv("ONO_HOST_NUMA");
+    if (e && !strcmp(e, "0")) return false;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return false;
+    for (char *c = bus; *c; c++) *c = (char)tolower(*c);
+    char path[256];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE *f = fopen(path, "r");
+    if (!f) return false;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    if (node < 0) return false;
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    f = fopen(path, "r");
+    if (!f) return false;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    int a, b;
+    char sep;
+    while (fscanf(f, "%d", &a) == 1) {  // "0-63,128-191"
+        b = a;
+        if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+            if (fscanf(f, "%d", &b) != 1) break;
+            if (fscanf(f, "%c", &sep) != 1) sep = 0;
+        }
+        for (int c = a; c <= b && c < CPU_SETSIZE; c++) CPU_SET(c, &set);
+        if (sep != ',') break;
+    }
+    fclose(f);
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) == 0) CPU_AND(&set, &set, &allowed);
+    if (CPU_COUNT(&set) == 0) return false;
+    *out = set;
+    return true;
+}
+
 class HostPool {
 public:
-    explicit HostPool(int t) : nt_(std::max(1, t)) {
-        for (int i = 1; i < nt_; i++) th_.emplace_back([this, i] { loop(i); });
+    HostPool(int t, int device) : nt_(std::max(1, t)) {
+        cpu_set_t set;
+        const bool bind = gpu_node_cpus(device, &set);
+        numa_bound_ = bind;
+        for (int i = 1; i < nt_; i++)
+            th_.emplace_back([this, i, bind, set] {
+                if (bind) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+                loop(i);
+            });
     }
+    bool numa_bound() const { return numa_bound_; }
     ~HostPool() {
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -113,6 +169,7 @@ private:
         }
     }
     int nt_;
+    bool numa_bound_ = false;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_;
@@ -697,7 +754,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const size_t nch = (n + CH - 1) / CH;
     int rc = ensure_events(r, nch);
     if (rc) return rc;
-    if (!reg && !r->pool) r->pool.reset(new HostPool(host_threads()));
+    if (!reg && !r->pool) r->pool.reset(new HostPool(host_threads(), r->device));
     if (!reg && !r->pin_in) {
         ONO_HIP(hipHostMalloc((void **)&r->pin_in, kSlots * CH * sizeof(float), hipHostMallocDefault));
         ONO_HIP(hipHostMalloc((void **)&r->pin_out, kSlots * CH * sizeof(float), hipHostMallocDefault));

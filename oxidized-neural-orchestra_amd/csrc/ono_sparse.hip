@@ -29,6 +29,7 @@
 #include <chrono>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ono_internal.h"
@@ -1293,50 +1294,100 @@ __device__ __forceinline__ uint32_t unit_plus2(const Units12 &U, uint32_t j) {
 // rec[4 t ..]: candidates, sum of offset + length, first candidate, exit (the
 // last candidate's successor: the next tile's first record or M).  The units
 // come straight from HBM into registers (no LDS staging); the masks and their
-// prefixes go through LDS for the successor checks.
-__global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, uint32_t *rec, uint32_t *tsum,
+// prefixes go through LDS for the successor checks.  TPB tiles per workgroup,
+// every thread's loads for all of them issued before the first is used: the
+// stream is small (~15 MB for a 64 MiB gradient at 10 % kept), so the kernel is
+// a few rounds of load latency, and TPB = 2 halves the rounds.
+template <int TPB> struct PatCnt {
+    uint32_t v[2 * TPB];
+};
+template <int TPB>
+__device__ __forceinline__ void block_scan_n(const uint32_t (&in)[2 * TPB], uint32_t (&ex)[2 * TPB],
+                                             uint32_t (&tot)[2 * TPB]) {
+    __shared__ uint32_t wt[2 * TPB][kPatT / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc[2 * TPB];
+#pragma unroll
+    for (int q = 0; q < 2 * TPB; q++) {
+        inc[q] = wave_incl_sum_dpp(in[q]);
+        if (lane == 63) wt[q][wave] = inc[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2 * TPB; q++) {
+        uint32_t pre = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < kPatT / 64; w++) {
+            pre += w < wave ? wt[q][w] : 0u;
+            all += wt[q][w];
+        }
+        ex[q] = pre + inc[q] - in[q];
+        tot[q] = all;
+    }
+}
+template <int TPB>
+__global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, size_t T, uint32_t *rec, uint32_t *tsum,
                                                   uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
                                                   uint64_t *badw, uint32_t epoch) {
-    __shared__ uint16_t lmask[kPatT], lpre[kPatT];  // (masks of kPatPer bits)
-    const size_t t = blockIdx.x, base = t * kPatU;
-    if (t == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
+    __shared__ uint16_t lmask[TPB][kPatT], lpre[TPB][kPatT];  // (masks of kPatPer bits)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
         host_word[1] = stream_total(b);
         *qcount = 0;
     }
     const uint32_t j0 = kPatPer * threadIdx.x;
-    const bool any = base + j0 < M;
-    const Units12 U = any ? units12_global(b, base + j0, M) : Units12{};
-    uint32_t sum = 0;
-    const uint32_t m = any ? pat_mask(U, base + j0, M, sum) : 0u;
-    uint32_t ec, es, tc, ts;
-    block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);
-    lmask[threadIdx.x] = (uint16_t)m;
-    lpre[threadIdx.x] = (uint16_t)ec;
+    Units12 U[TPB];
+#pragma unroll
+    for (int q = 0; q < TPB; q++) {
+        const size_t base = ((size_t)blockIdx.x * TPB + q) * kPatU;
+        U[q] = base + j0 < M ? units12_global(b, base + j0, M) : Units12{};
+    }
+    uint32_t m[TPB], in[2 * TPB], ex[2 * TPB], tot[2 * TPB];
+#pragma unroll
+    for (int q = 0; q < TPB; q++) {
+        const size_t base = ((size_t)blockIdx.x * TPB + q) * kPatU;
+        uint32_t sum = 0;
+        m[q] = base + j0 < M ? pat_mask(U[q], base + j0, M, sum) : 0u;
+        in[2 * q] = (uint32_t)__builtin_popcount(m[q]);
+        in[2 * q + 1] = sum;
+    }
+    block_scan_n<TPB>(in, ex, tot);
+#pragma unroll
+    for (int q = 0; q < TPB; q++) {
+        lmask[q][threadIdx.x] = (uint16_t)m[q];
+        lpre[q][threadIdx.x] = (uint16_t)ex[2 * q];
+    }
     __syncthreads();
     bool bad = false;
-    uint32_t rank = ec;
-    for (uint32_t mm = m; mm; mm &= mm - 1, rank++) {
-        const uint32_t j = (uint32_t)__builtin_ctz(mm), k = j0 + j;
-        const uint32_t nx = k + 4 + unit_plus2(U, j);  // tile-local successor
-        if (base + nx > M) { bad = true; break; }  // the run overruns the stream
-        if (nx < (uint32_t)kPatU && base + nx < M) {
-            const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
-            const uint32_t p2 = lpre[nx / kPatPer] + (uint32_t)__builtin_popcount(m2 & ((1u << b2) - 1u));
-            if (!(m2 >> b2 & 1u) || p2 != rank + 1) { bad = true; break; }
-        } else {  // the end of the stream or another tile: only the tile's last candidate goes there
-            if (rank + 1 != tc) { bad = true; break; }
-            rec[4 * t + 3] = (uint32_t)(base + nx);
+#pragma unroll
+    for (int q = 0; q < TPB; q++) {
+        const size_t t = (size_t)blockIdx.x * TPB + q, base = t * kPatU;
+        if (t >= T) break;  // (uniform)
+        const uint32_t ec = ex[2 * q], tc = tot[2 * q];
+        uint32_t rank = ec;
+        for (uint32_t mm = m[q]; mm && !bad; mm &= mm - 1, rank++) {
+            const uint32_t j = (uint32_t)__builtin_ctz(mm), k = j0 + j;
+            const uint32_t nx = k + 4 + unit_plus2(U[q], j);  // tile-local successor
+            if (base + nx > M) { bad = true; break; }  // the run overruns the stream
+            if (nx < (uint32_t)kPatU && base + nx < M) {
+                const uint32_t m2 = lmask[q][nx / kPatPer], b2 = nx % kPatPer;
+                const uint32_t p2 = lpre[q][nx / kPatPer] + (uint32_t)__builtin_popcount(m2 & ((1u << b2) - 1u));
+                if (!(m2 >> b2 & 1u) || p2 != rank + 1) { bad = true; break; }
+            } else {  // the end of the stream or another tile: only the tile's last candidate goes there
+                if (rank + 1 != tc) { bad = true; break; }
+                rec[4 * t + 3] = (uint32_t)(base + nx);
+            }
+        }
+        if (m[q] && ec == 0) rec[4 * t + 2] = (uint32_t)(base + j0 + __builtin_ctz(m[q]));
+        if (threadIdx.x == 0) {
+            rec[4 * t] = tc;
+            rec[4 * t + 1] = tot[2 * q + 1];
+            tsum[t] = tot[2 * q + 1];  // (again, contiguous: pl_place sums the earlier tiles' from here)
+            if (tc == 0) { rec[4 * t + 2] = kPatNone; rec[4 * t + 3] = kPatNone; }
         }
     }
     if (bad) raise_bad(badw, epoch);
-    if (m && ec == 0) rec[4 * t + 2] = (uint32_t)(base + j0 + __builtin_ctz(m));
-    if (threadIdx.x == 0) {
-        rec[4 * t] = tc;
-        rec[4 * t + 1] = ts;
-        tsum[t] = ts;  // (again, contiguous: pl_place sums the earlier tiles' from here)
-        if (tc == 0) { rec[4 * t + 2] = kPatNone; rec[4 * t + 3] = kPatNone; }
-    }
 }
+constexpr int kPatIndexTPB = 2;  // tiles per pl_index workgroup
 
 // E[t] = the element index tile t's range starts at: one workgroup scans the
 // tiles' sums, 4 per thread, kPatScanT x 4 tiles per step (DPP wave scans; the
@@ -1422,10 +1473,10 @@ constexpr size_t kPatDirect = 4096;  // up to this many tiles pl_place sums the 
 constexpr int kPatPasses = 8;
 __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, size_t T, int vec, size_t t,
                                           uint64_t E0, uint32_t sum_t, uint64_t total, bool allow_queue,
-                                          f4s *img4, uint4 *lw4, uint32_t *lq, uint32_t *lqn, uint4 *queue,
+                                          uint2 *img8, uint4 *lw4, uint32_t *lq, uint32_t *lqn, uint4 *queue,
                                           uint32_t *qcount, uint32_t qcap, uint64_t *host_word, uint64_t *badw,
                                           uint32_t epoch) {
-    float *img = (float *)img4;
+    uint16_t *img = (uint16_t *)img8;
     const uint16_t *lw = (const uint16_t *)lw4;
     const size_t base = t * kPatU;
     const uint64_t ea = min(E0, total);
@@ -1466,8 +1517,7 @@ __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, 
     for (uint64_t p = 0; p < npass; p++) {
         const uint64_t w0 = p * kPatImg, w1 = min(w0 + kPatImg, span);
         const uint32_t wn = (uint32_t)(w1 - w0);
-        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (uint32_t i = threadIdx.x; i < (wn + 3) / 4; i += kPatT) img4[i] = z;
+        for (uint32_t i = threadIdx.x; i < (wn + 3) / 4; i += kPatT) img8[i] = make_uint2(0u, 0u);
         if (threadIdx.x == 0) *lqn = 0;
         __syncthreads();
         uint64_t cur = E0 + es;
@@ -1480,7 +1530,7 @@ __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, 
             if (a >= e) continue;
             const uint32_t c = (uint32_t)(e - a), u0 = k + 4 + (uint32_t)(a - r0), ai = (uint32_t)(a - w0);
             if (len <= (uint32_t)kShortP) {
-                for (uint32_t i = 0; i < c; i++) img[ai + i] = from_f16_sp(lw[u0 + i]);
+                for (uint32_t i = 0; i < c; i++) img[ai + i] = lw[u0 + i];
             } else {
                 const uint32_t q = atomicAdd(lqn, 1u);
                 if (q < (uint32_t)kLQ) {
@@ -1488,8 +1538,7 @@ __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, 
                     lq[3 * q + 1] = (uint32_t)(8 + 2 * (base + u0));
                     lq[3 * q + 2] = c;
                 } else {
-                    for (uint32_t i = 0; i < c; i++)
-                        img[ai + i] = from_f16_sp(((glb_u16 *)(b + 8 + 2 * (base + u0)))[i]);
+                    for (uint32_t i = 0; i < c; i++) img[ai + i] = ((glb_u16 *)(b + 8 + 2 * (base + u0)))[i];
                 }
             }
         }
@@ -1498,12 +1547,12 @@ __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, 
         for (uint32_t q = 0; q < nl; q++) {
             const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
             glb_u16 *src = (glb_u16 *)(b + vp);
-            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
+            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = src[i];
         }
         __syncthreads();
         float *dst = g + ia + w0;
         for (uint32_t i = threadIdx.x; i < wn; i += kPatT)
-            if (w0 + i >= skip) dst[i] = img[i];
+            if (w0 + i >= skip) dst[i] = from_f16_sp(img[i]);
         __syncthreads();
     }
 }
@@ -1540,10 +1589,10 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
                                                   uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
                                                   uint32_t *wide, uint64_t *host_word, uint64_t *badw,
                                                   uint32_t epoch) {
-    __shared__ f4s img4[kPatImg / 4];
+    __shared__ uint2 img8[kPatImg / 4];  // the range as f16 bits (12 KiB: 8 workgroups per CU), widened on the way out
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
-    float *img = (float *)img4;
+    uint16_t *img = (uint16_t *)img8;
     const uint16_t *lw = (const uint16_t *)lw4;
     const uint32_t t = blockIdx.x, base = t * (uint32_t)kPatU, M32 = (uint32_t)M, T32 = (uint32_t)T;
     const bool direct = T <= kPatDirect;  // (uniform) else E[] from pl_scan
@@ -1606,7 +1655,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const bool is_wide = eb > ea && n > (uint32_t)kPatImg;
     if constexpr (ASYNC) {
         if (is_wide) {  // (uniform)
-            wide_tile(g, b, M, T, vec, t, E0, me.y, total, false, img4, lw4, lq, &lqn, nullptr, nullptr, 0,
+            wide_tile(g, b, M, T, vec, t, E0, me.y, total, false, img8, lw4, lq, &lqn, nullptr, nullptr, 0,
                       host_word, badw, epoch);
             return;
         }
@@ -1618,10 +1667,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
     }
     if (eb == ea || is_wide) return;  // (uniform) an empty tile inside a run; a wide range: pl_wide places it
-    {
-        const f4s z = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img4[i] = z;
-    }
+    for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img8[i] = make_uint2(0u, 0u);
     const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
     uint32_t sum;
@@ -1637,9 +1683,9 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
             raise_bad(badw, epoch);  // only a refuted stream
             break;
         }
-        float *d = img + (gi - ia);
+        uint16_t *d = img + (gi - ia);
         if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
-            for (uint32_t i = 0; i < len; i++) d[i] = from_f16_sp(lw[k + 4 + i]);
+            for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
         } else {
             const uint32_t q = atomicAdd(&lqn, 1u);
             const uint32_t vp = 8 + 2 * (base + k + 4);
@@ -1648,7 +1694,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
                 lq[3 * q + 1] = vp;
                 lq[3 * q + 2] = len;
             } else {
-                for (uint32_t i = 0; i < len; i++) d[i] = from_f16_sp(((glb_u16 *)(b + vp))[i]);
+                for (uint32_t i = 0; i < len; i++) d[i] = ((glb_u16 *)(b + vp))[i];
             }
         }
         cur = gi + len;
@@ -1659,25 +1705,30 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         for (uint32_t q = 0; q < nl; q++) {
             const uint32_t a = lq[3 * q], vp = lq[3 * q + 1], c = lq[3 * q + 2];
             glb_u16 *src = (glb_u16 *)(b + vp);
-            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = from_f16_sp(src[i]);
+            for (uint32_t i = threadIdx.x; i < c; i += kPatT) img[a + i] = src[i];
         }
         __syncthreads();
     }
-    // the range out: whole 16-B vectors inside [ea, eb), then the partial first and last vectors
+    // the range out, widened to f32: whole 16-B vectors inside [ea, eb), then the partial first and
+    // last vectors
     const uint32_t skip = ea - ia;
     float *gi0 = g + ia;
     if (vec) {
         const uint32_t v0 = skip ? 1u : 0u, v1 = n / 4;  // whole vectors [v0, v1)
-        for (uint32_t i = v0 + threadIdx.x; i < v1; i += kPatT)
-            __builtin_nontemporal_store(img4[i], (f4s *)gi0 + i);
+        for (uint32_t i = v0 + threadIdx.x; i < v1; i += kPatT) {
+            const uint2 h = img8[i];
+            const f4s x = {from_f16_sp((uint16_t)h.x), from_f16_sp((uint16_t)(h.x >> 16)), from_f16_sp((uint16_t)h.y),
+                           from_f16_sp((uint16_t)(h.y >> 16))};
+            __builtin_nontemporal_store(x, (f4s *)gi0 + i);
+        }
         if (threadIdx.x < 4) {
             const uint32_t e = threadIdx.x;
-            if (skip && e >= skip && e < n) gi0[e] = img[e];  // the first vector's part in range
+            if (skip && e >= skip && e < n) gi0[e] = from_f16_sp(img[e]);  // the first vector's part in range
             const uint32_t l = 4 * v1 + e;
-            if (l < n && l >= 4 * v0) gi0[l] = img[l];        // the last vector's part
+            if (l < n && l >= 4 * v0) gi0[l] = from_f16_sp(img[l]);        // the last vector's part
         }
     } else {
-        for (uint32_t i = threadIdx.x; i < n; i += kPatT) gi0[i] = img[i];
+        for (uint32_t i = threadIdx.x; i < n; i += kPatT) gi0[i] = from_f16_sp(img[i]);
     }
 }
 
@@ -1686,13 +1737,13 @@ __global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, siz
                                                  const uint64_t *E, const uint32_t *tsum, const uint32_t *wide,
                                                  uint4 *queue, uint32_t *qcount, uint32_t qcap, uint64_t *host_word,
                                                  uint64_t *badw, uint32_t epoch) {
-    __shared__ f4s img4[kPatImg / 4];
+    __shared__ uint2 img8[kPatImg / 4];
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
     const uint64_t total = stream_total(b);
     for (size_t t = blockIdx.x; t < T; t += gridDim.x) {
         if (!wide[t]) continue;  // (uniform)
-        wide_tile(g, b, M, T, vec, t, E[t], tsum[t], total, true, img4, lw4, lq, &lqn, queue, qcount, qcap,
+        wide_tile(g, b, M, T, vec, t, E[t], tsum[t], total, true, img8, lw4, lq, &lqn, queue, qcount, qcap,
                   host_word, badw, epoch);
     }
 }
@@ -1821,6 +1872,53 @@ int lift_parse_host(const uint8_t *buf, size_t nbytes, uint64_t total, std::vect
     return ONO_OK;
 }
 
+}  // namespace
+
+namespace ono {
+// f16 bits -> f32 on the host, as half 2.7.1 (and gfx950's v_cvt_f32_f16): exact, NaN -> sign |
+// quiet bit | payload << 13
+static float f16_to_f32_host(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    uint32_t bits;
+    if (e == 0x1F) bits = sign | (m ? 0x7FC00000u | m << 13 : 0x7F800000u);
+    else if (e) bits = sign | (e + 112u) << 23 | m << 13;
+    else if (!m) bits = sign;
+    else {  // subnormal: m * 2^-24, normalised
+        int sh = 0;
+        uint32_t mm = m;
+        while (!(mm & 0x400u)) { mm <<= 1; sh++; }
+        bits = sign | (uint32_t)(113 - sh) << 23 | (mm & 0x3FFu) << 13;
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+// A SparseGrad whose total exceeds what its receiver uses (the scatter adds
+// over the shorter length, worker_ring.rs:141-143): the reference's sequential
+// parse validates the whole stream (its errors), but only values [0, L) are
+// materialised — out[0, min(total, L)) on the host.  A frame's claimed total
+// never sizes a device allocation.
+int sparse_lift_prefix_host(const uint8_t *buf, size_t nbytes, float *out, size_t L, size_t *got) {
+    uint64_t total = 0;
+    if (nbytes < 8) return set_error(ONO_E_PROTO, "Missing total length bytes at grad lift");
+    for (int q = 0; q < 8; q++) total |= (uint64_t)buf[q] << (8 * q);
+    std::vector<uint64_t> start, cumF;
+    int rc = lift_parse_host(buf, nbytes, total, start, cumF);
+    if (rc) return rc;
+    const size_t k = (size_t)std::min<uint64_t>(total, L);
+    std::fill(out, out + k, 0.0f);
+    for (size_t j = 0; j < start.size() && start[j] < k; j++) {
+        const size_t len = (j + 1 < start.size() ? cumF[j + 1] : (nbytes - 8 - 8 * start.size()) / 2) - cumF[j];
+        const uint8_t *v = buf + 16 + 8 * j + 2 * cumF[j];
+        for (size_t i = 0; i < len && start[j] + i < k; i++) out[start[j] + i] = f16_to_f32_host((uint16_t)(v[2 * i] | v[2 * i + 1] << 8));
+    }
+    *got = (size_t)std::min<uint64_t>(total, (uint64_t)SIZE_MAX);
+    return ONO_OK;
+}
+}  // namespace ono
+
+namespace {
 // Sequential fallback: host parse, tables up, expand (the original lift).
 int lift_host_path(float *g, const uint8_t *hbuf, const uint8_t *dbuf, size_t nbytes, uint64_t total,
                    hipStream_t s) {
@@ -1855,10 +1953,21 @@ hipError_t host_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uin
     hipLaunchKernelGGL(sp_signal, dim3(1), dim3(64), 0, s, word_dev, epoch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // A tight spin for the lift's own few tens of microseconds; beyond that the
+    // stream had other work queued ahead of the call (training kernels before a
+    // TCP hop's drop or lift), so the thread backs off — pause, then yield —
+    // instead of burning a core while it holds the scratch lock, and past 2 s
+    // it blocks in the runtime.
     const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 0; *w != epoch; i++)
-        if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
-            return hipStreamSynchronize(s);
+    int mode = 0;  // 0 spin, 1 pause, 2 yield
+    for (uint32_t i = 0; *w != epoch; i++) {
+        if (mode == 1) __builtin_ia32_pause();
+        else if (mode == 2) std::this_thread::yield();
+        if ((i & 255) != 0) continue;
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt > std::chrono::seconds(2)) return hipStreamSynchronize(s);
+        mode = dt > std::chrono::microseconds(200) ? 2 : dt > std::chrono::microseconds(50) ? 1 : 0;
+    }
     return hipSuccess;
 }
 
@@ -1950,7 +2059,8 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
         }
         word[1] = word[2] = word[3] = word[4] = 0;
         uint32_t *tsum = L.prec + 4 * L.pt_cap;
-        hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, dbuf, M, L.prec, tsum, qcount, L.pwide,
+        hipLaunchKernelGGL(pl_index<kPatIndexTPB>, dim3((unsigned)((T + kPatIndexTPB - 1) / kPatIndexTPB)), dim3(kPatT), 0,
+                           s, dbuf, M, T, L.prec, tsum, qcount, L.pwide,
                            L.host_word_dev, L.host_word_dev + 2, epoch);
         if (T > kPatDirect)
             hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev + 2, epoch);
@@ -2247,7 +2357,8 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     }
     uint32_t *tsum = P.prec + 4 * P.cap, *qcount = (uint32_t *)(P.aw + 6);
     const int vec = ((uintptr_t)g & 15) == 0;
-    hipLaunchKernelGGL(pl_index, dim3((unsigned)T), dim3(kPatT), 0, s, buf_dev, M, P.prec, tsum, qcount, P.pwide, P.aw,
+    hipLaunchKernelGGL(pl_index<kPatIndexTPB>, dim3((unsigned)((T + kPatIndexTPB - 1) / kPatIndexTPB)), dim3(kPatT), 0, s,
+                       buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw,
                        status, epoch);
     if (T > kPatDirect)
         hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, buf_dev, P.prec, T, P.pE, status, epoch);

@@ -495,10 +495,21 @@ private:
                              "of %zu; the reference's copy_from_slice panics)", (unsigned long long)total, L);
         if (in.bytes >= 8 && total > (uint64_t(1) << 36))
             return set_error(ONO_E_IO, "sparse gradient of %llu values: capacity overflow", (unsigned long long)total);
-        const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
-        int rc = tmp(std::max(cap, L));
+        int rc = tmp(L);  // a frame's claimed total never sizes device memory
         if (rc) return rc;
         size_t got = 0;
+        if (in.bytes >= 8 && total > L) {  // scatter: only [0, L) is added (the zip); validate all, keep L
+            std::vector<float> h(L);
+            rc = sparse_lift_prefix_host(r_->sp_rx, in.bytes, h.data(), L, &got);
+            if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
+            if (rc) return rc;
+            *k = std::min(got, L);
+            ONO_HIP(hipMemcpyAsync(tmp_for(c), h.data(), *k * sizeof(float), hipMemcpyHostToDevice, s_));
+            ONO_HIP(hipStreamSynchronize(s_));  // h is released on return
+            *vals = tmp_for(c);
+            return ONO_OK;
+        }
+        const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
         rc = ono_sparse_lift(tmp_for(c), cap, &got, r_->sp_rx, in.bytes, s_);
         // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
         if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());

@@ -335,22 +335,47 @@ def test_worker_event_check_matches_the_ring():
     ono_amd.worker_event_check(1, b"\0\0")
 
 
-@pytest.mark.parametrize("form,delta", [("dense", -3), ("dense", 5), ("sparse", -2), ("sparse", 4)])
+def _sparse_with_far_run(stream: bytes, total: int, far: int, vals) -> bytes:
+    """`stream` (a grad_drop of some prefix) with its total raised to `total`
+    and one more record whose run starts at element `far`."""
+    import struct
+    body = bytearray(stream)
+    body[:8] = total.to_bytes(8, "little")
+    # the end of the last run in the stream: replay the parse
+    gi, bi = 0, 8
+    while bi < len(stream):
+        off, ln = struct.unpack_from("<II", stream, bi)
+        gi += off + ln
+        bi += 8 + 2 * ln
+    h = O.f16_encode(np.asarray(vals, dtype=np.float32))
+    body += struct.pack("<II", far - gi, len(h)) + h.tobytes()
+    return bytes(body)
+
+
+@pytest.mark.parametrize("form,delta", [("dense", -3), ("dense", 5), ("sparse", -2), ("sparse", 4),
+                                        ("sparse_far", 1 << 34)])
 def test_tcp_ring_scatter_zip(form, delta):
     """A scatter gradient of another length than the hop's chunk is added over
     the shorter of the two (the zip of worker_ring.rs:141-143): the rest of the
-    chunk keeps its value, values past the chunk are dropped."""
+    chunk keeps its value, values past the chunk are dropped.  sparse_far: a
+    SparseGrad claiming 2^34 values with a run near 2^33 — the whole stream is
+    validated but only the chunk's length is materialised (a frame's claimed
+    total never sizes a device allocation)."""
     length = 10001
     x = O.synth(length, SEED + 11, 0)
     y = O.synth(length, SEED + 11, 1)
     w, (from_gpu, to_gpu), pairs = start_two_rank(length, x)
     (a, b), (c, d) = O.split_chunks(length, 2)
-    m = d - c + delta
-    peer = y[c:c + m] if delta < 0 else np.concatenate([y[c:d], y[:delta]])
+    far = form == "sparse_far"
+    m = d - c + (4 if far else delta)
+    peer = y[c:c + m] if m < d - c else np.concatenate([y[c:d], y[:m - (d - c)]])
     try:
         recv_frame(from_gpu)
         if form == "dense":
             to_gpu.sendall(O.frame_dense(O.f16_encode(peer)))
+        elif far:
+            st = O.grad_drop(peer, O.sparse_threshold(peer, 0.1))
+            to_gpu.sendall(frame_sparse(_sparse_with_far_run(bytes(st), delta, 1 << 33, [1.5, -2.0, 3.25])))
         else:
             to_gpu.sendall(frame_sparse(O.grad_drop(peer, O.sparse_threshold(peer, 0.1))))
         g_frame = recv_frame(from_gpu)  # the owner's gather push of chunk 1
