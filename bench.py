@@ -281,17 +281,20 @@ def _cpu_model() -> str:
 
 
 # ---------------------------------------------------------- local reduce
-def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
+def local_reduce(torch, ono_amd, steps: int, warmup: int, ks=(2, 4, 8), warm_rotations: int = 1,
+                 settle_s: float = 0.0) -> dict:
     """BASELINE config 2: ono_sum_scale_f32 over k 64 MiB buckets (÷k),
     device time from one HIP event pair on the launch stream around the K
     back-to-back launches (per-launch event pairs add ~2 us to a 30 us
     kernel, tools/stream_variants.hip "pull" mode).  Launches rotate over
     enough input/output sets that every launch reads from HBM (the working
-    set exceeds the 256 MiB Infinity Cache by > 4x)."""
+    set exceeds the 256 MiB Infinity Cache by > 4x).  ks / warm_rotations /
+    settle_s: knobs for tools/lr_ab.py (the warm-up covers that many whole
+    rotations; settle_s: a synchronised pause before the warm-up)."""
     n = 16 << 20
     out = {}
     stream = torch.cuda.Stream()  # a stream of its own (the ring's reductions run on the caller's)
-    for k in (2, 4, 8):
+    for k in ks:
         nsets = 1536 // ((k + 1) * 64) + 2  # > 1.5 GiB per rotation: every launch reads HBM
         sets = []
         for si in range(nsets):
@@ -302,12 +305,19 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int) -> dict:
         # warm-up covers a whole rotation: every set's pages touched once (the
         # outputs are fresh allocations; their first write takes page-table
         # fills that a ring's long-lived buckets pay once, not per round)
-        warm = max(warmup, nsets)
+        if settle_s:
+            torch.cuda.synchronize()
+            time.sleep(settle_s)
+        warm = max(warmup, nsets * warm_rotations)
         for i in range(warm):
             ins, dst = sets[i % nsets]
             ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
+        # no synchronisation between the warm-up and the opening event: the GPU is
+        # still busy with the warm-up when `a` is recorded, so the host enqueues
+        # the timed launches ahead of the GPU and the span holds K back-to-back
+        # kernels, not the host's latency to the first one (~10 us through
+        # Python: 0.5 us per launch at K = 20, 1.5 % of a 64 MiB sum2)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
         a.record(stream)
         for i in range(steps):
             ins, dst = sets[(warm + i) % nsets]
@@ -362,8 +372,7 @@ def copy_ceiling(torch, ono_amd, steps: int, warmup: int) -> dict:
             for i in range(warm):
                 fn(sets[i % nsets])
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            a.record(stream)
+            a.record(stream)  # behind the warm-up, no synchronisation (see local_reduce)
             for i in range(steps):
                 fn(sets[(warm + i) % nsets])
             b.record(stream)
@@ -410,8 +419,7 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
         for i in range(warm):
             launch(sets[i % nsets])
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        a.record(stream)
+        a.record(stream)  # behind the warm-up, no synchronisation (see local_reduce)
         for i in range(steps):
             launch(sets[(warm + i) % nsets])
         b.record(stream)
@@ -530,6 +538,8 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     ono_amd.sparse.grad_drop_async(g, t, buf, nbd)
     torch.cuda.synchronize()
     assert int(nbd.item()) == len(wire) and bytes(buf[: len(wire)].cpu().numpy()) == wire
+    for i in range(8):  # the GPU busy while the timed drops are enqueued (no host gap at the opening event)
+        ono_amd.sparse.grad_drop_async(gs[i % NG], tg[i % NG], buf, nbd)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
     for i in range(K):
@@ -582,6 +592,8 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     for i in range(NG):
         ono_amd.sparse.grad_lift_dev_async(wires[i], outs[i], st, stream)
     torch.cuda.synchronize()
+    for i in range(NG):  # the GPU busy while the timed lifts are enqueued (no host gap at the opening event)
+        ono_amd.sparse.grad_lift_dev_async(wires[i], outs[i], st, stream)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(stream)
     tickets = [ono_amd.sparse.grad_lift_dev_async(wires[i % NG], outs[i % NG], st, stream) for i in range(K)]

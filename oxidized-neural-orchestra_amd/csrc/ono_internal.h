@@ -70,6 +70,9 @@ int sparse_lift_prefix_host(const uint8_t *buf, size_t nbytes, float *out, size_
 // the library's own pure streams (T = float or uint16_t): dst = src, dst = value
 template <class T> hipError_t launch_copy(T *dst, const T *src, size_t n, hipStream_t s);
 template <class T> hipError_t launch_fill(T *dst, T value, size_t n, hipStream_t s);
+// device copies / zero fills of any alignment on those streams (ono_ring.cpp)
+hipError_t dev_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
+hipError_t dev_zero(void *dst, size_t bytes, hipStream_t s);
 
 // wire-templated hop kernels: W = uint16_t (f16 wire) or float (f32 wire)
 template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, hipStream_t s);

@@ -162,17 +162,32 @@ template <class Op> unsigned ew_lds(const Op &op, size_t n) {
     return 0u;
 }
 
+// Ops with little work per element (the write-only fill, the f16 gather
+// decode) use 256-thread workgroups instead (block() = 256): a one-shot grid of
+// one-wave workgroups is bounded by the dispatcher's workgroup rate — an empty
+// kernel over the 65,536 one-wave workgroups of a 64 MiB bucket takes 14.9 us
+// — and a 64 MiB fill then runs at 0.52 of 8 TB/s against 0.77 with 256-thread
+// workgroups; the decode gains 1-3 % (tools/launch_phases.hip,
+// profiles/r04_launch_phases_s3.txt).  Every other shape moves enough bytes per
+// workgroup that 64 threads stay best (+1-4 %).
+template <class Op, class = void> struct HasBlock : std::false_type {};
+template <class Op> struct HasBlock<Op, std::void_t<decltype(Op::block())>> : std::true_type {};
+template <class Op> constexpr int block_of() {
+    if constexpr (HasBlock<Op>::value) return Op::block();
+    else return kBlock;
+}
+
 // LOOP = false: the grid covers every vector (the one-shot grid), so no loop
 // at all — one guarded vector per lane (dec 2.5 %, sum8 1 % faster than the
 // loop form, tools/skeleton_variants.hip; profiles/r02_skeleton_variants.txt).
-template <class Op, bool LOOP>
-__global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t nvec, size_t n) {
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+template <class Op, bool LOOP, int B = block_of<Op>()>
+__global__ __launch_bounds__(B) void ew_kernel(Op op, size_t head, size_t nvec, size_t n) {
+    const size_t tid = (size_t)blockIdx.x * B + threadIdx.x;
     const size_t tail0 = head + 4 * nvec;
     if (tid < head) op.scalar(tid);
     if (tid < n - tail0) op.scalar(tail0 + tid);
     if constexpr (LOOP) {
-        const size_t stride = (size_t)gridDim.x * kBlock;
+        const size_t stride = (size_t)gridDim.x * B;
         for (size_t v = tid; v < nvec; v += stride) op.store(head + 4 * v, op.load(head + 4 * v));
     } else {
         if (tid < nvec) op.store(head + 4 * tid, op.load(head + 4 * tid));
@@ -181,10 +196,10 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(Op op, size_t head, size_t n
 }
 
 // scalar-only fallback for operands whose 4-element phases differ
-template <class Op>
-__global__ __launch_bounds__(kBlock) void ew_scalar_kernel(Op op, size_t n) {
-    const size_t stride = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) op.scalar(i);
+template <class Op, int B = block_of<Op>()>
+__global__ __launch_bounds__(B) void ew_scalar_kernel(Op op, size_t n) {
+    const size_t stride = (size_t)gridDim.x * B;
+    for (size_t i = (size_t)blockIdx.x * B + threadIdx.x; i < n; i += stride) op.scalar(i);
     finish_wave(op);
 }
 
@@ -228,28 +243,27 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     unsigned ph = phases[0];
     bool same = true;
     for (int i = 0; i < nph; i++) same &= (phases[i] == ph);
+    constexpr int B = block_of<Op>();
     const int bpc = blocks_per_cu();
-    const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc : (size_t)0x7FFFFFFF;
+    const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc * kBlock / B : (size_t)0x7FFFFFFF;
     const unsigned lds = ew_lds(op, n);
     if (!same) {
-        size_t blocks = (n + kBlock - 1) / kBlock;
+        size_t blocks = (n + B - 1) / B;
         if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(kBlock), lds, s, op, n);
+        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(B), lds, s, op, n);
         return hipGetLastError();
     }
     size_t head = (4 - ph) & 3u;
     if (head > n) head = n;
     size_t nvec = (n - head) / 4;
     size_t work = nvec > 4 ? nvec : 4; // threads needed (>= head/tail lanes)
-    size_t blocks = (work + kBlock - 1) / kBlock;
+    size_t blocks = (work + B - 1) / B;
     if (blocks < 1) blocks = 1;
     if (blocks > cap) {
-        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(kBlock), lds, s, op, head,
-                           nvec, n);
+        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(B), lds, s, op, head, nvec, n);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(kBlock), lds, s, op, head,
-                       nvec, n);
+    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(B), lds, s, op, head, nvec, n);
     return hipGetLastError();
 }
 
@@ -461,7 +475,10 @@ template <int M> struct ScaleZeroOp { // dst = src / d; zero = 0
 // the same skeleton — the copy ceiling the path's kernels are read against
 // (bench.py copy_ceiling) and the plan interpreter's device copies / zero
 // fills (ONO_PLAN_COPY / ONO_PLAN_MEMSET), in place of the runtime's blit
-// kernels.  Read-once source: nt loads; write-once output: nt stores.
+// kernels.  Read-once source: nt loads.  The copy's stores are `nt sc1`
+// (tools/launch_phases.hip, profiles/r04_launch_phases_s1.txt: 64 MiB 22.02 ->
+// 21.18 us, 256 MiB 80.58 -> 78.49 us; the boundary to the next launch 1.9 ->
+// 1.2 us, as no dirty L2 lines are left to write back).
 template <class T> struct CopyOp {
     typedef typename Wire<T>::V V;
     T *dst;
@@ -469,10 +486,13 @@ template <class T> struct CopyOp {
     typedef V R;
     __device__ __forceinline__ void scalar(size_t i) const { dst[i] = src[i]; }
     __device__ __forceinline__ R load(size_t i) const { return ldn((const V *)(src + i)); }
-    __device__ __forceinline__ void store(size_t i, R x) const { st_nt((V *)(dst + i), x); }
+    __device__ __forceinline__ void store(size_t i, R x) const { st_sc1((V *)(dst + i), x); }
 };
+// The fill: 256-thread workgroups and `nt sc1` stores (64 MiB 16.0 -> 10.95
+// us, 256 MiB 57.5 -> 39.7 us, against the runtime's fill kernel 11.4 / 40.2).
 template <class T> struct FillOp {
     typedef typename Wire<T>::V V;
+    static constexpr int block() { return 256; }
     T *dst;
     T value;
     typedef int R;
@@ -481,7 +501,7 @@ template <class T> struct FillOp {
     __device__ __forceinline__ void store(size_t i, R) const {
         V x;
         x.x = value; x.y = value; x.z = value; x.w = value;
-        st_nt((V *)(dst + i), x);
+        st_sc1((V *)(dst + i), x);
     }
 };
 
@@ -497,6 +517,7 @@ template <class W> struct EncodeOp {
 
 template <class W, int M> struct DecodeScaleOp {
     typedef typename Wire<W>::V WV;
+    static constexpr int block() { return 256; }  // 64 MiB 17.69 -> 17.46 us, 256 MiB 63.5 -> 61.6 us
     float *out;
     const W *in;
     float v;

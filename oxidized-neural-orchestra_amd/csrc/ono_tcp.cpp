@@ -599,8 +599,7 @@ private:
             }
         }
         const int own = mod(pos_ + 1);  // gather (:155-204)
-        ONO_HIP(hipMemcpyAsync(grad + off(own), res + off(own), len(own) * sizeof(float), hipMemcpyDeviceToDevice,
-                               s_));  // :166
+        ONO_HIP(dev_copy(grad + off(own), res + off(own), len(own) * sizeof(float), s_));  // :166
         for (int j = 0; j < n_ - 1; j++) {
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
@@ -609,7 +608,7 @@ private:
             if (sparse) {  // :177-190: keep the sent values; the owned residual stays (:178-184 commented out)
                 if ((rc = ono_sparse_mask(grad + off(cs), len(cs), t, 0, s_))) return rc;
             } else if (j == 0) {  // :191-193
-                ONO_HIP(hipMemsetAsync(res + off(own), 0, len(own) * sizeof(float), s_));
+                ONO_HIP(dev_zero(res + off(own), len(own) * sizeof(float), s_));
             }
             if (in.kind == KIND_DENSE) {
                 ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(1, cr), len(cr), 1.0f, s_));
@@ -617,7 +616,7 @@ private:
                 const float *v = nullptr;
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
-                ONO_HIP(hipMemcpyAsync(grad + off(cr), v, len(cr) * sizeof(float), hipMemcpyDeviceToDevice, s_));
+                ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
             }
         }
         ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105

@@ -358,7 +358,7 @@ def test_tcp_ring_scatter_zip(form, delta):
     """A scatter gradient of another length than the hop's chunk is added over
     the shorter of the two (the zip of worker_ring.rs:141-143): the rest of the
     chunk keeps its value, values past the chunk are dropped.  sparse_far: a
-    SparseGrad claiming 2^34 values with a run near 2^33 — the whole stream is
+    SparseGrad claiming 2^34 values with a run at 3 x 2^30 — the whole stream is
     validated but only the chunk's length is materialised (a frame's claimed
     total never sizes a device allocation)."""
     length = 10001
@@ -375,7 +375,7 @@ def test_tcp_ring_scatter_zip(form, delta):
             to_gpu.sendall(O.frame_dense(O.f16_encode(peer)))
         elif far:
             st = O.grad_drop(peer, O.sparse_threshold(peer, 0.1))
-            to_gpu.sendall(frame_sparse(_sparse_with_far_run(bytes(st), delta, 1 << 33, [1.5, -2.0, 3.25])))
+            to_gpu.sendall(frame_sparse(_sparse_with_far_run(bytes(st), delta, 3 << 30, [1.5, -2.0, 3.25])))
         else:
             to_gpu.sendall(frame_sparse(O.grad_drop(peer, O.sparse_threshold(peer, 0.1))))
         g_frame = recv_frame(from_gpu)  # the owner's gather push of chunk 1

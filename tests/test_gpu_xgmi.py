@@ -112,11 +112,24 @@ def test_xgmi_recreate_rings_in_the_same_processes(n):
     processes (the first torn down, the peers' regions re-imported).  Rings are
     now created, used and destroyed six times in the same processes: every
     connect checks each peer mapping page by page against the peer's ring id
-    (a stale import fails there with IoError), teardown frees a region only
-    after every peer has released it, and each cycle's host-fed sub-round
-    round is bit-exact."""
+    (a stale import fails there with IoError), teardown returns a region to
+    the process's pool only after every peer has marked it, and each cycle's
+    host-fed sub-round round is bit-exact.  With pooling the later cycles reuse
+    the pooled regions and mappings."""
     check(run_ranks(n, [{"kind": "recreate", "cycles": 6, "wire": "f16"},
                         {"kind": "recreate", "cycles": 2, "wire": "f32"}], ONO_HOST_CHUNK_MIB="1"))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_xgmi_pool_release_then_fresh_rings(n):
+    """ono_xgmi_pool_release between cycles: refused while a ring
+    is alive; once every rank's ring is destroyed it frees the pooled region and
+    closes the n - 1 imports, and the next ring exports a fresh region that the
+    peers import anew — the free-and-re-import path whose stale mappings caused
+    round 2's wrong result, now checked page by page at connect.  Every cycle
+    bit-exact with the oracle."""
+    check(run_ranks(n, [{"kind": "recreate", "cycles": 4, "wire": "f16", "release": True},
+                        {"kind": "recreate", "cycles": 2, "wire": "f32", "release": True}], ONO_HOST_CHUNK_MIB="1"))
 
 
 def test_xgmi_timing_phases():

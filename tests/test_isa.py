@@ -136,7 +136,8 @@ def _vec_loads(code):
 
 def _one_shot(kernels, op):
     """the one-shot (loop-free) instances of ew_kernel<op...>"""
-    return {k: v for k, v in kernels.items() if "ew_kernel" in k and op in k and k.endswith("Lb0EEEvT_mmm")}
+    return {k: v for k, v in kernels.items()
+            if "ew_kernel" in k and op in k and re.search(r"Lb0E(Li\d+E)?EEvT_mmm$", k)}
 
 
 def test_direct_chain_reads_received_slices_non_temporal(kernels):

@@ -236,7 +236,8 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
     the ring id in that peer's handle (a stale import is an IoError at
     connect); every cycle runs the host-fed sub-round round bit-exact."""
     cycles, length = case.get("cycles", 6), case.get("length", (1 << 20) + 3)
-    seen, repeats = set(), 0
+    release = case.get("release", False)  # ono_xgmi_pool_release between cycles: fresh exports and imports
+    seen, repeats, freed = set(), 0, 0
     for cyc in range(cycles):
         blobs = {}
 
@@ -258,9 +259,24 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
                 return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats so far {repeats})"
             if bits(res_h).any():
                 return f"cycle {cyc}: host residual not zeroed"
+            if release:  # refused while this process's ring is alive
+                try:
+                    ono_amd.xgmi_pool_release()
+                    return f"cycle {cyc}: pool release accepted while a ring is alive"
+                except ono_amd.InvalidArgument:
+                    pass
         finally:
             ring.close()
-    print(json.dumps({"rank": rank, "recreate_ipc_handle_repeats": repeats, "cycles": cycles}), file=sys.stderr)
+        if release:
+            dist.barrier()  # every rank's ring destroyed before anyone frees
+            r = ono_amd.xgmi_pool_release()
+            st = ono_amd.xgmi_pool_stats()
+            if r["freed_bytes"] <= 0 or r["closed_imports"] != n - 1 or st["regions"] or st["imports"]:
+                return f"cycle {cyc}: release {r}, stats after {st}"
+            freed += r["freed_bytes"]
+            dist.barrier()  # every import closed before the next ring exports
+    print(json.dumps({"rank": rank, "recreate_ipc_handle_repeats": repeats, "cycles": cycles, "released_bytes": freed}),
+          file=sys.stderr)
     return None
 
 

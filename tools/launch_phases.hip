@@ -64,6 +64,17 @@ __device__ __forceinline__ void st_sc1(f4 *p, f4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
 }
 
+// store policies for the boundary question: does a kernel that leaves no dirty L2 lines end sooner?
+__device__ __forceinline__ void st_sys(f4 *p, f4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+template <int POL> __device__ __forceinline__ void st_pol(f4 *p, f4 v) {
+    if constexpr (POL == 0) stn(p, v);
+    else if constexpr (POL == 1) st_sc1(p, v);
+    else if constexpr (POL == 2) st_sys(p, v);
+    else *p = v;
+}
+
 template <bool STAMP> struct Clock {
     uint64_t t0 = 0;
     __device__ __forceinline__ void start() {
@@ -84,20 +95,48 @@ template <bool STAMP> struct Clock {
     }
 };
 
-enum Shape { COPY = 0, COPYZ, FILL, SUM2, SUM4, SUM8, DEC, EMPTY, NSHAPES };
+enum Shape {
+    COPY = 0, COPYZ, FILL, SUM2, SUM4, SUM8, DEC, EMPTY, COPY_SC1, COPY_SYS, SUM2_SC1, SUM2_SYS,
+    FILL_SC1, FILL_SYS, FILL_PLAIN, DEC_SC1, DEC_SYS, DEC_PLAIN,
+    FILL_U4, FILL_U16, FILL_B256, FILL_GRID, DEC_U2, DEC_U4, DEC_B256, COPY_U2, COPY_B256, NSHAPES
+};
 static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 2R1W", "sum4 4R1W", "sum8 8R1W",
-                              "f16 decode", "empty"};
-static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0}, kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0};
+                              "f16 decode", "empty", "copy st nt sc1", "copy st sc0sc1", "sum2 st nt sc1",
+                              "sum2 st sc0sc1", "fill st nt sc1", "fill st sc0sc1", "fill st plain", "decode st nt sc1",
+                              "decode st sc0sc1", "decode st plain", "fill U4/lane", "fill U16/lane",
+                              "fill 256-thr wg", "fill grid 4/CU", "decode U2/lane", "decode U4/lane",
+                              "decode 256-thr wg", "copy U2/lane", "copy 256-thr wg"};
+static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0, 1, 1, 2, 2, 0, 0, 0, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1};
+static const int kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
 // algorithmic bytes per f32 element
-static const double kBytes[] = {8, 12, 4, 12, 20, 36, 6, 0};
+static const double kBytes[] = {8, 12, 4, 12, 20, 36, 6, 0, 8, 8, 12, 12, 4, 4, 4, 6, 6, 6,
+                                4, 4, 4, 4, 6, 6, 6, 8, 8};
+// workgroups per launch for the shapes that do not use one-wave workgroups of one vector per lane
+static size_t grid_of(int shape, size_t nvec, int cus) {
+    switch (shape) {
+    case FILL_U4: case DEC_U4: return (nvec + 255) / 256;
+    case FILL_U16: return (nvec + 1023) / 1024;
+    case DEC_U2: case COPY_U2: return (nvec + 127) / 128;
+    case FILL_B256: case DEC_B256: case COPY_B256: return (nvec + 255) / 256;
+    case FILL_GRID: return (size_t)cus * 4;
+    default: return (nvec + 63) / 64;
+    }
+}
+static int block_of(int shape) {
+    return shape == FILL_B256 || shape == DEC_B256 || shape == COPY_B256 || shape == FILL_GRID ? 256 : 64;
+}
+static_assert(sizeof(kBytes) / sizeof(kBytes[0]) == NSHAPES, "one row per shape");
 
-template <bool STAMP> __global__ __launch_bounds__(64) void k_copy(Args a) {
+template <bool STAMP, int POL> __device__ __forceinline__ void copy_body(const Args &a) {
     Clock<STAMP> c;
     c.start();
     const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
-    if (v < a.nvec) stn(a.out[0] + v, ldn(a.in[0] + v));
+    if (v < a.nvec) st_pol<POL>(a.out[0] + v, ldn(a.in[0] + v));
     c.stop(a.st);
 }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copy(Args a) { copy_body<STAMP, 0>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copy_sc1(Args a) { copy_body<STAMP, 1>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copy_sys(Args a) { copy_body<STAMP, 2>(a); }
 template <bool STAMP> __global__ __launch_bounds__(64) void k_copyz(Args a) {
     Clock<STAMP> c;
     c.start();
@@ -109,20 +148,24 @@ template <bool STAMP> __global__ __launch_bounds__(64) void k_copyz(Args a) {
     }
     c.stop(a.st);
 }
-template <bool STAMP> __global__ __launch_bounds__(64) void k_fill(Args a) {
+template <bool STAMP, int POL> __device__ __forceinline__ void fill_body(const Args &a) {
     Clock<STAMP> c;
     c.start();
     const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
-    if (v < a.nvec) stn(a.out[0] + v, f4{0, 0, 0, 0});
+    if (v < a.nvec) st_pol<POL>(a.out[0] + v, f4{0, 0, 0, 0});
     c.stop(a.st);
 }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_fill(Args a) { fill_body<STAMP, 0>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_fill_sc1(Args a) { fill_body<STAMP, 1>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_fill_sys(Args a) { fill_body<STAMP, 2>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_fill_plain(Args a) { fill_body<STAMP, 3>(a); }
 template <bool STAMP> __global__ __launch_bounds__(64) void k_empty(Args a) {
     Clock<STAMP> c;
     c.start();
     c.stop(a.st);
 }
 // the product's K = 2 form: both inputs by LDS-DMA, one wait, add from LDS
-template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2(Args a) {
+template <bool STAMP, int POL> __device__ __forceinline__ void sum2_body(const Args &a) {
     Clock<STAMP> c;
     c.start();
     __shared__ f4 lds[2][64];
@@ -133,10 +176,13 @@ template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2(Args a) {
             __builtin_amdgcn_global_load_lds((const void *)(a.in[j] + v), (__attribute__((address_space(3))) void *)&lds[j][0],
                                              16, 0, 2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stn(a.out[0] + v, (lds[0][threadIdx.x] + lds[1][threadIdx.x]) * 0.5f);
+        st_pol<POL>(a.out[0] + v, (lds[0][threadIdx.x] + lds[1][threadIdx.x]) * 0.5f);
     }
     c.stop(a.st);
 }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2(Args a) { sum2_body<STAMP, 0>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2_sc1(Args a) { sum2_body<STAMP, 1>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2_sys(Args a) { sum2_body<STAMP, 2>(a); }
 // the product's K >= 4 form: one load in flight per wave (occupancy capped by the launch)
 template <int K, bool STAMP> __global__ __launch_bounds__(64) void k_sumser(Args a) {
     Clock<STAMP> c;
@@ -156,7 +202,7 @@ template <int K, bool STAMP> __global__ __launch_bounds__(64) void k_sumser(Args
     c.stop(a.st);
 }
 // gather decode: 8-B f16 load, 16-B f32 store (the f16 input is the first half of in[0])
-template <bool STAMP> __global__ __launch_bounds__(64) void k_dec(Args a) {
+template <bool STAMP, int POL> __device__ __forceinline__ void dec_body(const Args &a) {
     Clock<STAMP> c;
     c.start();
     const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
@@ -167,8 +213,84 @@ template <bool STAMP> __global__ __launch_bounds__(64) void k_dec(Args a) {
         r.y = (float)__builtin_bit_cast(_Float16, h.y);
         r.z = (float)__builtin_bit_cast(_Float16, h.z);
         r.w = (float)__builtin_bit_cast(_Float16, h.w);
-        stn(a.out[0] + v, r * 0.5f);
+        st_pol<POL>(a.out[0] + v, r * 0.5f);
     }
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(64) void k_dec(Args a) { dec_body<STAMP, 0>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_dec_sc1(Args a) { dec_body<STAMP, 1>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_dec_sys(Args a) { dec_body<STAMP, 2>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_dec_plain(Args a) { dec_body<STAMP, 3>(a); }
+
+// U vectors per lane, one wave apart (every store instruction 1 KiB contiguous); fewer workgroups
+template <bool STAMP, int U> __global__ __launch_bounds__(64) void k_fill_u(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v0 = (size_t)blockIdx.x * 64 * U + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (v0 + 64 * u < a.nvec) st_sc1(a.out[0] + v0 + 64 * u, f4{0, 0, 0, 0});
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(256) void k_fill_b256(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < a.nvec) st_sc1(a.out[0] + v, f4{0, 0, 0, 0});
+    c.stop(a.st);
+}
+// the runtime fill's shape: a few 256-thread workgroups per CU, grid-stride
+template <bool STAMP> __global__ __launch_bounds__(256) void k_fill_grid(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < a.nvec; v += (size_t)gridDim.x * 256)
+        st_sc1(a.out[0] + v, f4{0, 0, 0, 0});
+    c.stop(a.st);
+}
+__device__ __forceinline__ f4 dec4h(h4 h) {
+    f4 r;
+    r.x = (float)__builtin_bit_cast(_Float16, h.x);
+    r.y = (float)__builtin_bit_cast(_Float16, h.y);
+    r.z = (float)__builtin_bit_cast(_Float16, h.z);
+    r.w = (float)__builtin_bit_cast(_Float16, h.w);
+    return r;
+}
+template <bool STAMP, int U> __global__ __launch_bounds__(64) void k_dec_u(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v0 = (size_t)blockIdx.x * 64 * U + threadIdx.x;
+    h4 h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = v0 + 64 * u < a.nvec ? ldn((const h4 *)a.in[0] + v0 + 64 * u) : h4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (v0 + 64 * u < a.nvec) stn(a.out[0] + v0 + 64 * u, dec4h(h[u]) * 0.5f);
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(256) void k_dec_b256(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < a.nvec) stn(a.out[0] + v, dec4h(ldn((const h4 *)a.in[0] + v)) * 0.5f);
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copy_u2(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v0 = (size_t)blockIdx.x * 128 + threadIdx.x;
+    f4 x[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) x[u] = v0 + 64 * u < a.nvec ? ldn(a.in[0] + v0 + 64 * u) : f4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+        if (v0 + 64 * u < a.nvec) st_sc1(a.out[0] + v0 + 64 * u, x[u]);
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(256) void k_copy_b256(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (v < a.nvec) st_sc1(a.out[0] + v, ldn(a.in[0] + v));
     c.stop(a.st);
 }
 
@@ -187,12 +309,16 @@ static int L = 24;
 static unsigned lds_for_occ(int occ) { return (unsigned)(160 * 1024 * 2 / (2 * occ + 1)); }
 
 // mode: 0 = un-stamped tool kernel, 1 = stamped tool kernel, 2 = LIB
+static int g_cus = 256;
 static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) {
-    const unsigned grid = (unsigned)((a.nvec + 63) / 64);
+    const unsigned grid = (unsigned)grid_of(shape, a.nvec, g_cus), blk = (unsigned)block_of(shape);
     const bool st = mode == 1;
 #define L2(KER) \
-    if (st) hipLaunchKernelGGL(KER<true>, dim3(grid), dim3(64), 0, s, a); \
-    else hipLaunchKernelGGL(KER<false>, dim3(grid), dim3(64), 0, s, a);
+    if (st) hipLaunchKernelGGL(KER<true>, dim3(grid), dim3(blk), 0, s, a); \
+    else hipLaunchKernelGGL(KER<false>, dim3(grid), dim3(blk), 0, s, a);
+#define L2T(KER, P) \
+    if (st) hipLaunchKernelGGL((KER<true, P>), dim3(grid), dim3(blk), 0, s, a); \
+    else hipLaunchKernelGGL((KER<false, P>), dim3(grid), dim3(blk), 0, s, a);
     if (mode == 2) {
         switch (shape) {
         case COPY: OK(ono_copy_f32((float *)a.out[0], (const float *)a.in[0], n, s)); return;
@@ -216,6 +342,25 @@ static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) 
     case SUM2: L2(k_sum2) break;
     case DEC: L2(k_dec) break;
     case EMPTY: L2(k_empty) break;
+    case COPY_SC1: L2(k_copy_sc1) break;
+    case COPY_SYS: L2(k_copy_sys) break;
+    case SUM2_SC1: L2(k_sum2_sc1) break;
+    case SUM2_SYS: L2(k_sum2_sys) break;
+    case FILL_SC1: L2(k_fill_sc1) break;
+    case FILL_SYS: L2(k_fill_sys) break;
+    case FILL_PLAIN: L2(k_fill_plain) break;
+    case DEC_SC1: L2(k_dec_sc1) break;
+    case DEC_SYS: L2(k_dec_sys) break;
+    case DEC_PLAIN: L2(k_dec_plain) break;
+    case FILL_U4: L2T(k_fill_u, 4) break;
+    case FILL_U16: L2T(k_fill_u, 16) break;
+    case FILL_B256: L2(k_fill_b256) break;
+    case FILL_GRID: L2(k_fill_grid) break;
+    case DEC_U2: L2T(k_dec_u, 2) break;
+    case DEC_U4: L2T(k_dec_u, 4) break;
+    case DEC_B256: L2(k_dec_b256) break;
+    case COPY_U2: L2(k_copy_u2) break;
+    case COPY_B256: L2(k_copy_b256) break;
     case SUM4:
         if (st) hipLaunchKernelGGL((k_sumser<4, true>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
         else hipLaunchKernelGGL((k_sumser<4, false>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
@@ -226,6 +371,7 @@ static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) 
         break;
     }
 #undef L2
+#undef L2T
     CK(hipGetLastError());
 }
 
@@ -278,15 +424,62 @@ static Phases analyse(const std::vector<Stamp> &h, size_t nwg, double bytes) {
             median(xcd) / 1e3, median(rate), median(fls) / 1e3, median(tail) / 1e3};
 }
 
+// Per XCD of one launch (the median launch by span): workgroups, first start and last end relative to
+// the launch's first start, median workgroup lifetime; and how many workgroups each XCD finishes in
+// the launch's last microsecond.
+static void xcd_detail(const std::vector<Stamp> &h, size_t nwg, const char *name) {
+    std::vector<std::pair<double, int>> spans;
+    for (int i = 0; i < L; i++) {
+        const Stamp *s = &h[(size_t)i * nwg];
+        double lo = 1e300, hi = 0;
+        for (size_t w = 0; w < nwg; w++) {
+            const double t0 = (double)(((uint64_t)s[w].t0_hi << 32) | s[w].t0_lo) * 10.0;
+            lo = std::min(lo, t0);
+            hi = std::max(hi, t0 + s[w].dt * 10.0);
+        }
+        spans.push_back({hi - lo, i});
+    }
+    std::sort(spans.begin(), spans.end());
+    const int i = spans[spans.size() / 2].second;
+    const Stamp *s = &h[(size_t)i * nwg];
+    double lo = 1e300, hi = 0;
+    for (size_t w = 0; w < nwg; w++) {
+        const double t0 = (double)(((uint64_t)s[w].t0_hi << 32) | s[w].t0_lo) * 10.0;
+        lo = std::min(lo, t0);
+        hi = std::max(hi, t0 + s[w].dt * 10.0);
+    }
+    printf("#   %s, launch %d (median span %.2f us), per XCD: wgs first_start last_start last_end median_life "
+           "ends_in_last_us  (us from the launch's first start)\n", name, i, (hi - lo) / 1e3);
+    for (int x = 0; x < 8; x++) {
+        std::vector<double> life;
+        double fs = 1e300, ls = 0, le = 0;
+        int tail = 0;
+        for (size_t w = 0; w < nwg; w++) {
+            if (((s[w].ids >> 16) & 0xF) != (unsigned)x) continue;
+            const double t0 = (double)(((uint64_t)s[w].t0_hi << 32) | s[w].t0_lo) * 10.0 - lo;
+            const double t1 = t0 + s[w].dt * 10.0;
+            fs = std::min(fs, t0);
+            ls = std::max(ls, t0);
+            le = std::max(le, t1);
+            life.push_back(s[w].dt * 10.0);
+            tail += t1 > (hi - lo) - 1000.0;
+        }
+        if (life.empty()) continue;
+        printf("#     xcd %d  %6zu  %7.2f  %7.2f  %7.2f  %6.2f  %5d\n", x, life.size(), fs / 1e3, ls / 1e3, le / 1e3,
+               median(life) / 1e3, tail);
+    }
+}
+
 static void run_size(size_t mib, hipStream_t s) {
-    const size_t n = mib << 18, nvec = n / 4, nwg = (nvec + 63) / 64;
+    const size_t n = mib << 18, nvec = n / 4, nwg_max = (nvec + 63) / 64;
     Stamp *dst;
-    CK(hipMalloc(&dst, sizeof(Stamp) * nwg * L));
-    printf("\n# %zu MiB per buffer (%zu f32, %zu workgroups), %d back-to-back launches per row, medians\n", mib, n, nwg,
+    CK(hipMalloc(&dst, sizeof(Stamp) * nwg_max * L));
+    printf("\n# %zu MiB per buffer (%zu f32, %zu workgroups), %d back-to-back launches per row, medians\n", mib, n, nwg_max,
            L);
     printf("# %-16s %9s %9s %9s | %8s %7s %7s %7s %7s %7s %7s %7s | %8s %6s\n", "shape", "ev_us", "stamp_us", "lib_us",
            "span", "gap", "ramp", "ideal", "drain", "xcd", "dstart", "tail", "R_GB/s", "frac");
     for (int shape = 0; shape < NSHAPES; shape++) {
+        const size_t nwg = grid_of(shape, nvec, g_cus);
         const int per = kReads[shape] + kWrites[shape];
         const int nsets = per ? kPool / per : 1;
         auto args = [&](int it) {
@@ -301,7 +494,7 @@ static void run_size(size_t mib, hipStream_t s) {
         double us[3] = {0, 0, 0};
         std::vector<Stamp> h;
         for (int mode = 0; mode < 3; mode++) {
-            if (mode == 2 && (shape == EMPTY)) continue;
+            if (mode == 2 && (shape == EMPTY || shape >= COPY_SC1)) continue;
             for (int it = 0; it < nsets + 2; it++) launch(shape, mode, args(it), n, s);  // whole rotation touched
             CK(hipStreamSynchronize(s));
             hipEvent_t e0, e1;
@@ -327,6 +520,7 @@ static void run_size(size_t mib, hipStream_t s) {
         }
         const double bytes = kBytes[shape] * (double)n;
         const Phases p = analyse(h, nwg, bytes);
+        if (shape == SUM2 || shape == COPY || shape == SUM8) xcd_detail(h, nwg, kName[shape]);
         const double best = us[2] > 0 ? std::min(us[0], us[2]) : us[0];
         printf("%-18s %9.2f %9.2f %9.2f | %8.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f %7.2f | %8.0f %6.3f\n", kName[shape],
                us[0], us[1], us[2], p.span, p.gap, p.ramp, p.ideal, p.drain, p.xcd, p.first_to_last_start, p.tail,
@@ -348,6 +542,7 @@ int main(int argc, char **argv) {
     g_max_elems = mx << 18;
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
+    g_cus = p.multiProcessorCount;
     printf("# launch_phases: %s, %d CUs; stamps = s_memrealtime (100 MHz) per workgroup, lane 0\n", p.gcnArchName,
            p.multiProcessorCount);
     printf("# ev_us: HIP events around L launches (un-stamped tool kernel); stamp_us: the stamped build; lib_us: the\n"

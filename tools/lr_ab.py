@@ -5,6 +5,8 @@ rotation).  Variants of the bench loop:
   bench      bench.local_reduce as shipped (ono_amd.kernels.sum_scale per launch)
   raw        the same buffers, prebuilt ctypes argument arrays (no wrapper)
   fresh      raw over a newly allocated set of buffers each pass
+  bench_k_only / bench_warm4 / bench_settle   bench.local_reduce for this k alone; with four
+             rotations of warm-up; with a synchronised 0.5 s pause before the warm-up
 
 usage: python tools/lr_ab.py [passes=3] [steps=40]
 """
@@ -76,6 +78,12 @@ def main():
         for _ in range(passes):
             lr = bench.local_reduce(torch, ono_amd, steps, 3)
             res.setdefault((k, "bench"), []).append(lr[f"k{k}"]["us_per_launch"])
+            lr = bench.local_reduce(torch, ono_amd, steps, 3, ks=(k,))
+            res.setdefault((k, "bench_k_only"), []).append(lr[f"k{k}"]["us_per_launch"])
+            lr = bench.local_reduce(torch, ono_amd, steps, 3, ks=(k,), warm_rotations=4)
+            res.setdefault((k, "bench_warm4"), []).append(lr[f"k{k}"]["us_per_launch"])
+            lr = bench.local_reduce(torch, ono_amd, steps, 3, ks=(k,), settle_s=0.5)
+            res.setdefault((k, "bench_settle"), []).append(lr[f"k{k}"]["us_per_launch"])
             res.setdefault((k, "wrapped"), []).append(wrapped(sets, k, steps, stream))
             res.setdefault((k, "raw"), []).append(raw(sets, k, steps, stream))
             fresh = make_sets(k)
