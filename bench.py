@@ -282,60 +282,68 @@ def _cpu_model() -> str:
 
 # ---------------------------------------------------------- local reduce
 def local_reduce(torch, ono_amd, steps: int, warmup: int, ks=(2, 4, 8), warm_rotations: int = 1,
-                 settle_s: float = 0.0) -> dict:
+                 settle_s: float = 0.0, passes: int = 3) -> dict:
     """BASELINE config 2: ono_sum_scale_f32 over k 64 MiB buckets (÷k),
     device time from one HIP event pair on the launch stream around the K
     back-to-back launches (per-launch event pairs add ~2 us to a 30 us
     kernel, tools/stream_variants.hip "pull" mode).  Launches rotate over
     enough input/output sets that every launch reads from HBM (the working
-    set exceeds the 256 MiB Infinity Cache by > 4x).  ks / warm_rotations /
-    settle_s: knobs for tools/lr_ab.py (the warm-up covers that many whole
-    rotations; settle_s: a synchronised pause before the warm-up)."""
+    set exceeds the 256 MiB Infinity Cache by > 4x).
+
+    One pool of 64 MiB buffers serves every k (allocated once: the same
+    kernel measured over freshly allocated buffers moved by up to 4 % with the
+    placement, profiles/r04_lr_ab_s{3,4}.txt), and each k is measured in
+    `passes` passes interleaved with the other k's; the reported figure is the
+    median pass (min / max beside it).  ks / warm_rotations / settle_s: knobs
+    for tools/lr_ab.py (warm-up rotations; a synchronised pause before it)."""
     n = 16 << 20
     out = {}
     stream = torch.cuda.Stream()  # a stream of its own (the ring's reductions run on the caller's)
+    nsets = {k: 1536 // ((k + 1) * 64) + 2 for k in ks}  # > 1.5 GiB per rotation: every launch reads HBM
+    pool = []
+    for b in range(max(nsets[k] * (k + 1) for k in ks)):
+        pool.append(ono_amd.kernels.synth(torch.empty(n, dtype=torch.float32, device="cuda"), SEED + b // 9, b % 9))
+    sets = {k: [(pool[s * (k + 1):s * (k + 1) + k], pool[s * (k + 1) + k]) for s in range(nsets[k])] for k in ks}
+    ms = {k: [] for k in ks}
+    for _ in range(passes):
+        for k in ks:
+            ns = nsets[k]
+            if settle_s:
+                torch.cuda.synchronize()
+                time.sleep(settle_s)
+            # the warm-up covers a whole rotation (every set's pages touched); no synchronisation
+            # between it and the opening event: the GPU is still busy with the warm-up when `a` is
+            # recorded, so the host enqueues the timed launches ahead of the GPU and the span holds K
+            # back-to-back kernels, not the host's latency to the first one (~10 us through Python:
+            # 0.5 us per launch at K = 20, 1.5 % of a 64 MiB sum2)
+            warm = max(warmup, ns * warm_rotations)
+            for i in range(warm):
+                ins, dst = sets[k][i % ns]
+                ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for i in range(steps):
+                ins, dst = sets[k][(warm + i) % ns]
+                ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
+            b.record(stream)
+            b.synchronize()
+            ms[k].append(a.elapsed_time(b) / steps)
     for k in ks:
-        nsets = 1536 // ((k + 1) * 64) + 2  # > 1.5 GiB per rotation: every launch reads HBM
-        sets = []
-        for si in range(nsets):
-            ins = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(k)]
-            for r, t in enumerate(ins):
-                ono_amd.kernels.synth(t, SEED + si, r)
-            sets.append((ins, torch.empty(n, dtype=torch.float32, device="cuda")))
-        # warm-up covers a whole rotation: every set's pages touched once (the
-        # outputs are fresh allocations; their first write takes page-table
-        # fills that a ring's long-lived buckets pay once, not per round)
-        if settle_s:
-            torch.cuda.synchronize()
-            time.sleep(settle_s)
-        warm = max(warmup, nsets * warm_rotations)
-        for i in range(warm):
-            ins, dst = sets[i % nsets]
-            ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
-        # no synchronisation between the warm-up and the opening event: the GPU is
-        # still busy with the warm-up when `a` is recorded, so the host enqueues
-        # the timed launches ahead of the GPU and the span holds K back-to-back
-        # kernels, not the host's latency to the first one (~10 us through
-        # Python: 0.5 us per launch at K = 20, 1.5 % of a 64 MiB sum2)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for i in range(steps):
-            ins, dst = sets[(warm + i) % nsets]
-            ono_amd.kernels.sum_scale(dst, ins, float(k), stream)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / steps
+        v = sorted(ms[k])
+        med = v[len(v) // 2]
         nbytes = (k + 1) * 4 * n
-        gbs = nbytes / (ms * 1e-3) / 1e9
+        gbs = nbytes / (med * 1e-3) / 1e9
         pmc = pmc_traffic(f"SumScaleOp<{k},", n)
-        out[f"k{k}"] = {"bytes_per_launch": nbytes, "us_per_launch": round(ms * 1e3, 2),
+        out[f"k{k}"] = {"bytes_per_launch": nbytes, "us_per_launch": round(med * 1e3, 2),
                         "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
-                        "rotating_sets": nsets,
+                        "us_per_launch_min": round(v[0] * 1e3, 2), "us_per_launch_max": round(v[-1] * 1e3, 2),
+                        "passes": len(v), "rotating_sets": nsets[k],
                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
-        del sets
-        torch.cuda.empty_cache()
+    del sets, pool
+    torch.cuda.empty_cache()
     return {"workload": "sum_scale_f32, 64 MiB buckets, out = (sum of k inputs) / k", "hbm_peak_gbs": HBM_PEAK_GBS,
-            "timing": "one HIP event pair around K back-to-back launches (inter-kernel gaps included)",
+            "timing": f"one HIP event pair around K back-to-back launches (inter-kernel gaps included); median "
+                      f"of {passes} passes interleaved across k, over one buffer pool",
             **out}
 
 

@@ -162,19 +162,27 @@ template <class Op> unsigned ew_lds(const Op &op, size_t n) {
     return 0u;
 }
 
-// Ops with little work per element (the write-only fill, the f16 gather
-// decode) use 256-thread workgroups instead (block() = 256): a one-shot grid of
-// one-wave workgroups is bounded by the dispatcher's workgroup rate — an empty
-// kernel over the 65,536 one-wave workgroups of a 64 MiB bucket takes 14.9 us
-// — and a 64 MiB fill then runs at 0.52 of 8 TB/s against 0.77 with 256-thread
-// workgroups; the decode gains 1-3 % (tools/launch_phases.hip,
-// profiles/r04_launch_phases_s3.txt).  Every other shape moves enough bytes per
-// workgroup that 64 threads stay best (+1-4 %).
+// The write-only fill uses 256-thread workgroups instead (block() = 256): a
+// one-shot grid of one-wave workgroups is bounded by the dispatcher's workgroup
+// rate — an empty kernel over the 65,536 one-wave workgroups of a 64 MiB bucket
+// takes 14.9 us — and a 64 MiB fill then runs at 0.52 of 8 TB/s against 0.81
+// with 256-thread workgroups (tools/launch_phases.hip,
+// profiles/r04_launch_phases_s3.txt, tools/pk_ab.py).  Every other shape moves
+// enough bytes per workgroup that 64 threads stay best (+1-4 %; the f16 decode
+// too, on the bench's data).  ONO_EW_WIDE=0 runs the fill on 64 threads (A/B).
 template <class Op, class = void> struct HasBlock : std::false_type {};
 template <class Op> struct HasBlock<Op, std::void_t<decltype(Op::block())>> : std::true_type {};
 template <class Op> constexpr int block_of() {
     if constexpr (HasBlock<Op>::value) return Op::block();
     else return kBlock;
+}
+// ONO_EW_WIDE=0: the 256-thread ops run with 64-thread workgroups too (measurement A/B)
+bool wide_blocks() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_EW_WIDE");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
 }
 
 // LOOP = false: the grid covers every vector (the one-shot grid), so no loop
@@ -237,20 +245,22 @@ inline unsigned phase_of(const void *p, size_t esz) {
 }
 
 // Launch `op` over n elements.  phases: the 4-element phase of every operand.
-template <class Op>
+template <class Op, int B = block_of<Op>()>
 hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    if constexpr (B != kBlock) {
+        if (!wide_blocks()) return launch_ew_arr<Op, kBlock>(op, n, phases, nph, s);
+    }
     unsigned ph = phases[0];
     bool same = true;
     for (int i = 0; i < nph; i++) same &= (phases[i] == ph);
-    constexpr int B = block_of<Op>();
     const int bpc = blocks_per_cu();
     const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc * kBlock / B : (size_t)0x7FFFFFFF;
     const unsigned lds = ew_lds(op, n);
     if (!same) {
         size_t blocks = (n + B - 1) / B;
         if (blocks > cap) blocks = cap;
-        hipLaunchKernelGGL(ew_scalar_kernel<Op>, dim3((unsigned)blocks), dim3(B), lds, s, op, n);
+        hipLaunchKernelGGL((ew_scalar_kernel<Op, B>), dim3((unsigned)blocks), dim3(B), lds, s, op, n);
         return hipGetLastError();
     }
     size_t head = (4 - ph) & 3u;
@@ -260,10 +270,10 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
     size_t blocks = (work + B - 1) / B;
     if (blocks < 1) blocks = 1;
     if (blocks > cap) {
-        hipLaunchKernelGGL((ew_kernel<Op, true>), dim3((unsigned)cap), dim3(B), lds, s, op, head, nvec, n);
+        hipLaunchKernelGGL((ew_kernel<Op, true, B>), dim3((unsigned)cap), dim3(B), lds, s, op, head, nvec, n);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((ew_kernel<Op, false>), dim3((unsigned)blocks), dim3(B), lds, s, op, head, nvec, n);
+    hipLaunchKernelGGL((ew_kernel<Op, false, B>), dim3((unsigned)blocks), dim3(B), lds, s, op, head, nvec, n);
     return hipGetLastError();
 }
 
@@ -517,7 +527,8 @@ template <class W> struct EncodeOp {
 
 template <class W, int M> struct DecodeScaleOp {
     typedef typename Wire<W>::V WV;
-    static constexpr int block() { return 256; }  // 64 MiB 17.69 -> 17.46 us, 256 MiB 63.5 -> 61.6 us
+    // (64-thread workgroups: 256 measured 17.46 vs 17.69 us on the tool's data but 18.4 vs 17.6 us on the
+    // bench's synthetic f16 gradients, tools/pk_ab.py, profiles/r04_pk_ab_s6.txt)
     float *out;
     const W *in;
     float v;

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
 // prefixes and publishes the chunk's aggregate.  Each sp_move wave folds the
 // aggregates before / after its chunk into the chunk's carry itself (no
 // arrival counter, no serial pass over the chunks).
-constexpr int kRecT = 256, kRecPer = 2, kRecChunk = kRecT * kRecPer;  // 512 tiles per workgroup
+constexpr int kRecT = 64, kRecPer = 2, kRecChunk = kRecT * kRecPer;  // 128 tiles per one-wave workgroup
 __global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, uint4 *agg, size_t ntiles,
                                                       uint32_t n) {
     __shared__ uint32_t la[kRecChunk], lb[kRecChunk];
@@ -1387,7 +1387,25 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, si
     }
     if (bad) raise_bad(badw, epoch);
 }
-constexpr int kPatIndexTPB = 2;  // tiles per pl_index workgroup
+// tiles per pl_index workgroup: 1, or 2 (each thread's loads for both tiles issued together); env
+// ONO_PL_TPB selects for measurement (profiles/r04_*: 1 -> 8.7-9.1 us, 2 -> 9.35 us at 64 MiB / 10 %)
+int pl_index_tpb() {
+    static const int v = [] {
+        const char *e = getenv("ONO_PL_TPB");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
+hipError_t launch_pl_index(const uint8_t *b, size_t M, size_t T, uint32_t *rec, uint32_t *tsum, uint32_t *qcount,
+                           uint32_t *wide, uint64_t *host_word, uint64_t *badw, uint32_t epoch, hipStream_t s) {
+    if (pl_index_tpb() == 2)
+        hipLaunchKernelGGL(pl_index<2>, dim3((unsigned)((T + 1) / 2)), dim3(kPatT), 0, s, b, M, T, rec, tsum, qcount,
+                           wide, host_word, badw, epoch);
+    else
+        hipLaunchKernelGGL(pl_index<1>, dim3((unsigned)T), dim3(kPatT), 0, s, b, M, T, rec, tsum, qcount, wide, host_word,
+                           badw, epoch);
+    return hipGetLastError();
+}
 
 // E[t] = the element index tile t's range starts at: one workgroup scans the
 // tiles' sums, 4 per thread, kPatScanT x 4 tiles per step (DPP wave scans; the
@@ -1600,14 +1618,15 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     // tiles' sums), the record of each of the 256 tiles before it (the nearest non-empty one's exit is
     // the link into this tile)
     const uint4 me = ((const uint4 *)rec)[t];
-    constexpr int kSumPer = (int)(kPatDirect / kPatT);
-    uint32_t sums[kSumPer];
+    // (the earlier tiles' sums as 16-B vectors, 4 loads per thread: tsum holds a multiple of 4 entries)
+    constexpr int kSumVec = (int)(kPatDirect / (4 * kPatT));
+    uint4 sums[kSumVec];
     uint64_t E0 = 0, E1 = 0;
     if (direct) {
 #pragma unroll
-        for (int q = 0; q < kSumPer; q++) {
-            const uint32_t i = threadIdx.x + (uint32_t)q * kPatT;
-            sums[q] = i < t ? tsum[i] : 0u;
+        for (int q = 0; q < kSumVec; q++) {
+            const uint32_t i = 4 * (threadIdx.x + (uint32_t)q * kPatT);
+            sums[q] = i < t ? *(const uint4 *)(tsum + i) : make_uint4(0, 0, 0, 0);
         }
     } else {
         E0 = E[t];
@@ -1625,7 +1644,11 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         uint64_t part = 0;
         if (direct) {
 #pragma unroll
-            for (int q = 0; q < kSumPer; q++) part += sums[q];
+            for (int q = 0; q < kSumVec; q++) {
+                const uint32_t i = 4 * (threadIdx.x + (uint32_t)q * kPatT);
+                part += (i < t ? sums[q].x : 0u) + (i + 1 < t ? sums[q].y : 0u) + (i + 2 < t ? sums[q].z : 0u) +
+                        (i + 3 < t ? sums[q].w : 0u);
+            }
         }
         // (index + 1) << 32 | exit of the nearest non-empty tile among the 256 before t
         const uint64_t key0 = threadIdx.x < t && near.x > 0 ? (uint64_t)(t - threadIdx.x) << 32 | near.w : 0;
@@ -2045,6 +2068,7 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
     if (g_lift_mode.load() == 0 && M > 0 && (nbytes & 1) == 0) {
         const size_t T = (M + kPatU - 1) / kPatU;
         if (T > L.pt_cap) {
+            const size_t Tc = (T + 3) & ~(size_t)3;  // tile sums read as 16-B vectors
             (void)hipFree(L.prec);
             (void)hipFree(L.pE);
             (void)hipFree(L.pwide);
@@ -2052,16 +2076,15 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
             L.pE = nullptr;
             L.pwide = nullptr;
             L.pt_cap = 0;
-            ONO_HIP(hipMalloc((void **)&L.prec, 5 * T * sizeof(uint32_t)));  // records, then the sums again
-            ONO_HIP(hipMalloc((void **)&L.pE, (T + 1) * sizeof(uint64_t)));
-            ONO_HIP(hipMalloc((void **)&L.pwide, T * sizeof(uint32_t)));
-            L.pt_cap = T;
+            ONO_HIP(hipMalloc((void **)&L.prec, 5 * Tc * sizeof(uint32_t)));  // records, then the sums again
+            ONO_HIP(hipMalloc((void **)&L.pE, (Tc + 1) * sizeof(uint64_t)));
+            ONO_HIP(hipMalloc((void **)&L.pwide, Tc * sizeof(uint32_t)));
+            L.pt_cap = Tc;
         }
         word[1] = word[2] = word[3] = word[4] = 0;
         uint32_t *tsum = L.prec + 4 * L.pt_cap;
-        hipLaunchKernelGGL(pl_index<kPatIndexTPB>, dim3((unsigned)((T + kPatIndexTPB - 1) / kPatIndexTPB)), dim3(kPatT), 0,
-                           s, dbuf, M, T, L.prec, tsum, qcount, L.pwide,
-                           L.host_word_dev, L.host_word_dev + 2, epoch);
+        ONO_HIP(launch_pl_index(dbuf, M, T, L.prec, tsum, qcount, L.pwide, L.host_word_dev, L.host_word_dev + 2, epoch,
+                                s));
         if (T > kPatDirect)
             hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, dbuf, L.prec, T, L.pE, L.host_word_dev + 2, epoch);
         hipLaunchKernelGGL(pl_place<false>, dim3((unsigned)T), dim3(kPatT), 0, s, g, dbuf, M, T, cap, vec, L.pE, L.prec, tsum,
@@ -2343,6 +2366,7 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     }
     const size_t T = (M + kPatU - 1) / kPatU;
     if (T > P.cap) {  // (hipFree waits for the work that still uses the old arrays)
+        const size_t Tc = (T + 3) & ~(size_t)3;  // tile sums read as 16-B vectors
         (void)hipFree(P.prec);
         (void)hipFree(P.pE);
         (void)hipFree(P.pwide);
@@ -2350,16 +2374,14 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
         P.pE = nullptr;
         P.pwide = nullptr;
         P.cap = 0;
-        ONO_HIP(hipMalloc((void **)&P.prec, 5 * T * sizeof(uint32_t)));
-        ONO_HIP(hipMalloc((void **)&P.pE, (T + 1) * sizeof(uint64_t)));
-        ONO_HIP(hipMalloc((void **)&P.pwide, T * sizeof(uint32_t)));
-        P.cap = T;
+        ONO_HIP(hipMalloc((void **)&P.prec, 5 * Tc * sizeof(uint32_t)));
+        ONO_HIP(hipMalloc((void **)&P.pE, (Tc + 1) * sizeof(uint64_t)));
+        ONO_HIP(hipMalloc((void **)&P.pwide, Tc * sizeof(uint32_t)));
+        P.cap = Tc;
     }
     uint32_t *tsum = P.prec + 4 * P.cap, *qcount = (uint32_t *)(P.aw + 6);
     const int vec = ((uintptr_t)g & 15) == 0;
-    hipLaunchKernelGGL(pl_index<kPatIndexTPB>, dim3((unsigned)((T + kPatIndexTPB - 1) / kPatIndexTPB)), dim3(kPatT), 0, s,
-                       buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw,
-                       status, epoch);
+    ONO_HIP(launch_pl_index(buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw, status, epoch, s));
     if (T > kPatDirect)
         hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, buf_dev, P.prec, T, P.pE, status, epoch);
     hipLaunchKernelGGL(pl_place<true>, dim3((unsigned)T), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.pE, P.prec,

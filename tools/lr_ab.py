@@ -5,6 +5,7 @@ rotation).  Variants of the bench loop:
   bench      bench.local_reduce as shipped (ono_amd.kernels.sum_scale per launch)
   raw        the same buffers, prebuilt ctypes argument arrays (no wrapper)
   fresh      raw over a newly allocated set of buffers each pass
+  carved / carved_skew68k   raw over buffers carved from one allocation (each 68 KiB further)
   bench_k_only / bench_warm4 / bench_settle   bench.local_reduce for this k alone; with four
              rotations of warm-up; with a synchronised 0.5 s pause before the warm-up
 
@@ -33,6 +34,18 @@ def make_sets(k):
         ins = [ono_amd.kernels.synth(torch.empty(N, device="cuda"), 7 + si, r) for r in range(k)]
         sets.append((ins, torch.empty(N, device="cuda")))
     return sets
+
+
+def carved_sets(k, skew_bytes=0):
+    """every buffer of the rotation carved from ONE allocation (optionally each
+    one `skew_bytes` further than the previous one's end)"""
+    nsets = 1536 // ((k + 1) * 64) + 2
+    per = N + skew_bytes // 4
+    big = torch.empty(per * nsets * (k + 1), device="cuda")
+    views = [big[i * per:i * per + N] for i in range(nsets * (k + 1))]
+    for i, v in enumerate(views):
+        ono_amd.kernels.synth(v, 7 + i // (k + 1), i % (k + 1))
+    return [(views[s * (k + 1):s * (k + 1) + k], views[s * (k + 1) + k]) for s in range(nsets)], big
 
 
 def raw(sets, k, steps, stream, warmup=3):
@@ -73,7 +86,7 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     stream = torch.cuda.Stream()
     res = {}
-    for k in (8, 4):
+    for k in (8, 4, 2):
         sets = make_sets(k)
         for _ in range(passes):
             lr = bench.local_reduce(torch, ono_amd, steps, 3)
@@ -89,6 +102,12 @@ def main():
             fresh = make_sets(k)
             res.setdefault((k, "fresh"), []).append(raw(fresh, k, steps, stream))
             del fresh
+            cs, big = carved_sets(k)
+            res.setdefault((k, "carved"), []).append(raw(cs, k, steps, stream))
+            del cs, big
+            cs, big = carved_sets(k, 4096 * 17)
+            res.setdefault((k, "carved_skew68k"), []).append(raw(cs, k, steps, stream))
+            del cs, big
             torch.cuda.empty_cache()
         del sets
         torch.cuda.empty_cache()
