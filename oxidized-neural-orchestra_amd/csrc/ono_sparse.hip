@@ -1575,27 +1575,37 @@ __device__ __forceinline__ void wide_tile(float *g, const uint8_t *b, size_t M, 
     }
 }
 
-// One block-wide reduction of a u64 sum and a u64 max (one LDS exchange).
-template <int NT>
-__device__ __forceinline__ void block_sum_max64(uint64_t s, uint64_t x, uint64_t &S, uint64_t &X) {
-    __shared__ uint64_t ws[NT / 64], wx[NT / 64];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        s += (uint64_t)__shfl_xor((unsigned long long)s, d, 64);
-        x = max(x, (uint64_t)__shfl_xor((unsigned long long)x, d, 64));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        ws[threadIdx.x >> 6] = s;
-        wx[threadIdx.x >> 6] = x;
+// pl_place's prologue reduction, all DPP (no 64-bit lane shuffles): the sum of the threads' partial sums of
+// the earlier tiles' sums (each < 2^31: at most 16 tile sums of < 2^27) as two 16-bit-split 32-bit sums, exact
+// in 64 bits; the largest `kidx` (the nearest non-empty earlier tile, index + 1) and the `exit` of the thread
+// that holds it (kidx values are distinct or 0).  Two block syncs.
+__device__ __forceinline__ void block_sum_nearest(uint64_t part, uint32_t kidx, uint32_t exit, uint64_t &S,
+                                                  uint32_t &kmax, uint32_t &kexit) {
+    __shared__ uint32_t slo[kPatT / 64], shi[kPatT / 64], smx[kPatT / 64], sx;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t p = (uint32_t)part;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(p & 0xFFFFu), 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(p >> 16), 63);
+    const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(kidx), 63);
+    if (lane == 0) {
+        slo[wave] = lo;
+        shi[wave] = hi;
+        smx[wave] = mx;
     }
     __syncthreads();
-    S = 0;
-    X = 0;
+    uint64_t tl = 0, th = 0;
+    uint32_t m = 0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; w++) {
-        S += ws[w];
-        X = max(X, wx[w]);
+    for (int w = 0; w < kPatT / 64; w++) {
+        tl += slo[w];
+        th += shi[w];
+        m = max(m, smx[w]);
     }
+    if (m != 0 && kidx == m) sx = exit;
+    __syncthreads();
+    S = (th << 16) + tl;
+    kmax = m;
+    kexit = m ? sx : 0u;
 }
 
 // (32-bit element and unit arithmetic: total <= cap < 2^32 and M < 2^31 on the device path; the one
@@ -1607,10 +1617,11 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
                                                   uint64_t *E, const uint32_t *rec, const uint32_t *tsum,
                                                   uint32_t *wide, uint64_t *host_word, uint64_t *badw,
                                                   uint32_t epoch) {
-    __shared__ uint2 img8[kPatImg / 4];  // the range as f16 bits (12 KiB: 8 workgroups per CU), widened on the way out
+    __shared__ uint4 img16[kPatImg / 8];  // the range as f16 bits (12 KiB: 8 workgroups per CU), widened on the way out
     __shared__ uint4 lw4[kPatStage / 8 + 1];
     __shared__ uint32_t lq[3 * kLQ], lqn;
-    uint16_t *img = (uint16_t *)img8;
+    uint2 *img8 = (uint2 *)img16;
+    uint16_t *img = (uint16_t *)img16;
     const uint16_t *lw = (const uint16_t *)lw4;
     const uint32_t t = blockIdx.x, base = t * (uint32_t)kPatU, M32 = (uint32_t)M, T32 = (uint32_t)T;
     const bool direct = T <= kPatDirect;  // (uniform) else E[] from pl_scan
@@ -1650,12 +1661,13 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
                         (i + 3 < t ? sums[q].w : 0u);
             }
         }
-        // (index + 1) << 32 | exit of the nearest non-empty tile among the 256 before t
-        const uint64_t key0 = threadIdx.x < t && near.x > 0 ? (uint64_t)(t - threadIdx.x) << 32 | near.w : 0;
-        uint64_t S, key;
-        block_sum_max64<kPatT>(part, key0, S, key);  // (its sync also covers the staged units)
-        uint32_t pexit = (uint32_t)key;
-        bool found = key != 0;
+        // the nearest non-empty tile among the 256 before t: index + 1 (0: none), its exit
+        const uint32_t kidx = threadIdx.x < t && near.x > 0 ? t - threadIdx.x : 0u;
+        uint64_t S;
+        uint32_t kmax, kexit;
+        block_sum_nearest(part, kidx, near.w, S, kmax, kexit);  // (its sync also covers the staged units)
+        uint32_t pexit = kexit;
+        bool found = kmax != 0;
         if (!found && t > (uint32_t)kPatT) {  // none among those 256
             const int64_t q = prev_nonempty(rec, t - kPatT);
             found = q >= 0;
@@ -1690,7 +1702,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
     }
     if (eb == ea || is_wide) return;  // (uniform) an empty tile inside a run; a wide range: pl_wide places it
-    for (uint32_t i = threadIdx.x; i < (n + 3) / 4; i += kPatT) img8[i] = make_uint2(0u, 0u);
+    for (uint32_t i = threadIdx.x; i < (n + 7) / 8; i += kPatT) img16[i] = make_uint4(0u, 0u, 0u, 0u);
     const Units12 U = units12(lw4);
     const uint32_t j0 = kPatPer * threadIdx.x;
     uint32_t sum;

@@ -99,7 +99,7 @@ enum Shape {
     COPY = 0, COPYZ, FILL, SUM2, SUM4, SUM8, DEC, EMPTY, COPY_SC1, COPY_SYS, SUM2_SC1, SUM2_SYS,
     FILL_SC1, FILL_SYS, FILL_PLAIN, DEC_SC1, DEC_SYS, DEC_PLAIN,
     FILL_U4, FILL_U16, FILL_B256, FILL_GRID, DEC_U2, DEC_U4, DEC_B256, COPY_U2, COPY_B256,
-    DEC_B256_SC1, DEC_U2_B256, FILL_U4_B256, NSHAPES
+    DEC_B256_SC1, DEC_U2_B256, FILL_U4_B256, COPYZ_OCC24, COPYZ_B256, COPYZ_B256_OCC6, COPYZ_U2_OCC12, NSHAPES
 };
 static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 2R1W", "sum4 4R1W", "sum8 8R1W",
                               "f16 decode", "empty", "copy st nt sc1", "copy st sc0sc1", "sum2 st nt sc1",
@@ -107,12 +107,15 @@ static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 
                               "decode st sc0sc1", "decode st plain", "fill U4/lane", "fill U16/lane",
                               "fill 256-thr wg", "fill grid 4/CU", "decode U2/lane", "decode U4/lane",
                               "decode 256-thr wg", "copy U2/lane", "copy 256-thr wg", "decode 256 nt sc1",
-                              "decode U2 256-thr", "fill U4 256-thr"};
-static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0, 1, 1, 2, 2, 0, 0, 0, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 0};
-static const int kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+                              "decode U2 256-thr", "fill U4 256-thr", "copy+zero occ24", "copy+zero 256-thr",
+                              "copy+zero 256 occ6", "copy+zero U2 occ12"};
+static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0, 1, 1, 2, 2, 0, 0, 0, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 0,
+                             1, 1, 1, 1};
+static const int kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                              2, 2, 2, 2};
 // algorithmic bytes per f32 element
 static const double kBytes[] = {8, 12, 4, 12, 20, 36, 6, 0, 8, 8, 12, 12, 4, 4, 4, 6, 6, 6,
-                                4, 4, 4, 4, 6, 6, 6, 8, 8, 6, 6, 4};
+                                4, 4, 4, 4, 6, 6, 6, 8, 8, 6, 6, 4, 12, 12, 12, 12};
 // workgroups per launch for the shapes that do not use one-wave workgroups of one vector per lane
 static size_t grid_of(int shape, size_t nvec, int cus) {
     switch (shape) {
@@ -122,13 +125,16 @@ static size_t grid_of(int shape, size_t nvec, int cus) {
     case FILL_B256: case DEC_B256: case COPY_B256: case DEC_B256_SC1: return (nvec + 255) / 256;
     case DEC_U2_B256: return (nvec + 511) / 512;
     case FILL_U4_B256: return (nvec + 1023) / 1024;
+    case COPYZ_B256: case COPYZ_B256_OCC6: return (nvec + 255) / 256;
+    case COPYZ_U2_OCC12: return (nvec + 127) / 128;
     case FILL_GRID: return (size_t)cus * 4;
     default: return (nvec + 63) / 64;
     }
 }
 static int block_of(int shape) {
     return shape == FILL_B256 || shape == DEC_B256 || shape == COPY_B256 || shape == FILL_GRID ||
-                   shape == DEC_B256_SC1 || shape == DEC_U2_B256 || shape == FILL_U4_B256
+                   shape == DEC_B256_SC1 || shape == DEC_U2_B256 || shape == FILL_U4_B256 || shape == COPYZ_B256 ||
+                   shape == COPYZ_B256_OCC6
                ? 256
                : 64;
 }
@@ -310,6 +316,33 @@ template <bool STAMP> __global__ __launch_bounds__(256) void k_fill_u4_b256(Args
         if (v0 + 256 * u < a.nvec) st_sc1(a.out[0] + v0 + 256 * u, f4{0, 0, 0, 0});
     c.stop(a.st);
 }
+template <bool STAMP, int B> __device__ __forceinline__ void copyz_body(const Args &a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v = (size_t)blockIdx.x * B + threadIdx.x;
+    if (v < a.nvec) {
+        const f4 x = ldn(a.in[0] + v);
+        st_sc1(a.out[0] + v, x);
+        st_sc1(a.out[1] + v, f4{0, 0, 0, 0});
+    }
+    c.stop(a.st);
+}
+template <bool STAMP> __global__ __launch_bounds__(256) void k_copyz_b256(Args a) { copyz_body<STAMP, 256>(a); }
+template <bool STAMP> __global__ __launch_bounds__(64) void k_copyz_u2(Args a) {
+    Clock<STAMP> c;
+    c.start();
+    const size_t v0 = (size_t)blockIdx.x * 128 + threadIdx.x;
+    f4 x[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) x[u] = v0 + 64 * u < a.nvec ? ldn(a.in[0] + v0 + 64 * u) : f4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+        if (v0 + 64 * u < a.nvec) {
+            st_sc1(a.out[0] + v0 + 64 * u, x[u]);
+            st_sc1(a.out[1] + v0 + 64 * u, f4{0, 0, 0, 0});
+        }
+    c.stop(a.st);
+}
 template <bool STAMP> __global__ __launch_bounds__(64) void k_copy_u2(Args a) {
     Clock<STAMP> c;
     c.start();
@@ -400,6 +433,19 @@ static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) 
     case DEC_B256_SC1: L2(k_dec_b256_sc1) break;
     case DEC_U2_B256: L2(k_dec_u2_b256) break;
     case FILL_U4_B256: L2(k_fill_u4_b256) break;
+    case COPYZ_OCC24:
+        if (st) hipLaunchKernelGGL(k_copyz<true>, dim3(grid), dim3(blk), lds_for_occ(24), s, a);
+        else hipLaunchKernelGGL(k_copyz<false>, dim3(grid), dim3(blk), lds_for_occ(24), s, a);
+        break;
+    case COPYZ_B256: L2(k_copyz_b256) break;
+    case COPYZ_B256_OCC6:  // at most 6 four-wave workgroups per CU (24 waves)
+        if (st) hipLaunchKernelGGL(k_copyz_b256<true>, dim3(grid), dim3(blk), lds_for_occ(6), s, a);
+        else hipLaunchKernelGGL(k_copyz_b256<false>, dim3(grid), dim3(blk), lds_for_occ(6), s, a);
+        break;
+    case COPYZ_U2_OCC12:
+        if (st) hipLaunchKernelGGL(k_copyz_u2<true>, dim3(grid), dim3(blk), lds_for_occ(12), s, a);
+        else hipLaunchKernelGGL(k_copyz_u2<false>, dim3(grid), dim3(blk), lds_for_occ(12), s, a);
+        break;
     case SUM4:
         if (st) hipLaunchKernelGGL((k_sumser<4, true>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
         else hipLaunchKernelGGL((k_sumser<4, false>), dim3(grid), dim3(64), lds_for_occ(28), s, a);
