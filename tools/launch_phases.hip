@@ -56,6 +56,7 @@ struct Args {
     f4 *out[2];
     size_t nvec;
     Stamp *st;
+    uint32_t first;  // workgroups that fit the chip at once (CUs x 28)
 };
 
 template <class T> __device__ __forceinline__ T ldn(const T *p) { return __builtin_nontemporal_load(p); }
@@ -99,7 +100,8 @@ enum Shape {
     COPY = 0, COPYZ, FILL, SUM2, SUM4, SUM8, DEC, EMPTY, COPY_SC1, COPY_SYS, SUM2_SC1, SUM2_SYS,
     FILL_SC1, FILL_SYS, FILL_PLAIN, DEC_SC1, DEC_SYS, DEC_PLAIN,
     FILL_U4, FILL_U16, FILL_B256, FILL_GRID, DEC_U2, DEC_U4, DEC_B256, COPY_U2, COPY_B256,
-    DEC_B256_SC1, DEC_U2_B256, FILL_U4_B256, COPYZ_OCC24, COPYZ_B256, COPYZ_B256_OCC6, COPYZ_U2_OCC12, NSHAPES
+    DEC_B256_SC1, DEC_U2_B256, FILL_U4_B256, COPYZ_OCC24, COPYZ_B256, COPYZ_B256_OCC6, COPYZ_U2_OCC12,
+    SUM4_HYB, SUM8_HYB, SUM4_HYB2, SUM8_HYB2, NSHAPES
 };
 static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 2R1W", "sum4 4R1W", "sum8 8R1W",
                               "f16 decode", "empty", "copy st nt sc1", "copy st sc0sc1", "sum2 st nt sc1",
@@ -108,14 +110,15 @@ static const char *kName[] = {"copy 1R1W", "copy+zero 1R2W", "fill 0R1W", "sum2 
                               "fill 256-thr wg", "fill grid 4/CU", "decode U2/lane", "decode U4/lane",
                               "decode 256-thr wg", "copy U2/lane", "copy 256-thr wg", "decode 256 nt sc1",
                               "decode U2 256-thr", "fill U4 256-thr", "copy+zero occ24", "copy+zero 256-thr",
-                              "copy+zero 256 occ6", "copy+zero U2 occ12"};
+                              "copy+zero 256 occ6", "copy+zero U2 occ12", "sum4 parallel head", "sum8 parallel head",
+                              "sum4 parallel tail", "sum8 parallel tail"};
 static const int kReads[] = {1, 1, 0, 2, 4, 8, 1, 0, 1, 1, 2, 2, 0, 0, 0, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 0,
-                             1, 1, 1, 1};
+                             1, 1, 1, 1, 4, 8, 4, 8};
 static const int kWrites[] = {1, 2, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                              2, 2, 2, 2};
+                              2, 2, 2, 2, 1, 1, 1, 1};
 // algorithmic bytes per f32 element
 static const double kBytes[] = {8, 12, 4, 12, 20, 36, 6, 0, 8, 8, 12, 12, 4, 4, 4, 6, 6, 6,
-                                4, 4, 4, 4, 6, 6, 6, 8, 8, 6, 6, 4, 12, 12, 12, 12};
+                                4, 4, 4, 4, 6, 6, 6, 8, 8, 6, 6, 4, 12, 12, 12, 12, 20, 36, 20, 36};
 // workgroups per launch for the shapes that do not use one-wave workgroups of one vector per lane
 static size_t grid_of(int shape, size_t nvec, int cus) {
     switch (shape) {
@@ -196,11 +199,27 @@ template <bool STAMP, int POL> __device__ __forceinline__ void sum2_body(const A
 template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2(Args a) { sum2_body<STAMP, 0>(a); }
 template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2_sc1(Args a) { sum2_body<STAMP, 1>(a); }
 template <bool STAMP> __global__ __launch_bounds__(64) void k_sum2_sys(Args a) { sum2_body<STAMP, 2>(a); }
-// the product's K >= 4 form: one load in flight per wave (occupancy capped by the launch)
-template <int K, bool STAMP> __global__ __launch_bounds__(64) void k_sumser(Args a) {
+// the product's K >= 4 form: one load in flight per wave (occupancy capped by the launch);
+// HYB = 1: the first CUs x 28 workgroups (they start together at the launch) issue all K loads at
+// once instead; HYB = 2: the last CUs x 28 (the tail: each serialized chain of K load latencies ends
+// the launch while HBM has little else to serve)
+template <int K, bool STAMP, int HYB = 0> __global__ __launch_bounds__(64) void k_sumser(Args a) {
     Clock<STAMP> c;
     c.start();
     const size_t v = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if ((HYB == 1 && blockIdx.x < a.first) || (HYB == 2 && blockIdx.x + a.first >= gridDim.x)) {
+        if (v < a.nvec) {
+            f4 x[K];
+#pragma unroll
+            for (int j = 0; j < K; j++) x[j] = ldn(a.in[j] + v);
+            f4 s = x[0];
+#pragma unroll
+            for (int j = 1; j < K; j++) s += x[j];
+            stn(a.out[0] + v, s * (1.0f / K));
+        }
+        c.stop(a.st);
+        return;
+    }
     if (v < a.nvec) {
         f4 s = ldn(a.in[0] + v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -442,6 +461,23 @@ static void launch(int shape, int mode, const Args &a, size_t n, hipStream_t s) 
         if (st) hipLaunchKernelGGL(k_copyz_b256<true>, dim3(grid), dim3(blk), lds_for_occ(6), s, a);
         else hipLaunchKernelGGL(k_copyz_b256<false>, dim3(grid), dim3(blk), lds_for_occ(6), s, a);
         break;
+    case SUM4_HYB: case SUM8_HYB: case SUM4_HYB2: case SUM8_HYB2: {
+        const unsigned l = lds_for_occ(28);
+        if (shape == SUM4_HYB) {
+            if (st) hipLaunchKernelGGL((k_sumser<4, true, 1>), dim3(grid), dim3(blk), l, s, a);
+            else hipLaunchKernelGGL((k_sumser<4, false, 1>), dim3(grid), dim3(blk), l, s, a);
+        } else if (shape == SUM8_HYB) {
+            if (st) hipLaunchKernelGGL((k_sumser<8, true, 1>), dim3(grid), dim3(blk), l, s, a);
+            else hipLaunchKernelGGL((k_sumser<8, false, 1>), dim3(grid), dim3(blk), l, s, a);
+        } else if (shape == SUM4_HYB2) {
+            if (st) hipLaunchKernelGGL((k_sumser<4, true, 2>), dim3(grid), dim3(blk), l, s, a);
+            else hipLaunchKernelGGL((k_sumser<4, false, 2>), dim3(grid), dim3(blk), l, s, a);
+        } else {
+            if (st) hipLaunchKernelGGL((k_sumser<8, true, 2>), dim3(grid), dim3(blk), l, s, a);
+            else hipLaunchKernelGGL((k_sumser<8, false, 2>), dim3(grid), dim3(blk), l, s, a);
+        }
+        break;
+    }
     case COPYZ_U2_OCC12:
         if (st) hipLaunchKernelGGL(k_copyz_u2<true>, dim3(grid), dim3(blk), lds_for_occ(12), s, a);
         else hipLaunchKernelGGL(k_copyz_u2<false>, dim3(grid), dim3(blk), lds_for_occ(12), s, a);
@@ -573,6 +609,7 @@ static void run_size(size_t mib, hipStream_t s) {
             for (int j = 0; j < kReads[shape]; j++) a.in[j] = g_pool[set * per + j];
             for (int j = 0; j < kWrites[shape]; j++) a.out[j] = g_pool[set * per + kReads[shape] + j];
             a.nvec = nvec;
+            a.first = (uint32_t)g_cus * 28u;
             a.st = dst + (size_t)(it % L) * nwg;
             return a;
         };
