@@ -659,14 +659,15 @@ int main(int argc, char **argv) {
         for (char *t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) sizes.push_back((size_t)atol(t));
     }
     if (argc > 2) L = atoi(argv[2]);
+    const bool synth = argc > 3 && !strcmp(argv[3], "synth");  // the bench's gradient distribution in every buffer
     size_t mx = 0;
     for (size_t m : sizes) mx = std::max(mx, m);
     g_max_elems = mx << 18;
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     g_cus = p.multiProcessorCount;
-    printf("# launch_phases: %s, %d CUs; stamps = s_memrealtime (100 MHz) per workgroup, lane 0\n", p.gcnArchName,
-           p.multiProcessorCount);
+    printf("# launch_phases: %s, %d CUs; stamps = s_memrealtime (100 MHz) per workgroup, lane 0; data: %s\n",
+           p.gcnArchName, p.multiProcessorCount, synth ? "ono_synth_f32 (the bench's)" : "k_init pattern");
     printf("# ev_us: HIP events around L launches (un-stamped tool kernel); stamp_us: the stamped build; lib_us: the\n"
            "# product library on the same buffers; span/gap/ramp/ideal/drain/xcd/dstart/tail in us from the stamps\n"
            "# (dstart = first -> last workgroup start, tail = last start -> last end); R = fitted steady rate of\n"
@@ -676,7 +677,8 @@ int main(int argc, char **argv) {
     for (int i = 0; i < kPool; i++) {
         f4 *q;
         CK(hipMalloc(&q, g_max_elems * 4));
-        hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, q, g_max_elems / 4, 17u + i);
+        if (synth) OK(ono_synth_f32((float *)q, g_max_elems, 0x0402026 + i, (uint64_t)(i % 9), 0, s));
+        else hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, s, q, g_max_elems / 4, 17u + i);
         g_pool.push_back(q);
     }
     CK(hipStreamSynchronize(s));
