@@ -11,9 +11,10 @@
 // and run j (starting at s_j) has its header 8 bytes earlier, with
 //   offset_j = U(s_j) - U(s_{j-1}),  U(i) = i - F(i)  (unkept values before i)
 //   len_j    = F(s_{j+1}) - F(s_j)   (F_total for the last run).
-// Three launches (see "encoder" below): each tile's byte range built in LDS
-// and written to a scratch slot -> one scan of the tile records -> each slot
-// moved to its place with the two cross-tile header fields completed.  g is
+// Two launches (see "encoder" below): each tile's byte range built in LDS and
+// written to a scratch slot, its counts added to its chunk's aggregate -> each
+// slot moved to its place (its prefix from its chunk's records and the other
+// chunks' aggregates) with the two cross-tile header fields completed.  g is
 // read once; the totals stay on the device (the blocking form reads them once,
 // at the end, for the wire length; the stream-ordered form leaves it in HBM).
 // Decoding is a parallel parse on the device (the record stream is a linked
@@ -42,6 +43,23 @@ constexpr int kSB = 256;             // threads per block (4 waves)
 constexpr int kEPT = 8;              // elements per thread
 constexpr int kTile = kSB * kEPT;    // 2048 elements per tile
 constexpr int kIT = 128, kIE = kTile / kIT;  // the encoder's tile: 2 waves x 16 values per thread
+
+#ifdef ONO_SP_STAMP
+// Measurement build only (tools/sp_phases.hip compiles this file with ONO_SP_STAMP defined; the
+// library never does): {start, mid - start, end - start, XCC id} in 100 MHz ticks per sp_image
+// workgroup / sp_move wave, end = after the unit's own memory operations are acknowledged.
+__device__ uint4 g_sp_stamp_img[1 << 16], g_sp_stamp_mov[1 << 18];
+__device__ __forceinline__ void sp_stamp(uint4 *st, size_t i, uint64_t t0, uint64_t tm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    if ((threadIdx.x & 63) == 0) st[i] = make_uint4((unsigned)t0, (unsigned)(tm - t0), (unsigned)(t1 - t0), x & 0xF);
+}
+#define SP_CLOCK(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#else
+#define SP_CLOCK(v) (void)0
+#endif
 
 // half 2.7.1 conversions = the gfx950 cvt instructions, NaN rules included (ono_kernels.hip to_f16)
 __device__ __forceinline__ uint16_t to_f16_sp(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
@@ -136,10 +154,7 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
 
 
 // ------------------------------------------------------------- encoder ----
-// Three launches, g read once (64 MiB, 10 % kept, MI355X: about 19 + 4.8 +
-// 11 us, 33 us per drop back to back with the gradient read from HBM; the
-// four-launch count / scan / write / headers design it replaced read g twice
-// and took ~50):
+// Two launches, g read once:
 //  1. sp_image, one 128-thread workgroup per 2048-value tile (16 values per
 //     thread, plain 16-B loads): flags, one LDS exchange of the waves' DPP scans, then the
 //     tile's byte range of the wire built in LDS — its values, and its run
@@ -147,22 +162,23 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t &ea
 //     threads that hold the run starts — copied to the tile's slot of a
 //     scratch image (5 B per value), plus two 8-B records: recA = {kept | runs
 //     << 16, last kept + 1 | first unkept << 16}, recB = {first / last header
-//     position, first run's offset | last run's length} (all tile-local).
-//  2. sp_scan_rec, one workgroup per 1024 tiles (two levels, the last
-//     workgroup to arrive makes the chunk carries): per tile the exclusive prefix sums of kept
-//     and runs (its place in the wire), the exclusive prefix max of "last kept
-//     + 1" (P: where the run before the tile's first run ended) and the
-//     exclusive suffix min of "first unkept" (Q: where a run still open at the
-//     tile's end ends).
-//  3. sp_move, one wave per tile: the slot to its place in the wire (2-B
-//     aligned) in 16-B destination chunks, completing on the way the two
-//     header fields that depend on other tiles: the first run's offset (+=
-//     tile start - P) and, when the tile's last value is kept, the last run's
-//     length (+= Q - tile end).  A run's offset is the gap since the previous
-//     run's end, its length the distance to the first unkept value after its
-//     start.
+//     position, first run's offset | last run's length} (all tile-local), and
+//     four device-scope atomics into its chunk's aggregate (kRecChunk tiles:
+//     kept values, runs, last kept index + 1, first unkept index).
+//  2. sp_move, one wave per tile: its place in the wire from the records of
+//     its chunk and the aggregates of the others (tile_prefix), then the slot
+//     to that place (2-B aligned) in 16-B destination chunks, completing on the
+//     way the two header fields that depend on other tiles: the first run's
+//     offset (+= tile start - P) and, when the tile's last value is kept, the
+//     last run's length (+= Q - tile end).  A run's offset is the gap since the
+//     previous run's end, its length the distance to the first unkept value
+//     after its start.
+// (Round 4 folded a third launch, a scan of the tile records between the two,
+// into these: sp_image's atomics and the move's own reduction.)
 constexpr int kSlotU16 = 5128;  // the largest tile image, 3 S + 2049 <= 5121 units (S <= 1024), padded to 16 B
 static_assert((kSlotU16 * 2) % 16 == 0, "slots are 16-B aligned");
+constexpr int kRecChunk = 128;  // tiles per chunk of the aggregates: two records per lane of the move's wave
+constexpr int kAggStride = 8;   // one chunk aggregate per 128-B line (uint4 units): atomics of different chunks never share one
 
 // Block-wide scans over the threads of a tile (tile-local indices): the
 // exclusive prefix of (kept, runs), the last kept index + 1 before the thread
@@ -225,18 +241,25 @@ static_assert(kIE <= 32, "a thread's flags are one 32-bit mask; its counts are p
 // | runs << 16, last kept + 1 | first unkept << 16} (what the scan needs),
 // recB = {first header | last header << 16, the first run's offset | the
 // last run's length << 16} (what the move completes).
-__global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, float t, bool vec, uint16_t *img,
-                                                uint2 *recA, uint2 *recB) {
-    __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
-    __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
-    const size_t tile = blockIdx.x, tile0 = tile * kTile;
-    const uint32_t lo = threadIdx.x * kIE;  // the thread's first element, tile-local
-    const size_t base = tile0 + lo;
-    float x[kIE];
-    // four 16-B loads per thread, 2 KiB per wave in flight; plain loads: nt
-    // loads measured slower here even from HBM (64 MiB drop over 6 rotating
-    // gradients: 38.2 us with plain loads, 49.9 us with nt)
-    if (vec && base + kIE <= n) {
+// A tile's values and the value before the wave's first one (lane 0 uses
+// it).  That one is a vector load of a wave-uniform address, issued first:
+// as a scalar load it shares its counter with the LDS traffic of the tile
+// being processed while this one is in flight, and every LDS wait there
+// would wait for it.  FULL: all of the tile's values in range, 16-B aligned —
+// four 16-B loads per thread (plain loads: nt loads measured slower here even
+// from HBM, 38.2 vs 49.9 us per 64 MiB drop), five vector loads in all
+// whatever the data, which is what lets the pipelined loop keep them in
+// flight (a load count that differs by path makes the compiler wait for all).
+template <bool FULL>
+__device__ __forceinline__ void load_tile(const float *__restrict__ g, size_t n, size_t tile, float (&x)[kIE],
+                                          float &before) {
+    const size_t tile0 = tile * kTile, base = tile0 + threadIdx.x * kIE;
+    size_t wb = tile0 + (threadIdx.x & ~63u) * kIE;
+    wb = wb ? min(wb - 1, n - 1) : 0;
+    uint32_t wbv = (uint32_t)wb;
+    asm volatile("" : "+v"(wbv));  // a VGPR address: a vector load, not a scalar one
+    before = g[wbv];
+    if (FULL) {
 #pragma unroll
         for (int q = 0; q < kIE / 4; q++) {
             const f4s a = *((const f4s *)(g + base) + q);
@@ -246,12 +269,23 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
 #pragma unroll
         for (int e = 0; e < kIE; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
     }
-    // the value before the wave's first one (lane 0 uses it): a wave-uniform
-    // address, so a scalar load that waits on its own counter — as a vector
-    // load under lane 0's branch it was issued, and waited for, only after
-    // all of the values had landed (+6 us per drop)
-    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(tile0 + (threadIdx.x & ~63u) * kIE));
-    const float before = wbase ? g[min((size_t)wbase - 1, n - 1)] : 0.0f;
+}
+
+// A workgroup's part of its chunk's aggregate: kept values and runs (one 64-bit add), the last
+// kept index + 1 (0: none), the first unkept index complemented (0: none) — identity 0 all.
+struct ImgAgg {
+    uint64_t fr = 0;
+    uint32_t lk = 0, nfu = 0;
+};
+// One tile, its values in registers: flags, the block scans, the image in LDS, out to its slot,
+// its records; its counts into the workgroup's aggregate (uniform values).
+__device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], float before, size_t n, float t,
+                                           uint16_t *img, uint2 *recA, uint2 *recB, ImgAgg &acc) {
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
+    __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
+    const size_t tile0 = tile * kTile;
+    const uint32_t lo = threadIdx.x * kIE;  // the thread's first element, tile-local
+    const size_t base = tile0 + lo;
     const uint32_t full = kIE >= 32 ? 0xFFFFFFFFu : (1u << (kIE & 31)) - 1u;
     const uint32_t valid = base >= n ? 0u : (n - base >= (size_t)kIE ? full : (1u << (n - base)) - 1u);
     const Bits b = flags_of(x, before, n, t, base, valid);
@@ -309,117 +343,137 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
         recB[tile] = R ? make_uint2((rb[0] & 0xFFFFu) | rb[1] << 16, rb[0] >> 16 | (rb[1] & 0xFFFF0000u))
                        : make_uint2(0u, 0u);
     }
+    acc.fr += (uint64_t)F | (uint64_t)R << 32;
+    if (F) acc.lk = (uint32_t)tile0 + ts.last_kept1;  // tiles in order: the latest one's is the max
+    if (ts.first_unkept < (uint32_t)kTile && !acc.nfu) acc.nfu = ~((uint32_t)tile0 + ts.first_unkept);  // the first
 }
 
-
-// recA -> pre = {F0, S0, P, Q} per tile (F0 / S0: kept values / runs before
-// the tile; P: last kept index + 1 before it, 0 if none; Q: first unkept
-// index after it, n if none), in two levels within one launch: each
-// workgroup scans a chunk of kRecChunk tiles (LDS-staged, DPP wave scans;
-// the suffix min as a forward scan over the chunk reversed) into chunk-local
-// prefixes and publishes the chunk's aggregate.  Each sp_move wave folds the
-// aggregates before / after its chunk into the chunk's carry itself (no
-// arrival counter, no serial pass over the chunks).
-constexpr int kRecT = 64, kRecPer = 2, kRecChunk = kRecT * kRecPer;  // 128 tiles per one-wave workgroup
-__global__ __launch_bounds__(kRecT) void sp_scan_rec(const uint2 *recA, uint4 *pre, uint4 *agg, size_t ntiles,
-                                                      uint32_t n) {
-    __shared__ uint32_t la[kRecChunk], lb[kRecChunk];
-    __shared__ uint32_t rf[kRecChunk], rs[kRecChunk], rp[kRecChunk], rq[kRecChunk];
-    __shared__ uint32_t wa[kRecT / 64], wb[kRecT / 64], wc[kRecT / 64], wd[kRecT / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const size_t c0 = (size_t)blockIdx.x * kRecChunk;
-    const uint32_t m = (uint32_t)min((size_t)kRecChunk, ntiles - c0);
-    for (uint32_t i = threadIdx.x; i < kRecChunk; i += kRecT) {
-        const uint2 r = i < m ? recA[c0 + i] : make_uint2(0u, (uint32_t)kTile << 16);
-        la[i] = r.x;
-        lb[i] = r.y;
-    }
-    __syncthreads();
-    const uint32_t lo = threadIdx.x * kRecPer;
-    // forward: this thread's tiles lo .. lo + 3
-    uint32_t sumf = 0, sums = 0, mx = 0, lk[kRecPer], cnt[kRecPer];
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        cnt[k] = la[lo + k];
-        const uint32_t l1 = lb[lo + k] & 0xFFFFu;
-        sumf += cnt[k] & 0xFFFFu;
-        sums += cnt[k] >> 16;
-        lk[k] = l1 ? (uint32_t)((c0 + lo + k) * kTile) + l1 : 0u;  // global last kept + 1
-        mx = max(mx, lk[k]);
-    }
-    // backward, as a forward scan over the chunk reversed: tiles m-1-lo .. m-4-lo
-    uint32_t fu[kRecPer], mn = n;
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        const uint32_t idx = lo + k, i = m - 1 - idx;
-        const uint32_t f1 = idx < m ? lb[i] >> 16 : (uint32_t)kTile;
-        fu[k] = f1 < (uint32_t)kTile ? (uint32_t)((c0 + i) * kTile) + f1 : n;
-        mn = min(mn, fu[k]);
-    }
-    const uint32_t i_f = wave_incl_sum_dpp(sumf), i_s = wave_incl_sum_dpp(sums);
-    const uint32_t i_m = wave_incl_max_dpp(mx), i_u = wave_incl_min_dpp(mn);
-    if (lane == 63) { wa[wave] = i_f; wb[wave] = i_s; wc[wave] = i_m; wd[wave] = i_u; }
-    __syncthreads();
-    uint32_t pf = 0, ps = 0, pm = 0, q = n, tf = 0, tsum = 0, tm = 0, tq = n;
-#pragma unroll
-    for (int w = 0; w < kRecT / 64; w++) {
-        if (w < wave) { pf += wa[w]; ps += wb[w]; pm = max(pm, wc[w]); q = min(q, wd[w]); }
-        tf += wa[w];
-        tsum += wb[w];
-        tm = max(tm, wc[w]);
-        tq = min(tq, wd[w]);
-    }
-    pf += i_f - sumf;  // exclusive, within the wave
-    ps += i_s - sums;
-    pm = max(pm, lane_before(i_m));  // lane 0 gets 0, the identity
-    q = min(q, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)i_u, 0x138, 0xF, 0xF, false));  // lane 0: ~0
-#pragma unroll
-    for (int k = 0; k < kRecPer; k++) {
-        rf[lo + k] = pf;
-        rs[lo + k] = ps;
-        rp[lo + k] = pm;
-        pf += cnt[k] & 0xFFFFu;
-        ps += cnt[k] >> 16;
-        pm = max(pm, lk[k]);
-        const uint32_t idx = lo + k;
-        if (idx < m) rq[m - 1 - idx] = q;
-        q = min(q, fu[k]);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += kRecT) pre[c0 + i] = make_uint4(rf[i], rs[i], rp[i], rq[i]);
-    if (threadIdx.x == 0) agg[blockIdx.x] = make_uint4(tf, tsum, tm, tq);  // the chunk's aggregate
-}
-
-// The carry of chunk c (sp_scan_rec's aggregates, G chunks): kept values and
-// runs before it, the last kept index + 1 before it (max), the first unkept
-// index after it (min, n if none) — one wave, its lanes over the chunks.
-__device__ __forceinline__ uint4 chunk_carry(const uint4 *agg, uint32_t G, uint32_t c, uint32_t n) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t f = 0, r = 0, m = 0, q = n;
-    for (uint32_t j0 = 0; j0 < G; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        const uint4 a = j < G ? agg[j] : make_uint4(0u, 0u, 0u, n);
-        if (j < c) {
-            f += a.x;
-            r += a.y;
-            m = max(m, a.z);
-        } else if (j > c) {
-            q = min(q, a.w);
+// The encoder's first launch: workgroup w images tiles w tpw .. w tpw + tpw - 1 (tpw a power of two
+// <= kRecChunk, so all in one chunk).  Over the full tiles of an aligned gradient the next tile's
+// values are loaded while the current one is imaged, into two register sets in turn (no copy
+// between them to wait for the loads); the last one's "next" is the current tile again (L2 hits),
+// so that every pass has the same loads in flight.  A ragged last tile, or every tile of an
+// unaligned gradient, goes one at a time after that.  Then three device-scope atomics add the
+// workgroup's counts to its chunk's aggregate (one 128-B line per chunk: kRecChunk / tpw
+// workgroups per line).  It also zeroes the next call's aggregates (the previous call's sp_move,
+// which read them, is done).
+__global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, size_t ntiles, uint32_t tpw,
+                                                float t, bool vec, uint16_t *img, uint2 *recA, uint2 *recB,
+                                                uint4 *agg, uint4 *agg_next, uint32_t gcap) {
+    SP_CLOCK(sp_t0);
+    for (size_t i = (size_t)blockIdx.x * kIT + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kIT)
+        agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
+    const size_t nfull = vec ? n / kTile : 0;
+    const size_t t0 = (size_t)blockIdx.x * tpw, t1 = min(t0 + tpw, ntiles), f1 = min(t1, nfull);
+    size_t tile = t0;
+    ImgAgg acc;
+    float xa[kIE], xb[kIE], ba = 0.0f, bb = 0.0f;
+    if (tile < f1) {
+        load_tile<true>(g, n, tile, xa, ba);
+        for (;;) {
+            size_t next = tile + 1;
+            load_tile<true>(g, n, next < f1 ? next : tile, xb, bb);
+            __builtin_amdgcn_sched_barrier(0);  // the loads issued before any use of the current values
+            image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
+            tile = next;
+            __syncthreads();  // the LDS image is reused
+            if (tile >= f1) break;
+            next = tile + 1;
+            load_tile<true>(g, n, next < f1 ? next : tile, xa, ba);
+            __builtin_amdgcn_sched_barrier(0);
+            image_tile(tile, xb, bb, n, t, img, recA, recB, acc);
+            tile = next;
+            __syncthreads();
+            if (tile >= f1) break;
         }
     }
-    f = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(f), 63);
-    r = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(r), 63);
-    m = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(m), 63);
-    q = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(q), 63);
-    return make_uint4(f, r, m, q);
+    for (; tile < t1; tile++) {
+        load_tile<false>(g, n, tile, xa, ba);
+        image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && t0 < t1) {
+        uint32_t *a = (uint32_t *)(agg + (t0 / kRecChunk) * kAggStride);
+        if (acc.fr) {
+            atomicAdd((unsigned long long *)a, (unsigned long long)acc.fr);
+            atomicMax(a + 2, acc.lk);
+        }
+        if (acc.nfu) atomicMax(a + 3, acc.nfu);
+    }
+#ifdef ONO_SP_STAMP
+    SP_CLOCK(sp_tm);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64) sp_stamp(g_sp_stamp_img, blockIdx.x, sp_t0, sp_tm);
+#endif
 }
+
+// Tiles are grouped in chunks of kRecChunk; sp_image leaves per chunk {kept values, runs, last kept
+// index + 1 (0: none), ~first unkept index (0: none)} in agg.  A tile's place in the wire — kept
+// values and runs before it, the last kept index + 1 before it (P, 0 if none) and the first unkept
+// index after it (Q, n if none) — then takes one wave: the records of its own chunk (two per lane)
+// and the aggregates of the others, every load issued before the first is waited for, one DPP
+// reduction per field.  *own = the tile's own recA.
+__device__ __forceinline__ uint4 tile_prefix(const uint2 *recA, const uint4 *agg, size_t ntiles, uint32_t G,
+                                             size_t tile, uint32_t n, uint2 *own) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = (uint32_t)(tile / kRecChunk), cs = c * (uint32_t)kRecChunk;
+    const uint32_t i = (uint32_t)tile - cs, m = (uint32_t)min((size_t)kRecChunk, ntiles - cs);
+    // every load unconditional (clamped indices, out-of-range lanes masked afterwards): no
+    // exec-masked branches between them for the compiler to put waits in
+    uint2 r[kRecChunk / 64];
+#pragma unroll
+    for (int k = 0; k < kRecChunk / 64; k++) r[k] = recA[cs + min(lane + 64 * k, m - 1)];
+    uint32_t f = 0, s = 0, mx = 0, q = n;
+    // four aggregates per lane in flight (G >= 1 here); the first four straight after the records
+    // (a loop from 0 put a wait for them at its head), selects instead of branches
+    auto fold = [&](uint32_t j0) {
+        uint4 a[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) a[k] = agg[(size_t)min(j0 + 64 * k + lane, G - 1) * kAggStride];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t j = j0 + 64 * k + lane;
+            const bool before = j < c, after = j > c && j < G && a[k].w;
+            f += before ? a[k].x : 0u;
+            s += before ? a[k].y : 0u;
+            mx = max(mx, before ? a[k].z : 0u);
+            q = min(q, after ? ~a[k].w : q);
+        }
+    };
+    fold(0);
+    for (uint32_t j0 = 256; j0 < G; j0 += 256) fold(j0);
+#pragma unroll
+    for (int k = 0; k < kRecChunk / 64; k++) {
+        const uint32_t j = lane + 64 * k, t0 = (cs + j) * (uint32_t)kTile;
+        if (j < i) {
+            f += r[k].x & 0xFFFFu;
+            s += r[k].x >> 16;
+            const uint32_t l1 = r[k].y & 0xFFFFu;
+            if (l1) mx = max(mx, t0 + l1);
+        } else if (j > i && j < m) {
+            const uint32_t f1 = r[k].y >> 16;
+            if (f1 < (uint32_t)kTile) q = min(q, t0 + f1);
+        }
+    }
+    const uint2 o0 = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)r[0].x, i & 63),
+                                (uint32_t)__builtin_amdgcn_readlane((int)r[0].y, i & 63));
+    const uint2 o1 = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)r[1].x, i & 63),
+                                (uint32_t)__builtin_amdgcn_readlane((int)r[1].y, i & 63));
+    *own = i < 64 ? o0 : o1;
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(f), 63),
+                      (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(s), 63),
+                      (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(mx), 63),
+                      (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(q), 63));
+}
+static_assert(kRecChunk == 128, "tile_prefix holds two records per lane");
 
 // The totals (kept values, runs) over all chunks, by one wave.
 __device__ __forceinline__ uint2 chunk_totals(const uint4 *agg, uint32_t G) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t f = 0, r = 0;
     for (uint32_t j = lane; j < G; j += 64) {
-        const uint4 a = agg[j];
+        const uint4 a = agg[(size_t)j * kAggStride];
         f += a.x;
         r += a.y;
     }
@@ -515,8 +569,9 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
 // 1024 units (most tiles' whole image) issued at the same time, then the move.
 // Block 0 also writes the u64 total length and publishes the wire length.
 __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) void sp_move(
-    const uint16_t *img, const uint2 *recA, const uint2 *recB, const uint4 *pre, const uint4 *agg, size_t ntiles,
-    size_t n, uint8_t *buf, uint64_t *host_tot, uint64_t *nbytes_out) {
+    const uint16_t *__restrict__ img, const uint2 *__restrict__ recA, const uint2 *__restrict__ recB,
+    const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, uint64_t *__restrict__ host_tot,
+    uint64_t *__restrict__ nbytes_out) {
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         const uint2 t = chunk_totals(agg, G);
@@ -532,13 +587,18 @@ __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     // wave-uniform (readfirstlane): scalar base addresses and branches
     const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
     if (tile >= ntiles) return;
+    SP_CLOCK(sp_t0);
     const uint4 *src4 = (const uint4 *)(img + tile * kSlotU16);
     uint4 v[kMoveBatch];
 #pragma unroll
     for (int k = 0; k < kMoveBatch; k++) v[k] = ldn4(src4 + lane + 64 * k);
-    const uint2 a = recA[tile], hb = recB[tile];
-    const uint4 pl = pre[tile], cr = chunk_carry(agg, G, (uint32_t)(tile / kRecChunk), (uint32_t)n);  // + carry
-    const uint4 p = make_uint4(pl.x + cr.x, pl.y + cr.y, max(pl.z, cr.z), min(pl.w, cr.w));
+    const uint2 hb = recB[tile];
+    uint2 a;
+    const uint4 p = tile_prefix(recA, agg, ntiles, G, tile, (uint32_t)n, &a);
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the slot's first loads landed too)
+    SP_CLOCK(sp_tm);
+#endif
     const uint32_t F = a.x & 0xFFFFu, R = a.x >> 16, nu16 = 4 * R + F;
     const uint32_t tile0 = (uint32_t)(tile * kTile), tend = (uint32_t)min((size_t)tile0 + kTile, n);
     // the first run's offset and the last run's length (R > 0), completed
@@ -560,6 +620,9 @@ __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     case 6: move_chunks<6>(src4, v, nu16, R, fu, fv, base16); break;
     default: move_chunks<7>(src4, v, nu16, R, fu, fv, base16); break;
     }
+#ifdef ONO_SP_STAMP
+    sp_stamp(g_sp_stamp_mov, tile, sp_t0, sp_tm);
+#endif
 }
 
 // Fallback lift (after a host parse): value v belongs to run j with
@@ -1808,7 +1871,11 @@ struct Scratch {
     uint32_t calls = 0;       // the blocking drop's completion signal: a per-call tag in host_tot[2]
     size_t tiles_cap = 0;
     uint2 *rec = nullptr;     // 2 x tiles_cap: recA, then recB
-    uint4 *pre = nullptr;     // tiles_cap chunk-local prefixes, then the chunk aggregates
+    // two arrays of agg_cap chunk aggregates: call k accumulates into agg[parity] and zeroes the
+    // other one for call k + 1 (zeroed when allocated; flipped once a call's sp_image is launched)
+    uint4 *agg = nullptr;
+    size_t agg_cap = 0;
+    int parity = 0;
     uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
     uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;
 };
@@ -1826,16 +1893,20 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
     }
     if (ntiles > sc.tiles_cap) {
         (void)hipFree(sc.rec);
-        (void)hipFree(sc.pre);
+        (void)hipFree(sc.agg);
         (void)hipFree(sc.img);
         sc.rec = nullptr;
-        sc.pre = nullptr;
+        sc.agg = nullptr;
         sc.img = nullptr;
-        sc.tiles_cap = 0;
+        sc.tiles_cap = sc.agg_cap = 0;
+        const size_t gcap = (ntiles + kRecChunk - 1) / kRecChunk;
         ONO_HIP(hipMalloc((void **)&sc.rec, 2 * ntiles * sizeof(uint2)));
-        ONO_HIP(hipMalloc((void **)&sc.pre, (ntiles + 2 * (ntiles / kRecChunk + 1)) * sizeof(uint4)));
+        ONO_HIP(hipMalloc((void **)&sc.agg, 2 * gcap * kAggStride * sizeof(uint4)));
+        ONO_HIP(hipMemsetAsync(sc.agg, 0, 2 * gcap * kAggStride * sizeof(uint4), stream));
         ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
         sc.tiles_cap = ntiles;
+        sc.agg_cap = gcap;
+        sc.parity = 0;
     }
     *out = &sc;
     return ONO_OK;
@@ -2218,11 +2289,21 @@ size_t ono_sparse_max_bytes(size_t n) { return 8 + 10 * ((n + 1) / 2) + 2 * n; }
 
 namespace {
 
-// The four launches of the encoder.  nbytes_dev != NULL: the stream-ordered
-// form (the buffer holds the worst case, nothing waits; the headers kernel
-// stores the wire length there).  Otherwise blocking: the host reads the
+// The launches of the encoder.  nbytes_dev != NULL: the stream-ordered
+// form (the buffer holds the worst case, nothing waits; sp_move stores the
+// wire length there).  Otherwise blocking: the host reads the
 // totals at the end (and, for a buffer below the worst case, once before the
 // write pass to check the size).
+// tiles per sp_image workgroup (ONO_SP_TPW, a power of two <= kRecChunk: measurement)
+size_t image_tiles_per_wg() {
+    static const size_t v = [] {
+        const char *e = getenv("ONO_SP_TPW");
+        const long x = e ? atol(e) : 0;
+        return x >= 1 && x <= kRecChunk && (x & (x - 1)) == 0 ? (size_t)x : (size_t)4;
+    }();
+    return v;
+}
+
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
@@ -2234,17 +2315,18 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
     const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
-    uint4 *pre = sc->pre, *agg = sc->pre + sc->tiles_cap;
+    uint4 *agg = sc->agg + sc->parity * sc->agg_cap * kAggStride;
+    uint4 *agg_next = sc->agg + (1 - sc->parity) * sc->agg_cap * kAggStride;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     hipError_t e = hipSuccess;
     if (ntiles) {
-        hipLaunchKernelGGL(sp_image, dim3((unsigned)ntiles), dim3(kIT), 0, s, g, n, threshold, vec, sc->img, recA,
-                           recB);
-        hipLaunchKernelGGL(sp_scan_rec, dim3((unsigned)nchunks), dim3(kRecT), 0, s, recA, pre, agg, ntiles,
-                           (uint32_t)n);
+        const size_t tpw = image_tiles_per_wg(), grid = (ntiles + tpw - 1) / tpw;
+        hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold, vec,
+                           sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
+        e = hipGetLastError();
+        if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     }
-    if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip)
         hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, agg, (uint32_t)nchunks, sc->host_tot_dev);
         e = hipStreamSynchronize(s);
@@ -2254,7 +2336,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, pre, agg, ntiles, n, buf,
+    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
                        sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);

@@ -1,0 +1,133 @@
+// sp_phases — where a stream-ordered sparse drop's time goes (measurement build, not the product).
+//
+// Compiles the library's sparse codec source with ONO_SP_STAMP defined: every sp_image workgroup
+// and every sp_move wave stores {start, mid, end} real-time stamps (100 MHz) and its XCC id.
+// Runs K stream-ordered drops of 64 MiB gradients (6 in turn, ~10 % kept in isolated runs like the
+// bench's) back to back between two events, then reports for the last drop, per kernel: the span
+// (first start -> last end), when units start (dispatch), how long they live, the mid stamp
+// (sp_move: its loads landed and its prefix known; sp_image: its last tile imaged) and the
+// per-XCD last end.
+//
+// usage: sp_phases [MiB=64] [K=24]
+#define ONO_SP_STAMP 1
+#include "../oxidized-neural-orchestra_amd/csrc/ono_sparse.hip"
+
+#include <cstdarg>
+#include <cstdio>
+
+namespace ono {
+int set_error(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    fprintf(stderr, "error %d: ", code);
+    vfprintf(stderr, fmt, ap);
+    fprintf(stderr, "\n");
+    va_end(ap);
+    return code;
+}
+int hip_error(hipError_t e, const char *what, const char *file, int line) {
+    fprintf(stderr, "%s: %s (%s:%d)\n", what, hipGetErrorString(e), file, line);
+    return ONO_E_HIP;
+}
+}  // namespace ono
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s: %s (line %d)\n", #x, hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+// |x| uniform in [0, 1): with threshold 0.9 about 10 % kept, in runs of mean length 1.1
+__global__ void gen(float *g, size_t n, uint32_t seed) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
+        h ^= h >> 15; h *= 0x85EBCA77u; h ^= h >> 13; h *= 0xC2B2AE3Du; h ^= h >> 16;
+        const float u = (h >> 8) * (1.0f / 16777216.0f);
+        g[i] = (h & 1) ? -u : u;
+    }
+}
+
+static double pct(std::vector<double> v, double p) {
+    if (v.empty()) return 0;
+    std::sort(v.begin(), v.end());
+    return v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1) + 0.5))];
+}
+
+static void report(const char *name, const std::vector<uint4> &st, uint64_t base) {
+    // stamps: x = low 32 bits of start, y = mid - start, z = end - start, w = XCC
+    std::vector<double> start, life, mid, end;
+    double xend[16] = {0};
+    const double us = 0.01;  // 100 MHz ticks -> us
+    uint32_t b32 = (uint32_t)base;
+    for (const uint4 &s : st) {
+        const double t0 = (double)(uint32_t)(s.x - b32) * us;
+        start.push_back(t0);
+        life.push_back(s.z * us);
+        mid.push_back(s.y * us);
+        end.push_back(t0 + s.z * us);
+        xend[s.w & 15] = std::max(xend[s.w & 15], t0 + s.z * us);
+    }
+    const double first_end = pct(end, 0.0);
+    size_t late = 0;
+    for (double t : start) late += t > first_end;
+    printf("%-9s units %6zu | start p0 %6.2f p50 %6.2f p90 %6.2f max %6.2f | life p10 %5.2f p50 %5.2f p90 %5.2f "
+           "max %5.2f | mid p50 %5.2f | end p50 %6.2f p90 %6.2f max %6.2f | started after the first end %zu\n",
+           name, st.size(), pct(start, 0), pct(start, 0.5), pct(start, 0.9), pct(start, 1), pct(life, 0.1),
+           pct(life, 0.5), pct(life, 0.9), pct(life, 1), pct(mid, 0.5), pct(end, 0.5), pct(end, 0.9), pct(end, 1),
+           late);
+    printf("%-9s per-XCD last end:", name);
+    for (int x = 0; x < 8; x++) printf(" %6.2f", xend[x]);
+    printf("\n");
+}
+
+int main(int argc, char **argv) {
+    const size_t mib = argc > 1 ? (size_t)atoi(argv[1]) : 64;
+    const int K = argc > 2 ? atoi(argv[2]) : 24, NG = 6;
+    const size_t n = mib << 18;
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<float *> gs(NG);
+    for (int i = 0; i < NG; i++) {
+        CK(hipMalloc((void **)&gs[i], n * sizeof(float)));
+        hipLaunchKernelGGL(gen, dim3(4096), dim3(256), 0, s, gs[i], n, 0x5EED0u + 77u * i);
+    }
+    const size_t cap = ono_sparse_max_bytes(n);
+    uint8_t *buf;
+    uint64_t *nbd;
+    CK(hipMalloc((void **)&buf, cap));
+    CK(hipMalloc((void **)&nbd, 8));
+    const float thr = 0.9f;
+    for (int i = 0; i < 2 * K; i++)
+        if (drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s)) return 1;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipStreamSynchronize(s));
+    for (int i = 0; i < 8; i++) drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s);
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < K; i++) drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    uint64_t wire = 0;
+    CK(hipMemcpy(&wire, nbd, 8, hipMemcpyDeviceToHost));
+    const double per = ms * 1e3 / K, bytes = 4.0 * n + (double)wire;
+    printf("# sp_phases: %zu MiB, %d stream-ordered drops over %d gradients, tiles/workgroup %zu: %.2f us per drop "
+           "(events), wire %llu B, %.1f GB/s = %.3f of 8 TB/s\n",
+           mib, K, NG, image_tiles_per_wg(), per, (unsigned long long)wire, bytes / per * 1e-3,
+           bytes / per * 1e-3 / 8000.0);
+    const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + image_tiles_per_wg() - 1) / image_tiles_per_wg();
+    std::vector<uint4> si(nwg), sm(ntiles);
+    CK(hipMemcpyFromSymbol(si.data(), HIP_SYMBOL(g_sp_stamp_img), nwg * sizeof(uint4)));
+    CK(hipMemcpyFromSymbol(sm.data(), HIP_SYMBOL(g_sp_stamp_mov), ntiles * sizeof(uint4)));
+    uint32_t base = si[0].x;
+    for (const uint4 &v : si) base = (int32_t)(v.x - base) < 0 ? v.x : base;
+    printf("# times in us from sp_image's first workgroup start (the last drop of the timed loop)\n");
+    report("sp_image", si, base);
+    report("sp_move", sm, base);
+    return 0;
+}
