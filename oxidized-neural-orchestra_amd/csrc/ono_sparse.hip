@@ -48,7 +48,7 @@ constexpr int kIT = 128, kIE = kTile / kIT;  // the encoder's tile: 2 waves x 16
 // Measurement build only (tools/sp_phases.hip compiles this file with ONO_SP_STAMP defined; the
 // library never does): {start, mid - start, end - start, XCC id} in 100 MHz ticks per sp_image
 // workgroup / sp_move wave, end = after the unit's own memory operations are acknowledged.
-__device__ uint4 g_sp_stamp_img[1 << 16], g_sp_stamp_mov[1 << 18];
+__device__ uint4 g_sp_stamp_img[1 << 16], g_sp_stamp_mov[1 << 18], g_sp_stamp_pli[1 << 16], g_sp_stamp_plp[1 << 16];
 __device__ __forceinline__ void sp_stamp(uint4 *st, size_t i, uint64_t t0, uint64_t tm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -80,6 +80,16 @@ typedef float f4s __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t lane_before(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
+// Write-through stores (`nt sc1`): the line leaves the XCD's L2 with the store instead of staying
+// dirty there until the kernel's end (a boundary behind B dirty bytes costs about B / 6 TB/s more).
+// Used for sp_image's slots (the boundary to sp_move 2.8 -> 1.5 us); the wire (sp_move) and g
+// (pl_place) measured slower with them (23 vs 11 us, 25 vs 18.7 us: profiles/r04_s15_*).
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4_wt(void *p, uint4 v) {
+    const u4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+}
+
 // Inclusive sum over lanes 0..l, all DPP (row_shr 1 / 2 / 4 / 8 within rows
 // of 16, then row_bcast 15 and 31 across rows): six VALU adds.
 __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t v) {
@@ -233,14 +243,6 @@ __device__ __forceinline__ TileScan tile_scan(uint32_t keep, uint32_t start, uin
 }
 static_assert(kIE <= 32, "a thread's flags are one 32-bit mask; its counts are packed as 16-bit halves");
 
-// One workgroup per tile: flags, the block scans, then the tile's byte range
-// in LDS — each kept value at 8 S + 2 F, each run's header by the thread that
-// holds its start (offset = start - end of the previous run, length = first
-// unkept after it - start, both tile-local; a run open at either tile edge is
-// completed by sp_move) — and out to the tile's slot.  Records: recA = {kept
-// | runs << 16, last kept + 1 | first unkept << 16} (what the scan needs),
-// recB = {first header | last header << 16, the first run's offset | the
-// last run's length << 16} (what the move completes).
 // A tile's values and the value before the wave's first one (lane 0 uses
 // it).  That one is a vector load of a wave-uniform address, issued first:
 // as a scalar load it shares its counter with the LDS traffic of the tile
@@ -277,8 +279,19 @@ struct ImgAgg {
     uint64_t fr = 0;
     uint32_t lk = 0, nfu = 0;
 };
-// One tile, its values in registers: flags, the block scans, the image in LDS, out to its slot,
-// its records; its counts into the workgroup's aggregate (uniform values).
+// One tile, its values in registers: flags, the block scans, then the tile's byte range in LDS —
+// each kept value at 8 S + 2 F, each run's header by the thread that holds its start (offset =
+// start - end of the previous run, length = first unkept after it - start, both tile-local; a run
+// open at either tile edge is completed by sp_move) — and out to the tile's slot.  Records: recA =
+// {kept | runs << 16, last kept + 1 | first unkept << 16} (the prefix's terms), recB = {first
+// header | last header << 16, the first run's offset | the last run's length << 16} (what the move
+// completes); its counts into the workgroup's aggregate (uniform values).
+// VM = 1: one loop over the thread's kept values (in order, each position advanced from the last:
+// + 1, + 4 more at a run start), the headers written on the way (the offset at a start, the length
+// when the next run starts or after the loop); the values read back from the thread's own units
+// of an LDS copy (an indexable register file).  VM = 0: the value pass over all 16 elements, then
+// a loop over the run starts with popcounts for each (measurement).
+template <int VM>
 __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], float before, size_t n, float t,
                                            uint16_t *img, uint2 *recA, uint2 *recB, ImgAgg &acc) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
@@ -293,51 +306,97 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
     const TileScan ts = tile_scan(b.keep, b.start, unk);
     const uint32_t R = ts.ts, F = ts.tf;
     const uint32_t tend_l = (uint32_t)min((size_t)kTile, n - tile0);
-    // the values: one store per element, branch-free — to byte 8 S + 2 F of
-    // the tile's range when kept, else to this thread's spare unit past the
-    // image (no exec-mask branches around 16 conditional stores)
-    // (4 S + F, advanced value by value: + 4 at a run start, + 1 after a kept
-    // value — two bit extracts per value instead of two masked popcounts)
-    {
-        const uint32_t spare = (uint32_t)kSlotU16 + 2 * threadIdx.x;
-        uint32_t pos = 4 * ts.es + ts.ef;
-#pragma unroll
-        for (int e = 0; e < kIE; e++) {
-            pos += 4 * (b.start >> e & 1u);  // runs started at or before e
-            const uint32_t k = b.keep >> e & 1u;
-            stage[k ? pos : spare] = to_f16_sp(x[e]);
-            pos += k;
-        }
-    }
-    // the headers: a loop over this thread's run starts (offset = start - end
-    // of the previous run, length = first unkept after it - start, both
-    // tile-local; runs open at a tile edge are completed by sp_move).  The
-    // stores are volatile LDS stores so that they stay 2-byte stores: merged
-    // into wider ones they would be unaligned LDS accesses.
     typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
     lds_u16 *vst = (lds_u16 *)stage;
-    for (uint32_t m = b.start; m; m &= m - 1u) {
-        const int e = __ffs(m) - 1;
-        const uint32_t below = (1u << e) - 1u;
-        const uint32_t f = ts.ef + __popc(b.keep & below), sl = ts.es + __popc(b.start & below);
-        const uint32_t mk = b.keep & below, mu = unk & ~((2u << e) - 1u);
-        const uint32_t prev_end = mk ? lo + 32u - __clz(mk) : ts.kept1_before;
-        const uint32_t next_unkept =
-            mu ? lo + (uint32_t)(__ffs(mu) - 1) : (ts.unkept_after < (uint32_t)kTile ? ts.unkept_after : tend_l);
-        const uint32_t off = lo + e - prev_end, len = next_unkept - (lo + e);
-        const uint32_t p = 4 * sl + f;  // the header, 8 bytes before the run's first value
-        vst[p] = (uint16_t)off;
-        vst[p + 1] = 0;
-        vst[p + 2] = (uint16_t)len;
-        vst[p + 3] = 0;
-        if (sl == 0) rb[0] = p | off << 16;
-        if (sl == R - 1) rb[1] = p | len << 16;
-    }
+    if constexpr (VM == 1) {
+        __shared__ __attribute__((aligned(16))) uint32_t vals[kTile / 2];
+        uint32_t w[kIE / 2];
+#pragma unroll
+        for (int q = 0; q < kIE / 2; q++) w[q] = to_f16_sp(x[2 * q]) | (uint32_t)to_f16_sp(x[2 * q + 1]) << 16;
+        uint4 *v4 = (uint4 *)(vals + lo / 2);
+#pragma unroll
+        for (int q = 0; q < kIE / 8; q++) v4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+        lds_cu16 *v16 = (lds_cu16 *)vals;  // (an LDS read: a generic pointer would be a flat load)
+        uint32_t pos = 4 * ts.es + ts.ef;  // the next value's unit, before a header of its own
+        uint32_t sl = ts.es, last = ts.kept1_before, hp = 0, rs = 0, hsl = 0;
+        bool open = false;  // a run started in this thread, its length not written yet
+        for (uint32_t m = b.keep; m; m &= m - 1u) {
+            const uint32_t e = (uint32_t)__ffs(m) - 1u, i = lo + e;
+            if (b.start >> e & 1u) {
+                if (open) {  // the previous run ended at last (an unkept value before i)
+                    const uint32_t len = last - rs;
+                    vst[hp + 2] = (uint16_t)len;
+                    vst[hp + 3] = 0;
+                    if (hsl == R - 1) rb[1] = hp | len << 16;
+                }
+                hp = pos;
+                pos += 4;
+                rs = i;
+                hsl = sl++;
+                const uint32_t off = i - last;  // since the previous run's end (tile-local)
+                vst[hp] = (uint16_t)off;
+                vst[hp + 1] = 0;
+                if (hsl == 0) rb[0] = hp | off << 16;
+                open = true;
+            }
+            vst[pos++] = v16[i];
+            last = i + 1;
+        }
+        if (open) {  // the first unkept after the run: in the thread, else after it (tile-local)
+            const uint32_t eo = last - lo;
+            const uint32_t end = eo < (uint32_t)kIE && (valid >> eo & 1u)
+                                     ? last : (ts.unkept_after < (uint32_t)kTile ? ts.unkept_after : tend_l);
+            const uint32_t len = end - rs;
+            vst[hp + 2] = (uint16_t)len;
+            vst[hp + 3] = 0;
+            if (hsl == R - 1) rb[1] = hp | len << 16;
+        }
+    } else {
+        // the values: one store per element, branch-free — to byte 8 S + 2 F of
+        // the tile's range when kept, else to this thread's spare unit past the
+        // image (no exec-mask branches around 16 conditional stores)
+        // (4 S + F, advanced value by value: + 4 at a run start, + 1 after a kept
+        // value — two bit extracts per value instead of two masked popcounts)
+        {
+            const uint32_t spare = (uint32_t)kSlotU16 + 2 * threadIdx.x;
+            uint32_t pos = 4 * ts.es + ts.ef;
+    #pragma unroll
+            for (int e = 0; e < kIE; e++) {
+                pos += 4 * (b.start >> e & 1u);  // runs started at or before e
+                const uint32_t k = b.keep >> e & 1u;
+                stage[k ? pos : spare] = to_f16_sp(x[e]);
+                pos += k;
+            }
+        }
+        // the headers: a loop over this thread's run starts (offset = start - end
+        // of the previous run, length = first unkept after it - start, both
+        // tile-local; runs open at a tile edge are completed by sp_move).  The
+        // stores are volatile LDS stores so that they stay 2-byte stores: merged
+        // into wider ones they would be unaligned LDS accesses.
+        for (uint32_t m = b.start; m; m &= m - 1u) {
+            const int e = __ffs(m) - 1;
+            const uint32_t below = (1u << e) - 1u;
+            const uint32_t f = ts.ef + __popc(b.keep & below), sl = ts.es + __popc(b.start & below);
+            const uint32_t mk = b.keep & below, mu = unk & ~((2u << e) - 1u);
+            const uint32_t prev_end = mk ? lo + 32u - __clz(mk) : ts.kept1_before;
+            const uint32_t next_unkept =
+                mu ? lo + (uint32_t)(__ffs(mu) - 1) : (ts.unkept_after < (uint32_t)kTile ? ts.unkept_after : tend_l);
+            const uint32_t off = lo + e - prev_end, len = next_unkept - (lo + e);
+            const uint32_t p = 4 * sl + f;  // the header, 8 bytes before the run's first value
+            vst[p] = (uint16_t)off;
+            vst[p + 1] = 0;
+            vst[p + 2] = (uint16_t)len;
+            vst[p + 3] = 0;
+            if (sl == 0) rb[0] = p | off << 16;
+            if (sl == R - 1) rb[1] = p | len << 16;
+        }
+}
     __syncthreads();
     const uint32_t nu16 = 4 * R + F;
     uint4 *slot = (uint4 *)(img + tile * kSlotU16);
     const uint4 *st4 = (const uint4 *)stage;
-    for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) slot[k] = st4[k];
+    for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) st4_wt(slot + k, st4[k]);
     if (threadIdx.x == 0) {
         recA[tile] = make_uint2(F | R << 16, ts.last_kept1 | ts.first_unkept << 16);
         recB[tile] = R ? make_uint2((rb[0] & 0xFFFFu) | rb[1] << 16, rb[0] >> 16 | (rb[1] & 0xFFFF0000u))
@@ -357,6 +416,7 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
 // workgroup's counts to its chunk's aggregate (one 128-B line per chunk: kRecChunk / tpw
 // workgroups per line).  It also zeroes the next call's aggregates (the previous call's sp_move,
 // which read them, is done).
+template <int VM>
 __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, size_t ntiles, uint32_t tpw,
                                                 float t, bool vec, uint16_t *img, uint2 *recA, uint2 *recB,
                                                 uint4 *agg, uint4 *agg_next, uint32_t gcap) {
@@ -374,14 +434,14 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
             size_t next = tile + 1;
             load_tile<true>(g, n, next < f1 ? next : tile, xb, bb);
             __builtin_amdgcn_sched_barrier(0);  // the loads issued before any use of the current values
-            image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
+            image_tile<VM>(tile, xa, ba, n, t, img, recA, recB, acc);
             tile = next;
             __syncthreads();  // the LDS image is reused
             if (tile >= f1) break;
             next = tile + 1;
             load_tile<true>(g, n, next < f1 ? next : tile, xa, ba);
             __builtin_amdgcn_sched_barrier(0);
-            image_tile(tile, xb, bb, n, t, img, recA, recB, acc);
+            image_tile<VM>(tile, xb, bb, n, t, img, recA, recB, acc);
             tile = next;
             __syncthreads();
             if (tile >= f1) break;
@@ -389,7 +449,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
     }
     for (; tile < t1; tile++) {
         load_tile<false>(g, n, tile, xa, ba);
-        image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
+        image_tile<VM>(tile, xa, ba, n, t, img, recA, recB, acc);
         __syncthreads();
     }
     if (threadIdx.x == 0 && t0 < t1) {
@@ -487,10 +547,10 @@ __device__ __forceinline__ uint2 chunk_totals(const uint4 *agg, uint32_t G) {
 // — the last O units of slot chunk c - 1 (the lane before, by DPP) and the
 // first 8 - O of slot chunk c (this lane).  Whole chunks are one 16-B store;
 // the range's first and last chunk (shared with the neighbouring tiles) are
-// stored unit by unit.  The two completed header fields (slot units c0, c0 + 1
-// and hl + 2, hl + 3) are substituted in registers on the way.
+// stored unit by unit.  The two header fields completed from other tiles are
+// stored after these by one lane (same wave, same addresses, later in program
+// order).
 constexpr int kMoveBatch = 2;  // 16-B slot chunks per lane loaded up front: 1024 units per wave
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ldn4(const uint4 *p) {
     const u4v r = __builtin_nontemporal_load((const u4v *)p);
     return make_uint4(r.x, r.y, r.z, r.w);
@@ -503,17 +563,9 @@ __device__ __forceinline__ uint4 readlane4(uint4 v, int l) {
                       (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l));
 }
 template <int O>
-__device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveBatch], uint32_t nu16, uint32_t R,
-                                            const uint32_t (&fu)[4], const uint32_t (&fv)[4], uint16_t *base16) {
+__device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveBatch], uint32_t nu16, uint16_t *base16) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nchunks = nu16 ? (O + nu16 + 7) / 8 : 0;
-    // field unit f of the range lands at base16 unit f + O: chunk, word, half
-    uint32_t fc[4], fw[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        fc[j] = R ? (fu[j] + O) / 8 : 0xFFFFFFFFu;
-        fw[j] = (fu[j] + O) % 8;  // unit within the chunk
-    }
     uint4 carry = make_uint4(0, 0, 0, 0);  // slot chunk before this batch's first one
     auto batch = [&](uint32_t c0b) {
 #pragma unroll
@@ -531,20 +583,8 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
                 else o[j] = __builtin_amdgcn_alignbit(C[(sft + 1) / 2], C[(sft - 1) / 2], 16);
             }
             const uint32_t c = c0b + lane + 64 * k;
-            if (R) {
-#pragma unroll
-                for (int f = 0; f < 4; f++) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        if (c == fc[f] && fw[f] / 2 == (uint32_t)j) {
-                            const uint32_t sh = 16 * (fw[f] % 2);
-                            o[j] = (o[j] & ~(0xFFFFu << sh)) | fv[f] << sh;
-                        }
-                    }
-                }
-            }
             const bool whole = c * 8 >= (uint32_t)O && (size_t)c * 8 + 8 - O <= nu16;
-            if (whole) {
+            if (whole) {  // (write-through stores measured slower here: 23 vs 11 us)
                 const u4v ov = {o[0], o[1], o[2], o[3]};
                 __builtin_nontemporal_store(ov, (u4v *)(base16 + 8 * (size_t)c));
             } else if (c < nchunks) {  // the range's first / last chunk
@@ -565,28 +605,11 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
     }
 }
 
-// One wave per tile: its records and prefix by scalar loads, the slot's first
-// 1024 units (most tiles' whole image) issued at the same time, then the move.
-// Block 0 also writes the u64 total length and publishes the wire length.
-__global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) void sp_move(
-    const uint16_t *__restrict__ img, const uint2 *__restrict__ recA, const uint2 *__restrict__ recB,
-    const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, uint64_t *__restrict__ host_tot,
-    uint64_t *__restrict__ nbytes_out) {
-    const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
-    if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
-        const uint2 t = chunk_totals(agg, G);
-        if (threadIdx.x == 0) {
-            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
-            const uint64_t F = t.x, R = t.y;
-            host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
-            host_tot[1] = R;
-            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
-        }
-    }
+// One tile's slot to its place (sp_move).
+__device__ __forceinline__ void move_tile(const uint16_t *__restrict__ img, const uint2 *__restrict__ recA,
+                                          const uint2 *__restrict__ recB, const uint4 *__restrict__ agg, size_t ntiles,
+                                          uint32_t G, size_t n, uint8_t *__restrict__ buf, size_t tile) {
     const uint32_t lane = threadIdx.x & 63;
-    // wave-uniform (readfirstlane): scalar base addresses and branches
-    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
-    if (tile >= ntiles) return;
     SP_CLOCK(sp_t0);
     const uint4 *src4 = (const uint4 *)(img + tile * kSlotU16);
     uint4 v[kMoveBatch];
@@ -605,25 +628,67 @@ __global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const uint32_t off0 = (hb.y & 0xFFFFu) + (tile0 - p.z);
     const uint32_t lenl = (hb.y >> 16) + (tile0 + (a.y & 0xFFFFu) == tend ? p.w - tend : 0u);
     const uint32_t c0 = hb.x & 0xFFFFu, hl = hb.x >> 16;
-    const uint32_t fu[4] = {c0, c0 + 1, hl + 2, hl + 3};
-    const uint32_t fv[4] = {off0 & 0xFFFFu, off0 >> 16, lenl & 0xFFFFu, lenl >> 16};
     uint8_t *dst = buf + 8 + 8 * (size_t)p.y + 2 * (size_t)p.x;
     const uint32_t O = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uintptr_t)dst & 15u) >> 1));
     uint16_t *base16 = (uint16_t *)(dst - 2 * O);
     switch (O) {
-    case 0: move_chunks<0>(src4, v, nu16, R, fu, fv, base16); break;
-    case 1: move_chunks<1>(src4, v, nu16, R, fu, fv, base16); break;
-    case 2: move_chunks<2>(src4, v, nu16, R, fu, fv, base16); break;
-    case 3: move_chunks<3>(src4, v, nu16, R, fu, fv, base16); break;
-    case 4: move_chunks<4>(src4, v, nu16, R, fu, fv, base16); break;
-    case 5: move_chunks<5>(src4, v, nu16, R, fu, fv, base16); break;
-    case 6: move_chunks<6>(src4, v, nu16, R, fu, fv, base16); break;
-    default: move_chunks<7>(src4, v, nu16, R, fu, fv, base16); break;
+    case 0: move_chunks<0>(src4, v, nu16, base16); break;
+    case 1: move_chunks<1>(src4, v, nu16, base16); break;
+    case 2: move_chunks<2>(src4, v, nu16, base16); break;
+    case 3: move_chunks<3>(src4, v, nu16, base16); break;
+    case 4: move_chunks<4>(src4, v, nu16, base16); break;
+    case 5: move_chunks<5>(src4, v, nu16, base16); break;
+    case 6: move_chunks<6>(src4, v, nu16, base16); break;
+    default: move_chunks<7>(src4, v, nu16, base16); break;
+    }
+    if (R && lane == 0) {  // the first run's offset (units c0, c0 + 1) and the last run's length (hl + 2, + 3)
+        uint16_t *r16 = base16 + O;
+        r16[c0] = (uint16_t)off0;
+        r16[c0 + 1] = (uint16_t)(off0 >> 16);
+        r16[hl + 2] = (uint16_t)lenl;
+        r16[hl + 3] = (uint16_t)(lenl >> 16);
     }
 #ifdef ONO_SP_STAMP
     sp_stamp(g_sp_stamp_mov, tile, sp_t0, sp_tm);
 #endif
 }
+// the same as a call (the looping kernel: one copy of the eight alignments, not one per unrolled pass)
+__device__ __attribute__((noinline)) void move_tile_call(const uint16_t *__restrict__ img, const uint2 *__restrict__ recA,
+                                                          const uint2 *__restrict__ recB, const uint4 *__restrict__ agg,
+                                                          size_t ntiles, uint32_t G, size_t n, uint8_t *__restrict__ buf,
+                                                          size_t tile) {
+    move_tile(img, recA, recB, agg, ntiles, G, n, buf, tile);
+}
+
+// One wave per tile (ONO_SP_MTPW tiles per wave in turn: measurement): its records and prefix, the
+// slot's first 1024 units (most tiles' whole image) issued at the same time, then the move.
+// Block 0 also writes the u64 total length and publishes the wire length.
+template <bool LOOP>
+__global__ __launch_bounds__(kSB) void sp_move(
+    const uint16_t *__restrict__ img, const uint2 *__restrict__ recA, const uint2 *__restrict__ recB,
+    const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, uint64_t *__restrict__ host_tot,
+    uint64_t *__restrict__ nbytes_out) {
+    const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
+        const uint2 t = chunk_totals(agg, G);
+        if (threadIdx.x == 0) {
+            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
+            const uint64_t F = t.x, R = t.y;
+            host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
+            host_tot[1] = R;
+            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
+        }
+    }
+    // wave-uniform (readfirstlane): scalar base addresses and branches; tiles w, w + waves, ...
+    const size_t w0 = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
+    const size_t nw = (size_t)gridDim.x * (kSB / 64);
+    if constexpr (LOOP) {
+        for (size_t tile = w0; tile < ntiles; tile += nw) move_tile_call(img, recA, recB, agg, ntiles, G, n, buf, tile);
+    } else {
+        if (w0 < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, w0);
+    }
+}
+
 
 // Fallback lift (after a host parse): value v belongs to run j with
 // cumF[j] <= v < cumF[j+1] (binary search);
@@ -1393,6 +1458,7 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, si
                                                   uint32_t *qcount, uint32_t *wide, uint64_t *host_word,
                                                   uint64_t *badw, uint32_t epoch) {
     __shared__ uint16_t lmask[TPB][kPatT], lpre[TPB][kPatT];  // (masks of kPatPer bits)
+    SP_CLOCK(sp_t0);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // before pl_place: the total for the host, an empty queue
         host_word[1] = stream_total(b);
         *qcount = 0;
@@ -1414,6 +1480,7 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, si
         in[2 * q + 1] = sum;
     }
     block_scan_n<TPB>(in, ex, tot);
+    SP_CLOCK(sp_tm);
 #pragma unroll
     for (int q = 0; q < TPB; q++) {
         lmask[q][threadIdx.x] = (uint16_t)m[q];
@@ -1449,6 +1516,11 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, si
         }
     }
     if (bad) raise_bad(badw, epoch);
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64) sp_stamp(g_sp_stamp_pli, blockIdx.x, sp_t0, sp_tm);
+#endif
 }
 // tiles per pl_index workgroup: 1, or 2 (each thread's loads for both tiles issued together); env
 // ONO_PL_TPB selects for measurement (profiles/r04_*: 1 -> 8.7-9.1 us, 2 -> 9.35 us at 64 MiB / 10 %)
@@ -1688,6 +1760,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     const uint16_t *lw = (const uint16_t *)lw4;
     const uint32_t t = blockIdx.x, base = t * (uint32_t)kPatU, M32 = (uint32_t)M, T32 = (uint32_t)T;
     const bool direct = T <= kPatDirect;  // (uniform) else E[] from pl_scan
+    SP_CLOCK(sp_t0);
     // the prologue's loads issued together: the tile's record, its range (E from pl_scan, or the earlier
     // tiles' sums), the record of each of the 256 tiles before it (the nearest non-empty one's exit is
     // the link into this tile)
@@ -1745,6 +1818,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
         if (bad && threadIdx.x == 0) raise_bad(badw, epoch);
     }
+    SP_CLOCK(sp_tm);
     const uint32_t total32 = (uint32_t)total;
     const uint32_t ea = (uint32_t)min(E0, total);
     const uint32_t eb = max(t + 1 == T32 ? total32 : (uint32_t)min(E1, total), ea);
@@ -1817,7 +1891,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
             const uint2 h = img8[i];
             const f4s x = {from_f16_sp((uint16_t)h.x), from_f16_sp((uint16_t)(h.x >> 16)), from_f16_sp((uint16_t)h.y),
                            from_f16_sp((uint16_t)(h.y >> 16))};
-            __builtin_nontemporal_store(x, (f4s *)gi0 + i);
+            __builtin_nontemporal_store(x, (f4s *)gi0 + i);  // (write-through stores measured slower here: 25 vs 18.7 us)
         }
         if (threadIdx.x < 4) {
             const uint32_t e = threadIdx.x;
@@ -1828,6 +1902,11 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     } else {
         for (uint32_t i = threadIdx.x; i < n; i += kPatT) gi0[i] = from_f16_sp(img[i]);
     }
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64) sp_stamp(g_sp_stamp_plp, blockIdx.x, sp_t0, sp_tm);
+#endif
 }
 
 // The tiles pl_place flagged, one workgroup each, grid-stride over the tiles.
@@ -2304,6 +2383,25 @@ size_t image_tiles_per_wg() {
     return v;
 }
 
+// tiles per sp_move wave (ONO_SP_MTPW, 1-16: measurement)
+size_t move_tiles_per_wave() {
+    static const size_t v = [] {
+        const char *e = getenv("ONO_SP_MTPW");
+        const long x = e ? atol(e) : 0;
+        return x >= 1 && x <= 16 ? (size_t)x : (size_t)1;
+    }();
+    return v;
+}
+
+// sp_image's value pass (ONO_SP_VM = 0 / 1: measurement), see image_tile
+int image_value_mode() {
+    static const int v = [] {
+        const char *e = getenv("ONO_SP_VM");
+        return e && atoi(e) == 0 ? 0 : 1;
+    }();
+    return v;
+}
+
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
@@ -2322,8 +2420,12 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     hipError_t e = hipSuccess;
     if (ntiles) {
         const size_t tpw = image_tiles_per_wg(), grid = (ntiles + tpw - 1) / tpw;
-        hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold, vec,
-                           sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
+        if (image_value_mode() == 0)
+            hipLaunchKernelGGL(sp_image<0>, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold,
+                               vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
+        else
+            hipLaunchKernelGGL(sp_image<1>, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold,
+                               vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     }
@@ -2335,9 +2437,13 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
                              (size_t)(8 + 8 * tot[1] + 2 * tot[0]), cap);
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
-    const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
-                       sc->host_tot_dev, nbytes_dev);
+    const size_t mw = move_tiles_per_wave() * (kSB / 64), mblocks = std::max<size_t>(1, (ntiles + mw - 1) / mw);
+    if (move_tiles_per_wave() == 1)
+        hipLaunchKernelGGL(sp_move<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n,
+                           buf, sc->host_tot_dev, nbytes_dev);
+    else
+        hipLaunchKernelGGL(sp_move<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n,
+                           buf, sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     if (nbytes_dev) return ONO_OK;

@@ -8,6 +8,9 @@
 // (sp_move: its loads landed and its prefix known; sp_image: its last tile imaged) and the
 // per-XCD last end.
 //
+// Then the same for K stream-ordered lifts (pattern path) of the last drop's wire into 6 outputs
+// in turn: pl_index and pl_place stamped per workgroup.
+//
 // usage: sp_phases [MiB=64] [K=24]
 #define ONO_SP_STAMP 1
 #include "../oxidized-neural-orchestra_amd/csrc/ono_sparse.hip"
@@ -129,5 +132,37 @@ int main(int argc, char **argv) {
     printf("# times in us from sp_image's first workgroup start (the last drop of the timed loop)\n");
     report("sp_image", si, base);
     report("sp_move", sm, base);
+
+    // the stream-ordered lift (pattern path) of the last drop's wire, into 6 outputs in turn
+    const size_t nb = (size_t)wire;
+    std::vector<float *> outs(NG);
+    for (int i = 0; i < NG; i++) CK(hipMalloc((void **)&outs[i], n * sizeof(float)));
+    uint64_t *status, ticket = 0;
+    CK(hipMalloc((void **)&status, 8));
+    CK(hipMemset(status, 0, 8));
+    for (int i = 0; i < 2 * K; i++)
+        if (ono_sparse_lift_dev_async(outs[i % NG], n, buf, nb, status, &ticket, s)) return 1;
+    CK(hipStreamSynchronize(s));
+    for (int i = 0; i < 8; i++) ono_sparse_lift_dev_async(outs[i % NG], n, buf, nb, status, &ticket, s);
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < K; i++) ono_sparse_lift_dev_async(outs[i % NG], n, buf, nb, status, &ticket, s);
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    uint64_t st = 0;
+    CK(hipMemcpy(&st, status, 8, hipMemcpyDeviceToHost));
+    const double lper = ms * 1e3 / K, lbytes = 4.0 * n + (double)nb;
+    printf("# lift: %d stream-ordered lifts: %.2f us per lift (events), %.1f GB/s = %.3f of 8 TB/s, refused %d\n", K,
+           lper, lbytes / lper * 1e-3, lbytes / lper * 1e-3 / 8000.0, (int)(st == ticket));
+    const size_t T = ((nb - 8) / 2 + kPatU - 1) / kPatU;
+    std::vector<uint4> spi(T), spp(T);
+    CK(hipMemcpyFromSymbol(spi.data(), HIP_SYMBOL(g_sp_stamp_pli), T * sizeof(uint4)));
+    CK(hipMemcpyFromSymbol(spp.data(), HIP_SYMBOL(g_sp_stamp_plp), T * sizeof(uint4)));
+    base = spi[0].x;
+    for (const uint4 &v : spi) base = (int32_t)(v.x - base) < 0 ? v.x : base;
+    printf("# times in us from pl_index's first workgroup start (the last lift; mid: pl_index after its scan, "
+           "pl_place after its prologue)\n");
+    report("pl_index", spi, base);
+    report("pl_place", spp, base);
     return 0;
 }
