@@ -294,8 +294,14 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int, ks=(2, 4, 8), warm_rot
     kernel measured over freshly allocated buffers moved by up to 4 % with the
     placement, profiles/r04_lr_ab_s{3,4}.txt), and each k is measured in
     `passes` passes interleaved with the other k's; the reported figure is the
-    median pass (min / max beside it).  ks / warm_rotations / settle_s: knobs
-    for tools/lr_ab.py (warm-up rotations; a synchronised pause before it)."""
+    median pass (min / max beside it).  The same passes time the library's
+    1R2W copy (`scale_zero` with divisor 1: read one bucket, write two — the
+    12 B per element of k = 2) over k = 2's sets, so config 2 also reads
+    against a ceiling measured on the same buffers in the same passes
+    (`copy_zero_same_pool`, `frac_of_same_pool_copy_zero`): the placement of a
+    set moves a 64 MiB launch by 2-4 %, more than the kernels differ.
+    ks / warm_rotations / settle_s: knobs for tools/lr_ab.py (warm-up
+    rotations; a synchronised pause before it)."""
     n = 16 << 20
     out = {}
     stream = torch.cuda.Stream()  # a stream of its own (the ring's reductions run on the caller's)
@@ -304,8 +310,28 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int, ks=(2, 4, 8), warm_rot
     for b in range(max(nsets[k] * (k + 1) for k in ks)):
         pool.append(ono_amd.kernels.synth(torch.empty(n, dtype=torch.float32, device="cuda"), SEED + b // 9, b % 9))
     sets = {k: [(pool[s * (k + 1):s * (k + 1) + k], pool[s * (k + 1) + k]) for s in range(nsets[k])] for k in ks}
+    # the 1R2W copy over k = 2's sets: read the set's first input, write its output and a zero buffer of
+    # the set's own (the inputs stay intact for the sums)
+    cz_sets = []
+    if 2 in ks:
+        cz_sets = [(ins[0], dst, torch.zeros(n, dtype=torch.float32, device="cuda")) for ins, dst in sets[2]]
     ms = {k: [] for k in ks}
+    cz_ms = []
     for _ in range(passes):
+        if cz_sets:
+            ns = len(cz_sets)
+            warm = max(warmup, ns * warm_rotations)
+            for i in range(warm):
+                src, dst, zero = cz_sets[i % ns]
+                ono_amd.kernels.scale_zero(dst, src, 1.0, zero, stream)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for i in range(steps):
+                src, dst, zero = cz_sets[(warm + i) % ns]
+                ono_amd.kernels.scale_zero(dst, src, 1.0, zero, stream)
+            b.record(stream)
+            b.synchronize()
+            cz_ms.append(a.elapsed_time(b) / steps)
         for k in ks:
             ns = nsets[k]
             if settle_s:
@@ -339,7 +365,19 @@ def local_reduce(torch, ono_amd, steps: int, warmup: int, ks=(2, 4, 8), warm_rot
                         "us_per_launch_min": round(v[0] * 1e3, 2), "us_per_launch_max": round(v[-1] * 1e3, 2),
                         "passes": len(v), "rotating_sets": nsets[k],
                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None}
-    del sets, pool
+    if cz_ms:
+        v = sorted(cz_ms)
+        med = v[len(v) // 2]
+        gbs = 12 * n / (med * 1e-3) / 1e9
+        out["copy_zero_same_pool"] = {"bytes_per_launch": 12 * n, "us_per_launch": round(med * 1e3, 2),
+                                      "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                                      "us_per_launch_min": round(v[0] * 1e3, 2),
+                                      "us_per_launch_max": round(v[-1] * 1e3, 2), "passes": len(v),
+                                      "rotating_sets": len(cz_sets),
+                                      "shape": "ono_scale_zero_f32 /1 (1R2W, 12 B/elem) over k = 2's sets"}
+        for k in ks:
+            out[f"k{k}"]["frac_of_same_pool_copy_zero"] = round(out[f"k{k}"]["achieved_gbs"] / gbs, 4)
+    del sets, pool, cz_sets
     torch.cuda.empty_cache()
     return {"workload": "sum_scale_f32, 64 MiB buckets, out = (sum of k inputs) / k", "hbm_peak_gbs": HBM_PEAK_GBS,
             "timing": f"one HIP event pair around K back-to-back launches (inter-kernel gaps included); median "
@@ -1328,6 +1366,10 @@ def n1_roofline_summary(roofline: dict, lr: dict | None, cc: dict | None) -> dic
             fc = {k: round(lr[k]["achieved_gbs"] / c64["achieved_gbs"], 4) for k in fr}
             roofline["reduce_kernel"]["frac_of_copy_ceiling_64MiB"] = fc
             roofline["reduce_kernel_frac_of_ceiling_min"] = min(fc.values())
+        sp = {k: lr[k]["frac_of_same_pool_copy_zero"] for k in fr if "frac_of_same_pool_copy_zero" in lr[k]}
+        if sp:  # the 1R2W copy timed over the same buffers in the same passes (local_reduce)
+            roofline["reduce_kernel"]["frac_of_same_pool_copy_zero"] = sp
+            roofline["reduce_kernel_frac_of_same_pool_ceiling_min"] = min(sp.values())
     return roofline
 
 

@@ -151,7 +151,22 @@ def test_n1_line_carries_reduce_kernel_and_ceiling_as_flat_keys():
     assert flat["copy_ceiling_gbs"] == 6950.0 and flat["copy_ceiling_shape"] == "copy_zero"
     assert flat["frac_of_copy_ceiling"] == pytest.approx(6900 / 6950, abs=1e-4) and flat["frac_of_copy_ceiling"] <= 1
     assert flat["reduce_kernel_frac_of_ceiling_min"] == pytest.approx(6280 / 6400, abs=1e-4)
+    assert "reduce_kernel_frac_of_same_pool_ceiling_min" not in flat  # no same-pool copy timed
     json.dumps(line)
+
+
+def test_n1_line_carries_the_same_pool_ceiling_of_config2():
+    """local_reduce also times the 1R2W copy over k = 2's own buffers in the same
+    passes; its fractions travel flat as well."""
+    rl = {"bound": "hbm", "achieved": 6900.0, "frac": 0.8625}
+    lr = {"k2": {"frac_of_hbm_peak": 0.79, "achieved_gbs": 6320.0, "frac_of_same_pool_copy_zero": 0.991},
+          "k4": {"frac_of_hbm_peak": 0.785, "achieved_gbs": 6280.0, "frac_of_same_pool_copy_zero": 0.985},
+          "k8": {"frac_of_hbm_peak": 0.80, "achieved_gbs": 6400.0, "frac_of_same_pool_copy_zero": 1.004},
+          "copy_zero_same_pool": {"achieved_gbs": 6376.0}, "timing": "events"}
+    bench.n1_roofline_summary(rl, lr, {})
+    assert rl["reduce_kernel_frac_of_same_pool_ceiling_min"] == 0.985
+    assert rl["reduce_kernel"]["frac_of_same_pool_copy_zero"]["k8"] == 1.004
+    json.dumps(rl)
 
 
 @pytest.mark.parametrize("algo,wire", [("xgmi", "f32"), ("xgmi", "f16"), ("allreduce", "f32"), ("direct", "f16")])
