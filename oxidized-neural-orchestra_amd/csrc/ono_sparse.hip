@@ -286,12 +286,11 @@ struct ImgAgg {
 // {kept | runs << 16, last kept + 1 | first unkept << 16} (the prefix's terms), recB = {first
 // header | last header << 16, the first run's offset | the last run's length << 16} (what the move
 // completes); its counts into the workgroup's aggregate (uniform values).
-// VM = 1: one loop over the thread's kept values (in order, each position advanced from the last:
-// + 1, + 4 more at a run start), the headers written on the way (the offset at a start, the length
-// when the next run starts or after the loop); the values read back from the thread's own units
-// of an LDS copy (an indexable register file).  VM = 0: the value pass over all 16 elements, then
-// a loop over the run starts with popcounts for each (measurement).
-template <int VM>
+// One loop over the thread's kept values (in order, each position advanced from the last: + 1, + 4
+// more at a run start) writes values and headers (the offset at a start, the length when the next
+// run starts or after the loop); the values are read back from the thread's own units of an LDS
+// copy (an indexable register file).  It replaced a value pass over all 16 elements followed by a
+// loop over the run starts with two popcounts each (round 4: 33.9 vs 34.9 us per drop).
 __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], float before, size_t n, float t,
                                            uint16_t *img, uint2 *recA, uint2 *recB, ImgAgg &acc) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
@@ -308,7 +307,7 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
     const uint32_t tend_l = (uint32_t)min((size_t)kTile, n - tile0);
     typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
     lds_u16 *vst = (lds_u16 *)stage;
-    if constexpr (VM == 1) {
+    {
         __shared__ __attribute__((aligned(16))) uint32_t vals[kTile / 2];
         uint32_t w[kIE / 2];
 #pragma unroll
@@ -352,46 +351,7 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
             vst[hp + 3] = 0;
             if (hsl == R - 1) rb[1] = hp | len << 16;
         }
-    } else {
-        // the values: one store per element, branch-free — to byte 8 S + 2 F of
-        // the tile's range when kept, else to this thread's spare unit past the
-        // image (no exec-mask branches around 16 conditional stores)
-        // (4 S + F, advanced value by value: + 4 at a run start, + 1 after a kept
-        // value — two bit extracts per value instead of two masked popcounts)
-        {
-            const uint32_t spare = (uint32_t)kSlotU16 + 2 * threadIdx.x;
-            uint32_t pos = 4 * ts.es + ts.ef;
-    #pragma unroll
-            for (int e = 0; e < kIE; e++) {
-                pos += 4 * (b.start >> e & 1u);  // runs started at or before e
-                const uint32_t k = b.keep >> e & 1u;
-                stage[k ? pos : spare] = to_f16_sp(x[e]);
-                pos += k;
-            }
-        }
-        // the headers: a loop over this thread's run starts (offset = start - end
-        // of the previous run, length = first unkept after it - start, both
-        // tile-local; runs open at a tile edge are completed by sp_move).  The
-        // stores are volatile LDS stores so that they stay 2-byte stores: merged
-        // into wider ones they would be unaligned LDS accesses.
-        for (uint32_t m = b.start; m; m &= m - 1u) {
-            const int e = __ffs(m) - 1;
-            const uint32_t below = (1u << e) - 1u;
-            const uint32_t f = ts.ef + __popc(b.keep & below), sl = ts.es + __popc(b.start & below);
-            const uint32_t mk = b.keep & below, mu = unk & ~((2u << e) - 1u);
-            const uint32_t prev_end = mk ? lo + 32u - __clz(mk) : ts.kept1_before;
-            const uint32_t next_unkept =
-                mu ? lo + (uint32_t)(__ffs(mu) - 1) : (ts.unkept_after < (uint32_t)kTile ? ts.unkept_after : tend_l);
-            const uint32_t off = lo + e - prev_end, len = next_unkept - (lo + e);
-            const uint32_t p = 4 * sl + f;  // the header, 8 bytes before the run's first value
-            vst[p] = (uint16_t)off;
-            vst[p + 1] = 0;
-            vst[p + 2] = (uint16_t)len;
-            vst[p + 3] = 0;
-            if (sl == 0) rb[0] = p | off << 16;
-            if (sl == R - 1) rb[1] = p | len << 16;
-        }
-}
+    }
     __syncthreads();
     const uint32_t nu16 = 4 * R + F;
     uint4 *slot = (uint4 *)(img + tile * kSlotU16);
@@ -416,7 +376,6 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
 // workgroup's counts to its chunk's aggregate (one 128-B line per chunk: kRecChunk / tpw
 // workgroups per line).  It also zeroes the next call's aggregates (the previous call's sp_move,
 // which read them, is done).
-template <int VM>
 __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, size_t ntiles, uint32_t tpw,
                                                 float t, bool vec, uint16_t *img, uint2 *recA, uint2 *recB,
                                                 uint4 *agg, uint4 *agg_next, uint32_t gcap) {
@@ -434,14 +393,14 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
             size_t next = tile + 1;
             load_tile<true>(g, n, next < f1 ? next : tile, xb, bb);
             __builtin_amdgcn_sched_barrier(0);  // the loads issued before any use of the current values
-            image_tile<VM>(tile, xa, ba, n, t, img, recA, recB, acc);
+            image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
             tile = next;
             __syncthreads();  // the LDS image is reused
             if (tile >= f1) break;
             next = tile + 1;
             load_tile<true>(g, n, next < f1 ? next : tile, xa, ba);
             __builtin_amdgcn_sched_barrier(0);
-            image_tile<VM>(tile, xb, bb, n, t, img, recA, recB, acc);
+            image_tile(tile, xb, bb, n, t, img, recA, recB, acc);
             tile = next;
             __syncthreads();
             if (tile >= f1) break;
@@ -449,7 +408,7 @@ __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, siz
     }
     for (; tile < t1; tile++) {
         load_tile<false>(g, n, tile, xa, ba);
-        image_tile<VM>(tile, xa, ba, n, t, img, recA, recB, acc);
+        image_tile(tile, xa, ba, n, t, img, recA, recB, acc);
         __syncthreads();
     }
     if (threadIdx.x == 0 && t0 < t1) {
@@ -652,18 +611,11 @@ __device__ __forceinline__ void move_tile(const uint16_t *__restrict__ img, cons
     sp_stamp(g_sp_stamp_mov, tile, sp_t0, sp_tm);
 #endif
 }
-// the same as a call (the looping kernel: one copy of the eight alignments, not one per unrolled pass)
-__device__ __attribute__((noinline)) void move_tile_call(const uint16_t *__restrict__ img, const uint2 *__restrict__ recA,
-                                                          const uint2 *__restrict__ recB, const uint4 *__restrict__ agg,
-                                                          size_t ntiles, uint32_t G, size_t n, uint8_t *__restrict__ buf,
-                                                          size_t tile) {
-    move_tile(img, recA, recB, agg, ntiles, G, n, buf, tile);
-}
 
-// One wave per tile (ONO_SP_MTPW tiles per wave in turn: measurement): its records and prefix, the
-// slot's first 1024 units (most tiles' whole image) issued at the same time, then the move.
+// One wave per tile: its records and prefix, the slot's first 1024 units (most tiles' whole image)
+// issued at the same time, then the move.  (Two or four tiles per wave in turn measured slower in
+// round 4: 35.7 / 39.2 vs 33.9 us per drop.)
 // Block 0 also writes the u64 total length and publishes the wire length.
-template <bool LOOP>
 __global__ __launch_bounds__(kSB) void sp_move(
     const uint16_t *__restrict__ img, const uint2 *__restrict__ recA, const uint2 *__restrict__ recB,
     const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, uint64_t *__restrict__ host_tot,
@@ -679,14 +631,9 @@ __global__ __launch_bounds__(kSB) void sp_move(
             if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
         }
     }
-    // wave-uniform (readfirstlane): scalar base addresses and branches; tiles w, w + waves, ...
-    const size_t w0 = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
-    const size_t nw = (size_t)gridDim.x * (kSB / 64);
-    if constexpr (LOOP) {
-        for (size_t tile = w0; tile < ntiles; tile += nw) move_tile_call(img, recA, recB, agg, ntiles, G, n, buf, tile);
-    } else {
-        if (w0 < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, w0);
-    }
+    // wave-uniform (readfirstlane): scalar base addresses and branches
+    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
+    if (tile < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, tile);
 }
 
 
@@ -1522,23 +1469,12 @@ __global__ __launch_bounds__(kPatT) void pl_index(const uint8_t *b, size_t M, si
     if (threadIdx.x < 64) sp_stamp(g_sp_stamp_pli, blockIdx.x, sp_t0, sp_tm);
 #endif
 }
-// tiles per pl_index workgroup: 1, or 2 (each thread's loads for both tiles issued together); env
-// ONO_PL_TPB selects for measurement (profiles/r04_*: 1 -> 8.7-9.1 us, 2 -> 9.35 us at 64 MiB / 10 %)
-int pl_index_tpb() {
-    static const int v = [] {
-        const char *e = getenv("ONO_PL_TPB");
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
-    return v;
-}
 hipError_t launch_pl_index(const uint8_t *b, size_t M, size_t T, uint32_t *rec, uint32_t *tsum, uint32_t *qcount,
                            uint32_t *wide, uint64_t *host_word, uint64_t *badw, uint32_t epoch, hipStream_t s) {
-    if (pl_index_tpb() == 2)
-        hipLaunchKernelGGL(pl_index<2>, dim3((unsigned)((T + 1) / 2)), dim3(kPatT), 0, s, b, M, T, rec, tsum, qcount,
-                           wide, host_word, badw, epoch);
-    else
-        hipLaunchKernelGGL(pl_index<1>, dim3((unsigned)T), dim3(kPatT), 0, s, b, M, T, rec, tsum, qcount, wide, host_word,
-                           badw, epoch);
+    // (two tiles per workgroup, all their loads issued before the first use, measured slower in round 4:
+    // 9.35 vs 8.1 us; the template keeps the form)
+    hipLaunchKernelGGL(pl_index<1>, dim3((unsigned)T), dim3(kPatT), 0, s, b, M, T, rec, tsum, qcount, wide, host_word,
+                       badw, epoch);
     return hipGetLastError();
 }
 
@@ -2373,34 +2309,10 @@ namespace {
 // wire length there).  Otherwise blocking: the host reads the
 // totals at the end (and, for a buffer below the worst case, once before the
 // write pass to check the size).
-// tiles per sp_image workgroup (ONO_SP_TPW, a power of two <= kRecChunk: measurement)
-size_t image_tiles_per_wg() {
-    static const size_t v = [] {
-        const char *e = getenv("ONO_SP_TPW");
-        const long x = e ? atol(e) : 0;
-        return x >= 1 && x <= kRecChunk && (x & (x - 1)) == 0 ? (size_t)x : (size_t)4;
-    }();
-    return v;
-}
-
-// tiles per sp_move wave (ONO_SP_MTPW, 1-16: measurement)
-size_t move_tiles_per_wave() {
-    static const size_t v = [] {
-        const char *e = getenv("ONO_SP_MTPW");
-        const long x = e ? atol(e) : 0;
-        return x >= 1 && x <= 16 ? (size_t)x : (size_t)1;
-    }();
-    return v;
-}
-
-// sp_image's value pass (ONO_SP_VM = 0 / 1: measurement), see image_tile
-int image_value_mode() {
-    static const int v = [] {
-        const char *e = getenv("ONO_SP_VM");
-        return e && atoi(e) == 0 ? 0 : 1;
-    }();
-    return v;
-}
+// tiles per sp_image workgroup (a power of two <= kRecChunk: all in one chunk).  Round 4 measured
+// 1 / 2 / 8 / 16 at 41.9 / 37.1 / 37.4 / 51.4 us per drop against 35.1 for 4.
+constexpr size_t kImageTpw = 4;
+static_assert(kRecChunk % kImageTpw == 0, "a workgroup's tiles share one chunk aggregate");
 
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s) {
@@ -2419,13 +2331,9 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     hipError_t e = hipSuccess;
     if (ntiles) {
-        const size_t tpw = image_tiles_per_wg(), grid = (ntiles + tpw - 1) / tpw;
-        if (image_value_mode() == 0)
-            hipLaunchKernelGGL(sp_image<0>, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold,
-                               vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
-        else
-            hipLaunchKernelGGL(sp_image<1>, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)tpw, threshold,
-                               vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
+        const size_t grid = (ntiles + kImageTpw - 1) / kImageTpw;
+        hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)kImageTpw, threshold,
+                           vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     }
@@ -2437,13 +2345,9 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
                              (size_t)(8 + 8 * tot[1] + 2 * tot[0]), cap);
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
-    const size_t mw = move_tiles_per_wave() * (kSB / 64), mblocks = std::max<size_t>(1, (ntiles + mw - 1) / mw);
-    if (move_tiles_per_wave() == 1)
-        hipLaunchKernelGGL(sp_move<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n,
-                           buf, sc->host_tot_dev, nbytes_dev);
-    else
-        hipLaunchKernelGGL(sp_move<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n,
-                           buf, sc->host_tot_dev, nbytes_dev);
+    const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
+    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
+                       sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     if (nbytes_dev) return ONO_OK;

@@ -121,9 +121,9 @@ int main(int argc, char **argv) {
     const double per = ms * 1e3 / K, bytes = 4.0 * n + (double)wire;
     printf("# sp_phases: %zu MiB, %d stream-ordered drops over %d gradients, tiles/workgroup %zu: %.2f us per drop "
            "(events), wire %llu B, %.1f GB/s = %.3f of 8 TB/s\n",
-           mib, K, NG, image_tiles_per_wg(), per, (unsigned long long)wire, bytes / per * 1e-3,
+           mib, K, NG, kImageTpw, per, (unsigned long long)wire, bytes / per * 1e-3,
            bytes / per * 1e-3 / 8000.0);
-    const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + image_tiles_per_wg() - 1) / image_tiles_per_wg();
+    const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + kImageTpw - 1) / kImageTpw;
     std::vector<uint4> si(nwg), sm(ntiles);
     CK(hipMemcpyFromSymbol(si.data(), HIP_SYMBOL(g_sp_stamp_img), nwg * sizeof(uint4)));
     CK(hipMemcpyFromSymbol(sm.data(), HIP_SYMBOL(g_sp_stamp_mov), ntiles * sizeof(uint4)));
