@@ -626,9 +626,12 @@ __global__ __launch_bounds__(kSB) void sp_move(
         if (threadIdx.x == 0) {
             for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
             const uint64_t F = t.x, R = t.y;
-            host_tot[0] = F;  // the wire length's terms, for the caller (host-mapped)
-            host_tot[1] = R;
-            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form
+            if (nbytes_out) {
+                *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form: nothing crosses PCIe
+            } else {
+                host_tot[0] = F;  // the blocking form: the wire length's terms for the host (host-mapped)
+                host_tot[1] = R;
+            }
         }
     }
     // wave-uniform (readfirstlane): scalar base addresses and branches
