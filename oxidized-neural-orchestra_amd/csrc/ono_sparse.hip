@@ -49,6 +49,9 @@ constexpr int kIT = 128, kIE = kTile / kIT;  // the encoder's tile: 2 waves x 16
 // library never does): {start, mid - start, end - start, XCC id} in 100 MHz ticks per sp_image
 // workgroup / sp_move wave, end = after the unit's own memory operations are acknowledged.
 __device__ uint4 g_sp_stamp_img[1 << 16], g_sp_stamp_mov[1 << 18], g_sp_stamp_pli[1 << 16], g_sp_stamp_plp[1 << 16];
+// pl_fused's look-back per tile: {polls of the slowest chunk lane, of the slowest tile lane, first round's
+// loads back - start, publish - start}
+__device__ uint4 g_sp_stamp_plf[1 << 16];
 __device__ __forceinline__ void sp_stamp(uint4 *st, size_t i, uint64_t t0, uint64_t tm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -1848,6 +1851,332 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
 #endif
 }
 
+// The stream-ordered lift in ONE launch (ono_sparse_lift_dev_async, up to kPatDirect tiles): each
+// workgroup (tile t = blockIdx.x) stages its tile, finds and checks its candidates as pl_index does, publishes the
+// tile's record — {sum of offset + length}, {exit, kPatNone without a candidate}, each an 8-byte
+// granule {value, tag} written by one agent-scope store, so a reader needs no ordering — and adds its
+// sum and an arrival to its chunk's line in each of kFusedRep replicas (kPatChunk tiles per 128-B
+// line; one 64-bit agent-scope add: the sum in the low 40 bits, arrivals above; a reader polls one).  Its range start E_t is then the sum of the earlier
+// chunks (each polled until all its tiles arrived) and of its chunk's earlier tiles (each polled
+// until its granules carry this launch's tag); the link into it is the exit of the nearest earlier
+// tile that holds a record.  Every poll is bounded: one that times out refutes the call (the caller
+// takes the blocking lift), so no workgroup waits forever.  Then it places its range as pl_place
+// does.  pl_index's launch, the boundary and pl_place's far prologue loads are gone.
+// A tile waits only for lower tiles, and each XCD starts its workgroups in blockIdx order (observed,
+// not promised by HIP: a tile's ticket from one counter, which promises it, measured ~88 tickets/us —
+// 43 us for 3767 tiles, 77 us a lift); were that order ever broken, a poll would time out and the
+// caller would take the blocking lift.  The tag is the call's epoch (so the stream-ordered lift is
+// not for graph capture: a replay repeats it); a launch zeroes the chunk lines of the next.
+constexpr int kStageU4 = kPatStage / 8 + 1;
+constexpr int kPatChunk = 64;         // tiles per chunk line (kPatDirect / kPatChunk = 64 chunks: one per lane)
+constexpr int kFusedLine = 16;        // u64 per chunk line (128 B)
+constexpr int kFusedRep = 8;          // replicas of the chunk lines: a tile adds to all, a reader polls one
+static_assert(kPatDirect / kPatChunk <= 64 && kPatChunk <= 64, "pl_fused's look-back: one chunk or tile per lane");
+constexpr uint32_t kPollMax = 1u << 14;  // polls before a look-back gives up (~0.5-1 us each: ~10 ms)
+// between polls: ~1000 cycles (a poll every 53 ns from every resident workgroup measured 77 us a lift:
+// the polled lines' channels stall every other load)
+#ifndef ONO_POLL_SLEEP
+#define ONO_POLL_SLEEP 16
+#endif
+constexpr int kPollSleep = ONO_POLL_SLEEP;
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// pl_fused's staging (an 8-B aligned stream), 8 B per load: every tile's loads issued up front,
+// the first tile's first (a scheduling barrier keeps them ahead: the wait for them lets the later
+// tiles' loads stay in flight while the first tile is indexed and published), unconditional and
+// clamped into the tile — or onto the total when the tile has no 8-B word — so that no wait comes
+// before the last issue.  Tile q of the workgroup is blockIdx.x + q * gridDim.x.
+constexpr int kStageK = (kPatStage / 4 + kPatT - 1) / kPatT;  // 8-B loads per thread per tile
+template <int TPW>
+__device__ __forceinline__ void pat_stage_issue(uint2 (&v)[TPW][kStageK], uint32_t (&n16)[TPW], const uint8_t *b,
+                                                size_t M, size_t T) {
+#pragma unroll
+    for (int q = 0; q < TPW; q++) {
+        const size_t t = blockIdx.x + (size_t)q * gridDim.x, base = t * kPatU;
+        n16[q] = t < T ? (uint32_t)min(M - base, (size_t)kPatStage) : 0u;
+        const uint32_t n8 = (n16[q] + 3) / 4;  // (the last word may hold units past M: same page, unused)
+        const uint2 *src = n8 ? (const uint2 *)(b + 8 + 2 * base) : (const uint2 *)b;
+#pragma unroll
+        for (int k = 0; k < kStageK; k++) {
+            const uint32_t i = threadIdx.x + (uint32_t)k * kPatT;
+            v[q][k] = src[i < n8 ? i : 0u];
+        }
+        if (q == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+// tile q's loaded words into LDS (no loads of its own: a load loop here would make every later wait
+// a wait for all loads in flight)
+__device__ __forceinline__ void pat_stage_write(uint4 *lw4, const uint2 (&v)[kStageK], uint32_t n16) {
+    uint2 *dst = (uint2 *)lw4;
+#pragma unroll
+    for (int k = 0; k < kStageK; k++) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kPatT;
+        if (i < (n16 + 3) / 4) dst[i] = v[k];
+    }
+}
+
+// pl_fused's look-back for tile t, one wave: E_t (the sum of the earlier chunks' sums, each polled in
+// replica `rep` until all its tiles arrived, and of the earlier tiles of t's chunk, each polled until
+// its granules carry the call's tag: one round of loads for both, repeated for the lanes still
+// waiting) and the exit of the nearest earlier tile that holds a record.  False: a poll timed out.
+__device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const uint64_t *frec, const uint64_t *fchunk,
+                                               uint32_t gcap, uint32_t rep, uint64_t &E, bool &found,
+                                               uint32_t &pexit) {
+    const uint32_t lane = threadIdx.x & 63, c = t / kPatChunk, c0 = c * kPatChunk;
+    bool timeout = false;
+    const bool wchunk = lane < c, wtile = c0 + lane < t;
+    const uint64_t *w = fchunk + ((size_t)rep * gcap + lane) * kFusedLine;
+    const uint64_t *r = frec + 2 * (size_t)(c0 + lane);
+    uint64_t v = 0, a = 0, x3 = 0;
+    for (uint32_t it = 0;; it++) {
+        if (wchunk) v = ld_agent(w);
+        if (wtile) {
+            a = ld_agent(r);
+            x3 = ld_agent(r + 1);
+        }
+        const bool ready = (!wchunk || (v >> 40) == (uint64_t)kPatChunk) &&
+                           (!wtile || ((a >> 32) == tagv && (x3 >> 32) == tagv));
+        if (ready) break;
+        if (it > kPollMax) { timeout = true; break; }
+        __builtin_amdgcn_s_sleep(kPollSleep);
+    }
+    uint64_t part = (wchunk ? v & ((1ull << 40) - 1) : 0ull) + (wtile ? (uint32_t)a : 0u);
+    const uint32_t ex = (uint32_t)x3;
+    // the lanes' parts (each < 2^40) summed exactly
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) part += (uint64_t)__shfl_xor((long long)part, d, 64);
+    E = part;
+    const uint64_t hold = __ballot(wtile && ex != kPatNone);
+    found = hold != 0;
+    pexit = found ? (uint32_t)__builtin_amdgcn_readlane((int)ex, 63 - __clzll((long long)hold)) : 0u;
+    // none in this chunk: earlier chunks, 64 tiles at a time, nearest first (all published)
+    for (int64_t hi = (int64_t)c0; !found && hi > 0 && !timeout; hi -= 64) {
+        const int64_t i = hi - 1 - (int64_t)lane;
+        uint32_t xe = kPatNone;
+        if (i >= 0) {
+            const uint64_t *rr = frec + 2 * (size_t)i + 1;
+            uint64_t x = ld_agent(rr);
+            for (uint32_t it = 0; (x >> 32) != tagv; it++) {
+                if (it > kPollMax) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(kPollSleep);
+                x = ld_agent(rr);
+            }
+            xe = (uint32_t)x;
+        }
+        const uint64_t h = __ballot(i >= 0 && xe != kPatNone);
+        if (h) {
+            found = true;
+            pexit = (uint32_t)__builtin_amdgcn_readlane((int)xe, __ffsll((unsigned long long)h) - 1);
+        }
+    }
+    return __ballot(timeout) == 0;
+}
+
+// TPW tiles per workgroup, tile q = blockIdx.x + q * gridDim.x: every tile staged, indexed and published
+// first, then each in turn looked back and placed — the first tiles' ranges depend only on the first
+// tiles, published early, so their stores start while the later tiles' look-backs are still waiting.
+template <int TPW>
+__global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void pl_fused(
+    float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
+                                                  uint64_t *frec, uint64_t *fchunk, uint64_t *fchunk_next,
+                                                  uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch) {
+    __shared__ uint4 img16[kPatImg / 8];  // a range as f16 bits (12 KiB), widened on the way out
+    __shared__ uint4 lw4[TPW][kStageU4];
+    __shared__ uint32_t lq[3 * kLQ], lqn;
+    __shared__ uint16_t lmask[kPatT], lpre[kPatT];
+    __shared__ uint32_t s_first[TPW], s_exit[TPW], s_bad, s_pexit, s_found;
+    __shared__ uint64_t s_E0;
+    uint2 *img8 = (uint2 *)img16;
+    uint16_t *img = (uint16_t *)img16;
+    SP_CLOCK(sp_t0);
+    const uint32_t M32 = (uint32_t)M, T32 = (uint32_t)T, G = gridDim.x;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int q = 0; q < TPW; q++) s_first[q] = s_exit[q] = kPatNone;
+        s_bad = 0;
+    }
+    const uint32_t tagv = epoch;  // (never 0: frec starts zeroed)
+    uint2 v[TPW][kStageK];
+    uint32_t n16[TPW];
+    // the total (b is 8-B aligned: the host launches pl_fused for no other stream), issued first, from a
+    // lane-dependent address that is always b (cap < 2^32 on this path): a uniform load would be moved
+    // to a scalar register at once, waiting for it before the tiles' loads are issued
+    const uint64_t total = *(const uint64_t *)(b + 8 * (threadIdx.x * (cap >> 62)));
+    __builtin_amdgcn_sched_barrier(0);
+    pat_stage_issue<TPW>(v, n16, b, M, T);
+    // pl_index's part per tile: candidates, their counts and sums, the successor checks inside the tile;
+    // then the tile published: its two granules {sum}, {exit: kPatNone for no candidate}, and its
+    // chunk's sum and arrival in every replica
+    const uint32_t j0 = kPatPer * threadIdx.x;
+    uint32_t m[TPW], es[TPW], tc[TPW], ts[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; q++) {
+        const uint32_t t = blockIdx.x + q * G, base = t * (uint32_t)kPatU;
+        m[q] = es[q] = tc[q] = ts[q] = 0;
+        if (t >= T32) continue;  // (uniform)
+        pat_stage_write(lw4[q], v[q], n16[q]);
+        __syncthreads();
+        const uint16_t *lw = (const uint16_t *)lw4[q];
+        const Units12 U = units12(lw4[q]);
+        uint32_t sum, ec;
+        m[q] = base + j0 < M32 ? pat_mask(U, base + j0, M, sum) : (sum = 0, 0u);
+        block_scan2<kPatT>((uint32_t)__builtin_popcount(m[q]), sum, ec, es[q], tc[q], ts[q]);
+        lmask[threadIdx.x] = (uint16_t)m[q];
+        lpre[threadIdx.x] = (uint16_t)ec;
+        if (m[q] && ec == 0) s_first[q] = base + j0 + (uint32_t)__builtin_ctz(m[q]);
+        __syncthreads();
+        bool bad = false;
+        uint32_t rank = ec;
+        for (uint32_t mm = m[q]; mm; mm &= mm - 1, rank++) {
+            const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm);
+            const uint32_t nx = k + 4 + lw[k + 2];  // tile-local successor
+            if (base + nx > M32) { bad = true; break; }  // the run overruns the stream
+            if (nx < (uint32_t)kPatU && base + nx < M32) {
+                const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
+                const uint32_t p2 = lpre[nx / kPatPer] + (uint32_t)__builtin_popcount(m2 & ((1u << b2) - 1u));
+                if (!(m2 >> b2 & 1u) || p2 != rank + 1) { bad = true; break; }
+            } else {  // the end of the stream or another tile: only the tile's last candidate goes there
+                if (rank + 1 != tc[q]) { bad = true; break; }
+                s_exit[q] = base + nx;
+            }
+        }
+        if (bad) s_bad = 1;
+        __syncthreads();  // (lmask, lpre and the scan's words are reused by the next tile; s_exit is read)
+        if (threadIdx.x < kFusedRep) {
+            if (threadIdx.x == 0) {
+                const uint64_t tag = (uint64_t)tagv << 32;
+                uint64_t *r = frec + 2 * (size_t)t;
+                st_agent(r, tag | ts[q]);
+                st_agent(r + 1, tag | (tc[q] ? s_exit[q] : kPatNone));
+            }
+            atomicAdd((unsigned long long *)(fchunk + ((size_t)threadIdx.x * gcap + t / kPatChunk) * kFusedLine),
+                      (unsigned long long)ts[q] | 1ull << 40);
+        }
+    }
+    if (s_bad && threadIdx.x == 0) raise_bad(badw, epoch);
+    // (checked after the tiles are published, before any look-back: uniform over the grid, so nobody
+    // waits; checked first, the compiler would sink the later tiles' loads behind the total's)
+    if (total > cap) {  // ONO_E_SIZE: nothing is written
+        if (blockIdx.x == 0 && threadIdx.x == 0) raise_bad(badw, epoch);
+        return;
+    }
+    const uint32_t total32 = (uint32_t)total;
+#pragma unroll
+    for (int q = 0; q < TPW; q++) {  // the tiles in turn, the image reused
+        const uint32_t t = blockIdx.x + q * G, base = t * (uint32_t)kPatU;
+        if (t >= T32) break;  // (uniform)
+        if (threadIdx.x < 64) {
+            uint64_t E;
+            bool f;
+            uint32_t px;
+            const bool ok = fused_lookback(t, tagv, frec, fchunk, gcap, blockIdx.x % kFusedRep, E, f, px);
+            if (threadIdx.x == 0) {
+                s_E0 = E;
+                s_found = ok && f ? 1u : 0u;
+                s_pexit = px;
+                if (!ok) raise_bad(badw, epoch);
+            }
+        }
+        __syncthreads();
+#ifdef ONO_SP_STAMP
+        if (q == 0) {
+            SP_CLOCK(sp_tl);
+            if (threadIdx.x == 0) g_sp_stamp_plf[blockIdx.x] = make_uint4(0u, 0u, (unsigned)(sp_tl - sp_t0), 0u);
+        }
+#endif
+        const uint64_t E0 = s_E0, E1 = E0 + ts[q];
+        const bool found = s_found != 0;
+        const uint32_t pexit = s_pexit;
+        {
+            bool bad = tc[q] > 0 && (found ? pexit != s_first[q] : s_first[q] != 0u);
+            if (t + 1 == T32) bad |= (tc[q] > 0 ? s_exit[q] != M32 : !found || pexit != M32) || E1 > total;
+            if (bad && threadIdx.x == 0) raise_bad(badw, epoch);
+        }
+        const uint32_t ea = (uint32_t)min(E0, total);
+        const uint32_t eb = max(t + 1 == T32 ? total32 : (uint32_t)min(E1, total), ea);
+        const uint32_t ia = vec ? ea & ~3u : ea;
+        const uint32_t n = min(eb - ia, (uint32_t)kPatImg + 1);
+        const bool is_wide = eb > ea && n > (uint32_t)kPatImg;
+        if (is_wide) {  // (uniform) window by window
+            wide_tile(g, b, M, T, vec, t, E0, ts[q], total, false, img8, lw4[q], lq, &lqn, nullptr, nullptr, 0,
+                      host_word, badw, epoch);
+        } else if (eb != ea) {
+            const uint16_t *lw = (const uint16_t *)lw4[q];
+            for (uint32_t i = threadIdx.x; i < (n + 7) / 8; i += kPatT) img16[i] = make_uint4(0u, 0u, 0u, 0u);
+            if (threadIdx.x == 0) lqn = 0;
+            __syncthreads();
+            uint32_t cur = (uint32_t)E0 + es[q];  // where the run before the thread's first record ended
+            for (uint32_t mm = m[q]; mm; mm &= mm - 1) {
+                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+                const uint32_t gi = cur + off;
+                if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
+                    raise_bad(badw, epoch);  // only a refuted stream
+                    break;
+                }
+                uint16_t *d = img + (gi - ia);
+                if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
+                    for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
+                } else {
+                    const uint32_t qq = atomicAdd(&lqn, 1u);
+                    const uint32_t vp = 8 + 2 * (base + k + 4);
+                    if (qq < (uint32_t)kLQ) {
+                        lq[3 * qq] = gi - ia;
+                        lq[3 * qq + 1] = vp;
+                        lq[3 * qq + 2] = len;
+                    } else {
+                        for (uint32_t i = 0; i < len; i++) d[i] = ((glb_u16 *)(b + vp))[i];
+                    }
+                }
+                cur = gi + len;
+            }
+            __syncthreads();  // the short runs and the long-run queue
+            const uint32_t nl = min(lqn, (uint32_t)kLQ);
+            if (nl) {  // (uniform) long runs: the whole workgroup copies each
+                for (uint32_t qq = 0; qq < nl; qq++) {
+                    const uint32_t a = lq[3 * qq], vp = lq[3 * qq + 1], cn = lq[3 * qq + 2];
+                    glb_u16 *src = (glb_u16 *)(b + vp);
+                    for (uint32_t i = threadIdx.x; i < cn; i += kPatT) img[a + i] = src[i];
+                }
+                __syncthreads();
+            }
+            const uint32_t skip = ea - ia;
+            float *gi0 = g + ia;
+            if (vec) {
+                const uint32_t v0 = skip ? 1u : 0u, v1 = n / 4;  // whole vectors [v0, v1)
+                for (uint32_t i = v0 + threadIdx.x; i < v1; i += kPatT) {
+                    const uint2 h = img8[i];
+                    const f4s x = {from_f16_sp((uint16_t)h.x), from_f16_sp((uint16_t)(h.x >> 16)),
+                                   from_f16_sp((uint16_t)h.y), from_f16_sp((uint16_t)(h.y >> 16))};
+                    __builtin_nontemporal_store(x, (f4s *)gi0 + i);
+                }
+                if (threadIdx.x < 4) {
+                    const uint32_t e = threadIdx.x;
+                    if (skip && e >= skip && e < n) gi0[e] = from_f16_sp(img[e]);
+                    const uint32_t l = 4 * v1 + e;
+                    if (l < n && l >= 4 * v0) gi0[l] = from_f16_sp(img[l]);
+                }
+            } else {
+                for (uint32_t i = threadIdx.x; i < n; i += kPatT) gi0[i] = from_f16_sp(img[i]);
+            }
+        }
+        __syncthreads();  // (the image and the look-back's words are reused by the next tile)
+    }
+    // the next launch's chunk lines back to zero (the previous launch, which used them, is done; at the
+    // end: a store loop ahead of the first waits would make them wait for every load in flight)
+    for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
+        fchunk_next[(size_t)i * kFusedLine] = 0;
+#ifdef ONO_SP_STAMP
+    SP_CLOCK(sp_tm);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64) sp_stamp(g_sp_stamp_plp, blockIdx.x, sp_t0, sp_tm);
+#endif
+}
+
 // The tiles pl_place flagged, one workgroup each, grid-stride over the tiles.
 __global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, size_t M, size_t T, int vec,
                                                  const uint64_t *E, const uint32_t *tsum, const uint32_t *wide,
@@ -1956,6 +2285,11 @@ struct PatScratch {
     uint32_t *pwide = nullptr; // (unused flags: pl_place<true> places wide tiles itself)
     uint64_t *aw = nullptr;    // 8 device words standing in for the blocking lift's host words
     uint32_t epoch = 0;
+    // pl_fused: per tile 2 granules {value, epoch} (zeroed when allocated), two arrays of chunk lines
+    // (kFusedRep replicas each) in turn (a launch zeroes the other for the next)
+    size_t fcap = 0, fgcap = 0;
+    uint64_t *frec = nullptr, *fchunk = nullptr;
+    int fpar = 0;
 };
 std::map<std::pair<int, hipStream_t>, PatScratch> g_pat;
 std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
@@ -2447,6 +2781,40 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
     return ONO_OK;
 }
 
+}  // extern "C"
+namespace {
+// the stream-ordered lift in one launch (pl_fused) up to kPatDirect tiles; ONO_LIFT_FUSED=0 keeps the
+// pl_index + pl_place launches (measurement)
+bool lift_fused() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_LIFT_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+// pl_fused's workgroups co-resident on this device (one or three tiles each): occupancy x CUs, asked
+// once per device.  A tile waits for tiles of higher workgroups (the earlier tiles of later stripes),
+// so the grid must fit whole; a kernel of another stream that takes the slots delays it until a poll
+// times out (~10 ms) and the call is refused (the caller's blocking lift then does the work).
+size_t fused_slots(int tpw) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, size_t> memo;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = memo.find({dev, tpw});
+    if (it != memo.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    const hipError_t e1 = tpw == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pl_fused<1>, kPatT, 0)
+                                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pl_fused<3>, kPatT, 0);
+    const hipError_t e2 = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const size_t slots = e1 == hipSuccess && e2 == hipSuccess && per_cu > 0 && cus > 0 ? (size_t)per_cu * cus : 0;
+    memo[{dev, tpw}] = slots;
+    return slots;
+}
+}  // namespace
+extern "C" {
+
 int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
                               uint64_t *ticket, void *stream) {
     if (!status || !ticket || (!buf_dev && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
@@ -2488,6 +2856,35 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     }
     uint32_t *tsum = P.prec + 4 * P.cap, *qcount = (uint32_t *)(P.aw + 6);
     const int vec = ((uintptr_t)g & 15) == 0;
+    // one launch (pl_fused) when every workgroup fits on the device at once: one tile each, or three
+    // (an 8-B aligned stream of at most kPatDirect tiles)
+    if (T <= kPatDirect && ((uintptr_t)buf_dev & 7) == 0 && lift_fused() && (T + 2) / 3 <= fused_slots(3)) {
+        if (T > P.fcap) {
+            const size_t gc = (T + kPatChunk - 1) / kPatChunk;
+            (void)hipFree(P.frec);
+            (void)hipFree(P.fchunk);
+            P.frec = P.fchunk = nullptr;
+            P.fcap = P.fgcap = 0;
+            ONO_HIP(hipMalloc((void **)&P.frec, 2 * T * sizeof(uint64_t)));
+            ONO_HIP(hipMemsetAsync(P.frec, 0, 2 * T * sizeof(uint64_t), s));
+            ONO_HIP(hipMalloc((void **)&P.fchunk, 2 * kFusedRep * gc * kFusedLine * sizeof(uint64_t)));
+            ONO_HIP(hipMemsetAsync(P.fchunk, 0, 2 * kFusedRep * gc * kFusedLine * sizeof(uint64_t), s));
+            P.fcap = T;
+            P.fgcap = gc;
+            P.fpar = 0;
+        }
+        uint64_t *cur = P.fchunk + (size_t)P.fpar * kFusedRep * P.fgcap * kFusedLine;
+        uint64_t *next = P.fchunk + (size_t)(1 - P.fpar) * kFusedRep * P.fgcap * kFusedLine;
+        if (T <= fused_slots(1))
+            hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)T), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
+                               cur, next, (uint32_t)P.fgcap, P.aw, status, epoch);
+        else
+            hipLaunchKernelGGL(pl_fused<3>, dim3((unsigned)((T + 2) / 3)), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec,
+                               P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch);
+        ONO_HIP(hipGetLastError());
+        P.fpar ^= 1;
+        return ONO_OK;
+    }
     ONO_HIP(launch_pl_index(buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw, status, epoch, s));
     if (T > kPatDirect)
         hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, buf_dev, P.prec, T, P.pE, status, epoch);

@@ -316,3 +316,80 @@ def test_async_lifts_on_two_streams_concurrently():
     for b, total, out, st, tk in jobs:
         assert int(st.item()) != tk
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+# ---- the one-launch stream-ordered lift (pl_fused: an 8-B aligned stream of at most 4096 tiles; one
+# tile per workgroup up to 2048 tiles, three above, each tile's range from a look-back over the tiles
+# published before it)
+
+def tiles_of(b: bytes) -> int:
+    return ((len(b) - 8) // 2 + 2047) // 2048
+
+
+@pytest.mark.parametrize("target", [1, 2, 63, 64, 65, 2047, 2048, 2049, 2050, 3001, 4096])
+def test_async_lift_one_launch_at_tile_counts(target):
+    """Tile counts at the one-launch form's edges (chunks of 64 tiles, one and three tiles per
+    workgroup, the last tile ragged or whole): not refused, bit-exact."""
+    rng = np.random.default_rng(1000 + target)
+    # ~6.5 units a record (lengths 1-4): enough records to fill `target` tiles, the last one partly
+    nrec = max(1, int((target - 0.5) * 2048 / 6.5))
+    b, total = pattern_stream(rng, nrec, (1, 15), (1, 4))
+    assert abs(tiles_of(b) - target) <= 1
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out, ticket, refused = lift_async(b, total + 3, status)
+    assert not refused
+    assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
+    assert torch.all(out[total:] == 6.0)  # nothing written past the stream's total
+
+
+@pytest.mark.parametrize("where", [0.02, 0.4, 0.7, 0.99])
+def test_async_lift_one_launch_refuses_a_late_fault(where):
+    """A zero-length run in a tile of the first, second or third stripe of a three-tiles-per-workgroup
+    launch: the call is refused (every other tile still publishes, nobody waits forever)."""
+    rng = np.random.default_rng(77)
+    b, total = pattern_stream(rng, 900_000, (1, 15), (1, 4))
+    assert 2048 < tiles_of(b) <= 4096
+    bb = bytearray(b)
+    heads = header_positions(b, 900_000)
+    rec = heads[int(where * (len(heads) - 2))]
+    ln = int.from_bytes(bb[rec + 4:rec + 8], "little")
+    bb[rec + 8 + 2 * ln:rec + 8 + 2 * ln] = np.array([2, 0], np.uint32).tobytes()
+    total += 2
+    bb[:8] = np.uint64(total).tobytes()
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _, _, refused = lift_async(bytes(bb), total, status)
+    assert refused
+
+
+def test_async_lift_of_an_unaligned_stream():
+    """A stream at a 2-B (not 8-B) boundary takes the two-launch form: exact, not refused."""
+    rng = np.random.default_rng(31)
+    b, total = pattern_stream(rng, 700_000, (1, 15), (1, 4))
+    raw = torch.zeros(len(b) + 8, dtype=torch.uint8, device="cuda")
+    raw[2:2 + len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    buf = raw[2:2 + len(b)]
+    assert buf.data_ptr() % 8 == 2
+    out = torch.empty(total, dtype=torch.float32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ticket = SP.grad_lift_dev_async(buf, out, status)
+    torch.cuda.synchronize()
+    assert int(status.item()) != ticket
+    assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+def test_async_lift_one_launch_back_to_back_sizes():
+    """One-launch lifts of different tile counts queued back to back on one stream (the chunk lines
+    alternate between two arrays, each zeroed by the launch before): all exact."""
+    rng = np.random.default_rng(44)
+    jobs = []
+    for nrec in (700_000, 30_000, 1_200_000, 5_000, 900_000, 700_000):
+        b, total = pattern_stream(rng, nrec, (1, 15), (1, 4))
+        buf, out = to_dev(b), torch.empty(total, dtype=torch.float32, device="cuda")
+        st = torch.zeros(1, dtype=torch.int64, device="cuda")
+        jobs.append((b, total, buf, out, st))
+    torch.cuda.synchronize()
+    tickets = [SP.grad_lift_dev_async(buf, out, st) for _, _, buf, out, st in jobs]
+    torch.cuda.synchronize()
+    for (b, total, _, out, st), tk in zip(jobs, tickets):
+        assert int(st.item()) != tk
+        assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))

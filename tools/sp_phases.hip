@@ -9,7 +9,7 @@
 // per-XCD last end.
 //
 // Then the same for K stream-ordered lifts (pattern path) of the last drop's wire into 6 outputs
-// in turn: pl_index and pl_place stamped per workgroup.
+// in turn: pl_fused stamped per workgroup (ONO_LIFT_FUSED=0: pl_index and pl_place).
 //
 // usage: sp_phases [MiB=64] [K=24]
 #define ONO_SP_STAMP 1
@@ -158,11 +158,28 @@ int main(int argc, char **argv) {
     std::vector<uint4> spi(T), spp(T);
     CK(hipMemcpyFromSymbol(spi.data(), HIP_SYMBOL(g_sp_stamp_pli), T * sizeof(uint4)));
     CK(hipMemcpyFromSymbol(spp.data(), HIP_SYMBOL(g_sp_stamp_plp), T * sizeof(uint4)));
-    base = spi[0].x;
-    for (const uint4 &v : spi) base = (int32_t)(v.x - base) < 0 ? v.x : base;
-    printf("# times in us from pl_index's first workgroup start (the last lift; mid: pl_index after its scan, "
-           "pl_place after its prologue)\n");
-    report("pl_index", spi, base);
-    report("pl_place", spp, base);
+    // one launch (pl_fused, the default up to kPatDirect tiles) stamps only pl_place's array: start, after
+    // its last stores issued, end
+    const bool fused = spi[0].x == 0 && spi[0].z == 0;
+    if (fused && T > 2048) spp.resize((T + 2) / 3);  // (three tiles per workgroup above 2048 tiles)
+    const std::vector<uint4> &first = fused ? spp : spi;
+    base = first[0].x;
+    for (const uint4 &v : first) base = (int32_t)(v.x - base) < 0 ? v.x : base;
+    if (fused) {
+        printf("# times in us from pl_fused's first workgroup start (the last lift; mid: its last stores issued)\n");
+        report("pl_fused", spp, base);
+        const size_t nwg = spp.size();
+        std::vector<uint4> plf(nwg);
+        CK(hipMemcpyFromSymbol(plf.data(), HIP_SYMBOL(g_sp_stamp_plf), nwg * sizeof(uint4)));
+        std::vector<double> r1;
+        for (const uint4 &v : plf) r1.push_back(v.z * 0.01);
+        printf("pl_fused first tile's look-back done: p10 %.2f p50 %.2f p90 %.2f max %.2f us from start\n", pct(r1, 0.1),
+               pct(r1, 0.5), pct(r1, 0.9), pct(r1, 1));
+    } else {
+        printf("# times in us from pl_index's first workgroup start (the last lift; mid: pl_index after its scan, "
+               "pl_place after its prologue)\n");
+        report("pl_index", spi, base);
+        report("pl_place", spp, base);
+    }
     return 0;
 }
