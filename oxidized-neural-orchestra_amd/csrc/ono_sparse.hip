@@ -1870,7 +1870,10 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
 constexpr int kStageU4 = kPatStage / 8 + 1;
 constexpr int kPatChunk = 64;         // tiles per chunk line (kPatDirect / kPatChunk = 64 chunks: one per lane)
 constexpr int kFusedLine = 16;        // u64 per chunk line (128 B)
-constexpr int kFusedRep = 8;          // replicas of the chunk lines: a tile adds to all, a reader polls one
+#ifndef ONO_FUSED_REP
+#define ONO_FUSED_REP 2
+#endif
+constexpr int kFusedRep = ONO_FUSED_REP;  // replicas of the chunk lines: a tile adds to all, a reader polls one
 static_assert(kPatDirect / kPatChunk <= 64 && kPatChunk <= 64, "pl_fused's look-back: one chunk or tile per lane");
 constexpr uint32_t kPollMax = 1u << 14;  // polls before a look-back gives up (~0.5-1 us each: ~10 ms)
 // between polls: ~1000 cycles (a poll every 53 ns from every resident workgroup measured 77 us a lift:
