@@ -229,6 +229,27 @@ def run_timeout(rank: int, n: int, how: str = "env") -> str | None:
         ring.close()
 
 
+def describe_bad(bad, got, want, ins, prev, length, n) -> str:
+    """What a wrong host-fed result looks like, for the next diagnosis: the runs of
+    differing elements, the 1 MiB sub-rounds and the n owner chunks they fall in, and whether the wrong
+    values are the previous cycle's result, one rank's unreduced input, or zeros."""
+    runs = np.split(bad, np.flatnonzero(np.diff(bad) != 1) + 1)
+    spans = ", ".join(f"[{r[0]}, {r[-1] + 1})" for r in runs[:6]) + (" ..." if len(runs) > 6 else "")
+    sub = sorted(set((bad // (1 << 18)).tolist()))[:8]
+    chunk = -(-length // n)
+    owners = sorted(set((bad // chunk).tolist()))
+    g = got[bad]
+    kinds = []
+    if prev is not None and np.array_equal(bits(g), bits(prev[bad])):
+        kinds.append("= the previous cycle's result")
+    for r, x in enumerate(ins):
+        if np.array_equal(bits(g), bits(np.asarray(x, np.float32)[bad])):
+            kinds.append(f"= rank {r}'s input")
+    if not np.any(g):
+        kinds.append("all zero")
+    return f"{len(runs)} runs {spans}; sub-rounds {sub}; owner chunks {owners}; wrong values {kinds or ['other']}"
+
+
 def run_recreate(rank: int, n: int, case: dict) -> str | None:
     """Create, use and destroy an xGMI ring several times in the same processes
     (the situation of round 2's one wrong host-fed result: the second ring of a
@@ -238,6 +259,7 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
     cycles, length = case.get("cycles", 6), case.get("length", (1 << 20) + 3)
     release = case.get("release", False)  # ono_xgmi_pool_release between cycles: fresh exports and imports
     seen, repeats, freed = set(), 0, 0
+    prev = None  # the previous cycle's expected result (stale data from an earlier ring would equal it)
     for cyc in range(cycles):
         blobs = {}
 
@@ -256,7 +278,9 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
             ring.pull_grads_host(res_h, grad_h)
             bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
             if bad.size:
-                return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats so far {repeats})"
+                return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats so far {repeats}); " \
+                       + describe_bad(bad, grad_h, expect[rank], ins, prev, length, n)
+            prev = expect[rank]
             if bits(res_h).any():
                 return f"cycle {cyc}: host residual not zeroed"
             if release:  # refused while this process's ring is alive
