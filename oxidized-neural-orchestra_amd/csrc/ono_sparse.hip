@@ -2795,6 +2795,11 @@ bool lift_fused() {
     }();
     return v;
 }
+// one tile per workgroup up to this many tiles (and the device's slots), three above (measurement builds
+// move the switch)
+#ifndef ONO_FUSED_ONE_MAX
+#define ONO_FUSED_ONE_MAX 0xFFFFFFFFu
+#endif
 // pl_fused's workgroups co-resident on this device (one or three tiles each): occupancy x CUs, asked
 // once per device.  A tile waits for tiles of higher workgroups (the earlier tiles of later stripes),
 // so the grid must fit whole; a kernel of another stream that takes the slots delays it until a poll
@@ -2878,7 +2883,7 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
         }
         uint64_t *cur = P.fchunk + (size_t)P.fpar * kFusedRep * P.fgcap * kFusedLine;
         uint64_t *next = P.fchunk + (size_t)(1 - P.fpar) * kFusedRep * P.fgcap * kFusedLine;
-        if (T <= fused_slots(1))
+        if (T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX))
             hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)T), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
                                cur, next, (uint32_t)P.fgcap, P.aw, status, epoch);
         else
