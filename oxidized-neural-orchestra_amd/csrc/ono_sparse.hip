@@ -2787,14 +2787,16 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
 }  // extern "C"
 namespace {
 // the stream-ordered lift in one launch (pl_fused) up to kPatDirect tiles; ONO_LIFT_FUSED=0 keeps the
-// pl_index + pl_place launches (measurement)
-bool lift_fused() {
-    static const bool v = [] {
+// pl_index + pl_place launches (measurement), =2 takes the one launch even under stream capture (a
+// diagnostic: shows what the capture guard prevents)
+int lift_fused_mode() {
+    static const int v = [] {
         const char *e = getenv("ONO_LIFT_FUSED");
-        return !(e && atoi(e) == 0);
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
+bool lift_fused() { return lift_fused_mode() != 0; }
 // one tile per workgroup up to this many tiles (and the device's slots), three above (measurement builds
 // move the switch)
 #ifndef ONO_FUSED_ONE_MAX
@@ -2866,7 +2868,13 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     const int vec = ((uintptr_t)g & 15) == 0;
     // one launch (pl_fused) when every workgroup fits on the device at once: one tile each, or three
     // (an 8-B aligned stream of at most kPatDirect tiles)
-    if (T <= kPatDirect && ((uintptr_t)buf_dev & 7) == 0 && lift_fused() && (T + 2) / 3 <= fused_slots(3)) {
+    // Not under stream capture: a replayed graph repeats the epoch, and the granules of the previous
+    // replay would pass for this one's (the two launches carry no such state).
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    const bool capturing = lift_fused_mode() != 2 && hipStreamIsCapturing(s, &cap_st) == hipSuccess &&
+                           cap_st != hipStreamCaptureStatusNone;
+    if (T <= kPatDirect && ((uintptr_t)buf_dev & 7) == 0 && lift_fused() && !capturing &&
+        (T + 2) / 3 <= fused_slots(3)) {
         if (T > P.fcap) {
             const size_t gc = (T + kPatChunk - 1) / kPatChunk;
             (void)hipFree(P.frec);

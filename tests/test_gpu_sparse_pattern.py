@@ -393,3 +393,69 @@ def test_async_lift_one_launch_back_to_back_sizes():
     for (b, total, _, out, st), tk in zip(jobs, tickets):
         assert int(st.item()) != tk
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+def same_size_stream(rng, units: int, total: int) -> bytes:
+    """A drop-shaped stream of exactly `units` u16 after the total and the given total: records of
+    lengths 1-4 until the units are filled (the last record's length takes the rest), offsets 1-15
+    lowered where needed to fit the total, the rest of the total as the tail."""
+    lens = []
+    left = units
+    while left >= 9:
+        ln = int(rng.integers(1, 5))
+        if left - (4 + ln) < 5 and left - (4 + ln) != 0:
+            ln = left - 4
+        lens.append(ln)
+        left -= 4 + ln
+    if left:
+        lens.append(left - 4)  # (left >= 5 here)
+    lens = np.array(lens, np.int64)
+    offs = rng.integers(1, 16, lens.size).astype(np.int64)
+    excess = int(offs.sum() + lens.sum()) - total
+    if excess > 0:  # lower offsets towards 1
+        room = offs - 1
+        take = np.minimum(room, np.ceil(room * excess / max(int(room.sum()), 1)).astype(np.int64))
+        offs -= take
+        extra = int(offs.sum() + lens.sum()) - total
+        i = 0
+        while extra > 0:
+            if offs[i] > 1:
+                offs[i] -= 1
+                extra -= 1
+            i = (i + 1) % offs.size
+    assert offs.min() >= 1 and int(offs.sum() + lens.sum()) <= total
+    u_units = 4 + lens
+    starts = np.concatenate([[0], np.cumsum(u_units)[:-1]])
+    u = rng.integers(1, 0x7C00, int(u_units.sum())).astype(np.uint16)
+    u |= rng.integers(0, 2, u.size).astype(np.uint16) << 15
+    u[starts], u[starts + 1] = offs & 0xFFFF, offs >> 16
+    u[starts + 2], u[starts + 3] = lens & 0xFFFF, lens >> 16
+    assert u.size == units
+    return np.uint64(total).tobytes() + u.tobytes()
+
+
+def test_async_lift_under_graph_capture_replays_new_streams():
+    """Captured in a graph (the epoch frozen at capture), the stream-ordered lift takes the two launches,
+    which carry no per-call state: replays over new stream contents of the same length stay exact."""
+    rng = np.random.default_rng(88)
+    b, total = pattern_stream(rng, 700_000, (1, 15), (1, 4))
+    buf = to_dev(b)
+    out = torch.empty(total, dtype=torch.float32, device="cuda")
+    st = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        SP.grad_lift_dev_async(buf, out, st)  # scratch allocated before the capture
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ticket = SP.grad_lift_dev_async(buf, out, st)
+    for k in range(3):  # other records (the tiles' sums and links all change), the same length and total
+        b2 = same_size_stream(np.random.default_rng(500 + k), (len(b) - 8) // 2, total)
+        assert len(b2) == len(b) and b2[:8] == b[:8] and b2 != b
+        buf.copy_(torch.frombuffer(bytearray(b2), dtype=torch.uint8).cuda())
+        st.zero_()
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert int(st.item()) != ticket
+        assert_bitexact(out.cpu().numpy(), O.grad_lift(b2, cap=total))
