@@ -459,3 +459,24 @@ def test_async_lift_under_graph_capture_replays_new_streams():
         torch.cuda.synchronize()
         assert int(st.item()) != ticket
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b2, cap=total))
+
+
+def test_async_lifts_of_large_streams_on_two_streams_concurrently():
+    """Two lifts whose one-launch grids would each need most of the device, queued on two streams at
+    once: the second takes the two launches while the first may still run, so neither waits on slots
+    the other holds — both exact and not refused."""
+    rng = np.random.default_rng(61)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    prep = []
+    for k in range(4):
+        b, total = pattern_stream(rng, 1_150_000 + 10_000 * k, (1, 15), (1, 4))
+        assert 3 * 1536 // 2 < tiles_of(b) <= 4096
+        prep.append((b, total, to_dev(b), torch.empty(total, dtype=torch.float32, device="cuda"),
+                     torch.zeros(1, dtype=torch.int64, device="cuda")))
+    torch.cuda.synchronize()
+    jobs = [(b, total, out, st, SP.grad_lift_dev_async(buf, out, st, s1 if k % 2 == 0 else s2))
+            for k, (b, total, buf, out, st) in enumerate(prep)]
+    torch.cuda.synchronize()
+    for b, total, out, st, tk in jobs:
+        assert int(st.item()) != tk
+        assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
