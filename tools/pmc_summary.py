@@ -56,6 +56,27 @@ def main() -> int:
     for name in sorted(set(fetch) & set(write)):
         if not any(m in name for m in a.match):
             continue
+        if "ScaleZeroOp" in name and not re.search(r"SumScaleOp", name):
+            # the headline's launches (a.elems) and local_reduce's same-pool copy+zero ceiling
+            # (a.local_elems) are one kernel: split the launches by size (write = 8 B/elem), one entry each
+            for elems in (a.elems, a.local_elems):
+                ef, ew = 2.0 * elems / 1024, 8.0 * elems / 1024  # expected KiB: read 4 B/elem half-counted, write 8
+                fk = [v for v in fetch[name] if 0.7 * ef <= v <= 1.4 * ef]
+                wk = [v for v in write[name] if 0.7 * ew <= v <= 1.4 * ew]
+                if not fk or not wk:
+                    continue
+                f_kb, w_kb = statistics.median(fk), statistics.median(wk)
+                rd, wr = 2.0 * f_kb * 1024, w_kb * 1024
+                algo = 12.0 * elems
+                kernels.append({
+                    "name": name, "elems": elems, "launches_fetch": len(fk), "launches_write": len(wk),
+                    "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+                    "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                    "hbm_bytes_per_launch": rd + wr,
+                    "algorithmic_bytes_per_launch": algo,
+                    "traffic_over_algorithmic": (rd + wr) / algo,
+                })
+            continue
         f_kb, w_kb = statistics.median(fetch[name]), statistics.median(write[name])
         rd, wr = 2.0 * f_kb * 1024, w_kb * 1024
         m = re.search(r"SumScaleOp<(\d+),", name)
