@@ -320,17 +320,34 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
  * back to the process's pool once all peers have marked it, and is
  * quarantined (never reused) when the timeout passed or the ring was aborted.
  * RETENTION: pooled regions and peer imports are kept for the life of the
- * process (a later ring reuses them; re-importing a freed region's successor
- * handed out partly stale mappings on this ROCm) until ono_xgmi_pool_release. */
+ * process (a later ring reuses them) until released.  A fresh region whose
+ * IPC handle repeats one this process obtained before is parked and another
+ * allocated (re-importing a repeated handle handed out partly stale mappings on
+ * this ROCm); an import of a handle this process opened before is ONO_E_IO.   */
 #define ONO_XGMI_HANDLE_BYTES 128
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
 int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
-/* Frees every idle pooled exchange region and closes every peer import of
- * this process; ONO_E_ARG while an xGMI ring of the process is alive.  Call it
- * on every rank once all rings are destroyed (an import pins the exporter's
- * HBM until the importer closes it).  Quarantined regions stay.  Rings created
- * afterwards export and import fresh regions (verified at connect as always). */
+/* Releasing the pool is two-phase, on every rank once all its xGMI rings are
+ * destroyed (ONO_E_ARG while one is alive):
+ *   1. ono_xgmi_pool_close_imports on every rank: each peer region this
+ *      process maps is marked closed in the region itself (a system-scope add
+ *      to its close counter), then its import is closed;
+ *   2. a collective step (the caller's barrier over its control channel);
+ *   3. ono_xgmi_pool_free_exports on every rank: each idle region is freed
+ *      once its close counter has reached its open counter (each importer
+ *      bumped the open counter when it mapped the region), waiting up to wait_s
+ *      seconds; a region some peer still maps is kept (ONO_E_IO, *kept > 0)
+ *      and parked allocations are freed.  So no region is freed while a peer
+ *      still maps it.  Quarantined regions stay.
+ * Rings created afterwards export and import fresh regions (verified at
+ * connect as always).  ono_xgmi_pool_release = phase 1 then phase 3 in one
+ * call, waiting (ONO_XGMI_TIMEOUT_S, default 600 s) for the peers' phase 1:
+ * the counters still order the frees after the peers' close marks, but the
+ * mark precedes its import's close by one host call, so multi-process callers
+ * should use the two phases with the collective step between.               */
+int ono_xgmi_pool_close_imports(size_t *closed_imports);
+int ono_xgmi_pool_free_exports(size_t *freed_bytes, size_t *kept, double wait_s);
 int ono_xgmi_pool_release(size_t *freed_bytes, size_t *closed_imports);
 /* regions pooled (and their bytes, of which quarantined), peer imports held */
 int ono_xgmi_pool_stats(size_t *regions, size_t *region_bytes, size_t *quarantined, size_t *imports);

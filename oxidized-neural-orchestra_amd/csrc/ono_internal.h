@@ -140,6 +140,9 @@ struct XSignal {
     int n, pos;
 };
 hipError_t launch_xgmi_signal(const XSignal &sig, hipStream_t s);
+// Release bookkeeping (ono_xgmi_pool.h): one system-scope atomic add of 1 to a
+// u64 counter of a region (through a peer mapping), completed before the wave ends.
+hipError_t launch_xgmi_bump(uint64_t *counter, hipStream_t s);
 
 // PS shard update (storage/blocking/shard.rs:74-92 + optimization/*.rs), fused:
 //   g /= nworkers (if > 1); optimizer step on w (state v, s); g = 0 when zero_grad

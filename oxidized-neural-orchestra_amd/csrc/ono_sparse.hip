@@ -2065,6 +2065,10 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
     // waits; checked first, the compiler would sink the later tiles' loads behind the total's)
     if (total > cap) {  // ONO_E_SIZE: nothing is written
         if (blockIdx.x == 0 && threadIdx.x == 0) raise_bad(badw, epoch);
+        // the next launch's chunk lines are zeroed on this path too: the host flips the pair either way,
+        // and a line left holding this launch's counts would look complete to the next-but-one launch
+        for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
+            fchunk_next[(size_t)i * kFusedLine] = 0;
         return;
     }
     const uint32_t total32 = (uint32_t)total;

@@ -79,6 +79,7 @@
 
 #include "ono_internal.h"
 #include "ono_ring_impl.h"
+#include "ono_xgmi_pool.h"
 
 static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
 
@@ -86,38 +87,14 @@ namespace ono {
 
 constexpr size_t kFlagBytes = 4096;  // flag page: barrier slots (n x u64) at offset 0,
 constexpr size_t kDoneOff = 1024;    //   teardown markers (n x u64),
-constexpr size_t kIdOff = 2048;      //   the region's ring id
+constexpr size_t kIdOff = 2048;      //   the region's ring id,
+constexpr size_t kCountOff = 3072;   //   {opens, closes} of the region's peer imports (ono_xgmi_pool.h)
 constexpr size_t kPage = 4096;       // every later page starts with the id until the first round
 // the handle blob: [hipIpcMemHandle_t (64 B)][u64 ring id][u64 layout bytes][u64 region uid][u64 region
 // alloc bytes][zero to ONO_XGMI_HANDLE_BYTES]
 constexpr size_t kBlobId = sizeof(hipIpcMemHandle_t), kBlobBytes = kBlobId + 8, kBlobUid = kBlobBytes + 8,
                  kBlobAlloc = kBlobUid + 8;
 static_assert(kBlobAlloc + 8 <= ONO_XGMI_HANDLE_BYTES, "handle blob layout");
-
-// The process's exchange regions (never freed: see the header comment) and
-// the peer regions it has mapped (never unmapped), under one lock.
-struct PooledRegion {
-    int device;
-    uint8_t *ptr;
-    size_t bytes;
-    uint64_t uid;
-    hipIpcMemHandle_t handle;
-    bool busy;
-    // a ring's teardown ended without every peer's done marker (timeout, abort,
-    // a failed signal): a slow peer may still write into the region, so it is
-    // never reset for another ring and never freed by ono_xgmi_pool_release
-    bool quarantined;
-};
-struct MappedPeer {
-    int device;
-    uint64_t uid;
-    size_t bytes;
-    uint8_t *ptr;
-};
-std::mutex g_pool_mu;
-std::vector<PooledRegion> g_regions;
-std::vector<MappedPeer> g_mapped;
-int g_live = 0;  // xGMI states (rings holding a region) alive in this process
 
 struct XgmiState {
     uint8_t *xbuf = nullptr;          // this rank's exchange region (uncached HBM, exported)
@@ -139,8 +116,81 @@ struct XgmiState {
     uint64_t uid = 0;                 // the pooled region's uid
     hipIpcMemHandle_t handle{};       // its IPC handle
     bool exported = false;            // the handle left this process (a peer may have mapped the region)
+    bool counted = false;             // holds a pooled region (counted among the process's live rings)
     std::vector<uint64_t> peer_id;    // every peer region's id, from its blob
 };
+
+// The process's exchange regions and peer imports (ono_xgmi_pool.h) over the
+// HIP runtime.
+XgmiPool &pool() {
+    static XgmiPool *p = [] {
+        XgmiPoolOps o;
+        o.alloc = [](int dev, size_t bytes, uint8_t **ptr, IpcBytes *h, std::string &msg) -> int {
+            DeviceGuard g(dev);
+            hipError_t e = hipExtMallocWithFlags((void **)ptr, bytes, hipDeviceMallocUncached);
+            if (e != hipSuccess) {
+                msg = std::string("hipExtMallocWithFlags (exchange region): ") + hipGetErrorString(e);
+                return ONO_E_HIP;
+            }
+            hipIpcMemHandle_t ih;
+            if ((e = hipIpcGetMemHandle(&ih, *ptr)) != hipSuccess) {
+                (void)hipFree(*ptr);
+                msg = std::string("hipIpcGetMemHandle (exchange region): ") + hipGetErrorString(e);
+                return ONO_E_HIP;
+            }
+            memcpy(h->data(), &ih, sizeof ih);
+            return ONO_OK;
+        };
+        o.free = [](int dev, uint8_t *ptr, std::string &msg) -> int {
+            DeviceGuard g(dev);
+            hipError_t e = hipFree(ptr);
+            if (e != hipSuccess) msg = std::string("hipFree (pooled exchange region): ") + hipGetErrorString(e);
+            return e == hipSuccess ? ONO_OK : ONO_E_HIP;
+        };
+        o.open = [](int dev, const IpcBytes &h, uint8_t **ptr, std::string &msg) -> int {
+            DeviceGuard g(dev);
+            hipIpcMemHandle_t ih;
+            memcpy(&ih, h.data(), sizeof ih);
+            hipError_t e = hipIpcOpenMemHandle((void **)ptr, ih, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) msg = std::string("hipIpcOpenMemHandle (peer exchange region): ") + hipGetErrorString(e);
+            return e == hipSuccess ? ONO_OK : ONO_E_HIP;
+        };
+        o.close = [](int dev, uint8_t *ptr, std::string &msg) -> int {
+            DeviceGuard g(dev);
+            hipError_t e = hipIpcCloseMemHandle(ptr);
+            if (e != hipSuccess) msg = std::string("hipIpcCloseMemHandle (peer region): ") + hipGetErrorString(e);
+            return e == hipSuccess ? ONO_OK : ONO_E_HIP;
+        };
+        o.bump = [](int dev, uint64_t *c, std::string &msg) -> int {
+            DeviceGuard g(dev);
+            hipError_t e = launch_xgmi_bump(c, nullptr);
+            if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+            if (e != hipSuccess) msg = std::string("exchange region import count: ") + hipGetErrorString(e);
+            return e == hipSuccess ? ONO_OK : ONO_E_HIP;
+        };
+        o.read2 = [](int dev, const uint64_t *c, uint64_t out[2], std::string &msg) -> int {
+            DeviceGuard g(dev);  // uncached region: a copy reads what has landed
+            hipError_t e = hipMemcpy(out, c, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) msg = std::string("exchange region import count: ") + hipGetErrorString(e);
+            return e == hipSuccess ? ONO_OK : ONO_E_HIP;
+        };
+        o.pause = [] { std::this_thread::sleep_for(std::chrono::microseconds(200)); };
+        o.now = [] {
+            return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        };
+        return new XgmiPool(std::move(o), kCountOff);  // (never destroyed: regions outlive static destructors)
+    }();
+    return *p;
+}
+
+// The error word's values: 1 a barrier timed out, 2 ono_ring_abort, 3 a flag
+// ahead of the round (something other than this ring's peer wrote it).
+int xgmi_err(uint32_t w) {
+    if (w == 3u)
+        return set_error(ONO_E_IO, "xGMI ring: a barrier flag was ahead of the round (written by something other "
+                                   "than this ring's peer): the round's results are invalid");
+    return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+}
 
 }  // namespace ono
 
@@ -177,34 +227,21 @@ int xgmi_alloc(ono_ring *r) {
     const size_t bytes = x->push_gather ? x->gat_off + rb : x->gat_off;
     x->bytes = bytes;
     x->id = fresh_ring_id();
-    {  // the smallest free pooled region that fits, else a new one
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        PooledRegion *best = nullptr;
-        for (auto &pr : g_regions)
-            if (!pr.busy && pr.device == r->device && pr.bytes >= bytes && (!best || pr.bytes < best->bytes))
-                best = &pr;
-        if (!best) {
-            PooledRegion pr{};
-            pr.device = r->device;
-            pr.bytes = align_up(bytes, kPage);
-            pr.uid = fresh_ring_id();
-            ONO_HIP(hipExtMallocWithFlags((void **)&pr.ptr, pr.bytes, hipDeviceMallocUncached));
-            hipError_t e = hipIpcGetMemHandle(&pr.handle, pr.ptr);
-            if (e != hipSuccess) {
-                (void)hipFree(pr.ptr);
-                return hip_error(e, "hipIpcGetMemHandle (exchange region)", __FILE__, __LINE__);
-            }
-            g_regions.push_back(pr);
-            best = &g_regions.back();
-        }
-        best->busy = true;
-        g_live++;
-        x->xbuf = best->ptr;
-        x->alloc = best->bytes;
-        x->uid = best->uid;
-        x->handle = best->handle;
+    {  // the smallest free pooled region that fits, else a new one (never with a handle handed out before)
+        XgmiPool::Region reg{};
+        bool fresh = false;
+        std::string msg;
+        int rc = pool().acquire(r->device, bytes, align_up(bytes, kPage), fresh_ring_id(), &reg, &fresh, msg);
+        if (rc) return set_error(rc, "%s", msg.c_str());
+        x->counted = true;
+        x->xbuf = reg.ptr;
+        x->alloc = reg.bytes;
+        x->uid = reg.uid;
+        memcpy(&x->handle, reg.handle.data(), sizeof x->handle);
+        // flags start at epoch 0, no teardown markers; the import counters of a pooled region stay (its
+        // peers' mappings of it stay open across rings), a fresh region's start at zero
+        ONO_HIP(hipMemset(x->xbuf, 0, fresh ? kFlagBytes : kCountOff));
     }
-    ONO_HIP(hipMemset(x->xbuf, 0, kFlagBytes));  // flags start at epoch 0, no teardown markers
     ONO_HIP(launch_xgmi_stamp(x->xbuf, (bytes + kPage - 1) / kPage, kIdOff, x->id, nullptr));
     ONO_HIP(hipDeviceSynchronize());              // zeroed and stamped before the handle leaves this process
     x->peer.assign(r->n, nullptr);
@@ -267,20 +304,13 @@ void make_blob(const XgmiState *x, uint8_t *blob) {
 }
 
 // peer region `uid` as mapped in this process: the mapping made for an
-// earlier ring, else a new import (kept for the life of the process)
+// earlier ring, else a new import (kept until ono_xgmi_pool_close_imports)
 int map_peer(ono_ring *r, const hipIpcMemHandle_t &h, uint64_t uid, size_t alloc, uint8_t **out) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (const auto &m : g_mapped)
-        if (m.device == r->device && m.uid == uid && m.bytes == alloc) {
-            *out = m.ptr;
-            return ONO_OK;
-        }
-    void *p = nullptr;
-    hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return hip_error(e, "hipIpcOpenMemHandle (peer exchange region)", __FILE__, __LINE__);
-    g_mapped.push_back({r->device, uid, alloc, static_cast<uint8_t *>(p)});
-    *out = static_cast<uint8_t *>(p);
-    return ONO_OK;
+    IpcBytes hb;
+    memcpy(hb.data(), &h, sizeof h);
+    std::string msg;
+    int rc = pool().map(r->device, hb, uid, alloc, out, msg);
+    return rc ? set_error(rc, "%s", msg.c_str()) : ONO_OK;
 }
 
 // Every page of peer q's region as mapped here must show the id q stamped.
@@ -344,8 +374,8 @@ int xgmi_connect(ono_ring *r, const uint8_t *handles) {
     // stamps: a barrier that every rank passes only once all are connected.
     if ((rc = barrier(r, nullptr))) return rc;
     ONO_HIP(hipDeviceSynchronize());
-    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
-        return set_error(ONO_E_IO, "xGMI connect: a peer did not connect within the timeout");
+    if (uint32_t w = __atomic_load_n(x->err, __ATOMIC_ACQUIRE))
+        return w == 3u ? xgmi_err(w) : set_error(ONO_E_IO, "xGMI connect: a peer did not connect within the timeout");
     return ONO_OK;
 }
 
@@ -402,8 +432,7 @@ int xgmi_round(ono_ring *r, float *res, float *grad, hipStream_t s, const size_t
     const int n = r->n, pos = r->pos, c = (pos + 1) % n;
     auto len = [&](int q) { return plen[q]; };
     constexpr bool f16 = sizeof(W) == 2;
-    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
-        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    if (uint32_t w = __atomic_load_n(x->err, __ATOMIC_ACQUIRE)) return xgmi_err(w);
 
     XSegs push{};  // 1. my slice of every peer's chunk -> that owner's receive slot
     for (int d = 1; d < n; d++) {
@@ -497,8 +526,7 @@ int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t
     XgmiState *x = r->xgmi;
     if (C + 4 > x->slot)
         return set_error(ONO_E_SIZE, "PS shard of %zu elements exceeds the ring's exchange slot (%zu)", C, x->slot - 4);
-    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
-        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    if (uint32_t w = __atomic_load_n(x->err, __ATOMIC_ACQUIRE)) return xgmi_err(w);
     const int n = r->n, pos = r->pos;
     auto lo = [&](int q) { return std::min(N, (size_t)q * C); };
     auto len = [&](int q) { return std::min(N, lo(q) + C) - lo(q); };
@@ -622,8 +650,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     // A barrier that gave up let the later kernels run on partly landed slots:
     // the round's output is invalid and the host residual has already been
     // zeroed, so it must not report success (ono_ring_check's condition).
-    if (__atomic_load_n(x->err, __ATOMIC_ACQUIRE))
-        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    if (uint32_t w = __atomic_load_n(x->err, __ATOMIC_ACQUIRE)) return xgmi_err(w);
     return ONO_OK;
 }
 
@@ -681,15 +708,8 @@ void xgmi_free(ono_ring *r) {
         }
     }
     for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
-    {  // the region goes back to the pool (or into quarantine); peer mappings stay in the process's table
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        for (auto &pr : g_regions)
-            if (pr.ptr == x->xbuf) {
-                if (released) pr.busy = false;
-                else pr.quarantined = true;  // stays busy: never handed to another ring
-            }
-        g_live--;
-    }
+    // the region goes back to the pool (or into quarantine); peer mappings stay in the process's table
+    if (x->counted) pool().release_ring(x->xbuf, released);
     if (x->err) (void)hipHostFree(x->err);
     delete x;
     r->xgmi = nullptr;
@@ -734,59 +754,47 @@ int ono_ring_xgmi_handle(ono_ring *r, uint8_t handle[ONO_XGMI_HANDLE_BYTES]) {
     return ONO_OK;
 }
 
+int ono_xgmi_pool_close_imports(size_t *closed_imports) {
+    std::string msg;
+    int rc = pool().close_imports(closed_imports, msg);
+    return rc ? set_error(rc, "%s", msg.c_str()) : ONO_OK;
+}
+
+int ono_xgmi_pool_free_exports(size_t *freed_bytes, size_t *kept, double wait_s) {
+    if (!(wait_s >= 0) || wait_s > 1e7) return set_error(ONO_E_ARG, "wait %g s", wait_s);
+    std::string msg;
+    int rc = pool().free_exports(wait_s, freed_bytes, kept, msg);
+    return rc ? set_error(rc, "%s", msg.c_str()) : ONO_OK;
+}
+
 int ono_xgmi_pool_release(size_t *freed_bytes, size_t *closed_imports) {
     if (freed_bytes) *freed_bytes = 0;
     if (closed_imports) *closed_imports = 0;
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    if (g_live > 0) return set_error(ONO_E_ARG, "%d xGMI ring(s) of this process are alive", g_live);
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    size_t freed = 0, closed = 0;
-    int rc = ONO_OK;
-    std::vector<PooledRegion> keep;
-    for (auto &pr : g_regions) {
-        if (pr.busy) {  // quarantined: a peer's teardown never confirmed
-            keep.push_back(pr);
-            continue;
-        }
-        hipError_t e = hipSetDevice(pr.device);
-        if (e == hipSuccess) e = hipFree(pr.ptr);
-        if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "hipFree (pooled exchange region)", __FILE__, __LINE__);
-        freed += pr.bytes;
-    }
-    g_regions.swap(keep);
-    for (auto &m : g_mapped) {
-        hipError_t e = hipSetDevice(m.device);
-        if (e == hipSuccess) e = hipIpcCloseMemHandle(m.ptr);
-        if (e != hipSuccess && rc == ONO_OK) rc = hip_error(e, "hipIpcCloseMemHandle (peer region)", __FILE__, __LINE__);
-        closed++;
-    }
-    g_mapped.clear();
-    (void)hipSetDevice(cur);
-    if (freed_bytes) *freed_bytes = freed;
-    if (closed_imports) *closed_imports = closed;
-    return rc;
+    int rc = ono_xgmi_pool_close_imports(closed_imports);
+    if (rc) return rc;
+    // the peers close their imports of this process's regions in their own release: wait for them
+    // (bounded by the ring timeout's default; a region still mapped by a peer after it stays pooled)
+    const char *e = getenv("ONO_XGMI_TIMEOUT_S");
+    const double wait = e && atof(e) > 0 ? atof(e) : 600.0;
+    return ono_xgmi_pool_free_exports(freed_bytes, nullptr, wait);
 }
 
 int ono_xgmi_pool_stats(size_t *regions, size_t *region_bytes, size_t *quarantined, size_t *imports) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    size_t b = 0, q = 0;
-    for (const auto &pr : g_regions) {
-        b += pr.bytes;
-        q += pr.quarantined ? 1 : 0;
-    }
-    if (regions) *regions = g_regions.size();
-    if (region_bytes) *region_bytes = b;
-    if (quarantined) *quarantined = q;
-    if (imports) *imports = g_mapped.size();
+    const XgmiPool::Stats st = pool().stats();
+    if (regions) *regions = st.regions;
+    if (region_bytes) *region_bytes = st.region_bytes;
+    if (quarantined) *quarantined = st.quarantined;
+    if (imports) *imports = st.imports;
     return ONO_OK;
 }
 
 int ono_ring_check(const ono_ring *r) {
     if (!r) return set_error(ONO_E_ARG, "ring is NULL");
     if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
-    if (r->xgmi && r->xgmi->err && __atomic_load_n(r->xgmi->err, __ATOMIC_ACQUIRE) == 1u)
-        return set_error(ONO_E_IO, "xGMI ring: a peer did not reach a barrier within the timeout");
+    if (r->xgmi && r->xgmi->err) {
+        const uint32_t w = __atomic_load_n(r->xgmi->err, __ATOMIC_ACQUIRE);
+        if (w == 1u || w == 3u) return xgmi_err(w);
+    }
     return ONO_OK;
 }
 

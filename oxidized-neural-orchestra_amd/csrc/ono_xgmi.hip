@@ -136,7 +136,15 @@ __global__ __launch_bounds__(64) void xbarrier_kernel(XBarrier b) {
     if (q < b.n && q != b.pos) {
         const uint64_t t0 = wall_clock64();
         uint32_t spins = 0;
-        while (__hip_atomic_load(b.my_flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < b.epoch) {
+        for (;;) {
+            const uint64_t f = __hip_atomic_load(b.my_flags + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            // a peer is at most one barrier ahead (it cannot pass barrier e+1 without this rank's e+1);
+            // anything larger was not written by this ring's peer for this ring: fail the round loudly
+            if (f > b.epoch + 1) {
+                __hip_atomic_store(b.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            if (f >= b.epoch) break;
             if (wall_clock64() - t0 > b.timeout_ticks) {
                 __hip_atomic_store(b.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
@@ -166,6 +174,13 @@ __global__ __launch_bounds__(64) void xverify_kernel(const uint8_t *region, uint
 __global__ __launch_bounds__(64) void xsignal_kernel(XSignal sg) {
     const int q = threadIdx.x;
     if (q < sg.n && q != sg.pos) st_sys(sg.peer_done[q] + sg.pos, sg.peer_id[q]);
+    peer_stores_done();
+}
+
+// Release bookkeeping: an importer counts itself in (at import) and out (at
+// close) of the exporter's region; the exporter frees only when they match.
+__global__ __launch_bounds__(64) void xbump_kernel(uint64_t *counter) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     peer_stores_done();
 }
 
@@ -231,6 +246,11 @@ hipError_t launch_xgmi_verify(const uint8_t *region, size_t npages, size_t id_of
 hipError_t launch_xgmi_signal(const XSignal &sig, hipStream_t s) {
     if (sig.n < 1 || sig.n > ONO_MAX_INPUTS) return hipErrorInvalidValue;
     hipLaunchKernelGGL(xsignal_kernel, dim3(1), dim3(64), 0, s, sig);
+    return hipGetLastError();
+}
+
+hipError_t launch_xgmi_bump(uint64_t *counter, hipStream_t s) {
+    hipLaunchKernelGGL(xbump_kernel, dim3(1), dim3(64), 0, s, counter);
     return hipGetLastError();
 }
 

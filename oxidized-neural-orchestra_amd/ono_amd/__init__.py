@@ -15,7 +15,7 @@ from ._lib import (Aborted, HipError, InvalidArgument, InvalidWorkerEvent, IoErr
                    RcclError, SizeMismatch, header_functions, lib, worker_event_check)
 from . import kernels, plan, sparse
 from .ring import (DeviceOptimizer, ParamManager, WorkerRingManager, local_ring_pull_grads, unique_id,
-                   xgmi_pool_release, xgmi_pool_stats)
+                   xgmi_pool_close_imports, xgmi_pool_free_exports, xgmi_pool_release, xgmi_pool_stats)
 from .store import (Adam, AddOptimizer, BarrierSync, BlockingStore, DynBarrier, GradientDescent,
                     GradientDescentWithMomentum, NoBlockingSync, WildStore, shard_size_for)
 from .ps import ShardedParamServer
@@ -28,4 +28,5 @@ __all__ = [
     "local_ring_pull_grads", "unique_id", "Adam", "AddOptimizer", "BarrierSync", "BlockingStore",
     "DynBarrier", "GradientDescent", "GradientDescentWithMomentum", "NoBlockingSync", "WildStore",
     "shard_size_for", "ShardedParamServer", "worker_event_check", "xgmi_pool_release", "xgmi_pool_stats",
+    "xgmi_pool_close_imports", "xgmi_pool_free_exports",
 ]

@@ -130,6 +130,8 @@ _SIGS = {
     "ono_ring_xgmi_connect": (_i, [_vp, C.c_char_p]),
     "ono_ring_set_xgmi_timeout": (_i, [_vp, C.c_double]),
     "ono_xgmi_pool_release": (_i, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "ono_xgmi_pool_close_imports": (_i, [C.POINTER(C.c_size_t)]),
+    "ono_xgmi_pool_free_exports": (_i, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_double]),
     "ono_xgmi_pool_stats": (_i, [C.POINTER(C.c_size_t)] * 4),
     "ono_ring_check": (_i, [_vp]),
     "ono_ring_destroy": (_i, [_vp]),

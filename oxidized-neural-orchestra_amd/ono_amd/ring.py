@@ -273,10 +273,28 @@ class WorkerRingManager:
             pass
 
 
+def xgmi_pool_close_imports() -> int:
+    """Release, phase 1 (ono_xgmi_pool_close_imports): mark every peer region this
+    process maps as closed and close the imports.  Every rank, once its xGMI rings
+    are destroyed; then a collective step; then xgmi_pool_free_exports."""
+    closed = C.c_size_t(0)
+    call("ono_xgmi_pool_close_imports", C.byref(closed))
+    return closed.value
+
+
+def xgmi_pool_free_exports(wait_s: float = 60.0) -> dict:
+    """Release, phase 2 (ono_xgmi_pool_free_exports): free every idle exchange
+    region once all its importers have closed it (waits up to wait_s)."""
+    freed, kept = C.c_size_t(0), C.c_size_t(0)
+    call("ono_xgmi_pool_free_exports", C.byref(freed), C.byref(kept), float(wait_s))
+    return {"freed_bytes": freed.value, "kept": kept.value}
+
+
 def xgmi_pool_release() -> dict:
-    """Free this process's idle xGMI exchange regions and close its peer imports
-    (ono_xgmi_pool_release): only when no xGMI ring of the process is alive;
-    call it on every rank."""
+    """Both phases in one call (ono_xgmi_pool_release): close this process's peer
+    imports, then free its idle exchange regions once their importers have closed
+    them.  Only when no xGMI ring of the process is alive; multi-process callers
+    should prefer the two phases with a barrier between."""
     freed, closed = C.c_size_t(0), C.c_size_t(0)
     call("ono_xgmi_pool_release", C.byref(freed), C.byref(closed))
     return {"freed_bytes": freed.value, "closed_imports": closed.value}

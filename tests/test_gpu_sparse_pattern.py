@@ -395,6 +395,35 @@ def test_async_lift_one_launch_back_to_back_sizes():
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
 
 
+def test_async_lift_one_launch_after_an_over_cap_lift():
+    """an over-cap one-launch lift returns before its workgroups reach the end of the
+    kernel, where the next launch's chunk lines are zeroed; the host flips the pair anyway.  Queued on
+    one stream (the default one, as the other one-launch tests): a lift of > 64 tiles (its counts land
+    in one array of the pair), an over-cap lift (uses the other, must zero the first), then another lift
+    of > 64 tiles of the same shape (uses the first again).  The third must not see the first one's
+    complete chunk counts: exact and not refused; the over-cap one refused, g untouched."""
+    rng = np.random.default_rng(4242)
+    jobs = []
+    for k in range(3):
+        b, total = pattern_stream(rng, 700_000, (1, 15), (1, 4))
+        assert 64 < tiles_of(b) <= 4096
+        cap = total - 1 if k == 1 else total
+        buf = to_dev(b)
+        out = torch.full((cap + 8,), 3.0, dtype=torch.float32, device="cuda")
+        st = torch.zeros(1, dtype=torch.int64, device="cuda")
+        jobs.append((b, total, cap, buf, out, st))
+    torch.cuda.synchronize()
+    tickets = [SP.grad_lift_dev_async(buf, out[:cap], st) for _, _, cap, buf, out, st in jobs]
+    torch.cuda.synchronize()
+    for k, ((b, total, cap, _, out, st), tk) in enumerate(zip(jobs, tickets)):
+        if k == 1:
+            assert int(st.item()) == tk
+            assert torch.all(out == 3.0)
+        else:
+            assert int(st.item()) != tk, f"lift {k} refused"
+            assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
+
+
 def same_size_stream(rng, units: int, total: int) -> bytes:
     """A drop-shaped stream of exactly `units` u16 after the total and the given total: records of
     lengths 1-4 until the units are filled (the last record's length takes the rest), offsets 1-15

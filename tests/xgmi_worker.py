@@ -250,15 +250,23 @@ def describe_bad(bad, got, want, ins, prev, length, n) -> str:
     return f"{len(runs)} runs {spans}; sub-rounds {sub}; owner chunks {owners}; wrong values {kinds or ['other']}"
 
 
+# IPC handles this process has exported, across every case (a repeat of one from an earlier case is just
+# as much a repeat: round 4's wrong result came in the first cycle of a case after another case's release)
+SEEN_HANDLES: set = set()
+POOLED: set = set()  # handles of this process's regions pooled right now (reused by design: not a repeat)
+HANDLE_REPEATS = 0
+
+
 def run_recreate(rank: int, n: int, case: dict) -> str | None:
     """Create, use and destroy an xGMI ring several times in the same processes
     (the situation of round 2's one wrong host-fed result: the second ring of a
     process).  Every connect verifies each peer mapping page by page against
     the ring id in that peer's handle (a stale import is an IoError at
     connect); every cycle runs the host-fed sub-round round bit-exact."""
+    global HANDLE_REPEATS
     cycles, length = case.get("cycles", 6), case.get("length", (1 << 20) + 3)
-    release = case.get("release", False)  # ono_xgmi_pool_release between cycles: fresh exports and imports
-    seen, repeats, freed = set(), 0, 0
+    release = case.get("release", False)  # the pool released between cycles: fresh exports and imports
+    freed = 0
     prev = None  # the previous cycle's expected result (stale data from an earlier ring would equal it)
     for cyc in range(cycles):
         blobs = {}
@@ -269,8 +277,11 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
         ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, ag, wire=case.get("wire", "f16"))
         try:
             ipc = blobs["mine"][:64]
-            repeats += ipc in seen  # a pooled region serving again (same IPC handle, same memory)
-            seen.add(ipc)
+            if ipc in SEEN_HANDLES and ipc not in POOLED:  # a fresh region under a handle handed out before
+                HANDLE_REPEATS += 1
+                return f"cycle {cyc}: a fresh exchange region repeats an IPC handle exported before"
+            SEEN_HANDLES.add(ipc)
+            POOLED.add(ipc)  # back in the pool after close, until a release frees it
             ins = [O.synth(length, SEED + 1000 * cyc, r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, case.get("wire", "f16"))
             res_h = np.ascontiguousarray(ins[rank]).copy()
@@ -278,7 +289,7 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
             ring.pull_grads_host(res_h, grad_h)
             bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
             if bad.size:
-                return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats so far {repeats}); " \
+                return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats {HANDLE_REPEATS}); " \
                        + describe_bad(bad, grad_h, expect[rank], ins, prev, length, n)
             prev = expect[rank]
             if bits(res_h).any():
@@ -291,15 +302,22 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
                     pass
         finally:
             ring.close()
-        if release:
-            dist.barrier()  # every rank's ring destroyed before anyone frees
-            r = ono_amd.xgmi_pool_release()
+        if release:  # the two phases (ono_reduce.h): close imports everywhere, a collective step, free
+            dist.barrier()  # every rank's ring destroyed
+            closed = ono_amd.xgmi_pool_close_imports()
             st = ono_amd.xgmi_pool_stats()
-            if r["freed_bytes"] <= 0 or r["closed_imports"] != n - 1 or st["regions"] or st["imports"]:
-                return f"cycle {cyc}: release {r}, stats after {st}"
+            if closed != n - 1 or st["imports"]:
+                return f"cycle {cyc}: closed {closed} imports, stats after {st}"
+            dist.barrier()  # every import of every region closed before anyone frees
+            r = ono_amd.xgmi_pool_free_exports(30.0)
+            st = ono_amd.xgmi_pool_stats()
+            if r["freed_bytes"] <= 0 or r["kept"] or st["regions"]:
+                return f"cycle {cyc}: free_exports {r}, stats after {st}"
             freed += r["freed_bytes"]
-            dist.barrier()  # every import closed before the next ring exports
-    print(json.dumps({"rank": rank, "recreate_ipc_handle_repeats": repeats, "cycles": cycles, "released_bytes": freed}),
+            POOLED.clear()
+            dist.barrier()  # every region freed before the next ring allocates
+    print(json.dumps({"rank": rank, "recreate_ipc_handle_repeats": HANDLE_REPEATS, "cycles": cycles,
+                      "released_bytes": freed}),
           file=sys.stderr)
     return None
 
