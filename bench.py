@@ -103,6 +103,13 @@ def parse_args(argv=None):
                          "RCCL, the whole N > 1 flow runs: torchrun launch, rings, checks, children, JSON line)")
     ap.add_argument("--cpu-ranks", type=int, default=2)
     ap.add_argument("--cpu-rounds", type=int, default=3)
+    ap.add_argument("--deadline", type=float, default=420.0,
+                    help="seconds from the start for the whole line: the headline is measured and checked first, "
+                         "an informational leg that would not finish in time is skipped (recorded as skipped), and "
+                         "a leg still running at the deadline + 45 s is cut (the line is printed as it stands)")
+    # CPU plumbing tests only: no GPU, the steps and legs are sleeps (tests/test_bench_harness.py)
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-leg-s", type=float, default=0.0, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -972,27 +979,157 @@ class Runner:
         return {"ok": bad == 0 and left == 0, "max_err_over_bound": round(ratio, 4), "elems_over_bound": bad,
                 "residual_nonzero": left}
 
+# ------------------------------------------------------------ time budget
+# a leg still running this long after the deadline is cut (the line printed as it stands); env for CPU tests
+GRACE_S = float(os.environ.get("ONO_BENCH_GRACE_S", "45"))
+
+
+class Budget:
+    """The line's deadline, shared by every rank (ONO_BENCH_DEADLINE: absolute
+    time set by whoever started rank 0's job).  Rank 0 decides whether a leg
+    still fits and broadcasts the decision, so collective legs are entered or
+    skipped by every rank together."""
+
+    def __init__(self, ctl: Ctl, deadline: float):
+        self.ctl, self.deadline = ctl, deadline
+
+    def left(self) -> float:
+        return self.deadline - time.time()
+
+    def allow(self, est_s: float) -> bool:
+        ok = b"1" if self.left() >= est_s else b"0"
+        return self.ctl.bcast_bytes(ok) == b"1" if self.ctl.world > 1 else ok == b"1"
+
+
+class LineBox:
+    """The JSON line under a lock: legs store results into it, and the backstop
+    watchdog prints it as it stands if a leg overruns the deadline."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.line: dict = {}
+        self.running: str | None = None
+        self.children: list = []  # subprocess.Popen of the xGMI legs, killed by the watchdog
+
+    def put(self, path: tuple, value) -> None:
+        with self.lock:
+            d = self.line
+            for k in path[:-1]:
+                d = d.setdefault(k, {})
+            d[path[-1]] = value
+
+    def dump(self) -> str:
+        with self.lock:
+            return json.dumps(self.line)
+
+
+BOX = LineBox()
+
+
+def start_backstop(budget: Budget, rank: int) -> threading.Timer:
+    """At deadline + GRACE_S: kill the legs' child processes, mark the leg that
+    was running as cut, print the line (rank 0) and exit — the headline and every
+    finished leg are in it."""
+    def fire():
+        for p in list(BOX.children):
+            try:
+                p.kill()
+            except Exception:  # noqa: BLE001
+                pass
+        with BOX.lock:
+            if BOX.running:
+                d = BOX.line.setdefault("deadline", {})
+                d["cut"] = BOX.running
+        if rank == 0:
+            print(BOX.dump(), flush=True)
+        os._exit(0)
+
+    t = threading.Timer(max(0.0, budget.left() + GRACE_S), fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 with no launcher around it: start the N ranks here, one
+    process per GPU, before this process touches the GPU (it never does), with
+    the env torch.distributed.run would give them; relay rank 0's JSON line.
+    The ranks share this process's deadline."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    argv = list(sys.argv[1:] if argv is None else argv)
+    deadline = os.environ.get("ONO_BENCH_DEADLINE") or repr(time.time() + args.deadline)
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   ONO_BENCH_DEADLINE=deadline)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out = ""
+    try:  # rank 0 prints its line by deadline + GRACE_S at the latest (backstop); a little more for exit
+        out, _ = procs[0].communicate(timeout=max(30.0, float(deadline) - time.time() + GRACE_S + 30.0))
+    except subprocess.TimeoutExpired:
+        procs[0].kill()
+        out, _ = procs[0].communicate()
+    for p in procs[1:]:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if not lines:
+        print(f"bench.py: rank 0 printed no line (exit {procs[0].returncode})", file=sys.stderr)
+        return procs[0].returncode or 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+class DryRing:
+    """--dry-run: a ring that only sleeps (CPU plumbing tests)."""
+    algo = "dry"
+
+    def set_pipeline(self, _):
+        pass
+
+    def close(self):
+        pass
+
+
 # ------------------------------------------------------------------- main
 def main(argv=None) -> int:
     args = parse_args(argv)
     if args.xgmi_child:
         return xgmi_child_main(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    deadline = float(os.environ.get("ONO_BENCH_DEADLINE") or time.time() + args.deadline)
 
-    import torch
-    import ono_amd
-
-    torch.cuda.set_device(local_rank)
+    dry = args.dry_run
+    if dry:
+        torch = ono_amd = None
+    else:
+        import torch
+        import ono_amd
+        torch.cuda.set_device(local_rank)
     ctl = Ctl(world, rank)
+    budget = Budget(ctl, deadline)
     elems = args.bucket_mib * (1 << 20) // 4
     bucket_bytes = elems * 4
 
     def new_ring(wire: str, algo: str, size: int = elems):
+        if dry:
+            return DryRing()
         if algo == "xgmi" and world > 1:  # no communicator: IPC handles over the control plane
             return ono_amd.WorkerRingManager.over_xgmi(rank, world, size, ctl.allgather_bytes, wire=wire,
                                                        device=local_rank)
@@ -1000,16 +1137,25 @@ def main(argv=None) -> int:
         uid = ctl.bcast_bytes(uid) if world > 1 else None
         return ono_amd.WorkerRingManager(rank, world, size, uid=uid, wire=wire, device=local_rank, algo=algo)
 
+    # ---- the headline first: measured, checked and in the line before any informational leg
     ring = new_ring(args.wire, args.algo)
     ring.set_pipeline(args.segments)
-    run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
-    measure, stream = run.measure, run.stream
+    if dry:
+        run = None
 
-    link = xgmi_link_probe(torch) if (world > 1 and rank == 0) else None
+        def measure(_r):
+            el, _ = timed_region(lambda i: time.sleep(0.001), args.steps, args.warmup, lambda: None, ctl)
+            return el, {"kernel_ms": el * 1e3, "kernels": args.steps, "collective_ms": 0.0, "collectives": 0}
+        stream = None
+    else:
+        run = Runner(torch, ono_amd, args, ctl, world, rank, elems)
+        measure, stream = run.measure, run.stream
+
+    link = xgmi_link_probe(torch) if (world > 1 and rank == 0 and not dry) else None
     ctl.barrier()
     elapsed, tim = measure(ring)
 
-    extra = {"check": run.verify(args.wire)}
+    extra = {"check": {"ok": True, "dry_run": True} if dry else run.verify(args.wire)}
     if world == 1:
         avg_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
         per_launch = 12 * elems  # read residual, write grad, write zeros (12 N)
@@ -1032,11 +1178,40 @@ def main(argv=None) -> int:
         extra["roofline"] = nx_roofline(tim, bucket_bytes, elems, world, args.wire, ring.algo, args.steps, elapsed,
                                         link)
 
-    def leg(name, fn):  # informational legs: a failure is recorded in the line, never fatal to it
+    value = world * bucket_bytes * args.steps / elapsed / GIB
+    BOX.line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
+                          bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
+    line = BOX.line
+    line["config"]["schedule"] = ring.algo
+    if world > 1 and ring.algo == "xgmi":
+        line["config"]["collective"] = "xGMI peer-access kernels over IPC-mapped peer HBM (no RCCL)"
+    if world > 1 and args.wire == "f32" and ring.algo in ("auto", "allreduce"):
+        line["config"]["allreduce_segments"] = args.segments or "library default (ONO_AR_SEGMENTS or 4)"
+    line["deadline"] = {"s": args.deadline, "skipped": []}
+    backstop = start_backstop(budget, rank)
+
+    def leg(path, est_s: float, fn, collective: bool = False):
+        """An informational leg: skipped (and recorded) when it would end past the deadline, its failure
+        recorded in the line, never fatal to it.  Collective legs are decided by rank 0 for every rank."""
+        path = path if isinstance(path, tuple) else (path,)
+        name = ":".join(path)
+        ok = budget.allow(est_s) if collective else budget.left() >= est_s
+        if not ok:
+            BOX.put(("deadline", "skipped"), line["deadline"]["skipped"] + [name])
+            return None
+        BOX.running = name
         try:
-            extra[name] = fn()
+            if dry:
+                time.sleep(args.dry_leg_s)
+                res = {"dry_run": True}
+            else:
+                res = fn()
         except Exception as e:  # noqa: BLE001
-            extra[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            res = {"error": f"{type(e).__name__}: {e}"[:300]}
+        BOX.running = None
+        if res is not None:
+            BOX.put(path, res)
+        return res
 
     def tcp_legs():
         out = tcp_edge_native(elems, 10) or tcp_edge(ono_amd, elems, 3)
@@ -1052,54 +1227,40 @@ def main(argv=None) -> int:
         out["config1"] = small
         return out
 
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1:  # estimates: the legs' usual run time on an MI355X box, with margin
         if not args.no_host_fed:
-            leg("host_fed", lambda: host_fed(ono_amd, ring, elems, 5))
+            leg("host_fed", 15, lambda: host_fed(ono_amd, ring, elems, 5))
         if not args.no_tcp_edge:
-            leg("tcp_edge", tcp_legs)
+            leg("tcp_edge", 40, tcp_legs)
         if not args.no_host_fed:
-            leg("ps_host_fed", lambda: ps_host_fed(ono_amd, elems))
+            leg("ps_host_fed", 15, lambda: ps_host_fed(ono_amd, elems))
         if not args.no_local_reduce:
-            leg("local_reduce", lambda: local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
-            leg("path_kernels", lambda: path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
-            leg("sparse_codec", lambda: sparse_codec(torch, ono_amd))
-            leg("copy_ceiling", lambda: copy_ceiling(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
+            leg("local_reduce", 15, lambda: local_reduce(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
+            leg("path_kernels", 25, lambda: path_kernels(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
+            leg("sparse_codec", 25, lambda: sparse_codec(torch, ono_amd))
+            leg("copy_ceiling", 15, lambda: copy_ceiling(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
         if not args.no_cpu_baseline:
-            leg("cpu_baseline", lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
-        n1_roofline_summary(extra["roofline"], extra.get("local_reduce"), extra.get("copy_ceiling"))
+            leg("cpu_baseline", 60, lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
+        with BOX.lock:
+            n1_roofline_summary(line["roofline"], line.get("local_reduce"), line.get("copy_ceiling"))
 
-    value = world * bucket_bytes * args.steps / elapsed / GIB
-    line = build_line(value=value, n_gpus=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
-                      bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
-    line["config"]["schedule"] = ring.algo
-    if world > 1 and ring.algo == "xgmi":
-        line["config"]["collective"] = "xGMI peer-access kernels over IPC-mapped peer HBM (no RCCL)"
-    if world > 1 and args.wire == "f32" and ring.algo in ("auto", "allreduce"):
-        line["config"]["allreduce_segments"] = args.segments or "library default (ONO_AR_SEGMENTS or 4)"
-
-    # Informational: the other exchange schedules at N > 1 (never `value`).
-    # A watchdog keeps an untested-at-scale schedule from costing the main line.
+    # Informational: the other exchange schedules at N > 1 (never `value`), each entered by every rank
+    # together or skipped by every rank together (rank 0 reads the clock).
     extras = world > 1 or args.alt_at_n1
     alts = [a.split(":") for a in args.alt_schedules.split(",") if a] if extras else []
     if extras:
-        line["alt_schedules"] = {}
+        BOX.put(("alt_schedules",), {})
         if world > 1 and args.xgmi:  # in child processes: a fault there cannot take the main line down
-            line["alt_schedules"].update(xgmi_spawn(args, ctl, world, rank, local_rank))
-
-        def fire():
-            line["alt_schedules"]["error"] = f"watchdog: alternative schedules exceeded {args.alt_timeout:.0f} s"
-            if rank == 0:
-                print(json.dumps(line), flush=True)
-            os._exit(0)
-
-        dog = threading.Timer(args.alt_timeout, fire)
-        dog.daemon = True
-        dog.start()
+            def xgmi_leg():
+                args.xgmi_timeout = max(30.0, min(args.xgmi_timeout, budget.left() - 60.0))
+                for k, v in xgmi_spawn(args, ctl, world, rank, local_rank).items():
+                    BOX.put(("alt_schedules", k), v)
+            leg(("alt_schedules", "xgmi_children"), 90, xgmi_leg, collective=True)
         rings = {args.wire: ring}
         for alt in alts:
             algo, wire, seg = alt[0], alt[1], int(alt[2]) if len(alt) > 2 else args.segments
-            key = ":".join(alt)
-            try:
+
+            def alt_leg(algo=algo, wire=wire, seg=seg):
                 if wire not in rings:
                     rings[wire] = new_ring(wire, "auto")
                 r = rings[wire]
@@ -1107,24 +1268,23 @@ def main(argv=None) -> int:
                 r.set_pipeline(seg)
                 el, t = measure(r)
                 r.set_pipeline(args.segments)
-                line["alt_schedules"][key] = {
-                    "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
-                    "ms_per_step": round(el / args.steps * 1e3, 4),
-                    "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps),
-                    "check": run.verify(wire)}
-            except Exception as e:  # recorded, never fatal for the main line
-                line["alt_schedules"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+                return {"value": round(world * bucket_bytes * args.steps / el / GIB, 3),
+                        "ms_per_step": round(el / args.steps * 1e3, 4),
+                        "roofline": xgmi_roofline(t, bucket_bytes, elems, world, wire, algo, args.steps),
+                        "check": run.verify(wire)}
+            leg(("alt_schedules", ":".join(alt)), 20, alt_leg, collective=True)
         if world > 1 and not args.no_host_fed:  # the PCIe-inclusive round at N > 1 (north star)
-            line["host_fed"] = host_fed_n(ono_amd, new_ring(args.wire, args.algo), elems, ctl, world)
+            leg("host_fed", 30, lambda: host_fed_n(ono_amd, new_ring(args.wire, args.algo), elems, ctl, world),
+                collective=True)
         if args.sweep_mib:  # BASELINE config 4: the bandwidth-vs-bucket-size curve, main schedule
             def sweep_ring(e):
                 r = new_ring(args.wire, args.algo, e)
                 r.set_pipeline(args.segments)
                 return r
-            line["size_sweep"] = size_sweep(torch, ono_amd, ctl, sweep_ring, sweep_sizes(args.sweep_mib), world,
-                                            rank, stream)
+            leg("size_sweep", 45, lambda: size_sweep(torch, ono_amd, ctl, sweep_ring, sweep_sizes(args.sweep_mib),
+                                                     world, rank, stream), collective=True)
         if args.ps_mode:  # BASELINE config 5: sharded synchronizer, RS + fused GD + AG
-            try:
+            def ps_leg():
                 import numpy as np
                 init = np.zeros(elems, np.float32)
                 ps = ono_amd.ShardedParamServer(ring, init, ono_amd.GradientDescent(0.1))
@@ -1133,27 +1293,26 @@ def main(argv=None) -> int:
                 ring.timing(False)
                 el, _ = timed_region(lambda i: ps.step(run.residuals[i], params, stream), args.steps, args.warmup,
                                      torch.cuda.synchronize, ctl)
-                line["alt_schedules"]["ps:gd"] = {
-                    "value": round(world * bucket_bytes * args.steps / el / GIB, 3),
-                    "ms_per_step": round(el / args.steps * 1e3, 4),
-                    "workload": "ShardedParamServer.step: reduce-scatter(sum) -> fused /n + GD on the owned "
-                                "shard -> all-gather(params), 256 MiB gradient per GPU"}
                 ps.close()
                 del params
-            except Exception as e:
-                line["alt_schedules"]["ps:gd"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        dog.cancel()
+                return {"value": round(world * bucket_bytes * args.steps / el / GIB, 3),
+                        "ms_per_step": round(el / args.steps * 1e3, 4),
+                        "workload": "ShardedParamServer.step: reduce-scatter(sum) -> fused /n + GD on the owned "
+                                    "shard -> all-gather(params), 256 MiB gradient per GPU"}
+            leg(("alt_schedules", "ps:gd"), 20, ps_leg, collective=True)
         for w, r in rings.items():
             if r is not ring:
                 r.close()
 
     if world == 1 and args.xgmi_coresident > 1:
-        line["xgmi_coresident"] = xgmi_spawn(args, ctl, world, rank, local_rank, coresident=args.xgmi_coresident)
+        leg("xgmi_coresident", 60, lambda: xgmi_spawn(args, ctl, world, rank, local_rank,
+                                                      coresident=args.xgmi_coresident))
 
+    backstop.cancel()
     ring.close()
     ctl.close()
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(BOX.dump(), flush=True)
     return 0
 
 
@@ -1190,6 +1349,7 @@ def xgmi_spawn(args, ctl: Ctl, world: int, rank: int, local_rank: int, coresiden
         env = dict(base_env, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(local_rank), LOCAL_WORLD_SIZE=str(n),
                    ONO_BENCH_RDV="file://" + os.path.join(rdv_dir, "store"))
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    BOX.children.extend(procs)
     deadline = time.time() + args.xgmi_timeout
     outs = []
     for p in procs:

@@ -194,3 +194,61 @@ def test_nx_line_carries_xgmi_algbw_links_and_phases(algo, wire):
     else:
         assert r["per_link_gbs"] is None
     json.dumps(line)
+
+
+def _bench(args, timeout=120, **env):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ONO_BENCH_DEADLINE")}
+    e.update(env, HIP_VISIBLE_DEVICES="")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "3", "--warmup", "1",
+                        *args], capture_output=True, text=True, timeout=timeout, env=e, cwd=ROOT)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines, time.time() - t0
+
+
+def test_gpus_2_without_a_launcher_starts_its_ranks_and_prints_one_line():
+    """`bench.py --gpus 2` with no torch.distributed.run around it starts the two ranks
+    itself (one process each, before any GPU call) and relays rank 0's line: exactly one JSON line."""
+    r, lines, _ = _bench(["--gpus", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["check"]["ok"] and "alt_schedules" in line and "size_sweep" in line
+    assert line["deadline"]["skipped"] == []
+
+
+def test_a_leg_that_would_end_past_the_deadline_is_skipped_and_the_line_printed_in_time():
+    """With 20 s for the line and 8-s legs: the headline and the first leg are in, every later leg that
+    would end past the deadline is recorded as skipped, the line comes out before the deadline."""
+    r, lines, took = _bench(["--deadline", "20", "--dry-leg-s", "8"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["value"] > 0 and line["check"]["ok"]
+    assert line["host_fed"] == {"dry_run": True}
+    assert "tcp_edge" in line["deadline"]["skipped"] and "cpu_baseline" in line["deadline"]["skipped"]
+    assert took < 20
+
+
+def test_a_leg_that_overruns_is_cut_and_the_headline_survives():
+    """A leg that fits the estimate but runs on past the deadline: at deadline + grace the backstop prints
+    the line as it stands (headline, check, the cut leg named) and ends the process."""
+    r, lines, took = _bench(["--deadline", "16", "--dry-leg-s", "60"], ONO_BENCH_GRACE_S="2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["value"] > 0 and line["check"]["ok"]
+    assert line["deadline"]["cut"] == "host_fed" and "host_fed" not in line
+    assert took < 40
+
+
+def test_two_self_launched_ranks_cut_together():
+    """N = 2, self-launched: the ranks share the launcher's deadline; a collective leg that overruns is cut
+    on both, rank 0's line is relayed, nobody is left waiting."""
+    r, lines, took = _bench(["--gpus", "2", "--deadline", "25", "--dry-leg-s", "60"], ONO_BENCH_GRACE_S="2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["deadline"]["cut"]
+    assert took < 60
