@@ -380,16 +380,20 @@ int ono_ring_timing_enable(ono_ring *ring, int enable);
 int ono_ring_timing_read(ono_ring *ring, double *kernel_ms, int64_t *launches,
                          double *collective_ms, int64_t *collectives);
 /* The same split by phase (ms[ONO_PHASES], count[ONO_PHASES]): local kernels,
- * RCCL calls, and the xGMI schedule's scatter (push), barriers and gather
- * (pull, or owner chain + remote stores with ONO_XGMI_GATHER=push).  The
- * collective total of ono_ring_timing_read is phases 1..4.                  */
+ * RCCL calls (on a TCP ring: the socket exchange of a hop), the xGMI
+ * schedule's scatter (push), barriers and gather (pull, or owner chain +
+ * remote stores with ONO_XGMI_GATHER=push), and on a TCP ring with the
+ * SparseCapable serializer the sparse codec (threshold, drop, mask, lift of
+ * a received SparseGrad).  The collective total of ono_ring_timing_read is
+ * phases 1..4; the kernel total is phase 0.                                 */
 typedef enum {
     ONO_PHASE_KERNEL = 0,
     ONO_PHASE_RCCL = 1,
     ONO_PHASE_XGMI_SCATTER = 2,
     ONO_PHASE_XGMI_BARRIER = 3,
     ONO_PHASE_XGMI_GATHER = 4,
-    ONO_PHASES = 5
+    ONO_PHASE_SPARSE_CODEC = 5,
+    ONO_PHASES = 6
 } ono_phase;
 int ono_ring_timing_phases(ono_ring *ring, double *ms, int64_t *count);
 

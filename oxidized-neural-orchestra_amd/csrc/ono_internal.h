@@ -64,6 +64,20 @@ hipError_t launch_scale_zero(float *dst, const float *src, size_t n, float divis
                              hipStream_t s);
 hipError_t launch_synth(float *out, size_t n, uint64_t seed, uint64_t rank, size_t offset,
                         hipStream_t s);
+// The TCP ring's SparseCapable push in stream order (ono_sparse.hip): the
+// threshold of the sample (idx: the m indices in device memory or a pinned
+// host buffer the kernel reads in place, keys: m device words of scratch; or
+// idx NULL = the whole chunk) into t_dev, the drop (blocking for its length,
+// as ono_sparse_drop) and the masks reading the threshold there.
+int sparse_threshold_dev(float *t_dev, const float *g, size_t n, const uint32_t *idx, uint32_t *keys, size_t m, float r,
+                         hipStream_t s);
+int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, const float *t_dev,
+                     hipStream_t s);
+hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s);
+// Wait for everything enqueued on s so far by spinning on a host-mapped word
+// that a one-lane kernel sets to `epoch` (a stream synchronisation's wake-up
+// costs several microseconds more; used on the TCP ring's hops).
+hipError_t stream_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uint32_t epoch);
 // a SparseGrad's values [0, min(total, L)) on the host after the reference's
 // sequential parse of the whole stream (ono_sparse.hip); *got = its total
 int sparse_lift_prefix_host(const uint8_t *buf, size_t nbytes, float *out, size_t L, size_t *got);

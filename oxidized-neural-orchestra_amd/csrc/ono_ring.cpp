@@ -553,11 +553,17 @@ int ono_ring_destroy(ono_ring *r) {
         for (hipEvent_t ev : r->tx_ev) (void)hipEventDestroy(ev);
         for (uint8_t *z : r->zc)
             if (z) (void)hipHostFree(z);
-        for (uint8_t *h : {r->tx, r->rx, r->sp_rx})
+        for (uint8_t *h : {r->tx, r->rx, r->sp_rx, r->sp_tx})
             if (h) (void)hipHostFree(h);
         (void)hipFree(r->sp_dev);
         (void)hipFree(r->sp_tmp);
-        delete[] r->sample_idx;
+        sample_ahead_free(r->ahead);  // (joins its thread before its buffer goes)
+        if (r->sample_idx) (void)hipHostFree(r->sample_idx);
+        (void)hipFree(r->sp_idx_dev);
+        (void)hipFree(r->sp_t_dev);
+        (void)hipFree(r->sp_rx_dev);
+        if (r->sp_status) (void)hipHostFree(r->sp_status);
+        if (r->tcp_word) (void)hipHostFree(r->tcp_word);
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);

@@ -26,11 +26,13 @@
 namespace ono {
 
 class HostPool;
-struct XgmiState;  // ono_xgmi.cpp
+struct XgmiState;    // ono_xgmi.cpp
+struct SampleAhead;  // ono_tcp.cpp: the default sampler one push ahead
+void sample_ahead_free(SampleAhead *a);
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
-    int kind = 0;  // ono_phase: 0 = library kernel, 1 = RCCL collective, 2..4 = xGMI phases
+    int kind = 0;  // ono_phase: 0 = library kernel, 1 = RCCL collective / TCP exchange, 2..4 = xGMI, 5 = codec
 };
 
 // HIP-event timer for the library's own launches (on the launch stream).
@@ -67,8 +69,8 @@ struct Timer {
             float ms = 0;
             e = hipEventElapsedTime(&ms, p.a, p.b);
             if (e != hipSuccess) return e;
-            if (p.kind == 0) { kernel_ms += ms; kernels++; }
-            else { coll_ms += ms; colls++; }
+            if (p.kind == ONO_PHASE_KERNEL) { kernel_ms += ms; kernels++; }
+            else if (p.kind < ONO_PHASE_SPARSE_CODEC) { coll_ms += ms; colls++; }
             if (p.kind >= 0 && p.kind < ONO_PHASES) { phase_ms[p.kind] += ms; phase_n[p.kind]++; }
             pool.push_back(p);
         }
@@ -136,9 +138,19 @@ struct ono_ring {
     uint64_t sample_state = 0;
     ono_sample_fn sampler = nullptr;
     void *sampler_ctx = nullptr;
-    uint32_t *sample_idx = nullptr;
+    uint32_t *sample_idx = nullptr;   // pinned host: the sampler's output, uploaded in stream order
+    uint32_t *sp_idx_dev = nullptr;   // the sample indices on the device
+    ono::SampleAhead *ahead = nullptr;  // the default sampler's next draw (a helper thread)
+    float *sp_t_dev = nullptr;        // the push's threshold on the device (sparse_threshold_dev)
+    uint8_t *sp_rx_dev = nullptr;     // a received SparseGrad, uploaded for the stream-ordered lift
+    size_t sp_rx_dev_cap = 0;
+    uint64_t *sp_status = nullptr;    // host-mapped: the stream-ordered lift's status word
+    uint64_t *tcp_word = nullptr, *tcp_word_dev = nullptr;  // host-mapped: the hops' stream_wait word
+    uint32_t tcp_epoch = 0;
     uint8_t *sp_dev = nullptr;
     size_t sp_dev_cap = 0;
+    uint8_t *sp_tx = nullptr;  // pinned coherent: a small push's SparseGrad frame, encoded in place
+    size_t sp_tx_cap = 0;
     float *sp_tmp = nullptr;
     size_t sp_tmp_cap = 0;
     // small-frame TCP rings: the wire buffers are pinned host frames the codec

@@ -380,9 +380,10 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
 // workgroups per line).  It also zeroes the next call's aggregates (the previous call's sp_move,
 // which read them, is done).
 __global__ __launch_bounds__(kIT) void sp_image(const float *__restrict__ g, size_t n, size_t ntiles, uint32_t tpw,
-                                                float t, bool vec, uint16_t *img, uint2 *recA, uint2 *recB,
-                                                uint4 *agg, uint4 *agg_next, uint32_t gcap) {
+                                                float t, const float *t_dev, bool vec, uint16_t *img, uint2 *recA,
+                                                uint2 *recB, uint4 *agg, uint4 *agg_next, uint32_t gcap) {
     SP_CLOCK(sp_t0);
+    if (t_dev) t = *t_dev;  // the threshold a stream-ordered sp_threshold left (the TCP ring's push)
     for (size_t i = (size_t)blockIdx.x * kIT + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kIT)
         agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
     const size_t nfull = vec ? n / kTile : 0;
@@ -662,9 +663,10 @@ __global__ __launch_bounds__(kSB) void sp_expand(float *g, const uint8_t *buf, c
 
 // worker_ring.rs:128-131 (scatter: zero what was sent, |g| >= t) and
 // :183-187 (gather: keep only |g| >= t)
-__global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, int zero_kept) {
+__global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, const float *t_dev, int zero_kept) {
     size_t i = (size_t)blockIdx.x * kSB + threadIdx.x;
     if (i >= n) return;
+    if (t_dev) t = *t_dev;
     float x = g[i];
     if (zero_kept) {
         if (kept(x, t)) g[i] = 0.0f;        // scatter: the sent values leave the residual
@@ -2587,49 +2589,77 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
 // |g| values (f32::abs clears the sign bit), the k-th in f32::total_cmp order
 // (select_nth_unstable_by), then f32::max with f16::MIN_POSITIVE (NaN-ignoring).
 // total_cmp on sign-clear floats is the order of their bit patterns (NaN above
-// +inf), so this is an exact radix select over u32 keys: one workgroup, the
-// sample (<= 16384 keys) staged in LDS, four 8-bit digit passes, each a
-// histogram with LDS atomics and a scan for the digit that holds rank k.
-constexpr int kThrT = 1024;
+// +inf), so this is an exact radix select over u32 keys.  Two launches when
+// the sample is drawn: sp_gather_keys spreads the m random reads g[idx[i]]
+// over many workgroups (one CU alone took 9-18 us for them) and leaves the
+// keys where the indices were; sp_threshold then selects in one workgroup of
+// eight waves, 32 keys per lane in registers, one bit per step from the top:
+// each lane counts its keys that share the prefix found so far and have a 0 in
+// this bit (plain VALU compares), the wave sums the lanes' 6-bit counts with
+// one ballot per count bit (a ballot per key slot cost ~47 cycles each: the
+// VALU-to-SALU hand-off), the eight waves' sums meet in LDS, and the bit is
+// chosen by comparing with the rank still sought.  (Round 4's form, LDS-atomic
+// histograms in 1024 threads, spent ~60 us in contended bins: the exponent
+// byte of N(0, s) gradients puts most keys in a few of them.)
+constexpr int kThrT = 512;
 constexpr uint32_t kSampleMax = 16384;  // SAMPLE_SIZE, protocol.rs:13-19
-__global__ __launch_bounds__(kThrT) void sp_threshold(const float *g, const uint32_t *idx, uint32_t m, uint32_t k,
+constexpr int kThrK = (int)kSampleMax / kThrT;
+static_assert(kThrK < 64, "a lane's count fits the six ballots");
+constexpr int kGatherT = 256;
+__device__ __forceinline__ uint32_t abs_key(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7FFFFFFFu; }
+// idx: device memory, or the caller's pinned host buffer read in place (no copy engine in between)
+__global__ __launch_bounds__(kGatherT) void sp_gather_keys(const float *g, const uint32_t *idx, uint32_t *keys,
+                                                           uint32_t m) {
+    const uint32_t i = blockIdx.x * kGatherT + threadIdx.x;
+    if (i < m) keys[i] = abs_key(g[idx[i]]);
+}
+// keys: the gathered keys, or NULL: the sample is g[0, m) itself
+__global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, const float *g, uint32_t m, uint32_t k,
                                                       float *t_out) {
-    __shared__ uint32_t keys[kSampleMax];
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t sel[2];
-    for (uint32_t i = threadIdx.x; i < m; i += kThrT) {
-        const size_t j = idx ? idx[i] : i;
-        keys[i] = __builtin_bit_cast(uint32_t, g[j]) & 0x7FFFFFFFu;
+    __shared__ uint32_t wcount[2][kThrT / 64];
+    const int wave = threadIdx.x / 64;
+    uint32_t key[kThrK];
+#pragma unroll
+    for (int q = 0; q < kThrK; q++) {  // padding slots get bit 31, which no prefix has
+        const uint32_t i = threadIdx.x + (uint32_t)q * kThrT;
+        key[q] = i < m ? (keys ? keys[i] : abs_key(g[i])) : 0xFFFFFFFFu;
     }
-    uint32_t prefix = 0, mask = 0, kk = k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        for (uint32_t b = threadIdx.x; b < 256; b += kThrT) hist[b] = 0;
+    uint32_t prefix = 0, mask = 0x80000000u, kk = k;
+    for (int b = 30; b >= 0; b--) {
+        const uint32_t bit = 1u << b, mb = mask | bit;
+        uint32_t cl = 0;  // this lane's count, <= kThrK: 6 bits
+#pragma unroll
+        for (int q = 0; q < kThrK; q++) cl += (key[q] & mb) == prefix ? 1u : 0u;
+        uint32_t c = 0;
+#pragma unroll
+        for (int v = 0; v < 6; v++) c += (uint32_t)__popcll(__ballot((cl >> v) & 1u)) << v;
+        const int par = b & 1;  // two count arrays: the next step's writes never meet this step's reads
+        if ((threadIdx.x & 63) == 0) wcount[par][wave] = c;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += kThrT) {
-            const uint32_t key = keys[i];
-            if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        uint32_t zeros = 0;
+#pragma unroll
+        for (int w = 0; w < kThrT / 64; w++) zeros += wcount[par][w];
+        if (kk >= zeros) {  // the sought key has a 1 here
+            kk -= zeros;
+            prefix |= bit;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t c = 0, d = 0;
-            for (; d < 255; d++) {
-                if (c + hist[d] > kk) break;
-                c += hist[d];
-            }
-            sel[0] = prefix | (d << shift);
-            sel[1] = kk - c;
-        }
-        __syncthreads();
-        prefix = sel[0];
-        kk = sel[1];
-        mask |= 255u << shift;
-        __syncthreads();
+        mask = mb;
     }
     if (threadIdx.x == 0) {
         const float mp = 6.103515625e-05f;  // f16::MIN_POSITIVE
         const float t = __builtin_bit_cast(float, prefix);
         t_out[0] = prefix > 0x7F800000u ? mp : (t > mp ? t : mp);
     }
+}
+// the select over g[0, m) (idx NULL) or over g[idx[i]] (keys: m device words for the gathered keys; idx
+// may be the same buffer)
+hipError_t launch_threshold(const float *g, const uint32_t *idx, uint32_t *keys, uint32_t m, uint32_t k, float *t_out,
+                            hipStream_t s) {
+    if (idx)
+        hipLaunchKernelGGL(sp_gather_keys, dim3((m + kGatherT - 1) / kGatherT), dim3(kGatherT), 0, s, g, idx, keys, m);
+    hipLaunchKernelGGL(sp_threshold, dim3(1), dim3(kThrT), 0, s, idx ? (const uint32_t *)keys : nullptr, g, m, k,
+                       t_out);
+    return hipGetLastError();
 }
 
 struct ThrScratch {
@@ -2659,7 +2689,7 @@ constexpr size_t kImageTpw = 4;
 static_assert(kRecChunk % kImageTpw == 0, "a workgroup's tiles share one chunk aggregate");
 
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
-                float threshold, hipStream_t s) {
+                float threshold, hipStream_t s, const float *t_dev = nullptr) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
     const bool vec = ((uintptr_t)g & 15u) == 0;
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
@@ -2677,7 +2707,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (ntiles) {
         const size_t grid = (ntiles + kImageTpw - 1) / kImageTpw;
         hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)kImageTpw, threshold,
-                           vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
+                           t_dev, vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     }
@@ -2753,6 +2783,48 @@ int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, s
 }
 
 
+}  // extern "C"
+
+namespace ono {
+
+// (sample.len() as f32 * (1.0 - r)) as usize, clamped to the last index (protocol.rs:33-49)
+static size_t threshold_rank(size_t m, float r) {
+    const float kf = (float)m * (1.0f - r);
+    size_t k = kf <= 0.0f ? 0 : (size_t)kf;
+    return k > m - 1 ? m - 1 : k;
+}
+
+// The TCP ring's push in stream order (ono_tcp.cpp): the threshold into t_dev, the drop and the masks
+// reading it there — no host round trip between them.  idx_dev: the m sample indices in device memory
+// (the caller checked them against n), or NULL for the whole chunk (m == n <= 16384).
+hipError_t stream_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uint32_t epoch) {
+    return host_wait(s, word_host, word_dev, epoch);
+}
+
+int sparse_threshold_dev(float *t_dev, const float *g, size_t n, const uint32_t *idx, uint32_t *keys, size_t m, float r,
+                         hipStream_t s) {
+    if (!(r > 0.0f && r <= 1.0f)) return set_error(ONO_E_ARG, "ratio %g outside (0, 1]", (double)r);
+    if (m == 0 || m > kSampleMax || (!idx && m != n))
+        return set_error(ONO_E_ARG, "sample of %zu values from %zu", m, n);
+    ONO_HIP(launch_threshold(g, idx, keys, (uint32_t)m, (uint32_t)threshold_rank(m, r), t_dev, s));
+    return ONO_OK;
+}
+int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, const float *t_dev,
+                     hipStream_t s) {
+    int rc = drop_args(g, n, buf, cap);
+    if (rc) return rc;
+    return drop_launch(buf, cap, nbytes, nullptr, g, n, 0.0f, s, t_dev);
+}
+hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(sp_mask, dim3((unsigned)((n + kSB - 1) / kSB)), dim3(kSB), 0, s, g, n, 0.0f, t_dev, zero_kept);
+    return hipGetLastError();
+}
+
+}  // namespace ono
+
+extern "C" {
+
 int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t *idx_host, size_t m, float r,
                          void *stream) {
     if (!t_out || (n && !g)) return set_error(ONO_E_ARG, "NULL argument");
@@ -2764,10 +2836,7 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
     if (idx_host)
         for (size_t i = 0; i < m; i++)
             if (idx_host[i] >= n) return set_error(ONO_E_ARG, "sample index %u out of %zu", idx_host[i], n);
-    // (sample.len() as f32 * (1.0 - r)) as usize, clamped to the last index
-    const float kf = (float)m * (1.0f - r);
-    size_t k = kf <= 0.0f ? 0 : (size_t)kf;
-    if (k > m - 1) k = m - 1;
+    const size_t k = threshold_rank(m, r);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     int dev = 0;
@@ -2780,8 +2849,7 @@ int ono_sparse_threshold(float *t_out, const float *g, size_t n, const uint32_t 
         ONO_HIP(hipHostGetDevicePointer((void **)&T.t_dev, T.t_host, 0));
     }
     if (idx_host) ONO_HIP(hipMemcpyAsync(T.idx, idx_host, m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(sp_threshold, dim3(1), dim3(kThrT), 0, s, g, idx_host ? T.idx : nullptr, (uint32_t)m,
-                       (uint32_t)k, T.t_dev);
+    ONO_HIP(launch_threshold(g, idx_host ? T.idx : nullptr, T.idx, (uint32_t)m, (uint32_t)k, T.t_dev, s));
     ONO_HIP(hipGetLastError());
     ONO_HIP(hipStreamSynchronize(s));
     *t_out = *(volatile float *)T.t_host;
@@ -2969,7 +3037,7 @@ int ono_sparse_mask(float *g, size_t n, float threshold, int zero_kept, void *st
     if (n && !g) return set_error(ONO_E_ARG, "NULL argument");
     if (!n) return ONO_OK;
     hipLaunchKernelGGL(sp_mask, dim3((unsigned)((n + kSB - 1) / kSB)), dim3(kSB), 0,
-                       reinterpret_cast<hipStream_t>(stream), g, n, threshold, zero_kept);
+                       reinterpret_cast<hipStream_t>(stream), g, n, threshold, (const float *)nullptr, zero_kept);
     ONO_HIP(hipGetLastError());
     return ONO_OK;
 }

@@ -24,7 +24,7 @@ SYNC_KIND = {"barrier": 0, "nonblocking": 1}
 UID_BYTES = 128
 XGMI_HANDLE_BYTES = 128
 MAX_INPUTS = 16
-PHASES = ("kernel", "rccl", "xgmi_scatter", "xgmi_barrier", "xgmi_gather")  # ono_phase
+PHASES = ("kernel", "rccl", "xgmi_scatter", "xgmi_barrier", "xgmi_gather", "sparse_codec")  # ono_phase
 
 
 class OnoError(RuntimeError):

@@ -165,14 +165,14 @@ def run_timing(rank: int, n: int) -> str | None:
             ring.pull_grads()
         torch.cuda.synchronize()
         ph, tot = ring.timing_phases(), ring.timing_read()
-        want = {"kernel": 3, "rccl": 0, "xgmi_scatter": 3, "xgmi_barrier": 6, "xgmi_gather": 3}
+        want = {"kernel": 3, "rccl": 0, "xgmi_scatter": 3, "xgmi_barrier": 6, "xgmi_gather": 3, "sparse_codec": 0}
         got = {k: v[1] for k, v in ph.items()}
         if got != want:
             return f"phase counts {got} != {want}"
-        coll = sum(v[0] for k, v in ph.items() if k != "kernel")
+        coll = sum(v[0] for k, v in ph.items() if k not in ("kernel", "sparse_codec"))
         if abs(coll - tot["collective_ms"]) > 1e-6 or tot["collectives"] != 12 or tot["kernels"] != 3:
             return f"timing_read {tot} inconsistent with phases {ph}"
-        if not all(v[0] > 0 for k, v in ph.items() if k != "rccl"):
+        if not all(v[0] > 0 for k, v in ph.items() if k not in ("rccl", "sparse_codec")):
             return f"empty phase time {ph}"
         return None
     finally:

@@ -5,7 +5,11 @@
 // round = refill the residual in HBM (untimed) -> barrier -> pull_grads ->
 // barrier.  Prints one JSON line with the median round time.
 //
-//   make -C tools tcp_bench && tools/ono_tcp_bench --ranks 2 --len 109386 --rounds 200
+// --sparse R: every worker uses the SparseCapable{R} serializer (ono_ring_set_sparse);
+// the line then also carries rank 0's per-round phase split (ono_ring_timing_phases:
+// kernels, socket exchange, sparse codec) and the codec's share of the round.
+//
+//   make -C tools tcp_bench && tools/ono_tcp_bench --ranks 2 --len 109386 --rounds 200 [--sparse 0.1]
 #include <hip/hip_runtime.h>
 
 #include <arpa/inet.h>
@@ -63,10 +67,12 @@ void nodelay(int fd) {
 int main(int argc, char **argv) {
     int n = 2, rounds = 100;
     size_t len = 109386;
+    float sparse = 0.0f;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = strtoull(argv[++a], nullptr, 10);
         else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--sparse") && a + 1 < argc) sparse = (float)atof(argv[++a]);
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
     if (n < 2 || rounds < 1 || len < (size_t)n) { fprintf(stderr, "need ranks >= 2, len >= ranks\n"); return 1; }
@@ -77,6 +83,8 @@ int main(int argc, char **argv) {
     pthread_barrier_init(&bar, nullptr, (unsigned)n);
     std::vector<double> t(rounds, 0.0);
     std::vector<int> rc(n, ONO_OK);
+    double ph_ms[ONO_PHASES] = {0};
+    int64_t ph_n[ONO_PHASES] = {0};
     std::vector<std::thread> th;
     for (int r = 0; r < n; r++)
         th.emplace_back([&, r] {
@@ -90,7 +98,9 @@ int main(int argc, char **argv) {
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) _exit(2);
             ono_ring *ring = nullptr;
             int e = ono_ring_create_tcp(&ring, r, n, len, 0, prv, nxt);
+            if (e == ONO_OK && sparse > 0.0f) e = ono_ring_set_sparse(ring, sparse, 0x5EED0000ull + (uint64_t)r);
             for (int k = 0; k <= rounds && e == ONO_OK; k++) {  // round 0 is warmup
+                if (k == 1 && r == 0) e = ono_ring_timing_enable(ring, 1);
                 e = ono_synth_f32(ono_ring_residual(ring), len, 0x0402026 + k, (uint64_t)r, 0, s);
                 if (e == ONO_OK) e = hipStreamSynchronize(s) == hipSuccess ? ONO_OK : ONO_E_HIP;
                 pthread_barrier_wait(&bar);
@@ -105,6 +115,7 @@ int main(int argc, char **argv) {
                 fprintf(stderr, "worker %d: %s\n", r, ono_last_error());
                 _exit(2);
             }
+            if (r == 0 && e == ONO_OK) e = ono_ring_timing_phases(ring, ph_ms, ph_n);
             rc[r] = e;
             if (ring) ono_ring_destroy(ring);
             (void)hipStreamDestroy(s);
@@ -117,7 +128,17 @@ int main(int argc, char **argv) {
         if (e != ONO_OK) return 2;
     std::sort(t.begin(), t.end());
     const double med = t[t.size() / 2];
-    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"s_per_round\": %.9f, \"gib_s\": %.6f}\n", n, len,
-           rounds, med, (double)len * 4.0 / med / (double)(1ull << 30));
+    double mean = 0;
+    for (double x : t) mean += x;
+    mean /= (double)t.size();
+    // phase ms per round on rank 0 (events on its stream; the exchange and the codec block the host)
+    const double kern = ph_ms[ONO_PHASE_KERNEL] / rounds, xchg = ph_ms[ONO_PHASE_RCCL] / rounds,
+                 codec = ph_ms[ONO_PHASE_SPARSE_CODEC] / rounds;
+    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"sparse_r\": %g, \"s_per_round\": %.9f, "
+           "\"s_per_round_mean\": %.9f, \"gib_s\": %.6f, \"phase_ms_per_round\": {\"kernel\": %.5f, "
+           "\"exchange\": %.5f, \"sparse_codec\": %.5f}, \"codec_calls_per_round\": %.2f, "
+           "\"codec_share_of_round\": %.4f}\n",
+           n, len, rounds, (double)sparse, med, mean, (double)len * 4.0 / med / (double)(1ull << 30), kern, xchg, codec,
+           (double)ph_n[ONO_PHASE_SPARSE_CODEC] / rounds, codec * 1e-3 / mean);
     return 0;
 }
