@@ -273,7 +273,52 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
                                  "sample": f"BlockingStore: {ps['workers']} accumulates + 1 update (÷n, GD) of "
                                            f"{ps['len']} params, {ps['shards']} shards on {ps['threads']} pinned cores"},
         "march_native": native,
+        "sparse_ring": sparse_ring_baseline(),
     }
+
+
+def sparse_ring_baseline(ratio: float = 0.1, rounds: int = 20) -> dict:
+    """Config 1 with SparseCapable{ratio} workers: the reference-style CPU ring (one process per worker,
+    oracle/ono_cpu_ring.c) timed beside the MI355X TCP ring, and the MI355X ring's last round checked bit
+    for bit against the oracle's replay of every round (ono_ref_ring_pull_grads_sparse, the samplers'
+    states carried).  Checker-side code (the cpu_baseline leg)."""
+    import socket
+    import tempfile
+    import numpy as np
+    from oracle import oracle as O  # noqa: WPS433 (cpu_baseline leg only)
+    out = {"ratio": ratio, "elems": CONFIG1_ELEMS, "ranks": 2}
+    try:
+        ports = []
+        for _ in range(2):
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                ports.append(so.getsockname()[1])
+        ws = [O.CpuRingWorker(r, 2, CONFIG1_ELEMS, ports[(r + 1) % 2], rounds=rounds, listen_port=ports[r],
+                              sparse=ratio, sparse_seed=0x5EED0000 + r) for r in range(2)]
+        infos = [w.result(300)[2] for w in ws]
+        out["cpu_ms_per_round"] = round(max(i["s_per_round"] for i in infos) * 1e3, 4)
+        out["cpu_cores"] = 2
+    except Exception as e:  # noqa: BLE001
+        out["cpu_error"] = f"{type(e).__name__}: {e}"[:200]
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "r0.bin")
+        g = tcp_sparse_native(CONFIG1_ELEMS, rounds, 2, ratio, dump=path)
+        if not g or "error" in g:
+            out["gpu_error"] = (g or {}).get("error", "tools/ono_tcp_bench not built")
+            return out
+        out["gpu_ms_per_round"] = g["ms"]
+        got = np.fromfile(path, dtype=np.float32)
+    states = [0x5EED0000 + r for r in range(2)]
+    for k in range(rounds + 1):  # the tool's rounds: warmup + timed, a fresh bucket each, samplers carried
+        ins = [O.synth(CONFIG1_ELEMS, 0x0402026 + k, r) for r in range(2)]
+        grads, res, states = O.ring_pull_grads_sparse(ins, [ratio, ratio], states)
+    L = CONFIG1_ELEMS
+    bad = int((~O.same_or_both_nan(got[:L], grads[0])).sum() + (~O.same_or_both_nan(got[L:], res[0])).sum())
+    out["check"] = {"ok": bad == 0, "values_differing": bad, "rounds_replayed": rounds + 1,
+                    "what": "rank 0's grad and residual after the last round vs the oracle's sparse ring"}
+    if out.get("cpu_ms_per_round") and out.get("gpu_ms_per_round"):
+        out["speedup"] = round(out["cpu_ms_per_round"] / out["gpu_ms_per_round"], 2)
+    return out
 
 
 def _cpu_model() -> str:
@@ -832,6 +877,40 @@ def tcp_edge_native(elems: int, rounds: int, ranks: int = 2) -> dict | None:
             "ranks": ranks, "ms": round(d["s_per_round"] * 1e3, 4), "gib_s": round(d["gib_s"], 3)}
 
 
+def tcp_sparse_native(elems: int, rounds: int, ranks: int, ratio: float, dump: str | None = None) -> dict | None:
+    """The TCP edge with every worker's SparseCapable{ratio} serializer (tools/ono_tcp_bench --sparse): the
+    per-round time and rank 0's phase split (socket exchange, the sparse codec's calls, the other kernels).
+    dump: rank 0's grad + residual of the last round, for the checker (cpu_baseline.sparse_ring)."""
+    exe = os.path.join(ROOT, "tools", "ono_tcp_bench")
+    if not os.path.exists(exe):
+        return None
+    import subprocess
+    import numpy as np
+    cmd = [exe, "--ranks", str(ranks), "--len", str(elems), "--rounds", str(rounds), "--sparse",
+           repr(float(np.float32(ratio)))] + (["--dump", dump] if dump else [])
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        d = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001 — reported in the line
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+    return {"ranks": ranks, "elems": elems, "ratio": ratio, "ms": round(d["s_per_round"] * 1e3, 4),
+            "gib_s": round(d["gib_s"], 3), "phase_ms_per_round": d["phase_ms_per_round"],
+            "codec_share_of_round": d["codec_share_of_round"]}
+
+
+def tcp_sparse_legs() -> dict:
+    """SURVEY §8(f) row 3 on the product path: the sparse ring end to end."""
+    out = {"workload": "pull_grads over loopback TCP with SparseCapable{r} workers (SparseGrad frames, "
+                       "reference framing), C++ host threads on one GPU; ms per round, rank 0's phase split"}
+    for key, e, n, r, k in (("config1_2_ranks_r0.1", CONFIG1_ELEMS, 2, 0.1, 200),
+                            ("config1_2_ranks_r0.01", CONFIG1_ELEMS, 2, 0.01, 200),
+                            ("config1_4_ranks_r0.1", CONFIG1_ELEMS, 4, 0.1, 200),
+                            ("256MiB_2_ranks_r0.1", 1 << 26, 2, 0.1, 10),
+                            ("256MiB_2_ranks_r0.01", 1 << 26, 2, 0.01, 10)):
+        out[key] = tcp_sparse_native(e, k, n, r)
+    return out
+
+
 def tcp_edge(ono_amd, elems: int, rounds: int, ranks: int = 2) -> dict:
     """The TCP edge (never `value`): `ranks` MI355X workers on
     this one GPU, one thread each, in a loopback-TCP ring speaking the
@@ -1225,6 +1304,7 @@ def main(argv=None) -> int:
                 cr = O.cpu_ring(nr, CONFIG1_ELEMS, 50, check=False, pin=True, timeout=300)
                 small[k]["cpu_ring_ms"] = round(cr["s_per_round"] * 1e3, 4)
         out["config1"] = small
+        out["sparse"] = tcp_sparse_legs()
         return out
 
     if rank == 0 and world == 1:  # estimates: the legs' usual run time on an MI355X box, with margin

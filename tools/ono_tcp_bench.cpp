@@ -9,6 +9,10 @@
 // the line then also carries rank 0's per-round phase split (ono_ring_timing_phases:
 // kernels, socket exchange, sparse codec) and the codec's share of the round.
 //
+// --dump PATH: rank 0's grad and residual after the last round (2 x len f32), for a checker to
+// replay the rounds (residual k = synth(len, 0x0402026 + k, rank) for k = 0..rounds, sampler seed
+// 0x5EED0000 + rank, carried across rounds).
+//
 //   make -C tools tcp_bench && tools/ono_tcp_bench --ranks 2 --len 109386 --rounds 200 [--sparse 0.1]
 #include <hip/hip_runtime.h>
 
@@ -68,11 +72,13 @@ int main(int argc, char **argv) {
     int n = 2, rounds = 100;
     size_t len = 109386;
     float sparse = 0.0f;
+    const char *dump = nullptr;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = strtoull(argv[++a], nullptr, 10);
         else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--sparse") && a + 1 < argc) sparse = (float)atof(argv[++a]);
+        else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
     if (n < 2 || rounds < 1 || len < (size_t)n) { fprintf(stderr, "need ranks >= 2, len >= ranks\n"); return 1; }
@@ -116,6 +122,15 @@ int main(int argc, char **argv) {
                 _exit(2);
             }
             if (r == 0 && e == ONO_OK) e = ono_ring_timing_phases(ring, ph_ms, ph_n);
+            if (r == 0 && e == ONO_OK && dump) {
+                std::vector<float> h(2 * len);
+                if (hipMemcpy(h.data(), ono_ring_grad(ring), len * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                    hipMemcpy(h.data() + len, ono_ring_residual(ring), len * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                    e = ONO_E_HIP;
+                FILE *f = e == ONO_OK ? fopen(dump, "wb") : nullptr;
+                if (!f || fwrite(h.data(), 4, h.size(), f) != h.size()) e = ONO_E_IO;
+                if (f) fclose(f);
+            }
             rc[r] = e;
             if (ring) ono_ring_destroy(ring);
             (void)hipStreamDestroy(s);
