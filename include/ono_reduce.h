@@ -174,7 +174,13 @@ int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t
  * pattern's shape, a malformed one, or total > cap — and g is then
  * unspecified: call ono_sparse_lift_dev (blocking), which parses any stream and
  * returns the reference's errors and ONO_E_SIZE.  Otherwise g[0, total) holds
- * the lift (total: the stream's first 8 bytes).  Scratch is per stream.     */
+ * the lift (total: the stream's first 8 bytes).  Scratch is per stream.
+ * A refused call may already have written parts of g[0, total): check the
+ * status before using g.  The one-launch form (an 8-B aligned stream of at
+ * most 4096 tiles) needs its whole grid resident; when kernels of another
+ * stream or process hold CU slots so that the count of started workgroups
+ * stalls short of the grid for ~100 us, the call is refused rather than
+ * waiting for them (measured: refused in 0.75 ms with 3/4 of the CUs held).  */
 int ono_sparse_lift_dev_async(float *g_dev, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
                               uint64_t *ticket, void *stream);
 /* lifts so far (this process) that took the sequential host parse        */

@@ -1884,9 +1884,36 @@ constexpr uint32_t kPollMax = 1u << 14;  // polls before a look-back gives up (~
 #define ONO_POLL_SLEEP 16
 #endif
 constexpr int kPollSleep = ONO_POLL_SLEEP;
+// Residency bound: every workgroup counts itself in (one device-scope add) as it
+// starts; a look-back that is still waiting while the count stays short of the grid and has not moved
+// for kArriveTicks of the 100 MHz wall clock gives the call up (the status word), and so does one that
+// sees the status raised.  Short work of another stream (a two-launch lift, a few tens of us) frees
+// slots and the count moves on; a kernel of another stream or process that holds CU slots for long then
+// costs ~100 us and a refusal (the caller's blocking lift does the work), not the ~10 ms poll limit and
+// a wait for that kernel.
+constexpr uint64_t kArriveTicks = 10000;  // 100 us without a new arrival
+constexpr uint32_t kArriveEvery = 16;      // polls between two residency checks (~8 us)
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+struct FusedGrid {
+    const uint64_t *arrive;  // the stream's arrival counter (monotonic over launches)
+    uint64_t target;         // its value once this launch's whole grid has started
+    const uint64_t *badw;    // the call's status word (raise_bad)
+    uint32_t epoch;
+    uint64_t seen = 0, since = 0;  // the count last read, and when it last moved
+    __device__ bool give_up() {
+        if (*(const volatile uint64_t *)badw == (uint64_t)epoch) return true;  // refused elsewhere
+        const uint64_t c = ld_agent(arrive), now = wall_clock64();
+        if (c >= target) return false;  // the whole grid is resident: the awaited tiles will come
+        if (c != seen || since == 0) {
+            seen = c;
+            since = now;
+            return false;
+        }
+        return now - since > kArriveTicks;
+    }
+};
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1930,7 +1957,7 @@ __device__ __forceinline__ void pat_stage_write(uint4 *lw4, const uint2 (&v)[kSt
 // waiting) and the exit of the nearest earlier tile that holds a record.  False: a poll timed out.
 __device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const uint64_t *frec, const uint64_t *fchunk,
                                                uint32_t gcap, uint32_t rep, uint64_t &E, bool &found,
-                                               uint32_t &pexit) {
+                                               uint32_t &pexit, FusedGrid fg) {
     const uint32_t lane = threadIdx.x & 63, c = t / kPatChunk, c0 = c * kPatChunk;
     bool timeout = false;
     const bool wchunk = lane < c, wtile = c0 + lane < t;
@@ -1946,7 +1973,7 @@ __device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const 
         const bool ready = (!wchunk || (v >> 40) == (uint64_t)kPatChunk) &&
                            (!wtile || ((a >> 32) == tagv && (x3 >> 32) == tagv));
         if (ready) break;
-        if (it > kPollMax) { timeout = true; break; }
+        if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.give_up())) { timeout = true; break; }
         __builtin_amdgcn_s_sleep(kPollSleep);
     }
     uint64_t part = (wchunk ? v & ((1ull << 40) - 1) : 0ull) + (wtile ? (uint32_t)a : 0u);
@@ -1966,7 +1993,7 @@ __device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const 
             const uint64_t *rr = frec + 2 * (size_t)i + 1;
             uint64_t x = ld_agent(rr);
             for (uint32_t it = 0; (x >> 32) != tagv; it++) {
-                if (it > kPollMax) { timeout = true; break; }
+                if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.give_up())) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(kPollSleep);
                 x = ld_agent(rr);
             }
@@ -1988,7 +2015,8 @@ template <int TPW>
 __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void pl_fused(
     float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *frec, uint64_t *fchunk, uint64_t *fchunk_next,
-                                                  uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch) {
+                                                  uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch, uint64_t *arrive, uint64_t arrive_target) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ uint4 img16[kPatImg / 8];  // a range as f16 bits (12 KiB), widened on the way out
     __shared__ uint4 lw4[TPW][kStageU4];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -2082,7 +2110,8 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
             uint64_t E;
             bool f;
             uint32_t px;
-            const bool ok = fused_lookback(t, tagv, frec, fchunk, gcap, blockIdx.x % kFusedRep, E, f, px);
+            const bool ok = fused_lookback(t, tagv, frec, fchunk, gcap, blockIdx.x % kFusedRep, E, f, px,
+                                           FusedGrid{arrive, arrive_target, badw, epoch});
             if (threadIdx.x == 0) {
                 s_E0 = E;
                 s_found = ok && f ? 1u : 0u;
@@ -2299,6 +2328,8 @@ struct PatScratch {
     size_t fcap = 0, fgcap = 0;
     uint64_t *frec = nullptr, *fchunk = nullptr;
     int fpar = 0;
+    uint64_t *arrive = nullptr;  // pl_fused's arrival counter (device, zeroed once, monotonic)
+    uint64_t arrive_base = 0;    // its value once every earlier launch's grid has started
 };
 std::map<std::pair<int, hipStream_t>, PatScratch> g_pat;
 std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
@@ -2994,15 +3025,23 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
             P.fgcap = gc;
             P.fpar = 0;
         }
+        if (!P.arrive) {
+            ONO_HIP(hipMalloc((void **)&P.arrive, sizeof(uint64_t)));
+            ONO_HIP(hipMemsetAsync(P.arrive, 0, sizeof(uint64_t), s));
+        }
         uint64_t *cur = P.fchunk + (size_t)P.fpar * kFusedRep * P.fgcap * kFusedLine;
         uint64_t *next = P.fchunk + (size_t)(1 - P.fpar) * kFusedRep * P.fgcap * kFusedLine;
-        if (T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX))
-            hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)T), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
-                               cur, next, (uint32_t)P.fgcap, P.aw, status, epoch);
+        const bool one = T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX);
+        const size_t grid = one ? T : (T + 2) / 3;
+        const uint64_t target = P.arrive_base + grid;
+        if (one)
+            hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
+                               cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target);
         else
-            hipLaunchKernelGGL(pl_fused<3>, dim3((unsigned)((T + 2) / 3)), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec,
-                               P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch);
+            hipLaunchKernelGGL(pl_fused<3>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec,
+                               P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target);
         ONO_HIP(hipGetLastError());
+        P.arrive_base = target;
         P.fpar ^= 1;
         fused_device_mark(dev, s);
         return ONO_OK;

@@ -509,3 +509,42 @@ def test_async_lifts_of_large_streams_on_two_streams_concurrently():
     for b, total, out, st, tk in jobs:
         assert int(st.item()) != tk
         assert_bitexact(out.cpu().numpy(), O.grad_lift(b, cap=total))
+
+
+def test_async_lift_one_launch_with_cu_slots_held_by_another_process():
+    """the one-launch lift needs its whole grid resident (tiles wait on tiles of other
+    workgroups).  Another process holds three quarters of the CUs (every LDS byte of each) for 400 ms
+    while a ~4000-tile lift (~1350 workgroups of three tiles) is queued: the workgroups that start count
+    themselves in, find the count stalled short of the grid for ~100 us and give the call up; the rest
+    start in the freed slots, see the refusal and end.  So the call is refused quickly instead of polling ~10 ms per wave
+    (and waiting for the other process), and the blocking lift that follows is exact."""
+    import os
+    import subprocess
+    import time
+    hog = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "cu_hog")
+    if not os.path.exists(hog):
+        pytest.skip("tests/native/cu_hog not built")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(4096)
+    b, total = pattern_stream(rng, 1_280_000, (1, 15), (1, 4))
+    assert 3900 <= tiles_of(b) <= 4096
+    buf = to_dev(b)
+    out = torch.full((total + 8,), 3.0, dtype=torch.float32, device="cuda")
+    status = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    p = subprocess.Popen([hog, str(3 * cus // 4), "400"], stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().startswith("running")
+        t0 = time.perf_counter()
+        ticket = SP.grad_lift_dev_async(buf, out[:total], status)
+        torch.cuda.synchronize()
+        took = time.perf_counter() - t0
+        refused = int(status.item()) == ticket
+        if refused:
+            out[:total] = SP.grad_lift_dev(buf, total)
+        assert p.poll() is None, "the other process ended before the lift (timing void)"
+    finally:
+        p.wait(timeout=30)
+    assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
+    print(f"lift with 3/4 of the CUs held elsewhere: {took * 1e3:.2f} ms, refused={refused}")
+    assert took < 0.005, f"the one-launch lift took {took * 1e3:.1f} ms while CU slots were held elsewhere"
