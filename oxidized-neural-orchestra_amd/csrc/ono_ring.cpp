@@ -199,12 +199,34 @@ hipError_t dev_zero(void *dst, size_t bytes, hipStream_t s) {
     return hipMemsetAsync(dst, 0, bytes, s);
 }
 
+// The CPUs this process may actually keep busy: its affinity mask, and under a
+// cgroup v2 CPU quota (cpu.max "quota period") the quota's whole CPUs.  A pool
+// as wide as the machine under a 16-CPU quota is throttled for the rest of a
+// scheduling period whenever the copy threads, the caller and the HIP
+// runtime's threads together overrun it — round 4's occasional pageable round
+// at half the median rate.
+static long usable_cpus() {
+    long n = (long)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = std::min(n > 0 ? n : 1L, (long)CPU_COUNT(&set));
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long period = 0;
+        if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+            const long quota = atol(q) / period;
+            if (quota > 0) n = std::min(n, quota);
+        }
+        fclose(f);
+    }
+    return std::max(1L, n);
+}
+
 int host_threads() {
     const char *e = getenv("ONO_HOST_THREADS");
-    long t = e ? atol(e) : 16;
-    long hw = (long)std::thread::hardware_concurrency();
-    if (hw > 0) t = std::min(t, hw);
-    return (int)std::max(1L, t);
+    if (e && atol(e) > 0) return (int)std::min(atol(e), usable_cpus());
+    // default: 16, leaving two CPUs of the quota to the caller's thread and the runtime's
+    return (int)std::max(1L, std::min(16L, usable_cpus() - 2));
 }
 
 }  // namespace ono
