@@ -52,6 +52,11 @@ __device__ uint4 g_sp_stamp_img[1 << 16], g_sp_stamp_mov[1 << 18], g_sp_stamp_pl
 // pl_fused's look-back per tile: {polls of the slowest chunk lane, of the slowest tile lane, first round's
 // loads back - start, publish - start}
 __device__ uint4 g_sp_stamp_plf[1 << 16];
+// sp_drop1 per tile: {threshold read - start, tile imaged - start, blockIdx.x, own group's look-back done -
+// start} beside the sp_stamp record (mid = look-back done)
+__device__ uint4 g_sp_stamp_d1[1 << 16], g_sp_stamp_d1b[1 << 16];
+// sp_drop1 per tile, lane 0 of the look-back: {polls, their load ticks} of its own group, of earlier groups
+__device__ uint4 g_sp_stamp_d1c[1 << 16];
 __device__ __forceinline__ void sp_stamp(uint4 *st, size_t i, uint64_t t0, uint64_t tm) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -294,10 +299,18 @@ struct ImgAgg {
 // run starts or after the loop); the values are read back from the thread's own units of an LDS
 // copy (an indexable register file).  It replaced a value pass over all 16 elements followed by a
 // loop over the run starts with two popcounts each (round 4: 33.9 vs 34.9 us per drop).
-__device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], float before, size_t n, float t,
-                                           uint16_t *img, uint2 *recA, uint2 *recB, ImgAgg &acc) {
+// What a tile's image holds beside its units (in LDS until the workgroup's next tile): the tile-local
+// counts and edges, the first run's header unit and offset, the last run's header unit, length and start.
+struct TileImg {
+    uint32_t F, R;                  // kept values, runs
+    uint32_t last_kept1, first_unkept;  // tile-local (0: none / kTile: none)
+    uint32_t hp0, off0;             // the first run's header unit, its offset since the last kept value in the tile
+    uint32_t hpl, lenl, rs_last;    // the last run's header unit, its length within the tile, its start
+    const uint16_t *stage;          // the units (LDS)
+};
+__device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE], float before, size_t n, float t) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
-    __shared__ uint32_t rb[2];  // header position | offset of the tile's first run; position | length of its last
+    __shared__ uint32_t rb[3];  // position | offset of the tile's first run; position | length of its last; its start
     const size_t tile0 = tile * kTile;
     const uint32_t lo = threadIdx.x * kIE;  // the thread's first element, tile-local
     const size_t base = tile0 + lo;
@@ -340,6 +353,7 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
                 vst[hp] = (uint16_t)off;
                 vst[hp + 1] = 0;
                 if (hsl == 0) rb[0] = hp | off << 16;
+                if (hsl == R - 1) rb[2] = i;
                 open = true;
             }
             vst[pos++] = v16[i];
@@ -356,18 +370,32 @@ __device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], f
         }
     }
     __syncthreads();
-    const uint32_t nu16 = 4 * R + F;
+    TileImg ti{F, R, ts.last_kept1, ts.first_unkept, 0, 0, 0, 0, 0, stage};
+    if (R) {
+        ti.hp0 = rb[0] & 0xFFFFu;
+        ti.off0 = rb[0] >> 16;
+        ti.hpl = rb[1] & 0xFFFFu;
+        ti.lenl = rb[1] >> 16;
+        ti.rs_last = rb[2];
+    }
+    return ti;
+}
+
+__device__ __forceinline__ void image_tile(size_t tile, const float (&x)[kIE], float before, size_t n, float t,
+                                           uint16_t *img, uint2 *recA, uint2 *recB, ImgAgg &acc) {
+    const size_t tile0 = tile * kTile;
+    const TileImg ti = build_image(tile, x, before, n, t);
+    const uint32_t nu16 = 4 * ti.R + ti.F;
     uint4 *slot = (uint4 *)(img + tile * kSlotU16);
-    const uint4 *st4 = (const uint4 *)stage;
+    const uint4 *st4 = (const uint4 *)ti.stage;
     for (uint32_t k = threadIdx.x; k < (nu16 + 7) / 8; k += kIT) st4_wt(slot + k, st4[k]);
     if (threadIdx.x == 0) {
-        recA[tile] = make_uint2(F | R << 16, ts.last_kept1 | ts.first_unkept << 16);
-        recB[tile] = R ? make_uint2((rb[0] & 0xFFFFu) | rb[1] << 16, rb[0] >> 16 | (rb[1] & 0xFFFF0000u))
-                       : make_uint2(0u, 0u);
+        recA[tile] = make_uint2(ti.F | ti.R << 16, ti.last_kept1 | ti.first_unkept << 16);
+        recB[tile] = ti.R ? make_uint2(ti.hp0 | ti.hpl << 16, ti.off0 | ti.lenl << 16) : make_uint2(0u, 0u);
     }
-    acc.fr += (uint64_t)F | (uint64_t)R << 32;
-    if (F) acc.lk = (uint32_t)tile0 + ts.last_kept1;  // tiles in order: the latest one's is the max
-    if (ts.first_unkept < (uint32_t)kTile && !acc.nfu) acc.nfu = ~((uint32_t)tile0 + ts.first_unkept);  // the first
+    acc.fr += (uint64_t)ti.F | (uint64_t)ti.R << 32;
+    if (ti.F) acc.lk = (uint32_t)tile0 + ti.last_kept1;  // tiles in order: the latest one's is the max
+    if (ti.first_unkept < (uint32_t)kTile && !acc.nfu) acc.nfu = ~((uint32_t)tile0 + ti.first_unkept);  // the first
 }
 
 // The encoder's first launch: workgroup w images tiles w tpw .. w tpw + tpw - 1 (tpw a power of two
@@ -641,6 +669,313 @@ __global__ __launch_bounds__(kSB) void sp_move(
     // wave-uniform (readfirstlane): scalar base addresses and branches
     const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
     if (tile < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, tile);
+}
+
+
+// ------------------------------------------------- one-launch encoder ----
+// sp_drop1 (round 5): the drop in one launch, no slot image and no sp_move.
+// Workgroup b takes tile b, builds the tile's byte range in LDS exactly as sp_image does, publishes
+// its aggregate, looks back over the earlier tiles (decoupled look-back: per tile four 64-bit granules
+// {tag, value} for kept values, runs, last kept index + 1 and last run start + 1, tagged "aggregate"
+// or "inclusive prefix" with the call's epoch), publishes its inclusive prefix, and writes the range
+// straight to its place in the wire.  The look-back has two levels: the earlier tiles of the tile's
+// group of 64, then one descriptor per earlier group, which the group's last tile publishes as an
+// aggregate once it has seen its group and as an inclusive prefix with its own (a walk back over k
+// tiles is k / 4096 + 2 window reads, not k / 64).
+// No dispatch order is assumed (HIP promises none): a descriptor that has not come after fb_polls
+// polls (~80 us by default) — its workgroup may not have started — is computed by the waiting wave
+// from g itself (tile_agg_wave; a group's from its tiles' descriptors and those), the decoupled
+// fallback of Smith, Levien & Owens (2024), so every wait ends whatever the placement.  The first
+// version took tiles by an atomic ticket instead (in start order, so every wait was on a running
+// workgroup): one word takes ~88 returning atomics per us, and 8192 tickets per 64 MiB drop made it
+// 0.13 ms (tools/sp_phases: ticket p50 5 us, max 30 us per workgroup).
+// The two fields that depend on other tiles: the first run's offset (from the last kept index before
+// the tile, known after the look-back) and the length of a run still open at the tile's end, which
+// only a later tile knows — that tile (the first one with an unkept value after the run's start, or
+// the last tile) writes it, and the tile where the run starts leaves those two units alone.  The last
+// tile writes the stream's total and the wire length.
+// Traffic: g read once, the wire written once (4 N + wire bytes), plus 64 B of granules per tile.
+constexpr size_t kDropGroup = 64;            // tiles per group descriptor (the look-back's second level)
+#ifndef DR_SLEEP
+#define DR_SLEEP 4
+#endif
+#ifndef DR_BACK
+#define DR_BACK 8
+#endif
+constexpr uint32_t kDropFallbackPolls = 96;
+// the one launch up to 256 tiles (512 Ki values), the two launches above: stream-ordered drops at ~10 %
+// kept, one launch / two (tools/drop_sizes.py, profiles/r05_s28_drop_sizes.json): 54,693 values 9.6 /
+// 14.8 us, 256 Ki 12.7 / 15.5, 1 Mi 16.8 / 15.6, 16 Mi 95.9 / 33.4.  Past one residency wave of tiles a
+// tile's life (its loads under a saturated HBM queue, then the wait for the slowest earlier tile's
+// aggregate plus ~3 cross-XCD round trips: ~20 us) times the tiles LDS lets run at once (~2560, 20 MB
+// of input) bounds the one launch at ~1 TB/s
+constexpr size_t kDropOneLaunchTiles = 256;  // polls (backing off to ~0.85 us each) before the fallback
+__device__ __forceinline__ uint64_t dr_ld(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void dr_st(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the three data granules first, acknowledged, then the flag granule (0): a reader polls the flag alone
+// and reads the rest once it shows the tag (each still tagged, so a mixed read is seen and retried).
+// (Unordered stores with all four granules polled: 88 vs 77 us per 64 MiB drop.)
+__device__ __forceinline__ void dr_publish(uint64_t *d, uint32_t tag, uint32_t f, uint32_t r, uint32_t lk, uint32_t lrs) {
+    const uint64_t tg = (uint64_t)tag << 32;
+    dr_st(d + 1, tg | r);
+    dr_st(d + 2, tg | lk);
+    dr_st(d + 3, tg | lrs);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dr_st(d, tg | f);
+}
+struct DAgg {
+    uint32_t f = 0, r = 0, k = 0, s = 0;  // kept values, runs, last kept index + 1, last run start + 1
+};
+struct PollAcc {  // measurement build: polls and their load time (100 MHz ticks)
+    uint32_t polls = 0, ticks = 0;
+};
+// a descriptor, polled at most `polls` times (at least once), backing off ~0.1 -> ~0.85 us (thousands of
+// waiting waves polling every ~50 ns load the fabric): 0 not there, 1 an aggregate, 2 an inclusive prefix
+__device__ __forceinline__ int dr_poll(const uint64_t *e, uint32_t tagA, uint32_t tagP, uint32_t polls, DAgg &a,
+                                       PollAcc &pa) {
+    for (uint32_t it = 0, back = 1;; it++) {
+#ifdef ONO_SP_STAMP
+        const uint64_t q0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        const uint64_t a0 = dr_ld(e);
+        const uint32_t g0 = (uint32_t)(a0 >> 32);
+#ifdef ONO_SP_STAMP
+        if (g0 != 0xFFFFFFFFu) {  // (uses it: waits)
+            pa.polls++;
+            pa.ticks += (uint32_t)(__builtin_amdgcn_s_memrealtime() - q0);
+        }
+#endif
+        if (g0 == tagA || g0 == tagP) {
+            const uint64_t a1 = dr_ld(e + 1), a2 = dr_ld(e + 2), a3 = dr_ld(e + 3);
+            if ((uint32_t)(a1 >> 32) == g0 && (uint32_t)(a2 >> 32) == g0 && (uint32_t)(a3 >> 32) == g0) {
+                a.f = (uint32_t)a0;
+                a.r = (uint32_t)a1;
+                a.k = (uint32_t)a2;
+                a.s = (uint32_t)a3;
+                return g0 == tagP ? 2 : 1;
+            }
+        }
+        if (it + 1 >= polls) return 0;
+        for (uint32_t q = 0; q < back; q++) __builtin_amdgcn_s_sleep(DR_SLEEP);
+        back = min(2 * back, (uint32_t)DR_BACK);
+    }
+}
+// the wave's sums / maxima of one lane value each (all 64 lanes active)
+__device__ __forceinline__ uint32_t wsum(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(v), 63); }
+__device__ __forceinline__ uint32_t wmax(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(v), 63); }
+// tile j's aggregate straight from g, by one whole wave (j wave-uniform): lane l holds values
+// 32 l .. 32 l + 31 of the tile as a keep mask; a run starts at a kept value whose predecessor (the
+// value before the tile for the first) is not kept — flags_of's rule
+__device__ DAgg tile_agg_wave(const float *g, size_t n, uint32_t j, float t) {
+    static_assert(kTile == 64 * 32, "one 32-bit mask per lane");
+    const int lane = threadIdx.x & 63;
+    const size_t tile0 = (size_t)j * kTile, b = tile0 + 32 * (size_t)lane;
+    uint32_t k = 0;
+    for (int e = 0; e < 32; e++)
+        if (b + e < n && kept(g[b + e], t)) k |= 1u << e;
+    uint32_t prev = (uint32_t)__shfl_up((int)(k >> 31), 1, 64);
+    if (lane == 0) prev = tile0 > 0 && tile0 - 1 < n && kept(g[tile0 - 1], t) ? 1u : 0u;
+    const uint32_t st = k & ~((k << 1) | prev);
+    DAgg a;
+    a.f = wsum((uint32_t)__popc(k));
+    a.r = wsum((uint32_t)__popc(st));
+    a.k = wmax(k ? (uint32_t)b + 32u - (uint32_t)__clz(k) : 0u);
+    a.s = wmax(st ? (uint32_t)b + 32u - (uint32_t)__clz(st) : 0u);
+    return a;
+}
+// the lanes' results of a window: the nearest inclusive prefix (lane `near` first: lowest, or highest
+// when !low) ends the walk and everything from the window's start up to it is added in
+__device__ __forceinline__ bool dr_combine(DAgg a, bool isP, bool has, bool low, DAgg &acc) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t pm = __ballot(has && isP);
+    const bool take = has && (!pm || (low ? lane <= __ffsll((unsigned long long)pm) - 1 : lane >= 63 - __clzll(pm)));
+    acc.f += wsum(take ? a.f : 0u);
+    acc.r += wsum(take ? a.r : 0u);
+    acc.k = max(acc.k, wmax(take ? a.k : 0u));
+    acc.s = max(acc.s, wmax(take ? a.s : 0u));
+    return pm != 0;
+}
+__device__ __forceinline__ void st_u16(uint8_t *p, uint16_t v) { *(uint16_t *)p = v; }
+__device__ __forceinline__ void st_u32_2b(uint8_t *p, uint32_t v) {  // a 2-B aligned u32, as two halves
+    st_u16(p, (uint16_t)v);
+    st_u16(p + 2, (uint16_t)(v >> 16));
+}
+
+__global__ __launch_bounds__(kIT) void sp_drop1(const float *__restrict__ g, size_t n, size_t ntiles, float t,
+                                                const float *t_dev, bool vec, uint64_t *desc, uint32_t epoch,
+                                                uint32_t fb_polls, uint8_t *buf, uint64_t *host_tot,
+                                                uint64_t *nbytes_out) {
+    __shared__ uint32_t s_pre[4];
+    SP_CLOCK(sp_t0);
+    if (t_dev) t = *t_dev;
+    const size_t tile = blockIdx.x;
+    SP_CLOCK(sp_tk);
+    const uint32_t tagA = 2 * epoch, tagP = 2 * epoch + 1;
+    if (ntiles == 0) {  // an empty gradient: the total alone
+        if (threadIdx.x == 0) {
+            for (int q = 0; q < 4; q++) st_u16(buf + 2 * q, 0);
+            if (nbytes_out) *nbytes_out = 8;
+            else { host_tot[0] = 0; host_tot[1] = 0; }
+        }
+        return;
+    }
+    const size_t tile0 = tile * kTile;
+    float x[kIE], before = 0.0f;
+    if (vec && tile0 + kTile <= n) load_tile<true>(g, n, tile, x, before);
+    else load_tile<false>(g, n, tile, x, before);
+    const TileImg ti = build_image(tile, x, before, n, t);
+    SP_CLOCK(sp_ti);
+    const uint32_t tend = (uint32_t)min(tile0 + kTile, n);
+    const uint32_t lk = ti.F ? (uint32_t)tile0 + ti.last_kept1 : 0u;
+    const uint32_t lrs = ti.R ? (uint32_t)tile0 + ti.rs_last + 1u : 0u;
+    uint64_t *d = desc + 4 * tile;
+    uint64_t *gdesc = desc + 4 * ntiles;  // one descriptor per group of kDropGroup tiles, after the tiles'
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+        DAgg pre;
+        const uint32_t gi = (uint32_t)(tile / kDropGroup), pos = (uint32_t)(tile % kDropGroup);
+        const bool glast = pos == kDropGroup - 1;
+        // one look-back window: lane l reads descriptor j_l (if it has one); those that did not come are
+        // computed by the wave, one at a time (tile_agg_wave; a group from its tiles)
+        PollAcc pa0, pa1;  // (measurement build: lane 0's polls per level)
+        auto window = [&](uint32_t j, bool has, bool group) -> bool {
+            DAgg a;
+            const int st = has ? dr_poll((group ? gdesc : desc) + 4 * (size_t)j, tagA, tagP, fb_polls, a,
+                                         group ? pa1 : pa0) : 0;
+            bool isP = st == 2;
+            for (uint64_t m = __ballot(has && st == 0); m; m &= m - 1) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)j, l);
+                DAgg b;
+                bool bp = false;
+                if (!group) {
+                    b = tile_agg_wave(g, n, jl, t);
+                } else {  // the group's tiles, nearest inclusive prefix first (their descriptors, polled once)
+                    const uint32_t tj = jl * (uint32_t)kDropGroup + (uint32_t)lane;
+                    DAgg c;
+                    const int ct = dr_poll(desc + 4 * (size_t)tj, tagA, tagP, 1, c, pa1);
+                    for (uint64_t mm = __ballot(ct == 0); mm; mm &= mm - 1) {
+                        const int q = __ffsll((unsigned long long)mm) - 1;
+                        const DAgg e = tile_agg_wave(g, n, jl * (uint32_t)kDropGroup + (uint32_t)q, t);
+                        if (lane == q) c = e;
+                    }
+                    bp = dr_combine(c, ct == 2, true, false, b);
+                }
+                if (lane == l) { a = b; isP = bp; }
+            }
+            return dr_combine(a, isP, has, true, pre);
+        };
+        if (tile == 0) {
+            if (lane == 0) dr_publish(d, tagP, ti.F, ti.R, lk, lrs);
+        } else {
+            if (lane == 0) dr_publish(d, tagA, ti.F, ti.R, lk, lrs);
+            // level 0: the earlier tiles of the tile's own group, lane 0 the nearest
+            bool done = pos && window((uint32_t)tile - 1u - (uint32_t)lane, (uint32_t)lane < pos, false);
+#ifdef ONO_SP_STAMP
+            if (lane == 0 && tile < (1u << 16)) g_sp_stamp_d1b[tile].w = (unsigned)(__builtin_amdgcn_s_memrealtime() - sp_t0);
+#endif
+            // the group's aggregate, by its last tile, when no inclusive prefix came with it
+            if (!done && glast && lane == 0)
+                dr_publish(gdesc + 4 * (size_t)gi, tagA, pre.f + ti.F, pre.r + ti.R, max(pre.k, lk), max(pre.s, lrs));
+            // level 1: the earlier groups, 64 a window, lane 0 the nearest
+            for (int64_t hi = (int64_t)gi; !done && hi > 0; hi -= 64) {
+                const int64_t j = hi - 1 - lane;
+                done = window((uint32_t)(j >= 0 ? j : 0), j >= 0, true);
+            }
+#ifdef ONO_SP_STAMP
+            if (lane == 0 && tile < (1u << 16)) g_sp_stamp_d1c[tile] = make_uint4(pa0.polls, pa0.ticks, pa1.polls, pa1.ticks);
+#endif
+            if (lane == 0) {
+                dr_publish(d, tagP, pre.f + ti.F, pre.r + ti.R, max(pre.k, lk), max(pre.s, lrs));
+                if (glast) dr_publish(gdesc + 4 * (size_t)gi, tagP, pre.f + ti.F, pre.r + ti.R, max(pre.k, lk), max(pre.s, lrs));
+            }
+        }
+        if (lane == 0) {
+            s_pre[0] = pre.f;
+            s_pre[1] = pre.r;
+            s_pre[2] = pre.k;
+            s_pre[3] = pre.s;
+        }
+    }
+    __syncthreads();
+    SP_CLOCK(sp_tm);
+    const uint32_t F0 = s_pre[0], R0 = s_pre[1], LK0 = s_pre[2], LRS0 = s_pre[3];
+    const uint32_t nu16 = 4 * ti.R + ti.F;
+    uint8_t *dst = buf + 8 + 8 * (size_t)R0 + 2 * (size_t)F0;  // the tile's first unit
+    // the range's units with the cross-tile fields: the first run's offset (units hp0, + 1) completed
+    // from the last kept index before the tile; a last run still open at the tile's end (not the last
+    // tile) leaves its length units (hpl + 2, + 3) to the tile that ends it
+    const bool open_end = ti.R && ti.last_kept1 == tend - (uint32_t)tile0 && tile + 1 < ntiles;
+    const uint32_t off0 = ti.off0 + ((uint32_t)tile0 - LK0);
+    typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+    lds_cu16 *u16 = (lds_cu16 *)ti.stage;
+    auto unit = [&](uint32_t u, uint16_t &v) -> bool {
+        if (u >= nu16) return false;
+        if (ti.R && u == ti.hp0) { v = (uint16_t)off0; return true; }
+        if (ti.R && u == ti.hp0 + 1) { v = (uint16_t)(off0 >> 16); return true; }
+        if (open_end && (u == ti.hpl + 2 || u == ti.hpl + 3)) return false;
+        v = u16[u];
+        return true;
+    };
+    const uint32_t O = (uint32_t)(((uintptr_t)dst & 15u) >> 1);  // the range starts O units into a 16-B chunk
+    uint16_t *base16 = (uint16_t *)(dst - 2 * O);
+    const uint32_t nch = nu16 ? (O + nu16 + 7) / 8 : 0;
+    for (uint32_t c = threadIdx.x; c < nch; c += kIT) {
+        uint16_t v[8];
+        bool all = true, any = false;
+        bool ok[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int64_t u = (int64_t)c * 8 + i - O;
+            ok[i] = u >= 0 && unit((uint32_t)u, v[i]);
+            all &= ok[i];
+            any |= ok[i];
+        }
+        if (all) {
+            const u4v ov = {v[0] | (uint32_t)v[1] << 16, v[2] | (uint32_t)v[3] << 16, v[4] | (uint32_t)v[5] << 16,
+                            v[6] | (uint32_t)v[7] << 16};
+            __builtin_nontemporal_store(ov, (u4v *)(base16 + 8 * (size_t)c));
+        } else if (any) {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (ok[i]) base16[8 * (size_t)c + i] = v[i];
+        }
+    }
+    if (threadIdx.x == 0) {
+        // a run open at the tile's start (the value before it kept) ends here, at the first unkept value,
+        // or at n in the last tile: its length goes into its header, R0 - 1, whose values from its start s
+        // to this tile are all kept
+        if (tile0 > 0 && LK0 == (uint32_t)tile0 && LRS0 && (ti.first_unkept < (uint32_t)kTile || tile + 1 == ntiles)) {
+            const uint32_t s0 = LRS0 - 1u;
+            const uint32_t end = ti.first_unkept < (uint32_t)kTile && (uint32_t)tile0 + ti.first_unkept < tend
+                                     ? (uint32_t)tile0 + ti.first_unkept : (uint32_t)n;
+            const size_t hpos = 8 + 8 * (size_t)(R0 - 1) + 2 * (size_t)(F0 - ((uint32_t)tile0 - s0));
+            st_u32_2b(buf + hpos + 4, end - s0);
+        }
+        if (tile + 1 == ntiles) {  // the total (u64 LE, 2-B aligned buf) and the wire length
+            for (int q = 0; q < 4; q++) st_u16(buf + 2 * q, (uint16_t)((uint64_t)n >> (16 * q)));
+            const uint64_t F = F0 + ti.F, R = R0 + ti.R;
+            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;
+            else { host_tot[0] = F; host_tot[1] = R; }
+        }
+    }
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64 && tile < (1u << 16)) {
+        sp_stamp(g_sp_stamp_d1, tile, sp_t0, sp_tm);
+        if (threadIdx.x == 0) {
+            g_sp_stamp_d1b[tile].x = (unsigned)(sp_tk - sp_t0);
+            g_sp_stamp_d1b[tile].y = (unsigned)(sp_ti - sp_t0);
+            g_sp_stamp_d1b[tile].z = blockIdx.x;
+            if (tile == 0) g_sp_stamp_d1b[tile].w = (unsigned)(sp_ti - sp_t0);
+        }
+    }
+#endif
 }
 
 
@@ -2262,19 +2597,38 @@ struct Scratch {
     size_t agg_cap = 0;
     int parity = 0;
     uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
-    uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;
+    uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;  // [F, R, the completion tag, spare]
+    // the one-launch form (sp_drop1): 4 granules per tile and per group of tiles (zeroed when
+    // allocated, and when the epoch wraps), the call's epoch
+    uint64_t *desc = nullptr;
+    size_t desc_cap = 0;
+    uint32_t depoch = 0;
 };
 std::mutex g_scratch_mu;
 std::map<std::pair<int, hipStream_t>, Scratch> g_scratch;
 
-int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out) {
+int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = true) {
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
     Scratch &sc = g_scratch[{dev, stream}];
     if (!sc.host_tot) {
-        ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 3 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        ONO_HIP(hipHostMalloc((void **)&sc.host_tot, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
+        sc.host_tot[3] = 0;
+    }
+    if (!image) {  // sp_drop1's granules instead of the slot image
+        const size_t want = std::max<size_t>(ntiles + (ntiles + kDropGroup - 1) / kDropGroup, 1);  // tiles, groups
+        if (want > sc.desc_cap) {
+            (void)hipFree(sc.desc);
+            sc.desc = nullptr;
+            sc.desc_cap = 0;
+            ONO_HIP(hipMalloc((void **)&sc.desc, 4 * want * sizeof(uint64_t)));
+            ONO_HIP(hipMemsetAsync(sc.desc, 0, 4 * want * sizeof(uint64_t), stream));
+            sc.desc_cap = want;
+        }
+        *out = &sc;
+        return ONO_OK;
     }
     if (ntiles > sc.tiles_cap) {
         (void)hipFree(sc.rec);
@@ -2719,6 +3073,34 @@ namespace {
 constexpr size_t kImageTpw = 4;
 static_assert(kRecChunk % kImageTpw == 0, "a workgroup's tiles share one chunk aggregate");
 
+// ONO_DROP_FUSED=0 keeps the two launches (sp_image + sp_move): measurement, A/B
+bool drop_fused() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_DROP_FUSED");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
+}
+// ONO_DROP_FALLBACK_POLLS: sp_drop1's polls before its fallback (tests set 0: every descriptor not
+// there at the first read is computed by the waiting wave)
+uint32_t drop_fallback_polls() {
+    static const uint32_t v = [] {
+        const char *e = getenv("ONO_DROP_FALLBACK_POLLS");
+        return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : kDropFallbackPolls;
+    }();
+    return v;
+}
+
+// the largest gradient (in tiles) the one launch takes; above it the two launches (measured by
+// tools/drop_sizes.py; ONO_DROP_ONE_LAUNCH_TILES overrides)
+size_t drop_one_launch_tiles() {
+    static const size_t v = [] {
+        const char *e = getenv("ONO_DROP_ONE_LAUNCH_TILES");
+        return e && *e ? (size_t)strtoull(e, nullptr, 10) : kDropOneLaunchTiles;
+    }();
+    return v;
+}
+
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s, const float *t_dev = nullptr) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
@@ -2726,6 +3108,31 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
     std::lock_guard<std::mutex> lk(g_scratch_mu);  // the host side of one call at a time
     Scratch *sc = nullptr;
+    // the one-launch form when the buffer holds the worst case (it writes as it goes) and the stream is
+    // not being captured (a replayed graph would repeat the epoch: the last replay's descriptors would
+    // read as this one's)
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cap_st) == hipSuccess && cap_st != hipStreamCaptureStatusNone;
+    if (drop_fused() && worst_case_fits && !capturing && ntiles <= drop_one_launch_tiles()) {
+        int rc = scratch_for(ntiles, s, &sc, false);
+        if (rc) return rc;
+        if (++sc->depoch == 0 || sc->depoch >= 0x7FFFFFFFu) {  // tags 2 e, 2 e + 1 stay nonzero and distinct
+            ONO_HIP(hipMemsetAsync(sc->desc, 0, 4 * sc->desc_cap * sizeof(uint64_t), s));
+            sc->depoch = 1;
+        }
+        const uint32_t grid = (uint32_t)std::max<size_t>(ntiles, 1);
+        hipLaunchKernelGGL(sp_drop1, dim3(grid), dim3(kIT), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->desc,
+                           sc->depoch, drop_fallback_polls(), buf, sc->host_tot_dev, nbytes_dev);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
+        if (nbytes_dev) return ONO_OK;
+        volatile uint64_t *tot = sc->host_tot;
+        if (++sc->calls == 0) sc->calls = 1;
+        e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
+        if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
+        *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
+        return ONO_OK;
+    }
     int rc = scratch_for(ntiles, s, &sc);
     if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;

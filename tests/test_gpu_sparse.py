@@ -495,3 +495,64 @@ def test_lift_dev_range_modes(offs, lens, tail):
     assert _lift_into(to_dev(b), out, total + 64) == total
     assert_bitexact(out[:total].cpu().numpy(), want)
     assert torch.all(out[total:] == 3.0)
+
+
+_ONE_LAUNCH_CHILD = r"""
+import sys
+sys.path[:0] = {paths!r}
+import numpy as np, torch
+from ono_amd import sparse as SP
+from oracle import oracle as O
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+cases = []
+if {small!r}:
+    g = O.synth(300_001, 5, 1); cases.append((g, float(np.quantile(np.abs(g), 0.9))))
+    n = 64 * 2048 * 3 + 77                 # > 3 look-back groups, ragged
+    g = np.zeros(n, np.float32)
+    g[10:70_000] = 1.0                     # a run over 34 tiles and into the second group
+    g[131_071:131_074] = -2.0              # one across the first group edge
+    for k in range(1, n // 2048, 5):
+        g[2048 * k - 2:2048 * k + 1] = 3.0  # runs across tile edges
+    g[-1] = 4.0
+    cases.append((g, 0.5))
+    cases.append((np.full(5 * 2048, 2.0, np.float32), 1.0))   # all kept
+    cases.append((np.zeros(9 * 2048 + 3, np.float32), 1.0))   # none kept
+else:  # more than 64 groups: several level-1 windows; runs and gaps across many tiles and groups
+    n = 20_000_003
+    g = np.zeros(n, np.float32)
+    for i in (0, 5, 2047, 2048, 4_000_000, 8_388_607, 8_388_608, 16_777_215, 16_777_216, n - 1):
+        g[i] = 1.5
+    g[10_000:300_000] = -2.0
+    g[16_770_000:16_790_000] = 3.0
+    cases.append((g, 0.5))
+    g = O.synth(9_000_001, 7, 1); cases.append((g, float(np.quantile(np.abs(g), 0.9))))
+for g, t in cases:
+    got = SP.grad_drop_dev(dev(g), t)
+    assert bytes(got.cpu().numpy()) == O.grad_drop(g, t), (len(g), t)
+print("ok", len(cases))
+"""
+
+
+@pytest.mark.parametrize("polls,small", [("0", True), ("1", True), ("96", False)],
+                         ids=["fallback_always", "fallback_after_one_poll", "large_one_launch"])
+def test_drop_one_launch_matches_oracle(polls, small):
+    """sp_drop1 forced for every size (ONO_DROP_ONE_LAUNCH_TILES): its decoupled
+    fallback (ONO_DROP_FALLBACK_POLLS=0: every look-back descriptor not there at
+    the first read is computed by the waiting wave from the gradient itself, a
+    group's from its tiles) and, at 20 M values, look-backs over more than 64
+    groups: the same bytes as the oracle over runs across tile and group edges,
+    all and none kept."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    paths = [root, os.path.join(root, "oxidized-neural-orchestra_amd")]
+    env = dict(os.environ, ONO_DROP_FALLBACK_POLLS=polls, ONO_DROP_ONE_LAUNCH_TILES="1000000000")
+    r = subprocess.run([sys.executable, "-c", _ONE_LAUNCH_CHILD.format(paths=paths, small=small)], capture_output=True,
+                       text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == "ok %d" % (4 if small else 2)

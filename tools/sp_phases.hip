@@ -15,6 +15,7 @@
 #define ONO_SP_STAMP 1
 #include "../oxidized-neural-orchestra_amd/csrc/ono_sparse.hip"
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 
@@ -124,6 +125,65 @@ int main(int argc, char **argv) {
            mib, K, NG, kImageTpw, per, (unsigned long long)wire, bytes / per * 1e-3,
            bytes / per * 1e-3 / 8000.0);
     const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + kImageTpw - 1) / kImageTpw;
+    if (drop_fused()) {  // the one-launch encoder: per tile {start, look-back done, end} + ticket and image times
+        std::vector<uint4> d1(ntiles), d1b(ntiles);
+        CK(hipMemcpyFromSymbol(d1.data(), HIP_SYMBOL(g_sp_stamp_d1), ntiles * sizeof(uint4)));
+        CK(hipMemcpyFromSymbol(d1b.data(), HIP_SYMBOL(g_sp_stamp_d1b), ntiles * sizeof(uint4)));
+        uint32_t b = d1[0].x;
+        for (const uint4 &v : d1) b = (int32_t)(v.x - b) < 0 ? v.x : b;
+        printf("# times in us from sp_drop1's first workgroup start (the last drop; mid: look-back done)\n");
+        report("sp_drop1", d1, b);
+        std::vector<double> tk, img, lb, wr, dist;
+        for (size_t i = 0; i < ntiles; i++) {
+            tk.push_back(d1b[i].x * 0.01);
+            img.push_back((d1b[i].y - d1b[i].x) * 0.01);
+            lb.push_back(((double)d1[i].y - d1b[i].y) * 0.01);
+            wr.push_back(((double)d1[i].z - d1[i].y) * 0.01);
+            dist.push_back(std::fabs((double)d1b[i].z - (double)i));
+        }
+        printf("sp_drop1 ticket p50 %.2f p90 %.2f max %.2f | image p50 %.2f p90 %.2f max %.2f | look-back p50 %.2f p90 "
+               "%.2f max %.2f | write p50 %.2f p90 %.2f max %.2f | |block - ticket| p50 %.0f max %.0f\n",
+               pct(tk, .5), pct(tk, .9), pct(tk, 1), pct(img, .5), pct(img, .9), pct(img, 1), pct(lb, .5), pct(lb, .9),
+               pct(lb, 1), pct(wr, .5), pct(wr, .9), pct(wr, 1), pct(dist, .5), pct(dist, 1));
+        std::vector<double> l0, l1;
+        for (size_t i = 1; i < ntiles; i++) {
+            l0.push_back(((double)d1b[i].w - d1b[i].y) * 0.01);
+            l1.push_back(((double)d1[i].y - d1b[i].w) * 0.01);
+        }
+        printf("sp_drop1 own-group look-back p50 %.2f p90 %.2f max %.2f | earlier groups p50 %.2f p90 %.2f max %.2f\n",
+               pct(l0, .5), pct(l0, .9), pct(l0, 1), pct(l1, .5), pct(l1, .9), pct(l1, 1));
+        {
+            std::vector<uint4> d1c(ntiles);
+            CK(hipMemcpyFromSymbol(d1c.data(), HIP_SYMBOL(g_sp_stamp_d1c), ntiles * sizeof(uint4)));
+            std::vector<double> p0, p1, lat;
+            for (size_t i = 1; i < ntiles; i++) {
+                p0.push_back(d1c[i].x);
+                p1.push_back(d1c[i].z);
+                if (d1c[i].x + d1c[i].z) lat.push_back((d1c[i].y + d1c[i].w) * 0.01 / (d1c[i].x + d1c[i].z));
+            }
+            printf("sp_drop1 lane-0 polls own group p50 %.0f p90 %.0f max %.0f | earlier groups p50 %.0f p90 %.0f max %.0f | "
+                   "per-poll load time p10 %.2f p50 %.2f p90 %.2f max %.2f us\n",
+                   pct(p0, .5), pct(p0, .9), pct(p0, 1), pct(p1, .5), pct(p1, .9), pct(p1, 1), pct(lat, .1), pct(lat, .5),
+                   pct(lat, .9), pct(lat, 1));
+        }
+        printf("sp_drop1 tile: start/imaged/own-group/done/end (us)");
+        for (size_t i : {(size_t)0, (size_t)1, (size_t)63, (size_t)64, (size_t)127, (size_t)448, (size_t)511, (size_t)512,
+                         (size_t)575, (size_t)1023, (size_t)1024, (size_t)2047, (size_t)2048, (size_t)4095, (size_t)4096}) {
+            if (i >= ntiles) continue;
+            const double st = (double)(uint32_t)(d1[i].x - b) * 0.01;
+            printf(" %zu:%.1f/%.1f/%.1f/%.1f/%.1f", i, st, st + d1b[i].y * 0.01, st + d1b[i].w * 0.01, st + d1[i].y * 0.01,
+                   st + d1[i].z * 0.01);
+        }
+        printf("\n");
+        // the time line by tile index: start and end of every 512th tile
+        printf("sp_drop1 tile:start/lookback/end");
+        for (size_t i = 0; i < ntiles; i += std::max<size_t>(1, ntiles / 16))
+            printf(" %zu:%.1f/%.1f/%.1f", i, (double)(uint32_t)(d1[i].x - b) * 0.01,
+                   (double)(uint32_t)(d1[i].x - b) * 0.01 + d1[i].y * 0.01,
+                   (double)(uint32_t)(d1[i].x - b) * 0.01 + d1[i].z * 0.01);
+        printf("\n");
+        return 0;
+    }
     std::vector<uint4> si(nwg), sm(ntiles);
     CK(hipMemcpyFromSymbol(si.data(), HIP_SYMBOL(g_sp_stamp_img), nwg * sizeof(uint4)));
     CK(hipMemcpyFromSymbol(sm.data(), HIP_SYMBOL(g_sp_stamp_mov), ntiles * sizeof(uint4)));
