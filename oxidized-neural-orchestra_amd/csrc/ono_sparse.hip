@@ -328,11 +328,13 @@ __device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE
         uint32_t w[kIE / 2];
 #pragma unroll
         for (int q = 0; q < kIE / 2; q++) w[q] = to_f16_sp(x[2 * q]) | (uint32_t)to_f16_sp(x[2 * q + 1]) << 16;
-        uint4 *v4 = (uint4 *)(vals + lo / 2);
+        // transposed: the thread's word q at q kIT + thread, so that the lanes' reads below, each of some
+        // value of its own, fall in distinct banks whatever the values (a thread's 32 contiguous bytes
+        // put lanes 4 apart on one bank: up to 8-way conflicts on every read, and 2-way on the writes)
 #pragma unroll
-        for (int q = 0; q < kIE / 8; q++) v4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        for (int q = 0; q < kIE / 2; q++) vals[q * kIT + threadIdx.x] = w[q];
         typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
-        lds_cu16 *v16 = (lds_cu16 *)vals;  // (an LDS read: a generic pointer would be a flat load)
+        lds_cu16 *v16 = (lds_cu16 *)vals + 2 * threadIdx.x;  // (an LDS read: a generic pointer would be a flat load)
         uint32_t pos = 4 * ts.es + ts.ef;  // the next value's unit, before a header of its own
         uint32_t sl = ts.es, last = ts.kept1_before, hp = 0, rs = 0, hsl = 0;
         bool open = false;  // a run started in this thread, its length not written yet
@@ -356,7 +358,7 @@ __device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE
                 if (hsl == R - 1) rb[2] = i;
                 open = true;
             }
-            vst[pos++] = v16[i];
+            vst[pos++] = v16[2 * kIT * (e >> 1) + (e & 1)];
             last = i + 1;
         }
         if (open) {  // the first unkept after the run: in the thread, else after it (tile-local)
@@ -1646,13 +1648,32 @@ static_assert(kPatHalo >= 4 + kShortP, "short runs of the tile's records are sta
 struct Units12 {
     uint32_t w[6];
     __device__ __forceinline__ uint32_t u(int i) const { return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu; }
+    // unit i (< 12) for a lane-varying i: selects, not an indexed register array (that would be scratch)
+    __device__ __forceinline__ uint32_t sel(uint32_t i) const {
+        uint32_t x = w[0];
+#pragma unroll
+        for (int q = 1; q < 6; q++) {
+            uint32_t y = w[q];
+            asm volatile("" : "+v"(y));  // (else the chain is folded back into a scratch array load)
+            x = (i >> 1) == (uint32_t)q ? y : x;
+        }
+        return (x >> ((i & 1) * 16)) & 0xFFFFu;
+    }
 };
+// (every lane of the wave active) the 4 units after the thread's 8 are the next lane's first 4, taken
+// by a lane shift; only lane 63 reads them from LDS — an 8-B read per lane at a 16-B stride put two
+// lanes on every bank
 __device__ __forceinline__ Units12 units12(const uint4 *lw4) {
     Units12 r;
     const uint4 a = lw4[threadIdx.x];
-    const uint2 c = ((const uint2 *)lw4)[2 * threadIdx.x + 2];
+    uint32_t c0 = (uint32_t)__shfl_down((int)a.x, 1, 64), c1 = (uint32_t)__shfl_down((int)a.y, 1, 64);
+    if ((threadIdx.x & 63) == 63) {
+        const uint2 c = ((const uint2 *)lw4)[2 * threadIdx.x + 2];
+        c0 = c.x;
+        c1 = c.y;
+    }
     r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
-    r.w[4] = c.x; r.w[5] = c.y;
+    r.w[4] = c0; r.w[5] = c1;
     return r;
 }
 // Candidate mask of the thread's units (k = base + 8 t + j, a header needs k + 4 <= M) and the sum of
@@ -2126,8 +2147,8 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     uint32_t ec, es, tc, ts;
     block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);  // (its sync: the zeros)
     uint32_t cur = (uint32_t)E0 + es;  // where the run before the thread's first record ended
-    for (uint32_t mm = m; mm; mm &= mm - 1) {
-        const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+    for (uint32_t mm = m; mm; mm &= mm - 1) {  // (the thread's own units from registers: pl_fused's loop)
+        const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = U.sel(e), len = U.sel(e + 2);
         const uint32_t gi = cur + off;
         // (overflow-free: in a refuted stream cur + off may wrap; then gi < ea or it lies past eb)
         if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
@@ -2136,7 +2157,7 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
         uint16_t *d = img + (gi - ia);
         if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
-            for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
+            for (uint32_t i = 0; i < len; i++) d[i] = e + 4 + i < 12u ? (uint16_t)U.sel(e + 4 + i) : lw[k + 4 + i];
         } else {
             const uint32_t q = atomicAdd(&lqn, 1u);
             const uint32_t vp = 8 + 2 * (base + k + 4);
@@ -2388,7 +2409,6 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         if (t >= T32) continue;  // (uniform)
         pat_stage_write(lw4[q], v[q], n16[q]);
         __syncthreads();
-        const uint16_t *lw = (const uint16_t *)lw4[q];
         const Units12 U = units12(lw4[q]);
         uint32_t sum, ec;
         m[q] = base + j0 < M32 ? pat_mask(U, base + j0, M, sum) : (sum = 0, 0u);
@@ -2400,8 +2420,8 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         bool bad = false;
         uint32_t rank = ec;
         for (uint32_t mm = m[q]; mm; mm &= mm - 1, rank++) {
-            const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm);
-            const uint32_t nx = k + 4 + lw[k + 2];  // tile-local successor
+            const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e;
+            const uint32_t nx = k + 4 + U.sel(e + 2);  // tile-local successor
             if (base + nx > M32) { bad = true; break; }  // the run overruns the stream
             if (nx < (uint32_t)kPatU && base + nx < M32) {
                 const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
@@ -2481,10 +2501,12 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
             const uint16_t *lw = (const uint16_t *)lw4[q];
             for (uint32_t i = threadIdx.x; i < (n + 7) / 8; i += kPatT) img16[i] = make_uint4(0u, 0u, 0u, 0u);
             if (threadIdx.x == 0) lqn = 0;
+            const Units12 U = units12(lw4[q]);  // (the thread's units from registers below: lanes 16 B apart
+                                                // reading their own units from LDS hit one bank 4 at a time)
             __syncthreads();
             uint32_t cur = (uint32_t)E0 + es[q];  // where the run before the thread's first record ended
             for (uint32_t mm = m[q]; mm; mm &= mm - 1) {
-                const uint32_t k = j0 + (uint32_t)__builtin_ctz(mm), off = lw[k], len = lw[k + 2];
+                const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = U.sel(e), len = U.sel(e + 2);
                 const uint32_t gi = cur + off;
                 if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
                     raise_bad(badw, epoch);  // only a refuted stream
@@ -2492,7 +2514,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
                 }
                 uint16_t *d = img + (gi - ia);
                 if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
-                    for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
+                    for (uint32_t i = 0; i < len; i++) d[i] = e + 4 + i < 12u ? (uint16_t)U.sel(e + 4 + i) : lw[k + 4 + i];
                 } else {
                     const uint32_t qq = atomicAdd(&lqn, 1u);
                     const uint32_t vp = 8 + 2 * (base + k + 4);

@@ -80,3 +80,14 @@ if KL:  # stream-ordered lifts back to back (ono_sparse_lift_dev_async): the dev
     print(f"lift_dev {ev0.elapsed_time(ev1) / KL * 1e3:.1f} us per stream-ordered lift, back to back "
           f"(refused: {int(st.item()) in tks})")
 print("lift fallbacks", L.ono_sparse_lift_fallbacks(), "wire", wire.numel())
+# the config-1 chunk (54,693 values, 27 tiles: the one-launch encoder sp_drop1) K times, stream-ordered
+gc = ono_amd.kernels.synth(torch.empty(54_693, dtype=torch.float32, device="cuda"), 99, 7)
+tc = float(torch.quantile(gc.abs().float(), 0.9).item())
+bc = torch.empty(L.ono_sparse_max_bytes(gc.numel()), dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+ev0.record()
+for _ in range(K):
+    ono_amd.sparse.grad_drop_async(gc, tc, bc, nbd)
+ev1.record()
+torch.cuda.synchronize()
+print(f"drop (config-1 chunk) {ev0.elapsed_time(ev1) / K * 1e3:.1f} us per stream-ordered drop")
