@@ -3000,18 +3000,19 @@ int lift_device(float *g, size_t cap, size_t *out_len, const uint8_t *dbuf, cons
 // the sample is drawn: sp_gather_keys spreads the m random reads g[idx[i]]
 // over many workgroups (one CU alone took 9-18 us for them) and leaves the
 // keys where the indices were; sp_threshold then selects in one workgroup of
-// eight waves, 32 keys per lane in registers, one bit per step from the top:
-// each lane counts its keys that share the prefix found so far and have a 0 in
-// this bit (plain VALU compares), the wave sums the lanes' 6-bit counts with
-// one ballot per count bit (a ballot per key slot cost ~47 cycles each: the
-// VALU-to-SALU hand-off), the eight waves' sums meet in LDS, and the bit is
-// chosen by comparing with the rank still sought.  (Round 4's form, LDS-atomic
-// histograms in 1024 threads, spent ~60 us in contended bins: the exponent
-// byte of N(0, s) gradients puts most keys in a few of them.)
+// eight waves, 32 keys per lane in registers, two bits per step from the top (round 5, bit-sliced): a
+// lane's 32 keys are transposed into 32 bit planes (bit 31 - q of plane p = bit p of key q), so one step is four AND / popcount pairs on the lane's
+// candidate mask for the whole 32 keys instead of 32 compares per bit; the counts of the digits
+// 00 / 01 / 10 among the candidates are summed by two DPP reductions per wave (two counts packed in
+// 16-bit halves) and across the eight waves in LDS, and the digit chosen by the rank still sought:
+// 16 steps of a few hundred cycles.  (The compare-per-key form was VALU-bound on its one CU — 16384
+// keys x 3 ops x 31 bits — at 20.5 us per call, the TCP ring's largest codec kernel.)  (Round 4's
+// form, LDS-atomic histograms in 1024 threads, spent ~60 us in contended bins: the exponent byte of
+// N(0, s) gradients puts most keys in a few of them.)
 constexpr int kThrT = 512;
 constexpr uint32_t kSampleMax = 16384;  // SAMPLE_SIZE, protocol.rs:13-19
 constexpr int kThrK = (int)kSampleMax / kThrT;
-static_assert(kThrK < 64, "a lane's count fits the six ballots");
+static_assert(kThrK == 32, "a lane's keys are one 32 x 32 bit matrix");
 constexpr int kGatherT = 256;
 __device__ __forceinline__ uint32_t abs_key(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7FFFFFFFu; }
 // idx: device memory, or the caller's pinned host buffer read in place (no copy engine in between)
@@ -3020,37 +3021,70 @@ __global__ __launch_bounds__(kGatherT) void sp_gather_keys(const float *g, const
     const uint32_t i = blockIdx.x * kGatherT + threadIdx.x;
     if (i < m) keys[i] = abs_key(g[idx[i]]);
 }
+// 32 x 32 bit transpose in registers (Hacker's Delight 7-3): afterwards bit 31 - c of A[r] is bit 31 - r
+// of the former A[c]
+__device__ __forceinline__ void transpose32(uint32_t (&A)[32]) {
+    uint32_t m = 0x0000FFFFu;
+#pragma unroll
+    for (int j = 16; j != 0; j >>= 1, m ^= (m << j)) {
+#pragma unroll
+        for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+            const uint32_t t = (A[k] ^ (A[k + j] >> j)) & m;
+            A[k] ^= t;
+            A[k + j] ^= t << j;
+        }
+    }
+}
 // keys: the gathered keys, or NULL: the sample is g[0, m) itself
 __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, const float *g, uint32_t m, uint32_t k,
                                                       float *t_out) {
-    __shared__ uint32_t wcount[2][kThrT / 64];
+    __shared__ uint32_t wc[2][kThrT / 64][2];
     const int wave = threadIdx.x / 64;
-    uint32_t key[kThrK];
+    uint32_t A[32], C = 0;  // keys, then planes (plane p = A[31 - p]); candidates: bit 31 - q for key q
 #pragma unroll
-    for (int q = 0; q < kThrK; q++) {  // padding slots get bit 31, which no prefix has
+    for (int q = 0; q < kThrK; q++) {
         const uint32_t i = threadIdx.x + (uint32_t)q * kThrT;
-        key[q] = i < m ? (keys ? keys[i] : abs_key(g[i])) : 0xFFFFFFFFu;
+        A[q] = i < m ? (keys ? keys[i] : abs_key(g[i])) : 0u;
+        C |= i < m ? 1u << (31 - q) : 0u;
     }
-    uint32_t prefix = 0, mask = 0x80000000u, kk = k;
-    for (int b = 30; b >= 0; b--) {
-        const uint32_t bit = 1u << b, mb = mask | bit;
-        uint32_t cl = 0;  // this lane's count, <= kThrK: 6 bits
+    transpose32(A);
+    uint32_t prefix = 0, kk = k;
+    // bits 30..1 two at a time (bit 31 is clear in every key), then bit 0
 #pragma unroll
-        for (int q = 0; q < kThrK; q++) cl += (key[q] & mb) == prefix ? 1u : 0u;
-        uint32_t c = 0;
-#pragma unroll
-        for (int v = 0; v < 6; v++) c += (uint32_t)__popcll(__ballot((cl >> v) & 1u)) << v;
-        const int par = b & 1;  // two count arrays: the next step's writes never meet this step's reads
-        if ((threadIdx.x & 63) == 0) wcount[par][wave] = c;
-        __syncthreads();
-        uint32_t zeros = 0;
-#pragma unroll
-        for (int w = 0; w < kThrT / 64; w++) zeros += wcount[par][w];
-        if (kk >= zeros) {  // the sought key has a 1 here
-            kk -= zeros;
-            prefix |= bit;
+    for (int s = 0; s < 16; s++) {
+        const int hi = 30 - 2 * s, lo = hi - 1;  // s == 15: hi = 0, lo = -1 (one bit)
+        const uint32_t P1 = A[31 - hi], P0 = lo >= 0 ? A[31 - lo] : 0u;
+        const uint32_t c0 = C & ~P1;
+        const uint32_t x = (uint32_t)__popc(c0 & ~P0) | (uint32_t)__popc(c0 & P0) << 16;
+        const uint32_t y = (uint32_t)__popc(C & P1 & ~P0);
+        const uint32_t X = wsum(x), Y = lo >= 0 ? wsum(y) : 0u;
+        const int par = s & 1;  // two count arrays: the next step's writes never meet this step's reads
+        if ((threadIdx.x & 63) == 0) {
+            wc[par][wave][0] = X;
+            wc[par][wave][1] = Y;
         }
-        mask = mb;
+        __syncthreads();
+        uint32_t sx = 0, sy = 0;
+#pragma unroll
+        for (int w = 0; w < kThrT / 64; w++) {
+            sx += wc[par][w][0];
+            sy += wc[par][w][1];
+        }
+        const uint32_t n00 = sx & 0xFFFFu, n01 = sx >> 16, n10 = sy;
+        uint32_t d;
+        if (lo < 0) {  // one bit: n00 = candidates with a 0 there
+            d = kk < n00 ? 0u : 1u;
+            if (d) kk -= n00;
+            C &= d ? P1 : ~P1;
+            prefix |= d;
+        } else {
+            if (kk < n00) d = 0;
+            else if (kk < n00 + n01) { d = 1; kk -= n00; }
+            else if (kk < n00 + n01 + n10) { d = 2; kk -= n00 + n01; }
+            else { d = 3; kk -= n00 + n01 + n10; }
+            C &= (d & 2 ? P1 : ~P1) & (d & 1 ? P0 : ~P0);
+            prefix |= d << lo;
+        }
     }
     if (threadIdx.x == 0) {
         const float mp = 6.103515625e-05f;  // f16::MIN_POSITIVE

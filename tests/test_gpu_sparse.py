@@ -392,6 +392,48 @@ def test_threshold_drawn_sample_vs_oracle(n, r):
     assert np.float32(got).view(np.uint32) == np.float32(O.sparse_threshold_sample(x, r, idx)).view(np.uint32)
 
 
+@pytest.mark.parametrize("kind", ["all_equal", "two_values", "all_nan", "denormals", "every_rank", "wide_exponents",
+                                  "one_bit_apart"])
+def test_threshold_adversarial_samples(kind):
+    """The bit-sliced select (two key bits per step over transposed bit
+    planes) against the restated calculate_threshold on samples that stress
+    each digit path: all keys equal (every step keeps all candidates), two
+    values, all NaN, denormals (the high bits all zero), every rank of one
+    sample, keys spread over every exponent, keys one ulp apart."""
+    rng = np.random.default_rng(5)
+    n = 16384
+    if kind == "all_equal":
+        xs = [np.full(n, 0.3, np.float32), np.full(777, -2.5, np.float32)]
+    elif kind == "two_values":
+        xs = [np.where(rng.random(n) < 0.37, 1.0, 2.0).astype(np.float32)]
+    elif kind == "all_nan":
+        x = np.empty(n, np.float32)
+        x.view(np.uint32)[:] = 0x7FC00000 | rng.integers(0, 1 << 22, n).astype(np.uint32)
+        xs = [x]
+    elif kind == "denormals":
+        x = np.empty(n, np.float32)
+        x.view(np.uint32)[:] = rng.integers(0, 1 << 23, n).astype(np.uint32)
+        xs = [x]
+    elif kind == "wide_exponents":
+        x = np.empty(n, np.float32)
+        x.view(np.uint32)[:] = rng.integers(0, 0x7F800000, n).astype(np.uint32) | (rng.integers(0, 2, n) << 31).astype(np.uint32)
+        xs = [x]
+    elif kind == "one_bit_apart":
+        base = np.uint32(0x3F800000)
+        x = np.empty(n, np.float32)
+        x.view(np.uint32)[:] = base + rng.integers(0, 4, n).astype(np.uint32)
+        xs = [x]
+    else:  # every rank: r from 0 to 1 in fine steps over one sample of 513 values (a partial last lane column)
+        xs = [O.synth(513, SEED + 3, 0)]
+    rs = [0.001, 0.1, 0.5, 0.9, 1.0] if kind != "every_rank" else [i / 512 for i in range(1, 513)]
+    for x in xs:
+        xd = torch.from_numpy(x).cuda()
+        for r in rs:
+            got = SP.threshold(xd, r)
+            want = O.sparse_threshold_sample(x, r)
+            assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32), (kind, len(x), r, got, want)
+
+
 def test_threshold_argument_errors():
     g = torch.zeros(20000, device="cuda")
     with pytest.raises(ono_amd.InvalidArgument):
