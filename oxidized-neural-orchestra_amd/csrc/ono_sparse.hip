@@ -1645,6 +1645,19 @@ static_assert(kPatPer == 8, "a thread's 8 units and the 4 after them are one 16-
 static_assert(kPatHalo >= 4 + kShortP, "short runs of the tile's records are staged whole");
 
 // A thread's units and the 4 after them from the staged tile.
+// the 4 units after a thread's 8: the next lane's by a lane shift (1: no 2-way conflicts of the 8-B
+// read, measured no faster: 23.9-24.1 vs 23.7 us per lift, profiles/r05_s45_lift_ab.txt) or LDS (0)
+#ifndef ONO_UNITS12_SHFL
+#define ONO_UNITS12_SHFL 0
+#endif
+// The pattern lift's records read their units from LDS (a 16-B lane stride: 4-way bank conflicts, ~1.1
+// conflict cycles per LDS instruction) — not from the registers units12 already holds, selected per lane
+// (`Units12::sel`; 0.17 conflict cycles per instruction, but 25.9 vs 24.1 us per 64 MiB lift: the
+// selects' VALU cost more than the conflicts, profiles/r05_s44_lift_ab.txt); 1 builds that form.
+#ifndef ONO_PL_UNITS_REG
+#define ONO_PL_UNITS_REG 0
+#endif
+__device__ __forceinline__ const uint16_t *lw4u16(const uint4 *p) { return (const uint16_t *)p; }
 struct Units12 {
     uint32_t w[6];
     __device__ __forceinline__ uint32_t u(int i) const { return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu; }
@@ -1666,8 +1679,13 @@ struct Units12 {
 __device__ __forceinline__ Units12 units12(const uint4 *lw4) {
     Units12 r;
     const uint4 a = lw4[threadIdx.x];
+#if ONO_UNITS12_SHFL
     uint32_t c0 = (uint32_t)__shfl_down((int)a.x, 1, 64), c1 = (uint32_t)__shfl_down((int)a.y, 1, 64);
     if ((threadIdx.x & 63) == 63) {
+#else
+    uint32_t c0 = 0, c1 = 0;
+    {
+#endif
         const uint2 c = ((const uint2 *)lw4)[2 * threadIdx.x + 2];
         c0 = c.x;
         c1 = c.y;
@@ -2147,8 +2165,12 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
     uint32_t ec, es, tc, ts;
     block_scan2<kPatT>((uint32_t)__builtin_popcount(m), sum, ec, es, tc, ts);  // (its sync: the zeros)
     uint32_t cur = (uint32_t)E0 + es;  // where the run before the thread's first record ended
-    for (uint32_t mm = m; mm; mm &= mm - 1) {  // (the thread's own units from registers: pl_fused's loop)
+    for (uint32_t mm = m; mm; mm &= mm - 1) {
+#if ONO_PL_UNITS_REG
         const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = U.sel(e), len = U.sel(e + 2);
+#else
+        const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = lw[k], len = lw[k + 2];
+#endif
         const uint32_t gi = cur + off;
         // (overflow-free: in a refuted stream cur + off may wrap; then gi < ea or it lies past eb)
         if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
@@ -2157,7 +2179,11 @@ __global__ __launch_bounds__(kPatT) void pl_place(float *g, const uint8_t *b, si
         }
         uint16_t *d = img + (gi - ia);
         if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
+#if ONO_PL_UNITS_REG
             for (uint32_t i = 0; i < len; i++) d[i] = e + 4 + i < 12u ? (uint16_t)U.sel(e + 4 + i) : lw[k + 4 + i];
+#else
+            for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
+#endif
         } else {
             const uint32_t q = atomicAdd(&lqn, 1u);
             const uint32_t vp = 8 + 2 * (base + k + 4);
@@ -2247,19 +2273,52 @@ constexpr int kPollSleep = ONO_POLL_SLEEP;
 // slots and the count moves on; a kernel of another stream or process that holds CU slots for long then
 // costs ~100 us and a refusal (the caller's blocking lift does the work), not the ~10 ms poll limit and
 // a wait for that kernel.
+// The count is sharded (round 5): workgroup b adds to line b % 64, and the last of a line's workgroups
+// to arrive resets it and adds one to the top word, which the look-back reads — one word taking every
+// workgroup's add serialised them at ~88 per us (the guide's dequeue row): 1256 workgroups, +14 us
+// before the last could start its look-back (the 64 MiB lift 22.9 -> 36.8 us per call,
+// profiles/r05_mid_sp_phases.txt; sharded 23.9-24.1 us, profiles/r05_s45_lift_ab.txt; the add's value
+// used only after the first tile is indexed 23.6-23.9 us against round 4's 22.7-23.2 on the same box,
+// r05_s48).  (No-return adds summed by the check instead: 26.4-26.9 us — the check's 64 loads per
+// waiting lane, r05_s46; a check every 64 polls instead of 16: no change, r05_s48.)
 constexpr uint64_t kArriveTicks = 10000;  // 100 us without a new arrival
-constexpr uint32_t kArriveEvery = 16;      // polls between two residency checks (~8 us)
+#ifndef ONO_ARRIVE_EVERY
+#define ONO_ARRIVE_EVERY 16
+#endif
+constexpr uint32_t kArriveEvery = ONO_ARRIVE_EVERY;  // polls between two residency checks (~8 us)
+constexpr uint32_t kArriveShards = 64;     // lines of the count (16 u64 each), then the top word's line
+// (two halves: the add is issued with the tile's loads, its returned value used only after the first tile
+// is indexed, so no wave waits for it)
+__device__ __forceinline__ uint64_t arrive_add(uint64_t *arrive) {
+#ifdef ONO_NO_ARRIVE  // (measurement build only: no residency count)
+    return ~0ull;
+#endif
+    return __hip_atomic_fetch_add(arrive + (size_t)(blockIdx.x % kArriveShards) * 16, (uint64_t)1, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void arrive_done(uint64_t *arrive, uint64_t old) {
+    const uint32_t G = gridDim.x, sh = blockIdx.x % kArriveShards;
+    const uint64_t cnt = (G - sh + kArriveShards - 1) / kArriveShards;  // this line's workgroups
+    if (old + 1 == cnt) {  // the line's last: every add of this launch to it is in
+        __hip_atomic_store(arrive + (size_t)sh * 16, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(arrive + (size_t)kArriveShards * 16, (uint64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 struct FusedGrid {
-    const uint64_t *arrive;  // the stream's arrival counter (monotonic over launches)
+    const uint64_t *arrive;  // the stream's count of complete arrival lines (the top word, monotonic)
     uint64_t target;         // its value once this launch's whole grid has started
     const uint64_t *badw;    // the call's status word (raise_bad)
     uint32_t epoch;
     uint64_t seen = 0, since = 0;  // the count last read, and when it last moved
     __device__ bool give_up() {
         if (*(const volatile uint64_t *)badw == (uint64_t)epoch) return true;  // refused elsewhere
+#ifdef ONO_NO_ARRIVE
+        return false;
+#endif
         const uint64_t c = ld_agent(arrive), now = wall_clock64();
         if (c >= target) return false;  // the whole grid is resident: the awaited tiles will come
         if (c != seen || since == 0) {
@@ -2372,7 +2431,6 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
     float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *frec, uint64_t *fchunk, uint64_t *fchunk_next,
                                                   uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch, uint64_t *arrive, uint64_t arrive_target) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ uint4 img16[kPatImg / 8];  // a range as f16 bits (12 KiB), widened on the way out
     __shared__ uint4 lw4[TPW][kStageU4];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -2397,6 +2455,9 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
     const uint64_t total = *(const uint64_t *)(b + 8 * (threadIdx.x * (cap >> 62)));
     __builtin_amdgcn_sched_barrier(0);
     pat_stage_issue<TPW>(v, n16, b, M, T);
+    // counted in once its loads are in flight
+    uint64_t arr_old = 0;
+    if (threadIdx.x == 0) arr_old = arrive_add(arrive);
     // pl_index's part per tile: candidates, their counts and sums, the successor checks inside the tile;
     // then the tile published: its two granules {sum}, {exit: kPatNone for no candidate}, and its
     // chunk's sum and arrival in every replica
@@ -2421,7 +2482,11 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         uint32_t rank = ec;
         for (uint32_t mm = m[q]; mm; mm &= mm - 1, rank++) {
             const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e;
+#if ONO_PL_UNITS_REG
             const uint32_t nx = k + 4 + U.sel(e + 2);  // tile-local successor
+#else
+            const uint32_t nx = k + 4 + lw4u16(lw4[q])[k + 2];  // tile-local successor
+#endif
             if (base + nx > M32) { bad = true; break; }  // the run overruns the stream
             if (nx < (uint32_t)kPatU && base + nx < M32) {
                 const uint32_t m2 = lmask[nx / kPatPer], b2 = nx % kPatPer;
@@ -2445,6 +2510,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
                       (unsigned long long)ts[q] | 1ull << 40);
         }
     }
+    if (threadIdx.x == 0) arrive_done(arrive, arr_old);
     if (s_bad && threadIdx.x == 0) raise_bad(badw, epoch);
     // (checked after the tiles are published, before any look-back: uniform over the grid, so nobody
     // waits; checked first, the compiler would sink the later tiles' loads behind the total's)
@@ -2466,7 +2532,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
             bool f;
             uint32_t px;
             const bool ok = fused_lookback(t, tagv, frec, fchunk, gcap, blockIdx.x % kFusedRep, E, f, px,
-                                           FusedGrid{arrive, arrive_target, badw, epoch});
+                                           FusedGrid{arrive + (size_t)kArriveShards * 16, arrive_target, badw, epoch});
             if (threadIdx.x == 0) {
                 s_E0 = E;
                 s_found = ok && f ? 1u : 0u;
@@ -2501,12 +2567,17 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
             const uint16_t *lw = (const uint16_t *)lw4[q];
             for (uint32_t i = threadIdx.x; i < (n + 7) / 8; i += kPatT) img16[i] = make_uint4(0u, 0u, 0u, 0u);
             if (threadIdx.x == 0) lqn = 0;
-            const Units12 U = units12(lw4[q]);  // (the thread's units from registers below: lanes 16 B apart
-                                                // reading their own units from LDS hit one bank 4 at a time)
+#if ONO_PL_UNITS_REG
+            const Units12 U = units12(lw4[q]);  // (the thread's units from registers below)
+#endif
             __syncthreads();
             uint32_t cur = (uint32_t)E0 + es[q];  // where the run before the thread's first record ended
             for (uint32_t mm = m[q]; mm; mm &= mm - 1) {
+#if ONO_PL_UNITS_REG
                 const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = U.sel(e), len = U.sel(e + 2);
+#else
+                const uint32_t e = (uint32_t)__builtin_ctz(mm), k = j0 + e, off = lw[k], len = lw[k + 2];
+#endif
                 const uint32_t gi = cur + off;
                 if (gi < ea || gi > eb || len > eb - gi || cur > eb || base + k + 4 + len > M32) {
                     raise_bad(badw, epoch);  // only a refuted stream
@@ -2514,7 +2585,11 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
                 }
                 uint16_t *d = img + (gi - ia);
                 if (len <= (uint32_t)kShortP) {  // staged whole (kPatHalo)
+#if ONO_PL_UNITS_REG
                     for (uint32_t i = 0; i < len; i++) d[i] = e + 4 + i < 12u ? (uint16_t)U.sel(e + 4 + i) : lw[k + 4 + i];
+#else
+                    for (uint32_t i = 0; i < len; i++) d[i] = lw[k + 4 + i];
+#endif
                 } else {
                     const uint32_t qq = atomicAdd(&lqn, 1u);
                     const uint32_t vp = 8 + 2 * (base + k + 4);
@@ -2704,8 +2779,8 @@ struct PatScratch {
     size_t fcap = 0, fgcap = 0;
     uint64_t *frec = nullptr, *fchunk = nullptr;
     int fpar = 0;
-    uint64_t *arrive = nullptr;  // pl_fused's arrival counter (device, zeroed once, monotonic)
-    uint64_t arrive_base = 0;    // its value once every earlier launch's grid has started
+    uint64_t *arrive = nullptr;  // pl_fused's arrival count: kArriveShards lines + the top word (zeroed once)
+    uint64_t arrive_base = 0;    // the top word once every earlier launch's grid has started
 };
 std::map<std::pair<int, hipStream_t>, PatScratch> g_pat;
 std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
@@ -3488,15 +3563,15 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
             P.fgcap = gc;
             P.fpar = 0;
         }
-        if (!P.arrive) {
-            ONO_HIP(hipMalloc((void **)&P.arrive, sizeof(uint64_t)));
-            ONO_HIP(hipMemsetAsync(P.arrive, 0, sizeof(uint64_t), s));
+        if (!P.arrive) {  // kArriveShards lines + the top word's line, 128 B each
+            ONO_HIP(hipMalloc((void **)&P.arrive, (kArriveShards + 1) * 16 * sizeof(uint64_t)));
+            ONO_HIP(hipMemsetAsync(P.arrive, 0, (kArriveShards + 1) * 16 * sizeof(uint64_t), s));
         }
         uint64_t *cur = P.fchunk + (size_t)P.fpar * kFusedRep * P.fgcap * kFusedLine;
         uint64_t *next = P.fchunk + (size_t)(1 - P.fpar) * kFusedRep * P.fgcap * kFusedLine;
         const bool one = T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX);
         const size_t grid = one ? T : (T + 2) / 3;
-        const uint64_t target = P.arrive_base + grid;
+        const uint64_t target = P.arrive_base + std::min<size_t>(grid, kArriveShards);  // complete lines
         if (one)
             hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
                                cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target);

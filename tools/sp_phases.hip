@@ -125,7 +125,7 @@ int main(int argc, char **argv) {
            mib, K, NG, kImageTpw, per, (unsigned long long)wire, bytes / per * 1e-3,
            bytes / per * 1e-3 / 8000.0);
     const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + kImageTpw - 1) / kImageTpw;
-    if (drop_fused()) {  // the one-launch encoder: per tile {start, look-back done, end} + ticket and image times
+    if (drop_fused() && ntiles <= drop_one_launch_tiles()) {  // the one-launch encoder: per tile {start, look-back done, end} + ticket and image times
         std::vector<uint4> d1(ntiles), d1b(ntiles);
         CK(hipMemcpyFromSymbol(d1.data(), HIP_SYMBOL(g_sp_stamp_d1), ntiles * sizeof(uint4)));
         CK(hipMemcpyFromSymbol(d1b.data(), HIP_SYMBOL(g_sp_stamp_d1b), ntiles * sizeof(uint4)));
