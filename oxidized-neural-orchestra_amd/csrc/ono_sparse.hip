@@ -308,6 +308,12 @@ struct TileImg {
     uint32_t hpl, lenl, rs_last;    // the last run's header unit, its length within the tile, its start
     const uint16_t *stage;          // the units (LDS)
 };
+// the tile's f16 values in LDS for the kept-value loop: 1 transposed (word q of thread t at q kIT + t:
+// every read conflict-free), 0 the thread's 32 contiguous bytes (two 16-B stores; lanes 4 apart share a
+// bank on the reads, up to 8-way)
+#ifndef ONO_VALS_T
+#define ONO_VALS_T 1
+#endif
 __device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE], float before, size_t n, float t) {
     __shared__ __attribute__((aligned(16))) uint16_t stage[kSlotU16 + 2 * kIT];  // + a spare dword per thread
     __shared__ uint32_t rb[3];  // position | offset of the tile's first run; position | length of its last; its start
@@ -331,10 +337,18 @@ __device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE
         // transposed: the thread's word q at q kIT + thread, so that the lanes' reads below, each of some
         // value of its own, fall in distinct banks whatever the values (a thread's 32 contiguous bytes
         // put lanes 4 apart on one bank: up to 8-way conflicts on every read, and 2-way on the writes)
+#if ONO_VALS_T
 #pragma unroll
         for (int q = 0; q < kIE / 2; q++) vals[q * kIT + threadIdx.x] = w[q];
         typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
         lds_cu16 *v16 = (lds_cu16 *)vals + 2 * threadIdx.x;  // (an LDS read: a generic pointer would be a flat load)
+#else
+        uint4 *v4 = (uint4 *)(vals + lo / 2);
+#pragma unroll
+        for (int q = 0; q < kIE / 8; q++) v4[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+        lds_cu16 *v16 = (lds_cu16 *)vals;  // (an LDS read: a generic pointer would be a flat load)
+#endif
         uint32_t pos = 4 * ts.es + ts.ef;  // the next value's unit, before a header of its own
         uint32_t sl = ts.es, last = ts.kept1_before, hp = 0, rs = 0, hsl = 0;
         bool open = false;  // a run started in this thread, its length not written yet
@@ -358,7 +372,11 @@ __device__ __forceinline__ TileImg build_image(size_t tile, const float (&x)[kIE
                 if (hsl == R - 1) rb[2] = i;
                 open = true;
             }
+#if ONO_VALS_T
             vst[pos++] = v16[2 * kIT * (e >> 1) + (e & 1)];
+#else
+            vst[pos++] = v16[i];
+#endif
             last = i + 1;
         }
         if (open) {  // the first unkept after the run: in the thread, else after it (tile-local)
