@@ -435,6 +435,9 @@ private:
     }
 
     // everything enqueued on the ring's stream so far has run (a spin on a host-mapped word)
+    // (the sparse hop's waits; a dense zero-copy hop synchronizes the stream instead: config-1 rings,
+    // ms per round spin / synchronize, one box: dense 2 workers 0.106 / 0.101, 4 workers 0.250 / 0.243,
+    // sparse r = 0.1 0.243 / 0.265 — profiles/r05_s51_wait_ab.txt)
     int wait() {
         if (++r_->tcp_epoch == 0) r_->tcp_epoch = 1;
         ONO_HIP(stream_wait(s_, r_->tcp_word, r_->tcp_word_dev, r_->tcp_epoch));
@@ -477,7 +480,8 @@ private:
             uint8_t *f = reinterpret_cast<uint8_t *>(slot(b, c)) - 12;
             put_header(f, bytes, KIND_DENSE);
             o.frame = f;
-            return wait();
+            ONO_HIP(hipStreamSynchronize(s_));
+            return ONO_OK;
         }
         int rc = grow_pinned(&r_->tx, &r_->tx_cap, 12 + bytes);
         if (rc) return rc;
