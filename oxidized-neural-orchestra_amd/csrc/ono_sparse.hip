@@ -2305,10 +2305,17 @@ constexpr uint64_t kArriveTicks = 10000;  // 100 us without a new arrival
 #endif
 constexpr uint32_t kArriveEvery = ONO_ARRIVE_EVERY;  // polls between two residency checks (~8 us)
 constexpr uint32_t kArriveShards = 64;     // lines of the count (16 u64 each), then the top word's line
+// ONO_LIFT_PROGRESS (default): no count at all — a waiting lane gives the call up when the words it polls
+// (its chunk line's arrival count, its tile's granules) have not changed for kArriveTicks: a producer
+// that runs publishes within microseconds of starting, so a standstill that long means it is not
+// resident (the same bound as the count's, without its adds: see DESIGN §3)
+#ifndef ONO_LIFT_PROGRESS
+#define ONO_LIFT_PROGRESS 1
+#endif
 // (two halves: the add is issued with the tile's loads, its returned value used only after the first tile
 // is indexed, so no wave waits for it)
 __device__ __forceinline__ uint64_t arrive_add(uint64_t *arrive) {
-#ifdef ONO_NO_ARRIVE  // (measurement build only: no residency count)
+#if defined(ONO_NO_ARRIVE) || ONO_LIFT_PROGRESS  // (no residency count)
     return ~0ull;
 #endif
     return __hip_atomic_fetch_add(arrive + (size_t)(blockIdx.x % kArriveShards) * 16, (uint64_t)1, __ATOMIC_RELAXED,
@@ -2345,6 +2352,25 @@ struct FusedGrid {
             return false;
         }
         return now - since > kArriveTicks;
+    }
+    // the progress form (ONO_LIFT_PROGRESS): the lane's polled words (key) unchanged for kArriveTicks
+    __device__ bool stalled(uint64_t key) {
+        if (*(const volatile uint64_t *)badw == (uint64_t)epoch) return true;  // refused elsewhere
+        const uint64_t now = wall_clock64();
+        if (key != seen || since == 0) {
+            seen = key;
+            since = now;
+            return false;
+        }
+        return now - since > kArriveTicks;
+    }
+    __device__ bool check(uint64_t key) {
+#if ONO_LIFT_PROGRESS
+        return stalled(key);
+#else
+        (void)key;
+        return give_up();
+#endif
     }
 };
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
@@ -2406,7 +2432,10 @@ __device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const 
         const bool ready = (!wchunk || (v >> 40) == (uint64_t)kPatChunk) &&
                            (!wtile || ((a >> 32) == tagv && (x3 >> 32) == tagv));
         if (ready) break;
-        if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.give_up())) { timeout = true; break; }
+        if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.check(v ^ (a * 0x9E3779B97F4A7C15ull) ^ x3))) {
+            timeout = true;
+            break;
+        }
         __builtin_amdgcn_s_sleep(kPollSleep);
     }
     uint64_t part = (wchunk ? v & ((1ull << 40) - 1) : 0ull) + (wtile ? (uint32_t)a : 0u);
@@ -2426,7 +2455,7 @@ __device__ __forceinline__ bool fused_lookback(uint32_t t, uint32_t tagv, const 
             const uint64_t *rr = frec + 2 * (size_t)i + 1;
             uint64_t x = ld_agent(rr);
             for (uint32_t it = 0; (x >> 32) != tagv; it++) {
-                if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.give_up())) { timeout = true; break; }
+                if (it > kPollMax || (it % kArriveEvery == kArriveEvery - 1 && fg.check(x))) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(kPollSleep);
                 x = ld_agent(rr);
             }
