@@ -178,9 +178,10 @@ int ono_sparse_lift_dev(float *g_dev, size_t cap, size_t *out_len, const uint8_t
  * A refused call may already have written parts of g[0, total): check the
  * status before using g.  The one-launch form (an 8-B aligned stream of at
  * most 4096 tiles) needs its whole grid resident; when kernels of another
- * stream or process hold CU slots so that the count of started workgroups
- * stalls short of the grid for ~100 us, the call is refused rather than
- * waiting for them (measured: refused in 0.75 ms with 3/4 of the CUs held).  */
+ * stream or process hold CU slots so that a waiting tile sees the words it
+ * polls stand still for ~100 us, the call is refused rather than waiting for
+ * them (tests/test_gpu_sparse_pattern.py: 3/4 of the CUs held by another
+ * process — refused early, exact after the blocking lift).  */
 int ono_sparse_lift_dev_async(float *g_dev, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
                               uint64_t *ticket, void *stream);
 /* lifts so far (this process) that took the sequential host parse        */
