@@ -692,6 +692,182 @@ __global__ __launch_bounds__(kSB) void sp_move(
 }
 
 
+// -------------------------------------------------- count + emit encoder ----
+// Round 5 (the 64 MiB drop): two launches without the slot image.  sp_count reads g
+// once, one wave per tile with 32 values per lane: the keep flags as one 32-bit word per lane (256 B
+// per tile, the "mask"), the tile's record (recA, as sp_image writes it) and the chunk aggregates (four
+// tiles per workgroup, one set of atomics).  sp_emit, one wave per tile: the tile's prefix from the
+// records and aggregates (tile_prefix, as sp_move), the run starts and the thread's place from the mask
+// and one DPP scan, the tile's values read again (an L2 / Infinity Cache hit straight after sp_count)
+// into f16 words in LDS (transposed: every read conflict-free), and every unit stored straight to its
+// place in the wire — each header with its global offset and length (the previous kept index and the
+// next unkept one from the thread, the wave, or the prefix P / Q), so no field is completed later.
+// Traffic: 4 N (+ the re-read from cache) + the wire + the mask (N / 8, written and read).
+constexpr int kCW = 32;                // values per lane: one wave per 2048-value tile
+static_assert(64 * kCW == kTile, "a wave holds a tile");
+constexpr int kCountTpw = kSB / 64;   // tiles per sp_count workgroup (a wave each): one set of atomics
+static_assert(kRecChunk % kCountTpw == 0, "a workgroup's tiles share one chunk aggregate");
+
+template <bool FULL>
+__device__ __forceinline__ void load_w32(const float *__restrict__ g, size_t n, size_t tile, float (&x)[kCW]) {
+    const size_t base = tile * kTile + (size_t)(threadIdx.x & 63) * kCW;
+    if (FULL) {
+#pragma unroll
+        for (int q = 0; q < kCW / 4; q++) {
+            const f4s a = *((const f4s *)(g + base) + q);
+            x[4 * q] = a.x; x[4 * q + 1] = a.y; x[4 * q + 2] = a.z; x[4 * q + 3] = a.w;
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < kCW; e++) x[e] = base + e < n ? g[base + e] : 0.0f;
+    }
+}
+// the lane's valid values as a mask (the last tile may end inside the lane)
+__device__ __forceinline__ uint32_t valid_w32(size_t n, size_t tile) {
+    const size_t base = tile * kTile + (size_t)(threadIdx.x & 63) * kCW;
+    return base >= n ? 0u : (n - base >= (size_t)kCW ? 0xFFFFFFFFu : (1u << (n - base)) - 1u);
+}
+// kept(g[tile0 - 1]) for lane 0 (0 for the first tile): a vector load of a wave-uniform address
+__device__ __forceinline__ uint32_t kept_before_tile(const float *__restrict__ g, size_t tile, float t) {
+    if (tile == 0) return 0u;
+    uint32_t a = (uint32_t)(tile * kTile - 1);
+    asm volatile("" : "+v"(a));
+    return kept(g[a], t) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, size_t n, size_t ntiles, float t,
+                                                const float *t_dev, bool vec, uint32_t *__restrict__ mask,
+                                                uint2 *__restrict__ recA, uint4 *agg, uint4 *agg_next, uint32_t gcap) {
+    __shared__ uint32_t s_fr[kCountTpw][2], s_lk[kCountTpw], s_fu[kCountTpw];
+    if (t_dev) t = *t_dev;
+    for (size_t i = (size_t)blockIdx.x * kSB + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kSB)
+        agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t tile = (size_t)blockIdx.x * kCountTpw + wave;
+    uint32_t F = 0, R = 0, LK = 0, FU = kTile;
+    if (tile < ntiles) {
+        float x[kCW];
+        const uint32_t pb = kept_before_tile(g, tile, t);
+        if (vec && (tile + 1) * kTile <= n) load_w32<true>(g, n, tile, x);
+        else load_w32<false>(g, n, tile, x);
+        const uint32_t valid = valid_w32(n, tile);
+        uint32_t keep = 0;
+#pragma unroll
+        for (int e = 0; e < kCW; e++) keep |= kept(x[e], t) ? 1u << e : 0u;
+        keep &= valid;
+        uint32_t prev = lane_before(keep >> 31);
+        if (lane == 0) prev = pb;
+        const uint32_t start = keep & ~((keep << 1) | prev), unk = valid & ~keep;
+        mask[tile * 64 + lane] = keep;
+        const uint32_t lo = (uint32_t)lane * kCW;
+        F = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(keep)), 63);
+        R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(start)), 63);
+        LK = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(keep ? lo + 32u - (uint32_t)__clz(keep) : 0u), 63);
+        FU = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile), 63);
+        if (lane == 0) recA[tile] = make_uint2(F | R << 16, LK | FU << 16);
+    }
+    if (lane == 0) {
+        s_fr[wave][0] = F;
+        s_fr[wave][1] = R;
+        s_lk[wave] = F ? (uint32_t)(tile * kTile) + LK : 0u;  // global last kept + 1 (0: none)
+        s_fu[wave] = FU < (uint32_t)kTile ? ~((uint32_t)(tile * kTile) + FU) : 0u;  // complemented (0: none)
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && (size_t)blockIdx.x * kCountTpw < ntiles) {
+        uint64_t fr = 0;
+        uint32_t lk = 0, nfu = 0;
+#pragma unroll
+        for (int w = 0; w < kCountTpw; w++) {
+            fr += (uint64_t)s_fr[w][0] | (uint64_t)s_fr[w][1] << 32;
+            lk = max(lk, s_lk[w]);
+            if (!nfu) nfu = s_fu[w];  // the first tile's first unkept
+        }
+        uint32_t *a = (uint32_t *)(agg + ((size_t)blockIdx.x * kCountTpw / kRecChunk) * kAggStride);
+        if (fr) {
+            atomicAdd((unsigned long long *)a, (unsigned long long)fr);
+            atomicMax(a + 2, lk);
+        }
+        if (nfu) atomicMax(a + 3, nfu);
+    }
+}
+
+__global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size_t n, size_t ntiles, bool vec,
+                                               const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
+                                               const uint4 *__restrict__ agg, uint8_t *__restrict__ buf,
+                                               uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
+    __shared__ uint32_t vals[kSB / 64][(kCW / 2) * 64];  // per wave: word q of lane l at q * 64 + l
+    const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
+        const uint2 t = chunk_totals(agg, G);
+        if (threadIdx.x == 0) {
+            for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
+            const uint64_t F = t.x, R = t.y;
+            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;
+            else { host_tot[0] = F; host_tot[1] = R; }
+        }
+    }
+    const int wave = threadIdx.x >> 6;
+    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + wave));
+    if (tile >= ntiles) return;  // (no barrier below)
+    const uint32_t lane = threadIdx.x & 63, lo = lane * kCW;
+    const uint32_t tile0 = (uint32_t)(tile * kTile);
+    // every load first: the lane's mask word, the bit before the tile, the values, the prefix's records
+    const uint32_t keep = mask[tile * 64 + lane];
+    uint32_t pa = (uint32_t)(tile ? tile * 64 - 1 : 0);
+    asm volatile("" : "+v"(pa));  // (a vector load)
+    const uint32_t pw = mask[pa];
+    float x[kCW];
+    if (vec && (tile + 1) * kTile <= n) load_w32<true>(g, n, tile, x);
+    else load_w32<false>(g, n, tile, x);
+    uint2 own;
+    const uint4 p = tile_prefix(recA, agg, ntiles, G, tile, (uint32_t)n, &own);  // F0, R0, P, Q
+    const uint32_t valid = valid_w32(n, tile), unk = valid & ~keep;
+    uint32_t prev = lane_before(keep >> 31);
+    if (lane == 0) prev = tile ? pw >> 31 : 0u;
+    const uint32_t start = keep & ~((keep << 1) | prev);
+    // the thread's place: kept values and runs of the lanes before it (one DPP scan of both)
+    const uint32_t ownc = (uint32_t)__popc(keep) | (uint32_t)__popc(start) << 16;
+    const uint32_t exc = wave_incl_sum_dpp(ownc) - ownc;
+    const uint32_t ef = exc & 0xFFFFu, es = exc >> 16;
+    // the nearest kept value before the lane and unkept one after it, within the tile (tile-local + 1 /
+    // index; 0 / kTile: none)
+    const uint32_t k1 = keep ? lo + 32u - (uint32_t)__clz(keep) : 0u;
+    const uint32_t u1 = unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile;
+    const uint64_t mk = __ballot(keep != 0), mu = __ballot(unk != 0);
+    const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
+    const uint64_t kbm = mk & below, uam = mu & above;
+    const int lk = kbm ? 63 - __clzll((long long)kbm) : 0, lu = uam ? __ffsll((unsigned long long)uam) - 1 : 0;
+    const uint32_t ykb = (uint32_t)__shfl((int)k1, lk, 64), yua = (uint32_t)__shfl((int)u1, lu, 64);
+    const uint32_t kept1_before = kbm ? ykb : 0u, unkept_after = uam ? yua : (uint32_t)kTile;
+    // the values as f16 words in LDS (an indexable copy; only this lane reads its words)
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    lds_u32 *vw = (lds_u32 *)vals[wave];
+#pragma unroll
+    for (int q = 0; q < kCW / 2; q++) vw[q * 64 + lane] = to_f16_sp(x[2 * q]) | (uint32_t)to_f16_sp(x[2 * q + 1]) << 16;
+    typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+    lds_cu16 *v16 = (lds_cu16 *)vals[wave] + 2 * lane;
+    uint16_t *w16 = (uint16_t *)(buf + 8);
+    size_t pos = 4 * ((size_t)p.y + es) + (size_t)p.x + ef;  // the lane's first unit
+    for (uint32_t m = keep; m; m &= m - 1u) {
+        const uint32_t e = (uint32_t)__ffs(m) - 1u, gi = tile0 + lo + e;
+        if (start >> e & 1u) {
+            const uint32_t kb = keep & ((1u << e) - 1u);
+            const uint32_t prev_end = kb ? tile0 + lo + 32u - (uint32_t)__clz(kb)
+                                         : (kept1_before ? tile0 + kept1_before : p.z);
+            const uint32_t ua = e == 31u ? 0u : unk >> (e + 1u);
+            const uint32_t end = ua ? gi + 1u + (uint32_t)__ffs(ua) - 1u
+                                    : (unkept_after < (uint32_t)kTile ? tile0 + unkept_after : p.w);
+            const uint32_t off = gi - prev_end, len = end - gi;
+            w16[pos] = (uint16_t)off;
+            w16[pos + 1] = (uint16_t)(off >> 16);
+            w16[pos + 2] = (uint16_t)len;
+            w16[pos + 3] = (uint16_t)(len >> 16);
+            pos += 4;
+        }
+        w16[pos++] = v16[2 * 64 * (e >> 1) + (e & 1)];
+    }
+}
+
 // ------------------------------------------------- one-launch encoder ----
 // sp_drop1 (round 5): the drop in one launch, no slot image and no sp_move.
 // Workgroup b takes tile b, builds the tile's byte range in LDS exactly as sp_image does, publishes
@@ -2740,7 +2916,10 @@ struct Scratch {
     uint4 *agg = nullptr;
     size_t agg_cap = 0;
     int parity = 0;
-    uint16_t *img = nullptr;  // tiles_cap slots of kSlotU16 units (5 B per value)
+    uint16_t *img = nullptr;  // img_cap slots of kSlotU16 units (5 B per value): sp_image / sp_move
+    size_t img_cap = 0;
+    uint32_t *mask = nullptr;  // mask_cap tiles of 64 keep words (N / 8 bytes): sp_count / sp_emit
+    size_t mask_cap = 0;
     uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;  // [F, R, the completion tag, spare]
     // the one-launch form (sp_drop1): 4 granules per tile and per group of tiles (zeroed when
     // allocated, and when the epoch wraps), the call's epoch
@@ -2751,7 +2930,7 @@ struct Scratch {
 std::mutex g_scratch_mu;
 std::map<std::pair<int, hipStream_t>, Scratch> g_scratch;
 
-int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = true) {
+int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = true, bool emit = false) {
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
@@ -2777,19 +2956,30 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = t
     if (ntiles > sc.tiles_cap) {
         (void)hipFree(sc.rec);
         (void)hipFree(sc.agg);
-        (void)hipFree(sc.img);
         sc.rec = nullptr;
         sc.agg = nullptr;
-        sc.img = nullptr;
         sc.tiles_cap = sc.agg_cap = 0;
         const size_t gcap = (ntiles + kRecChunk - 1) / kRecChunk;
         ONO_HIP(hipMalloc((void **)&sc.rec, 2 * ntiles * sizeof(uint2)));
         ONO_HIP(hipMalloc((void **)&sc.agg, 2 * gcap * kAggStride * sizeof(uint4)));
         ONO_HIP(hipMemsetAsync(sc.agg, 0, 2 * gcap * kAggStride * sizeof(uint4), stream));
-        ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
         sc.tiles_cap = ntiles;
         sc.agg_cap = gcap;
         sc.parity = 0;
+    }
+    if (!emit && ntiles > sc.img_cap) {
+        (void)hipFree(sc.img);
+        sc.img = nullptr;
+        sc.img_cap = 0;
+        ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
+        sc.img_cap = ntiles;
+    }
+    if (emit && ntiles > sc.mask_cap) {
+        (void)hipFree(sc.mask);
+        sc.mask = nullptr;
+        sc.mask_cap = 0;
+        ONO_HIP(hipMalloc((void **)&sc.mask, ntiles * 64 * sizeof(uint32_t)));
+        sc.mask_cap = ntiles;
     }
     *out = &sc;
     return ONO_OK;
@@ -3259,6 +3449,15 @@ bool drop_fused() {
     }();
     return v;
 }
+// ONO_DROP_FORM=emit: the two launches without the slot image (sp_count + sp_emit); image (default):
+// sp_image + sp_move
+bool drop_emit() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_DROP_FORM");
+        return e && !strcmp(e, "emit");
+    }();
+    return v;
+}
 // ONO_DROP_FALLBACK_POLLS: sp_drop1's polls before its fallback (tests set 0: every descriptor not
 // there at the first read is computed by the waiting wave)
 uint32_t drop_fallback_polls() {
@@ -3311,7 +3510,8 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
         *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
         return ONO_OK;
     }
-    int rc = scratch_for(ntiles, s, &sc);
+    const bool emit = drop_emit();
+    int rc = scratch_for(ntiles, s, &sc, true, emit);
     if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
     const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
@@ -3320,7 +3520,13 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     hipError_t e = hipSuccess;
-    if (ntiles) {
+    if (ntiles && emit) {
+        const size_t grid = (ntiles + kCountTpw - 1) / kCountTpw;
+        hipLaunchKernelGGL(sp_count, dim3((unsigned)grid), dim3(kSB), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->mask,
+                           recA, agg, agg_next, (uint32_t)sc->agg_cap);
+        e = hipGetLastError();
+        if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
+    } else if (ntiles) {
         const size_t grid = (ntiles + kImageTpw - 1) / kImageTpw;
         hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)kImageTpw, threshold,
                            t_dev, vec, sc->img, recA, recB, agg, agg_next, (uint32_t)sc->agg_cap);
@@ -3336,8 +3542,12 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
-                       sc->host_tot_dev, nbytes_dev);
+    if (emit)
+        hipLaunchKernelGGL(sp_emit, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg, buf,
+                           sc->host_tot_dev, nbytes_dev);
+    else
+        hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
+                           sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     if (nbytes_dev) return ONO_OK;
