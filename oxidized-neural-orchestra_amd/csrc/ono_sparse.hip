@@ -664,6 +664,46 @@ __device__ __forceinline__ void move_tile(const uint16_t *__restrict__ img, cons
 #endif
 }
 
+// sp_emit's staged range (LDS, 16-B aligned, at least one spare block past nu16 units) to its place in
+// the wire in 16-B destination chunks, as move_chunks does from a slot
+typedef __attribute__((address_space(3))) uint4 lds_u4;
+template <int O>
+__device__ __forceinline__ void stage_out(const lds_u4 *src4, uint32_t nu16, uint16_t *base16) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nchunks = nu16 ? (O + nu16 + 7) / 8 : 0;
+    uint4 carry = make_uint4(0, 0, 0, 0);
+    for (uint32_t c0b = 0; c0b < nchunks; c0b += 64) {
+        const uint32_t c = c0b + lane;
+        uint4 own = make_uint4(0, 0, 0, 0);
+        if (c < nchunks) {
+            const lds_u4 &q = src4[c];
+            own = make_uint4(q.x, q.y, q.z, q.w);
+        }
+        const uint4 up = lane_before4(own);
+        const uint4 prev = lane ? up : carry;
+        const uint32_t C[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {  // out word j = concat units 8 - O + 2j, + 1
+            const int sft = 8 - O + 2 * j;
+            if (sft % 2 == 0) o[j] = C[sft / 2];
+            else o[j] = __builtin_amdgcn_alignbit(C[(sft + 1) / 2], C[(sft - 1) / 2], 16);
+        }
+        const bool whole = c * 8 >= (uint32_t)O && (size_t)c * 8 + 8 - O <= nu16;
+        if (whole) {
+            const u4v ov = {o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(ov, (u4v *)(base16 + 8 * (size_t)c));
+        } else if (c < nchunks) {  // the range's first / last chunk (shared with the neighbouring tiles)
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int64_t u = (int64_t)c * 8 + i - O;
+                if (u >= 0 && u < (int64_t)nu16) base16[8 * (size_t)c + i] = (uint16_t)(o[i / 2] >> (16 * (i % 2)));
+            }
+        }
+        carry = readlane4(own, 63);
+    }
+}
+
 // One wave per tile: its records and prefix, the slot's first 1024 units (most tiles' whole image)
 // issued at the same time, then the move.  (Two or four tiles per wave in turn measured slower in
 // round 4: 35.7 / 39.2 vs 33.9 us per drop.)
@@ -791,11 +831,16 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
     }
 }
 
+// STAGE: a tile's range of at most kEmitStage units is built in LDS and stored in 16-B chunks (a longer
+// one, and every range without STAGE, unit by unit straight to the wire)
+constexpr int kEmitStage = 2048;
+template <bool STAGE>
 __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size_t n, size_t ntiles, bool vec,
                                                const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
                                                const uint4 *__restrict__ agg, uint8_t *__restrict__ buf,
                                                uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
     __shared__ uint32_t vals[kSB / 64][(kCW / 2) * 64];  // per wave: word q of lane l at q * 64 + l
+    __shared__ __attribute__((aligned(16))) uint16_t stage[STAGE ? kSB / 64 : 1][STAGE ? kEmitStage + 16 : 8];
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         const uint2 t = chunk_totals(agg, G);
@@ -847,7 +892,49 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
     typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
     lds_cu16 *v16 = (lds_cu16 *)vals[wave] + 2 * lane;
     uint16_t *w16 = (uint16_t *)(buf + 8);
-    size_t pos = 4 * ((size_t)p.y + es) + (size_t)p.x + ef;  // the lane's first unit
+    const size_t U0 = 4 * (size_t)p.y + (size_t)p.x;  // the tile's first unit
+    const uint32_t nu16 = 4 * (own.x >> 16) + (own.x & 0xFFFFu);
+    if (STAGE && nu16 <= (uint32_t)kEmitStage) {  // (uniform)
+        typedef __attribute__((address_space(3))) uint16_t lds_u16;
+        lds_u16 *st = (lds_u16 *)stage[STAGE ? wave : 0];
+        uint32_t lp = 4 * es + ef;  // the lane's first unit within the tile's range
+        for (uint32_t m = keep; m; m &= m - 1u) {
+            const uint32_t e = (uint32_t)__ffs(m) - 1u, gi = tile0 + lo + e;
+            if (start >> e & 1u) {
+                const uint32_t kb = keep & ((1u << e) - 1u);
+                const uint32_t prev_end = kb ? tile0 + lo + 32u - (uint32_t)__clz(kb)
+                                             : (kept1_before ? tile0 + kept1_before : p.z);
+                const uint32_t ua = e == 31u ? 0u : unk >> (e + 1u);
+                const uint32_t end = ua ? gi + 1u + (uint32_t)__ffs(ua) - 1u
+                                        : (unkept_after < (uint32_t)kTile ? tile0 + unkept_after : p.w);
+                const uint32_t off = gi - prev_end, len = end - gi;
+                st[lp] = (uint16_t)off;
+                st[lp + 1] = (uint16_t)(off >> 16);
+                st[lp + 2] = (uint16_t)len;
+                st[lp + 3] = (uint16_t)(len >> 16);
+                lp += 4;
+            }
+            st[lp++] = v16[2 * 64 * (e >> 1) + (e & 1)];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's stage writes, before its reads
+        __builtin_amdgcn_wave_barrier();
+        uint8_t *dst = buf + 8 + 2 * U0;
+        const uint32_t O = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uintptr_t)dst & 15u) >> 1));
+        uint16_t *base16 = (uint16_t *)(dst - 2 * O);
+        const lds_u4 *s4 = (const lds_u4 *)stage[STAGE ? wave : 0];
+        switch (O) {
+        case 0: stage_out<0>(s4, nu16, base16); break;
+        case 1: stage_out<1>(s4, nu16, base16); break;
+        case 2: stage_out<2>(s4, nu16, base16); break;
+        case 3: stage_out<3>(s4, nu16, base16); break;
+        case 4: stage_out<4>(s4, nu16, base16); break;
+        case 5: stage_out<5>(s4, nu16, base16); break;
+        case 6: stage_out<6>(s4, nu16, base16); break;
+        default: stage_out<7>(s4, nu16, base16); break;
+        }
+        return;
+    }
+    size_t pos = U0 + 4 * (size_t)es + ef;  // the lane's first unit
     for (uint32_t m = keep; m; m &= m - 1u) {
         const uint32_t e = (uint32_t)__ffs(m) - 1u, gi = tile0 + lo + e;
         if (start >> e & 1u) {
@@ -3458,6 +3545,14 @@ bool drop_emit() {
     }();
     return v;
 }
+// ONO_EMIT_STAGE=0: sp_emit stores every unit straight to the wire (default: through an LDS stage)
+bool emit_stage() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_EMIT_STAGE");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
+}
 // ONO_DROP_FALLBACK_POLLS: sp_drop1's polls before its fallback (tests set 0: every descriptor not
 // there at the first read is computed by the waiting wave)
 uint32_t drop_fallback_polls() {
@@ -3542,9 +3637,12 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
-    if (emit)
-        hipLaunchKernelGGL(sp_emit, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg, buf,
-                           sc->host_tot_dev, nbytes_dev);
+    if (emit && emit_stage())
+        hipLaunchKernelGGL(sp_emit<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg,
+                           buf, sc->host_tot_dev, nbytes_dev);
+    else if (emit)
+        hipLaunchKernelGGL(sp_emit<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg,
+                           buf, sc->host_tot_dev, nbytes_dev);
     else
         hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
                            sc->host_tot_dev, nbytes_dev);
