@@ -777,7 +777,8 @@ __device__ __forceinline__ uint32_t kept_before_tile(const float *__restrict__ g
 
 __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, size_t n, size_t ntiles, float t,
                                                 const float *t_dev, bool vec, uint32_t *__restrict__ mask,
-                                                uint2 *__restrict__ recA, uint4 *agg, uint4 *agg_next, uint32_t gcap) {
+                                                uint16_t *__restrict__ cv, uint2 *__restrict__ recA, uint4 *agg,
+                                                uint4 *agg_next, uint32_t gcap) {
     __shared__ uint32_t s_fr[kCountTpw][2], s_lk[kCountTpw], s_fu[kCountTpw];
     if (t_dev) t = *t_dev;
     for (size_t i = (size_t)blockIdx.x * kSB + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kSB)
@@ -800,7 +801,14 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
         const uint32_t start = keep & ~((keep << 1) | prev), unk = valid & ~keep;
         mask[tile * 64 + lane] = keep;
         const uint32_t lo = (uint32_t)lane * kCW;
-        F = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(keep)), 63);
+        // the tile's kept values as f16, compact, in its slot of cv (in order: the lanes' exclusive prefix)
+        const uint32_t kc = (uint32_t)__popc(keep), incl = wave_incl_sum_dpp(kc);
+        uint32_t cp = incl - kc;
+        uint16_t *cvt = cv + tile * kTile;
+#pragma unroll
+        for (int e = 0; e < kCW; e++)
+            if (keep >> e & 1u) cvt[cp++] = to_f16_sp(x[e]);
+        F = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(start)), 63);
         LK = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(keep ? lo + 32u - (uint32_t)__clz(keep) : 0u), 63);
         FU = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile), 63);
@@ -835,11 +843,11 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
 // one, and every range without STAGE, unit by unit straight to the wire)
 constexpr int kEmitStage = 2048;
 template <bool STAGE>
-__global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size_t n, size_t ntiles, bool vec,
+__global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
                                                const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
                                                const uint4 *__restrict__ agg, uint8_t *__restrict__ buf,
                                                uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
-    __shared__ uint32_t vals[kSB / 64][(kCW / 2) * 64];  // per wave: word q of lane l at q * 64 + l
+    __shared__ __attribute__((aligned(16))) uint16_t vals[kSB / 64][kTile];  // per wave: the tile's compact values
     __shared__ __attribute__((aligned(16))) uint16_t stage[STAGE ? kSB / 64 : 1][STAGE ? kEmitStage + 16 : 8];
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
@@ -861,9 +869,6 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
     uint32_t pa = (uint32_t)(tile ? tile * 64 - 1 : 0);
     asm volatile("" : "+v"(pa));  // (a vector load)
     const uint32_t pw = mask[pa];
-    float x[kCW];
-    if (vec && (tile + 1) * kTile <= n) load_w32<true>(g, n, tile, x);
-    else load_w32<false>(g, n, tile, x);
     uint2 own;
     const uint4 p = tile_prefix(recA, agg, ntiles, G, tile, (uint32_t)n, &own);  // F0, R0, P, Q
     const uint32_t valid = valid_w32(n, tile), unk = valid & ~keep;
@@ -884,20 +889,26 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
     const int lk = kbm ? 63 - __clzll((long long)kbm) : 0, lu = uam ? __ffsll((unsigned long long)uam) - 1 : 0;
     const uint32_t ykb = (uint32_t)__shfl((int)k1, lk, 64), yua = (uint32_t)__shfl((int)u1, lu, 64);
     const uint32_t kept1_before = kbm ? ykb : 0u, unkept_after = uam ? yua : (uint32_t)kTile;
-    // the values as f16 words in LDS (an indexable copy; only this lane reads its words)
-    typedef __attribute__((address_space(3))) uint32_t lds_u32;
-    lds_u32 *vw = (lds_u32 *)vals[wave];
-#pragma unroll
-    for (int q = 0; q < kCW / 2; q++) vw[q * 64 + lane] = to_f16_sp(x[2 * q]) | (uint32_t)to_f16_sp(x[2 * q + 1]) << 16;
+    // the tile's compact values (sp_count's slot) into LDS in 16-B pieces, read below by position: the
+    // lane's k-th kept value is the tile's (ef + k)-th
+    const uint32_t Ft = own.x & 0xFFFFu;
+    {
+        typedef __attribute__((address_space(3))) u4v lds_w4;
+        lds_w4 *vw = (lds_w4 *)vals[wave];
+        const u4v *src = (const u4v *)(cv + tile * kTile);
+        for (uint32_t c = lane; c < (Ft + 7) / 8; c += 64) vw[c] = src[c];
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
     typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
-    lds_cu16 *v16 = (lds_cu16 *)vals[wave] + 2 * lane;
+    lds_cu16 *v16 = (lds_cu16 *)vals[wave] + ef;
     uint16_t *w16 = (uint16_t *)(buf + 8);
     const size_t U0 = 4 * (size_t)p.y + (size_t)p.x;  // the tile's first unit
     const uint32_t nu16 = 4 * (own.x >> 16) + (own.x & 0xFFFFu);
     if (STAGE && nu16 <= (uint32_t)kEmitStage) {  // (uniform)
         typedef __attribute__((address_space(3))) uint16_t lds_u16;
         lds_u16 *st = (lds_u16 *)stage[STAGE ? wave : 0];
-        uint32_t lp = 4 * es + ef;  // the lane's first unit within the tile's range
+        uint32_t lp = 4 * es + ef, kv = 0;  // the lane's first unit within the tile's range; its kept values
         for (uint32_t m = keep; m; m &= m - 1u) {
             const uint32_t e = (uint32_t)__ffs(m) - 1u, gi = tile0 + lo + e;
             if (start >> e & 1u) {
@@ -914,7 +925,7 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
                 st[lp + 3] = (uint16_t)(len >> 16);
                 lp += 4;
             }
-            st[lp++] = v16[2 * 64 * (e >> 1) + (e & 1)];
+            st[lp++] = v16[kv++];
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's stage writes, before its reads
         __builtin_amdgcn_wave_barrier();
@@ -935,6 +946,7 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
         return;
     }
     size_t pos = U0 + 4 * (size_t)es + ef;  // the lane's first unit
+    uint32_t kv = 0;
     for (uint32_t m = keep; m; m &= m - 1u) {
         const uint32_t e = (uint32_t)__ffs(m) - 1u, gi = tile0 + lo + e;
         if (start >> e & 1u) {
@@ -951,7 +963,7 @@ __global__ __launch_bounds__(kSB) void sp_emit(const float *__restrict__ g, size
             w16[pos + 3] = (uint16_t)(len >> 16);
             pos += 4;
         }
-        w16[pos++] = v16[2 * 64 * (e >> 1) + (e & 1)];
+        w16[pos++] = v16[kv++];
     }
 }
 
@@ -3006,6 +3018,7 @@ struct Scratch {
     uint16_t *img = nullptr;  // img_cap slots of kSlotU16 units (5 B per value): sp_image / sp_move
     size_t img_cap = 0;
     uint32_t *mask = nullptr;  // mask_cap tiles of 64 keep words (N / 8 bytes): sp_count / sp_emit
+    uint16_t *cv = nullptr;    // mask_cap tile slots of kTile f16 (the kept values, compact): sp_count / sp_emit
     size_t mask_cap = 0;
     uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;  // [F, R, the completion tag, spare]
     // the one-launch form (sp_drop1): 4 granules per tile and per group of tiles (zeroed when
@@ -3063,9 +3076,12 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = t
     }
     if (emit && ntiles > sc.mask_cap) {
         (void)hipFree(sc.mask);
+        (void)hipFree(sc.cv);
         sc.mask = nullptr;
+        sc.cv = nullptr;
         sc.mask_cap = 0;
         ONO_HIP(hipMalloc((void **)&sc.mask, ntiles * 64 * sizeof(uint32_t)));
+        ONO_HIP(hipMalloc((void **)&sc.cv, ntiles * kTile * sizeof(uint16_t)));
         sc.mask_cap = ntiles;
     }
     *out = &sc;
@@ -3618,7 +3634,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (ntiles && emit) {
         const size_t grid = (ntiles + kCountTpw - 1) / kCountTpw;
         hipLaunchKernelGGL(sp_count, dim3((unsigned)grid), dim3(kSB), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->mask,
-                           recA, agg, agg_next, (uint32_t)sc->agg_cap);
+                           sc->cv, recA, agg, agg_next, (uint32_t)sc->agg_cap);
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     } else if (ntiles) {
@@ -3638,11 +3654,11 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
     if (emit && emit_stage())
-        hipLaunchKernelGGL(sp_emit<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg,
-                           buf, sc->host_tot_dev, nbytes_dev);
+        hipLaunchKernelGGL(sp_emit<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA,
+                           agg, buf, sc->host_tot_dev, nbytes_dev);
     else if (emit)
-        hipLaunchKernelGGL(sp_emit<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, g, n, ntiles, vec, sc->mask, recA, agg,
-                           buf, sc->host_tot_dev, nbytes_dev);
+        hipLaunchKernelGGL(sp_emit<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA,
+                           agg, buf, sc->host_tot_dev, nbytes_dev);
     else
         hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
                            sc->host_tot_dev, nbytes_dev);
