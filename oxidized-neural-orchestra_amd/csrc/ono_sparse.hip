@@ -496,24 +496,30 @@ __device__ __forceinline__ uint4 tile_prefix(const uint2 *recA, const uint4 *agg
 #pragma unroll
     for (int k = 0; k < kRecChunk / 64; k++) r[k] = recA[cs + min(lane + 64 * k, m - 1)];
     uint32_t f = 0, s = 0, mx = 0, q = n;
-    // four aggregates per lane in flight (G >= 1 here); the first four straight after the records
-    // (a loop from 0 put a wait for them at its head), selects instead of branches
+    // the aggregates of the chunks before (kept values, runs, last kept) and of the next one (first
+    // unkept; a later one only when neither the tile's own chunk after it nor the next chunk has one):
+    // the other lanes issue no load.  Every wave of the grid reads these few lines at once, so each
+    // line request counts (a load per lane of all G lines, clamped duplicates included, held the move's
+    // loads at 4 us); four per lane in flight, blocks of 64 past the first only when G needs them
     auto fold = [&](uint32_t j0) {
         uint4 a[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) a[k] = agg[(size_t)min(j0 + 64 * k + lane, G - 1) * kAggStride];
+        for (int k = 0; k < 4; k++) {
+            const uint32_t j = j0 + 64 * k + lane;
+            a[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (j0 + 64 * k < G && (j < c || j == c + 1) && j < G) a[k] = agg[(size_t)j * kAggStride];
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t j = j0 + 64 * k + lane;
-            const bool before = j < c, after = j > c && j < G && a[k].w;
+            const bool before = j < c;
             f += before ? a[k].x : 0u;
             s += before ? a[k].y : 0u;
             mx = max(mx, before ? a[k].z : 0u);
-            q = min(q, after ? ~a[k].w : q);
+            q = min(q, j == c + 1 && a[k].w ? ~a[k].w : q);
         }
     };
-    fold(0);
-    for (uint32_t j0 = 256; j0 < G; j0 += 256) fold(j0);
+    for (uint32_t j0 = 0; j0 <= c + 1 && j0 < G; j0 += 256) fold(j0);
 #pragma unroll
     for (int k = 0; k < kRecChunk / 64; k++) {
         const uint32_t j = lane + 64 * k, t0 = (cs + j) * (uint32_t)kTile;
@@ -525,6 +531,16 @@ __device__ __forceinline__ uint4 tile_prefix(const uint2 *recA, const uint4 *agg
         } else if (j > i && j < m) {
             const uint32_t f1 = r[k].y >> 16;
             if (f1 < (uint32_t)kTile) q = min(q, t0 + f1);
+        }
+    }
+    // no unkept value after the tile in its chunk nor in the next: the first later chunk with one
+    // (wave-uniform, rare: a chunk of 128 tiles all kept)
+    if (c + 2 < G && !__ballot(q < n)) {
+        for (uint32_t j0 = c + 2; j0 < G; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const uint32_t w = j < G ? agg[(size_t)j * kAggStride].w : 0u;
+            q = min(q, w ? ~w : q);
+            if (__ballot(q < n)) break;
         }
     }
     const uint2 o0 = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)r[0].x, i & 63),
@@ -692,8 +708,16 @@ __device__ __forceinline__ void stage_out(const lds_u4 *src4, uint32_t nu16, uin
         const bool whole = c * 8 >= (uint32_t)O && (size_t)c * 8 + 8 - O <= nu16;
         if (whole) {
             const u4v ov = {o[0], o[1], o[2], o[3]};
+#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 3  // measurement only (tools/sp_phases_e3): plain stores
+            *(u4v *)(base16 + 8 * (size_t)c) = ov;
+#else
             __builtin_nontemporal_store(ov, (u4v *)(base16 + 8 * (size_t)c));
+#endif
+#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 4  // measurement only (tools/sp_phases_e4): no boundary stores
+        } else if (false) {
+#else
         } else if (c < nchunks) {  // the range's first / last chunk (shared with the neighbouring tiles)
+#endif
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const int64_t u = (int64_t)c * 8 + i - O;
@@ -767,88 +791,166 @@ __device__ __forceinline__ uint32_t valid_w32(size_t n, size_t tile) {
     const size_t base = tile * kTile + (size_t)(threadIdx.x & 63) * kCW;
     return base >= n ? 0u : (n - base >= (size_t)kCW ? 0xFFFFFFFFu : (1u << (n - base)) - 1u);
 }
-// kept(g[tile0 - 1]) for lane 0 (0 for the first tile): a vector load of a wave-uniform address
-__device__ __forceinline__ uint32_t kept_before_tile(const float *__restrict__ g, size_t tile, float t) {
-    if (tile == 0) return 0u;
-    uint32_t a = (uint32_t)(tile * kTile - 1);
-    asm volatile("" : "+v"(a));
-    return kept(g[a], t) ? 1u : 0u;
+// A workgroup takes kCountTpw tiles at a time (a wave each) and strides over the tiles by the grid
+// (count_grid: a few workgroups per CU), the wave's next tile loaded while the current one is
+// counted and stored.  One tile per wave in a single pass (every workgroup resident at once, 8 KiB
+// requested per wave at the start) read g at about 4.5 TB/s: the one-shot shape of DESIGN §2.
+//
+// The compaction walks only the lanes' kept values — the lane's 32 values as f16 in its LDS row
+// (80 B apart: the 16-B writes conflict-free), then max-over-lanes-of-kept steps of one LDS read and one
+// write each (a lane out of values writes its dummy slot) — 1 us per drop less than 32 predicated
+// LDS writes per lane (profiles/r05_s67_*).
+constexpr int kCRow = 40;  // u16 per padded lane row (64 B of values + 16 B)
+typedef _Float16 h2s __attribute__((ext_vector_type(2)));
+typedef float f2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {  // v_cvt_pk_f16_f32: the to_f16_sp rounding
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2s){a, b}, h2s));
 }
-
 __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, size_t n, size_t ntiles, float t,
                                                 const float *t_dev, bool vec, uint32_t *__restrict__ mask,
                                                 uint16_t *__restrict__ cv, uint2 *__restrict__ recA, uint4 *agg,
                                                 uint4 *agg_next, uint32_t gcap) {
     __shared__ uint32_t s_fr[kCountTpw][2], s_lk[kCountTpw], s_fu[kCountTpw];
+    // a wave's compact values (+ a dummy slot per lane)
+    __shared__ __attribute__((aligned(16))) uint16_t s_cv[kCountTpw][kTile + 64];
+    __shared__ __attribute__((aligned(16))) uint16_t s_row[kCountTpw][64 * kCRow];  // the lanes' values as f16
+    SP_CLOCK(sp_t0);
     if (t_dev) t = *t_dev;
     for (size_t i = (size_t)blockIdx.x * kSB + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kSB)
         agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const size_t tile = (size_t)blockIdx.x * kCountTpw + wave;
-    uint32_t F = 0, R = 0, LK = 0, FU = kTile;
-    if (tile < ntiles) {
-        float x[kCW];
-        const uint32_t pb = kept_before_tile(g, tile, t);
-        if (vec && (tile + 1) * kTile <= n) load_w32<true>(g, n, tile, x);
-        else load_w32<false>(g, n, tile, x);
-        const uint32_t valid = valid_w32(n, tile);
-        uint32_t keep = 0;
+    const size_t step = (size_t)gridDim.x * kCountTpw;
+#ifdef ONO_SP_STAMP
+    uint64_t sp_tm = sp_t0;
+#endif
+    // the wave's tile's values and the value before the tile (lane 0's previous bit), loaded ahead
+    float x[kCW];
+    float xb = 0.0f;
+    auto load = [&](size_t tl) {
+        if (tl >= ntiles) return;
+        if (vec && (tl + 1) * kTile <= n) load_w32<true>(g, n, tl, x);
+        else load_w32<false>(g, n, tl, x);
+        uint32_t a = (uint32_t)(tl ? tl * kTile - 1 : 0);
+        asm volatile("" : "+v"(a));  // (a vector load)
+        xb = g[a];
+    };
+    size_t tile = (size_t)blockIdx.x * kCountTpw + wave;
+    load(tile);
+    for (size_t b0 = (size_t)blockIdx.x * kCountTpw; b0 < ntiles; b0 += step, tile += step) {
+        uint32_t F = 0, R = 0, LK = 0, FU = kTile;
+        if (tile < ntiles) {
+            const uint32_t valid = valid_w32(n, tile);
+#ifdef ONO_SP_STAMP
+            if (b0 == (size_t)blockIdx.x * kCountTpw) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                sp_tm = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
+            uint32_t keep = 0;
 #pragma unroll
-        for (int e = 0; e < kCW; e++) keep |= kept(x[e], t) ? 1u << e : 0u;
-        keep &= valid;
-        uint32_t prev = lane_before(keep >> 31);
-        if (lane == 0) prev = pb;
-        const uint32_t start = keep & ~((keep << 1) | prev), unk = valid & ~keep;
-        mask[tile * 64 + lane] = keep;
-        const uint32_t lo = (uint32_t)lane * kCW;
-        // the tile's kept values as f16, compact, in its slot of cv (in order: the lanes' exclusive prefix)
-        const uint32_t kc = (uint32_t)__popc(keep), incl = wave_incl_sum_dpp(kc);
-        uint32_t cp = incl - kc;
-        uint16_t *cvt = cv + tile * kTile;
+            for (int e = 0; e < kCW; e++) keep |= kept(x[e], t) ? 1u << e : 0u;
+            keep &= valid;
+            uint32_t prev = lane_before(keep >> 31);
+            if (lane == 0) prev = tile && kept(xb, t) ? 1u : 0u;
+            const uint32_t start = keep & ~((keep << 1) | prev), unk = valid & ~keep;
+#if defined(ONO_EXP_COUNT) && ONO_EXP_COUNT >= 2  // measurement only (tools/sp_phases_c2): the loads and the flags
+            if (lane == 0) recA[tile] = make_uint2(keep, start);
+            load(tile + step);
+            continue;
+#endif
+            mask[tile * 64 + lane] = keep;
+            const uint32_t lo = (uint32_t)lane * kCW;
+            // the tile's kept values as f16, compact, in its slot of cv (in order: the lanes' exclusive
+            // prefix), through LDS so that the stores are 16-B pieces (2-byte stores from every lane: +5 us
+            // per drop); the wave's next tile requested once its values are in LDS
+            const uint32_t kc = (uint32_t)__popc(keep), incl = wave_incl_sum_dpp(kc);
+            F = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            typedef __attribute__((address_space(3))) uint16_t lds_u16;
+            lds_u16 *sc = (lds_u16 *)s_cv[wave];
+            uint32_t cp = incl - kc;
+#ifndef ONO_EXP_COUNT  // (measurement builds: no compaction)
+            typedef __attribute__((address_space(3))) u4v lds_w4;
+            lds_u16 *rw = (lds_u16 *)s_row[wave] + lane * kCRow;
 #pragma unroll
-        for (int e = 0; e < kCW; e++)
-            if (keep >> e & 1u) cvt[cp++] = to_f16_sp(x[e]);
-        F = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(start)), 63);
-        LK = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(keep ? lo + 32u - (uint32_t)__clz(keep) : 0u), 63);
-        FU = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile), 63);
-        if (lane == 0) recA[tile] = make_uint2(F | R << 16, LK | FU << 16);
+            for (int q = 0; q < kCW / 8; q++) {
+                u4v w;
+                w.x = pk_f16(x[8 * q], x[8 * q + 1]);
+                w.y = pk_f16(x[8 * q + 2], x[8 * q + 3]);
+                w.z = pk_f16(x[8 * q + 4], x[8 * q + 5]);
+                w.w = pk_f16(x[8 * q + 6], x[8 * q + 7]);
+                ((lds_w4 *)rw)[q] = w;
+            }
+            const uint32_t steps = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(kc), 63);
+            uint32_t m = keep;
+            for (uint32_t k = 0; k < steps; k++) {
+                const bool has = m != 0u;
+                const uint32_t e = has ? (uint32_t)__ffs(m) - 1u : 0u;
+                const uint16_t v = rw[e];
+                sc[has ? cp : (uint32_t)kTile + lane] = v;
+                cp += has ? 1u : 0u;
+                m &= m - 1u;
+            }
+#endif
+            load(tile + step);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            typedef __attribute__((address_space(3))) const u4v lds_cw4;
+            const lds_cw4 *s4 = (const lds_cw4 *)s_cv[wave];
+            u4v *d4 = (u4v *)(cv + tile * kTile);
+            for (uint32_t c = (uint32_t)lane; c < (F + 7) / 8; c += 64) d4[c] = s4[c];
+            R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(start)), 63);
+            LK = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(keep ? lo + 32u - (uint32_t)__clz(keep) : 0u), 63);
+            FU = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile), 63);
+            if (lane == 0) recA[tile] = make_uint2(F | R << 16, LK | FU << 16);
+        }
+        if (lane == 0) {
+            s_fr[wave][0] = F;
+            s_fr[wave][1] = R;
+            s_lk[wave] = F ? (uint32_t)(tile * kTile) + LK : 0u;  // global last kept + 1 (0: none)
+            s_fu[wave] = FU < (uint32_t)kTile ? ~((uint32_t)(tile * kTile) + FU) : 0u;  // complemented (0: none)
+        }
+        __syncthreads();
+#ifdef ONO_EXP_NOATOM  // measurement only (tools/sp_phases_na): sp_count without its chunk atomics, wrong wire
+        if (false) {
+#else
+        if (threadIdx.x == 0) {
+#endif
+            uint64_t fr = 0;
+            uint32_t lk = 0, nfu = 0;
+#pragma unroll
+            for (int w = 0; w < kCountTpw; w++) {
+                fr += (uint64_t)s_fr[w][0] | (uint64_t)s_fr[w][1] << 32;
+                lk = max(lk, s_lk[w]);
+                if (!nfu) nfu = s_fu[w];  // the first tile's first unkept
+            }
+            uint32_t *a = (uint32_t *)(agg + (b0 / kRecChunk) * kAggStride);
+            if (fr) {
+                atomicAdd((unsigned long long *)a, (unsigned long long)fr);
+                atomicMax(a + 2, lk);
+            }
+            if (nfu) atomicMax(a + 3, nfu);
+        }
+        __syncthreads();  // s_fr.. read before the next round writes them
     }
-    if (lane == 0) {
-        s_fr[wave][0] = F;
-        s_fr[wave][1] = R;
-        s_lk[wave] = F ? (uint32_t)(tile * kTile) + LK : 0u;  // global last kept + 1 (0: none)
-        s_fu[wave] = FU < (uint32_t)kTile ? ~((uint32_t)(tile * kTile) + FU) : 0u;  // complemented (0: none)
-    }
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0 && (size_t)blockIdx.x * kCountTpw < ntiles) {
-        uint64_t fr = 0;
-        uint32_t lk = 0, nfu = 0;
-#pragma unroll
-        for (int w = 0; w < kCountTpw; w++) {
-            fr += (uint64_t)s_fr[w][0] | (uint64_t)s_fr[w][1] << 32;
-            lk = max(lk, s_lk[w]);
-            if (!nfu) nfu = s_fu[w];  // the first tile's first unkept
-        }
-        uint32_t *a = (uint32_t *)(agg + ((size_t)blockIdx.x * kCountTpw / kRecChunk) * kAggStride);
-        if (fr) {
-            atomicAdd((unsigned long long *)a, (unsigned long long)fr);
-            atomicMax(a + 2, lk);
-        }
-        if (nfu) atomicMax(a + 3, nfu);
-    }
+    if (threadIdx.x < 64) sp_stamp(g_sp_stamp_img, blockIdx.x, sp_t0, sp_tm);  // mid: the wave's first values loaded
+#endif
 }
 
 // STAGE: a tile's range of at most kEmitStage units is built in LDS and stored in 16-B chunks (a longer
 // one, and every range without STAGE, unit by unit straight to the wire)
-constexpr int kEmitStage = 2048;
+constexpr int kEmitStage = 1520;  // units (+16 spare: 3 KB); with kEmitVals values (2 KB) 8 workgroups of 4 waves per CU
+constexpr int kEmitVals = 1024;
 template <bool STAGE>
 __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
                                                const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
                                                const uint4 *__restrict__ agg, uint8_t *__restrict__ buf,
                                                uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
-    __shared__ __attribute__((aligned(16))) uint16_t vals[kSB / 64][kTile];  // per wave: the tile's compact values
+    __shared__ __attribute__((aligned(16))) uint16_t vals[kSB / 64][kEmitVals];  // per wave: the tile's compact values
     __shared__ __attribute__((aligned(16))) uint16_t stage[STAGE ? kSB / 64 : 1][STAGE ? kEmitStage + 16 : 8];
+    SP_CLOCK(sp_t0);
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         const uint2 t = chunk_totals(agg, G);
@@ -869,8 +971,17 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     uint32_t pa = (uint32_t)(tile ? tile * 64 - 1 : 0);
     asm volatile("" : "+v"(pa));  // (a vector load)
     const uint32_t pw = mask[pa];
+    // the first 512 of the tile's compact values, before the count is known (sp_count's slot; the
+    // rest, rarely there, after it)
+    const u4v *src = (const u4v *)(cv + tile * kTile);
+    const u4v v0 = src[lane];
     uint2 own;
+#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 2  // measurement only (tools/sp_phases_e2): no prefix, wrong wire
+    own = recA[tile];
+    const uint4 p = make_uint4(0u, 0u, 0u, (uint32_t)n);
+#else
     const uint4 p = tile_prefix(recA, agg, ntiles, G, tile, (uint32_t)n, &own);  // F0, R0, P, Q
+#endif
     const uint32_t valid = valid_w32(n, tile), unk = valid & ~keep;
     uint32_t prev = lane_before(keep >> 31);
     if (lane == 0) prev = tile ? pw >> 31 : 0u;
@@ -892,20 +1003,26 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     // the tile's compact values (sp_count's slot) into LDS in 16-B pieces, read below by position: the
     // lane's k-th kept value is the tile's (ef + k)-th
     const uint32_t Ft = own.x & 0xFFFFu;
-    {
+    const bool fits = Ft <= (uint32_t)kEmitVals;  // (uniform) else the values are read from cv one by one
+    if (fits) {
         typedef __attribute__((address_space(3))) u4v lds_w4;
         lds_w4 *vw = (lds_w4 *)vals[wave];
-        const u4v *src = (const u4v *)(cv + tile * kTile);
-        for (uint32_t c = lane; c < (Ft + 7) / 8; c += 64) vw[c] = src[c];
+        if (lane < (Ft + 7) / 8) vw[lane] = v0;
+        for (uint32_t c = lane + 64; c < (Ft + 7) / 8; c += 64) vw[c] = src[c];
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
+#ifdef ONO_SP_STAMP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SP_CLOCK(sp_tm);  // the mask, the prefix and the values in
+#endif
     typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
     lds_cu16 *v16 = (lds_cu16 *)vals[wave] + ef;
+    const uint16_t *g16 = cv + tile * kTile + ef;
     uint16_t *w16 = (uint16_t *)(buf + 8);
     const size_t U0 = 4 * (size_t)p.y + (size_t)p.x;  // the tile's first unit
     const uint32_t nu16 = 4 * (own.x >> 16) + (own.x & 0xFFFFu);
-    if (STAGE && nu16 <= (uint32_t)kEmitStage) {  // (uniform)
+    if (STAGE && fits && nu16 <= (uint32_t)kEmitStage) {  // (uniform)
         typedef __attribute__((address_space(3))) uint16_t lds_u16;
         lds_u16 *st = (lds_u16 *)stage[STAGE ? wave : 0];
         uint32_t lp = 4 * es + ef, kv = 0;  // the lane's first unit within the tile's range; its kept values
@@ -933,6 +1050,9 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
         const uint32_t O = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uintptr_t)dst & 15u) >> 1));
         uint16_t *base16 = (uint16_t *)(dst - 2 * O);
         const lds_u4 *s4 = (const lds_u4 *)stage[STAGE ? wave : 0];
+#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 1  // measurement only (tools/sp_phases_e1): no wire stores
+        if (nu16 != 0xFFFFFFFFu) return;
+#endif
         switch (O) {
         case 0: stage_out<0>(s4, nu16, base16); break;
         case 1: stage_out<1>(s4, nu16, base16); break;
@@ -943,6 +1063,9 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
         case 6: stage_out<6>(s4, nu16, base16); break;
         default: stage_out<7>(s4, nu16, base16); break;
         }
+#ifdef ONO_SP_STAMP
+        sp_stamp(g_sp_stamp_mov, tile, sp_t0, sp_tm);
+#endif
         return;
     }
     size_t pos = U0 + 4 * (size_t)es + ef;  // the lane's first unit
@@ -963,8 +1086,12 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
             w16[pos + 3] = (uint16_t)(len >> 16);
             pos += 4;
         }
-        w16[pos++] = v16[kv++];
+        w16[pos++] = fits ? v16[kv] : g16[kv];
+        kv++;
     }
+#ifdef ONO_SP_STAMP
+    sp_stamp(g_sp_stamp_mov, tile, sp_t0, sp_tm);
+#endif
 }
 
 // ------------------------------------------------- one-launch encoder ----
@@ -3552,14 +3679,27 @@ bool drop_fused() {
     }();
     return v;
 }
-// ONO_DROP_FORM=emit: the two launches without the slot image (sp_count + sp_emit); image (default):
-// sp_image + sp_move
+// The two launches above the one-launch size: sp_count + sp_emit (default: 30.2 vs 34.0 us per 64 MiB
+// drop, profiles/r05_s69_*); ONO_DROP_FORM=image: sp_image + sp_move (the round-4 form, kept for A/B)
 bool drop_emit() {
     static const bool v = [] {
         const char *e = getenv("ONO_DROP_FORM");
-        return e && !strcmp(e, "emit");
+        return !(e && !strcmp(e, "image"));
     }();
     return v;
+}
+// sp_count's grid: ONO_COUNT_WGS workgroups per CU (default 4), at most one per kCountTpw tiles
+size_t count_grid(size_t ntiles) {
+    static const size_t per = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        const char *e = getenv("ONO_COUNT_WGS");
+        const size_t w = e && *e ? (size_t)strtoul(e, nullptr, 10) : 4;
+        return (size_t)cus * (w ? w : 1);
+    }();
+    return std::max<size_t>(1, std::min(per, (ntiles + kCountTpw - 1) / kCountTpw));
 }
 // ONO_EMIT_STAGE=0: sp_emit stores every unit straight to the wire (default: through an LDS stage)
 bool emit_stage() {
@@ -3632,9 +3772,8 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     hipError_t e = hipSuccess;
     if (ntiles && emit) {
-        const size_t grid = (ntiles + kCountTpw - 1) / kCountTpw;
-        hipLaunchKernelGGL(sp_count, dim3((unsigned)grid), dim3(kSB), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->mask,
-                           sc->cv, recA, agg, agg_next, (uint32_t)sc->agg_cap);
+        hipLaunchKernelGGL(sp_count, dim3((unsigned)count_grid(ntiles)), dim3(kSB), 0, s, g, n, ntiles, threshold, t_dev, vec,
+                           sc->mask, sc->cv, recA, agg, agg_next, (uint32_t)sc->agg_cap);
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     } else if (ntiles) {
@@ -3653,6 +3792,9 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (e != hipSuccess) return hip_error(e, "sparse encode", __FILE__, __LINE__);
     const size_t mblocks = std::max<size_t>(1, (ntiles + kSB / 64 - 1) / (kSB / 64));
+#ifdef ONO_EXP_COUNT
+    if (emit) return 0;  // measurement builds: sp_count alone
+#endif
     if (emit && emit_stage())
         hipLaunchKernelGGL(sp_emit<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA,
                            agg, buf, sc->host_tot_dev, nbytes_dev);

@@ -300,6 +300,22 @@ def test_drop_headers_across_tiles_and_scan_chunks(pattern):
     assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
 
 
+@pytest.mark.parametrize("first_unkept", [128 * 2048 * 2 + 5, 128 * 2048 * 3 - 1, 128 * 2048 * 4 + 77, None])
+def test_drop_whole_chunks_kept(first_unkept):
+    """Chunks of 128 tiles with every value kept: the last run's length in a
+    tile comes from the first unkept value in a later chunk (two, three or
+    more chunks on), or from n when there is none."""
+    n = 128 * 2048 * 5 + 301
+    g = np.full(n, 2.0, np.float32)
+    if first_unkept is not None:
+        g[first_unkept] = 0.0
+        g[first_unkept + 1000::7] = 0.0
+    got = SP.grad_drop_dev(dev(g), 0.5)
+    want = O.grad_drop(g, 0.5)
+    assert bytes(got.cpu().numpy()) == want
+    assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
+
+
 @pytest.mark.parametrize("pattern", ["all_kept", "none_kept", "tile_edges", "clustered", "single_tail"])
 def test_drop_tile_boundary_patterns(pattern):
     """The encoder's cross-tile header fields (sp_move completes the first
@@ -598,3 +614,33 @@ def test_drop_one_launch_matches_oracle(polls, small):
                        text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip() == "ok %d" % (4 if small else 2)
+
+
+IMAGE_FORM_WORKER = r"""
+import sys
+import numpy as np
+import torch
+sys.path[:0] = [{root!r}, {root!r} + "/oxidized-neural-orchestra_amd", {root!r} + "/tests"]
+from ono_amd import sparse as SP
+from oracle import oracle as O
+rng = np.random.default_rng(11)
+for n, r in [(256 * 2048 + 1, 0.9), (1 << 20, 0.5), (3 * 128 * 2048 + 77, 0.0), (5_000_003, 0.99)]:
+    g = rng.standard_normal(n).astype(np.float32)
+    t = float(np.quantile(np.abs(g), r))
+    got = bytes(SP.grad_drop_dev(torch.from_numpy(g).cuda(), t).cpu().numpy())
+    assert got == O.grad_drop(g, t), (n, r)
+print("ok")
+"""
+
+
+def test_drop_image_form_matches_oracle():
+    """The round-4 form (sp_image + sp_move, ONO_DROP_FORM=image, read once per
+    process) still gives the reference's bytes above the one-launch size."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ONO_DROP_FORM="image")
+    r = subprocess.run([sys.executable, "-c", IMAGE_FORM_WORKER.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]

@@ -184,6 +184,18 @@ int main(int argc, char **argv) {
         printf("\n");
         return 0;
     }
+    if (drop_emit()) {  // sp_count per workgroup (mid: its waves' values loaded), sp_emit per wave
+        const size_t ncw = count_grid(ntiles);
+        std::vector<uint4> sc(ncw), se(ntiles);
+        CK(hipMemcpyFromSymbol(sc.data(), HIP_SYMBOL(g_sp_stamp_img), ncw * sizeof(uint4)));
+        CK(hipMemcpyFromSymbol(se.data(), HIP_SYMBOL(g_sp_stamp_mov), ntiles * sizeof(uint4)));
+        uint32_t base = sc[0].x;
+        for (const uint4 &v : sc) base = (int32_t)(v.x - base) < 0 ? v.x : base;
+        printf("# times in us from sp_count's first workgroup start (the last drop; sp_emit mid: its loads in)\n");
+        report("sp_count", sc, base);
+        report("sp_emit", se, base);
+        return 0;
+    }
     std::vector<uint4> si(nwg), sm(ntiles);
     CK(hipMemcpyFromSymbol(si.data(), HIP_SYMBOL(g_sp_stamp_img), nwg * sizeof(uint4)));
     CK(hipMemcpyFromSymbol(sm.data(), HIP_SYMBOL(g_sp_stamp_mov), ntiles * sizeof(uint4)));
