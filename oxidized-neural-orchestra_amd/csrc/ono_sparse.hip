@@ -568,6 +568,108 @@ __device__ __forceinline__ uint2 chunk_totals(const uint4 *agg, uint32_t G) {
                       (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(r), 63));
 }
 
+// tile_prefix for kGP consecutive tiles tb.. (one chunk: tb % kGP == 0), by one wave:
+// the records and aggregates are loaded once, reduced once for the first tile (kept values, runs and
+// last kept before it; first unkept after the last), and the other tiles' prefixes follow from the
+// group's own records.  pre[k] / own[k] for tile tb + k (tiles past ntiles: left alone).  sp_emit's
+// four waves then share one set of loads: every wave of the grid reads the same few aggregate lines
+// at the same moment, and a quarter of the requests shortens that phase.
+constexpr int kGP = kSB / 64;  // tiles per group_prefix (sp_emit's workgroup, sp_count's kCountTpw)
+__device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg, size_t ntiles, uint32_t G, size_t tb,
+                                             uint32_t n, uint4 (&pre)[kGP], uint2 (&own)[kGP]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = (uint32_t)(tb / kRecChunk), cs = c * (uint32_t)kRecChunk;
+    const uint32_t i0 = (uint32_t)tb - cs, m = (uint32_t)min((size_t)kRecChunk, ntiles - cs);
+    uint2 r[kRecChunk / 64];
+#pragma unroll
+    for (int k = 0; k < kRecChunk / 64; k++) r[k] = recA[cs + min(lane + 64 * k, m - 1)];
+#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 6  // measurement only (tools/sp_phases_e6): no records, wrong wire
+    r[0] = r[1] = make_uint2(0u, 0u);
+#endif
+    uint4 a[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t j = 64 * k + lane;
+        a[k] = make_uint4(0u, 0u, 0u, 0u);
+#if !defined(ONO_EXP_EMIT) || ONO_EXP_EMIT != 5  // (measurement only, tools/sp_phases_e5: no aggregates, wrong wire)
+        if (64 * k < G && (j < c || j == c + 1) && j < G) a[k] = agg[(size_t)j * kAggStride];
+#endif
+    }
+    uint32_t f = 0, s = 0, mx = 0, q = n;
+    for (uint32_t j0 = 256; j0 < c; j0 += 64) {  // chunks before past the first 256 (G > 256: n > 2^26)
+        const uint32_t j = j0 + lane;
+        const uint4 b = j < c ? agg[(size_t)j * kAggStride] : make_uint4(0u, 0u, 0u, 0u);
+        f += b.x;
+        s += b.y;
+        mx = max(mx, b.z);
+    }
+    if (c + 1 >= 256 && c + 1 < G && lane == 0) {
+        const uint32_t w = agg[(size_t)(c + 1) * kAggStride].w;
+        q = w ? ~w : q;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t j = 64 * k + lane;
+        const bool before = j < c;
+        f += before ? a[k].x : 0u;
+        s += before ? a[k].y : 0u;
+        mx = max(mx, before ? a[k].z : 0u);
+        q = min(q, j == c + 1 && a[k].w ? ~a[k].w : q);
+    }
+    const uint32_t ilast = i0 + kGP - 1;
+#pragma unroll
+    for (int k = 0; k < kRecChunk / 64; k++) {
+        const uint32_t j = lane + 64 * k, t0 = (cs + j) * (uint32_t)kTile;
+        if (j < i0) {
+            f += r[k].x & 0xFFFFu;
+            s += r[k].x >> 16;
+            const uint32_t l1 = r[k].y & 0xFFFFu;
+            if (l1) mx = max(mx, t0 + l1);
+        } else if (j > ilast && j < m) {
+            const uint32_t f1 = r[k].y >> 16;
+            if (f1 < (uint32_t)kTile) q = min(q, t0 + f1);
+        }
+    }
+    if (c + 2 < G && !__ballot(q < n)) {  // as tile_prefix: the first later chunk with an unkept value
+        for (uint32_t j0 = c + 2; j0 < G; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            const uint32_t w = j < G ? agg[(size_t)j * kAggStride].w : 0u;
+            q = min(q, w ? ~w : q);
+            if (__ballot(q < n)) break;
+        }
+    }
+    uint32_t F = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(f), 63);
+    uint32_t S = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(s), 63);
+    uint32_t MX = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(mx), 63);
+    uint32_t Q = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(q), 63);
+    uint2 rg[kGP];
+#pragma unroll
+    for (int k = 0; k < kGP; k++) {  // the group's own records (i0 + k < 128: one of the two per lane)
+        const uint32_t i = i0 + k;
+        const uint2 lo2 = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)r[0].x, i & 63),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)r[0].y, i & 63));
+        const uint2 hi2 = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)r[1].x, i & 63),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)r[1].y, i & 63));
+        rg[k] = i < 64 ? lo2 : hi2;
+        own[k] = rg[k];
+    }
+    uint32_t Qk[kGP];
+    Qk[kGP - 1] = Q;
+#pragma unroll
+    for (int k = kGP - 2; k >= 0; k--) {  // first unkept after tile i0 + k: tile i0 + k + 1's, or later
+        const uint32_t i = i0 + k + 1, f1 = rg[k + 1].y >> 16;
+        Qk[k] = i < m && f1 < (uint32_t)kTile ? min(Qk[k + 1], (cs + i) * (uint32_t)kTile + f1) : Qk[k + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < kGP; k++) {
+        pre[k] = make_uint4(F, S, MX, Qk[k]);
+        const uint32_t l1 = rg[k].y & 0xFFFFu;
+        F += rg[k].x & 0xFFFFu;
+        S += rg[k].x >> 16;
+        if (l1) MX = max(MX, (cs + i0 + k) * (uint32_t)kTile + l1);
+    }
+}
+
 // One tile's slot -> its place in the wire, in 16-B chunks of the
 // destination: the range starts O units (0..7, uniform) into its first
 // aligned chunk, so destination chunk c takes slot units 8c - O .. 8c - O + 7
@@ -769,7 +871,7 @@ __global__ __launch_bounds__(kSB) void sp_move(
 // Traffic: 4 N (+ the re-read from cache) + the wire + the mask (N / 8, written and read).
 constexpr int kCW = 32;                // values per lane: one wave per 2048-value tile
 static_assert(64 * kCW == kTile, "a wave holds a tile");
-constexpr int kCountTpw = kSB / 64;   // tiles per sp_count workgroup (a wave each): one set of atomics
+constexpr int kCountTpw = kGP;        // tiles per sp_count workgroup (a wave each): one set of atomics
 static_assert(kRecChunk % kCountTpw == 0, "a workgroup's tiles share one chunk aggregate");
 
 template <bool FULL>
@@ -941,7 +1043,7 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
 
 // STAGE: a tile's range of at most kEmitStage units is built in LDS and stored in 16-B chunks (a longer
 // one, and every range without STAGE, unit by unit straight to the wire)
-constexpr int kEmitStage = 1520;  // units (+16 spare: 3 KB); with kEmitVals values (2 KB) 8 workgroups of 4 waves per CU
+constexpr int kEmitStage = 1504;  // units (+16 spare); with kEmitVals values and the shared prefixes 20 KB: 8 workgroups per CU
 constexpr int kEmitVals = 1024;
 template <bool STAGE>
 __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
@@ -962,26 +1064,36 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
         }
     }
     const int wave = threadIdx.x >> 6;
-    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + wave));
-    if (tile >= ntiles) return;  // (no barrier below)
+    const size_t tb = (size_t)blockIdx.x * kCountTpw;  // the workgroup's first tile (< ntiles)
+    const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(tb + wave));
+    const bool live = tile < ntiles;  // (wave-uniform; every wave reaches the barrier below)
+    const size_t tl = live ? tile : tb;  // (a dead wave's loads: the group's first tile, unused)
     const uint32_t lane = threadIdx.x & 63, lo = lane * kCW;
     const uint32_t tile0 = (uint32_t)(tile * kTile);
     // every load first: the lane's mask word, the bit before the tile, the values, the prefix's records
-    const uint32_t keep = mask[tile * 64 + lane];
-    uint32_t pa = (uint32_t)(tile ? tile * 64 - 1 : 0);
+    const uint32_t keep = mask[tl * 64 + lane];
+    uint32_t pa = (uint32_t)(tl ? tl * 64 - 1 : 0);
     asm volatile("" : "+v"(pa));  // (a vector load)
     const uint32_t pw = mask[pa];
     // the first 512 of the tile's compact values, before the count is known (sp_count's slot; the
     // rest, rarely there, after it)
-    const u4v *src = (const u4v *)(cv + tile * kTile);
+    const u4v *src = (const u4v *)(cv + tl * kTile);
     const u4v v0 = src[lane];
-    uint2 own;
-#if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 2  // measurement only (tools/sp_phases_e2): no prefix, wrong wire
-    own = recA[tile];
-    const uint4 p = make_uint4(0u, 0u, 0u, (uint32_t)n);
-#else
-    const uint4 p = tile_prefix(recA, agg, ntiles, G, tile, (uint32_t)n, &own);  // F0, R0, P, Q
-#endif
+    // the prefixes of the workgroup's tiles (F0, R0, P, Q) and their records, by wave 0, through LDS
+    __shared__ uint4 s_pre[kCountTpw];
+    __shared__ uint2 s_own[kCountTpw];
+    if (wave == 0) {
+        uint4 pre[kCountTpw];
+        uint2 ow[kCountTpw];
+        group_prefix(recA, agg, ntiles, G, tb, (uint32_t)n, pre, ow);
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < kCountTpw; k++) {
+                s_pre[k] = pre[k];
+                s_own[k] = ow[k];
+            }
+        }
+    }
     const uint32_t valid = valid_w32(n, tile), unk = valid & ~keep;
     uint32_t prev = lane_before(keep >> 31);
     if (lane == 0) prev = tile ? pw >> 31 : 0u;
@@ -1000,6 +1112,10 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     const int lk = kbm ? 63 - __clzll((long long)kbm) : 0, lu = uam ? __ffsll((unsigned long long)uam) - 1 : 0;
     const uint32_t ykb = (uint32_t)__shfl((int)k1, lk, 64), yua = (uint32_t)__shfl((int)u1, lu, 64);
     const uint32_t kept1_before = kbm ? ykb : 0u, unkept_after = uam ? yua : (uint32_t)kTile;
+    __syncthreads();
+    if (!live) return;  // (no barrier below)
+    const uint4 p = s_pre[wave];
+    const uint2 own = s_own[wave];
     // the tile's compact values (sp_count's slot) into LDS in 16-B pieces, read below by position: the
     // lane's k-th kept value is the tile's (ef + k)-th
     const uint32_t Ft = own.x & 0xFFFFu;

@@ -644,3 +644,22 @@ def test_drop_image_form_matches_oracle():
     r = subprocess.run([sys.executable, "-c", IMAGE_FORM_WORKER.format(root=root)], env=env, capture_output=True,
                        text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_drop_past_256_chunks():
+    """A gradient of more than 256 chunks of 128 tiles (n > 2^26): the
+    aggregates before the tile's chunk past the first 256, read in blocks of
+    64, and the next chunk's first unkept value past 256; runs across the chunk
+    edges there."""
+    n = (1 << 26) + 3 * 128 * 2048 + 999
+    g = np.zeros(n, np.float32)
+    chunk = 128 * 2048
+    for c in (0, 255, 256, 257, 300):
+        e = c * chunk
+        g[max(0, e - 5):e + 7] = 1.25 + c
+    g[260 * chunk:262 * chunk + 3] = -0.75          # a run over two whole chunks
+    g[n - 10:] = 2.5
+    got = SP.grad_drop_dev(dev(g), 0.5)
+    want = O.grad_drop(g, 0.5)
+    assert bytes(got.cpu().numpy()) == want
+    assert_bitexact(SP.grad_lift_dev(got, n).cpu().numpy(), O.grad_lift(want, cap=n))
