@@ -1045,6 +1045,10 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
 // one, and every range without STAGE, unit by unit straight to the wire)
 constexpr int kEmitStage = 1504;  // units (+16 spare); with kEmitVals values and the shared prefixes 20 KB: 8 workgroups per CU
 constexpr int kEmitVals = 1024;
+#ifndef ONO_EMIT_SPEC
+#define ONO_EMIT_SPEC 256
+#endif
+constexpr int kEmitSpec = ONO_EMIT_SPEC;  // values loaded speculatively (10 % kept: 205 +- 14 per tile)
 template <bool STAGE>
 __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
                                                const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
@@ -1075,10 +1079,11 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     uint32_t pa = (uint32_t)(tl ? tl * 64 - 1 : 0);
     asm volatile("" : "+v"(pa));  // (a vector load)
     const uint32_t pw = mask[pa];
-    // the first 512 of the tile's compact values, before the count is known (sp_count's slot; the
-    // rest, rarely there, after it)
+    // the first kEmitSpec of the tile's compact values, before the count is known (sp_count's slot;
+    // the rest, rarely there, after it)
     const u4v *src = (const u4v *)(cv + tl * kTile);
-    const u4v v0 = src[lane];
+    u4v v0 = {0u, 0u, 0u, 0u};
+    if (lane < kEmitSpec / 8) v0 = src[lane];
     // the prefixes of the workgroup's tiles (F0, R0, P, Q) and their records, by wave 0, through LDS
     __shared__ uint4 s_pre[kCountTpw];
     __shared__ uint2 s_own[kCountTpw];
@@ -1123,8 +1128,8 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     if (fits) {
         typedef __attribute__((address_space(3))) u4v lds_w4;
         lds_w4 *vw = (lds_w4 *)vals[wave];
-        if (lane < (Ft + 7) / 8) vw[lane] = v0;
-        for (uint32_t c = lane + 64; c < (Ft + 7) / 8; c += 64) vw[c] = src[c];
+        if (lane < (Ft + 7) / 8 && lane < kEmitSpec / 8) vw[lane] = v0;
+        for (uint32_t c = lane + (lane < kEmitSpec / 8 ? 64 : 0); c < (Ft + 7) / 8; c += 64) vw[c] = src[c];
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
