@@ -594,8 +594,9 @@ def path_kernels(torch, ono_amd, steps: int, warmup: int) -> dict:
 def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
     """the device top-k codec (comms/src/sparse/protocol.rs:57-144) on a 64 MiB
     gradient with the threshold at the 90th |g| percentile (~10 % of the values kept, the
-    reference's r = 0.9).  Drop = tile images + record scan + move, as a blocking call (the wire
-    length is needed on the host) and stream-ordered back to back; bytes = 4 N read + the wire
+    reference's r = 0.9).  Drop = count (flags, compact values, chunk aggregates) + emit (each
+    tile's runs and values to their place in the wire), as a blocking call (the wire length is needed
+    on the host) and stream-ordered back to back; bytes = 4 N read + the wire
     written.  Lift parses the
     run headers on the host and expands on the device (host buffer in)."""
     import ctypes as C
@@ -716,7 +717,7 @@ def sparse_codec(torch, ono_amd, rounds: int = 5) -> dict:
                      "stream_achieved_gbs": round(drop_bytes / tstream / 1e9, 1),
                      "stream_frac_of_hbm_peak": round(drop_bytes / tstream / 1e9 / HBM_PEAK_GBS, 4),
                      "note": "ms = wall time of the blocking C call; device_ms = HIP events around it on its "
-                             "stream (tile images + record scan + move, then the host read of the totals); "
+                             "stream (sp_count + sp_emit, then the host read of the totals); "
                              "stream_ms = per drop of %d stream-ordered drops back to back "
                              "(ono_sparse_drop_async) over %d different 64 MiB gradients in turn "
                              "(each read from HBM), one event pair" % (K, NG)},
