@@ -912,7 +912,8 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
                                                 const float *t_dev, bool vec, uint32_t *__restrict__ mask,
                                                 uint16_t *__restrict__ cv, uint2 *__restrict__ recA, uint4 *agg,
                                                 uint4 *agg_next, uint32_t gcap) {
-    __shared__ uint32_t s_fr[kCountTpw][2], s_lk[kCountTpw], s_fu[kCountTpw];
+    // per round's parity (thread 0 reads one round's while a faster wave writes the next one's)
+    __shared__ uint32_t s_fr[2][kCountTpw][2], s_lk[2][kCountTpw], s_fu[2][kCountTpw];
     // a wave's compact values (+ a dummy slot per lane)
     __shared__ __attribute__((aligned(16))) uint16_t s_cv[kCountTpw][kTile + 64];
     __shared__ __attribute__((aligned(16))) uint16_t s_row[kCountTpw][64 * kCRow];  // the lanes' values as f16
@@ -938,6 +939,7 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
     };
     size_t tile = (size_t)blockIdx.x * kCountTpw + wave;
     load(tile);
+    int par = 0;
     for (size_t b0 = (size_t)blockIdx.x * kCountTpw; b0 < ntiles; b0 += step, tile += step) {
         uint32_t F = 0, R = 0, LK = 0, FU = kTile;
         if (tile < ntiles) {
@@ -1006,10 +1008,10 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
             if (lane == 0) recA[tile] = make_uint2(F | R << 16, LK | FU << 16);
         }
         if (lane == 0) {
-            s_fr[wave][0] = F;
-            s_fr[wave][1] = R;
-            s_lk[wave] = F ? (uint32_t)(tile * kTile) + LK : 0u;  // global last kept + 1 (0: none)
-            s_fu[wave] = FU < (uint32_t)kTile ? ~((uint32_t)(tile * kTile) + FU) : 0u;  // complemented (0: none)
+            s_fr[par][wave][0] = F;
+            s_fr[par][wave][1] = R;
+            s_lk[par][wave] = F ? (uint32_t)(tile * kTile) + LK : 0u;  // global last kept + 1 (0: none)
+            s_fu[par][wave] = FU < (uint32_t)kTile ? ~((uint32_t)(tile * kTile) + FU) : 0u;  // complemented (0: none)
         }
         __syncthreads();
 #ifdef ONO_EXP_NOATOM  // measurement only (tools/sp_phases_na): sp_count without its chunk atomics, wrong wire
@@ -1021,9 +1023,9 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
             uint32_t lk = 0, nfu = 0;
 #pragma unroll
             for (int w = 0; w < kCountTpw; w++) {
-                fr += (uint64_t)s_fr[w][0] | (uint64_t)s_fr[w][1] << 32;
-                lk = max(lk, s_lk[w]);
-                if (!nfu) nfu = s_fu[w];  // the first tile's first unkept
+                fr += (uint64_t)s_fr[par][w][0] | (uint64_t)s_fr[par][w][1] << 32;
+                lk = max(lk, s_lk[par][w]);
+                if (!nfu) nfu = s_fu[par][w];  // the first tile's first unkept
             }
             uint32_t *a = (uint32_t *)(agg + (b0 / kRecChunk) * kAggStride);
             if (fr) {
@@ -1032,7 +1034,7 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
             }
             if (nfu) atomicMax(a + 3, nfu);
         }
-        __syncthreads();  // s_fr.. read before the next round writes them
+        par ^= 1;  // (a round's words are written again two rounds on, after the next round's barrier)
     }
 #ifdef ONO_SP_STAMP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
