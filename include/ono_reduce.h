@@ -147,7 +147,9 @@ int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t
 /* The drop keeps device scratch per (device, stream), grown to the largest
  * gradient seen and never shrunk: above 256 tiles of 2048 values about 2.1
  * bytes per value (the keep flags and a f16 slot per tile for the kept
- * values) plus 16 bytes per tile; up to 256 tiles 32 bytes per tile.       */
+ * values) plus 16 bytes per tile; up to 256 tiles 32 bytes per tile.
+ * Neither drop can be captured into a HIP graph (ONO_E_ARG): the launches
+ * keep host-side state between calls that a replay would not follow.       */
 int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
                     float threshold, void *stream);
 /* The stream-ordered drop: the same bytes, nothing waits on the host; the

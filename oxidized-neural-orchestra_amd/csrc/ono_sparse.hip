@@ -3884,6 +3884,9 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
         *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
         return ONO_OK;
     }
+    // not under stream capture: the two launches keep host-side state between calls (which chunk
+    // aggregates are zero), which a replayed graph would not follow
+    if (capturing) return set_error(ONO_E_ARG, "the sparse drop cannot be captured into a graph");
     const bool emit = drop_emit();
     int rc = scratch_for(ntiles, s, &sc, true, emit);
     if (rc) return rc;
