@@ -35,6 +35,9 @@ __global__ __launch_bounds__(256) void ranges(uint16_t *w, size_t ntiles, unsign
     }
 }
 
+__global__ __launch_bounds__(512) void empty512(uint16_t *w) { if (threadIdx.x == 1023) w[0] = 0; }
+__global__ __launch_bounds__(1024) void empty1024(uint16_t *w) { if (threadIdx.x == 2047) w[0] = 0; }
+
 int main(int argc, char **argv) {
     const size_t ntiles = argc > 1 ? atoi(argv[1]) : 8192;
     const unsigned U = argc > 2 ? atoi(argv[2]) : 941;
@@ -68,5 +71,11 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(ranges<true>, dim3((ntiles + 3) / 4), dim3(256), 0, 0, p, ntiles, U); });
     run("empty kernel, same grid", [&](uint16_t *p) {
         hipLaunchKernelGGL(ranges<false>, dim3((ntiles + 3) / 4), dim3(256), 0, 0, p, 0, U); });
+    run("empty kernel, half the workgroups x 512", [&](uint16_t *p) {
+        hipLaunchKernelGGL(empty512, dim3((ntiles + 7) / 8), dim3(512), 0, 0, p); });
+    run("empty kernel, a quarter x 1024", [&](uint16_t *p) {
+        hipLaunchKernelGGL(empty1024, dim3((ntiles + 15) / 16), dim3(1024), 0, 0, p); });
+    run("empty kernel, 1 workgroup", [&](uint16_t *p) {
+        hipLaunchKernelGGL(ranges<false>, dim3(1), dim3(256), 0, 0, p, 0, U); });
     return 0;
 }
