@@ -859,16 +859,18 @@ __global__ __launch_bounds__(kSB) void sp_move(
 
 
 // -------------------------------------------------- count + emit encoder ----
-// Round 5 (the 64 MiB drop): two launches without the slot image.  sp_count reads g
-// once, one wave per tile with 32 values per lane: the keep flags as one 32-bit word per lane (256 B
-// per tile, the "mask"), the tile's record (recA, as sp_image writes it) and the chunk aggregates (four
-// tiles per workgroup, one set of atomics).  sp_emit, one wave per tile: the tile's prefix from the
-// records and aggregates (tile_prefix, as sp_move), the run starts and the thread's place from the mask
-// and one DPP scan, the tile's values read again (an L2 / Infinity Cache hit straight after sp_count)
-// into f16 words in LDS (transposed: every read conflict-free), and every unit stored straight to its
-// place in the wire — each header with its global offset and length (the previous kept index and the
-// next unkept one from the thread, the wave, or the prefix P / Q), so no field is completed later.
-// Traffic: 4 N (+ the re-read from cache) + the wire + the mask (N / 8, written and read).
+// Round 5 (the 64 MiB drop): two launches without the slot image, the default above
+// kDropOneLaunchTiles (ONO_DROP_FORM=image keeps sp_image + sp_move).  sp_count reads g once, one wave
+// per tile with 32 values per lane: the keep flags as one 32-bit word per lane (256 B per tile, the
+// "mask"), the tile's kept values as compact f16 in its slot of cv, the tile's record (recA, as sp_image
+// writes it) and the chunk aggregates (four tiles per workgroup round, one set of atomics).  sp_emit,
+// one wave per tile: the workgroup's four prefixes from one wave (group_prefix, through LDS), the run
+// starts and the thread's place from the mask and one DPP scan, the compact values into LDS, and the
+// tile's range built in an LDS stage — each header with its global offset and length (the previous
+// kept index and the next unkept one from the thread, the wave, or the prefix P / Q), so no field is
+// completed later — then stored in 16-B chunks.  Traffic: 4 N + the wire + the mask (N / 8, written
+// and read) + the kept values' f16 (written and read).  29.4-29.9 vs 33.3-34.1 us per 64 MiB drop for
+// the image form (profiles/r05_final_e_ab.txt; DESIGN.md §3 "count + emit").
 constexpr int kCW = 32;                // values per lane: one wave per 2048-value tile
 static_assert(64 * kCW == kTile, "a wave holds a tile");
 constexpr int kCountTpw = kGP;        // tiles per sp_count workgroup (a wave each): one set of atomics
