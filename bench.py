@@ -1130,23 +1130,22 @@ def start_backstop(budget: Budget, rank: int) -> threading.Timer:
     return t
 
 
-def launch_ranks(args, argv) -> int:
-    """--gpus N > 1 with no launcher around it: start the N ranks here, one
-    process per GPU, before this process touches the GPU (it never does), with
-    the env torch.distributed.run would give them; relay rank 0's JSON line.
-    The ranks share this process's deadline."""
+def _run_ranks(args, argv: list, deadline: str, env_extra: dict) -> tuple[int, dict | None]:
+    """Start the N ranks (one process per GPU, the env torch.distributed.run
+    would give them) and return rank 0's exit code and JSON line (None: none).
+    When rank 0 ends without a headline the others are killed at once (they may
+    be waiting in a collective for it)."""
     import socket
     import subprocess
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    argv = list(sys.argv[1:] if argv is None else argv)
-    deadline = os.environ.get("ONO_BENCH_DEADLINE") or repr(time.time() + args.deadline)
+    base = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     procs = []
     for r in range(args.gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   ONO_BENCH_DEADLINE=deadline)
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ONO_BENCH_DEADLINE=deadline, ONO_BENCH_RANK="1",
+                   **env_extra)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
     out = ""
@@ -1155,23 +1154,67 @@ def launch_ranks(args, argv) -> int:
     except subprocess.TimeoutExpired:
         procs[0].kill()
         out, _ = procs[0].communicate()
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    line = None
+    if lines:
+        try:
+            line = json.loads(lines[-1])
+        except ValueError:
+            line = None
+    failed = line is None or "headline_error" in line
     for p in procs[1:]:
         try:
-            p.wait(timeout=30)
+            p.wait(timeout=1 if failed else 30)
         except subprocess.TimeoutExpired:
             p.kill()
             p.wait()
-    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
-    if not lines:
-        print(f"bench.py: rank 0 printed no line (exit {procs[0].returncode})", file=sys.stderr)
-        return procs[0].returncode or 1
-    print(lines[-1], flush=True)
-    return 0
+    return procs[0].returncode, line
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1: start the N ranks from this process, which never touches
+    the GPU, and relay rank 0's JSON line.  The ranks share this process's
+    deadline.  If the headline schedule could not run — rank 0 reports a
+    headline_error (the RCCL ring's creation failed, or the headline did not
+    finish within ONO_BENCH_HEADLINE_TIMEOUT_S), or printed nothing — a fresh
+    set of ranks measures the headline on the xGMI schedule, which needs no
+    RCCL (the node-local form of the reference's ring, worker/src/builder.rs:
+    272-311), and the line records headline_fallback {from, reason}.  No rank
+    that has touched the GPU is ever asked to retry."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    deadline = os.environ.get("ONO_BENCH_DEADLINE") or repr(time.time() + args.deadline)
+    rc, line = _run_ranks(args, argv, deadline, {})
+    if (line is None or "headline_error" in line) and args.algo != "xgmi":
+        frm = {"auto": "allreduce" if args.wire == "f32" else "direct"}.get(args.algo, args.algo)
+        reason = line["headline_error"] if line else f"rank 0 printed no line (exit {rc})"
+        fb = {"from": frm, "reason": str(reason)[:400]}
+        print(f"bench.py: headline on {frm} failed ({fb['reason']}); measuring it on the xGMI schedule",
+              file=sys.stderr, flush=True)
+        # the RCCL schedules stay out of the fallback's legs too (alt schedules; the xGMI children would repeat it)
+        argv2 = argv + ["--algo", "xgmi", "--alt-schedules", "", "--no-xgmi"]
+        rc, line = _run_ranks(args, argv2, deadline, {"ONO_BENCH_FALLBACK": json.dumps(fb)})
+    if line is None:
+        print(f"bench.py: rank 0 printed no line (exit {rc})", file=sys.stderr)
+        return rc or 1
+    print(json.dumps(line), flush=True)
+    return 0 if "headline_error" not in line else (rc or 1)
+
+
+def headline_abort(rank: int, reason: str) -> None:
+    """The headline could not be measured in this rank (its ring failed, or it did
+    not finish in time): rank 0 says why in a one-key JSON line for the launcher
+    (launch_ranks, which falls back to the xGMI schedule), and the process ends
+    without retrying anything."""
+    if rank == 0:
+        print(json.dumps({"headline_error": reason[:400]}), flush=True)
+    sys.stdout.flush()
+    os._exit(5)
 
 
 class DryRing:
     """--dry-run: a ring that only sleeps (CPU plumbing tests)."""
-    algo = "dry"
+    def __init__(self, algo: str = "dry"):
+        self.algo = algo
 
     def set_pipeline(self, _):
         pass
@@ -1186,6 +1229,12 @@ def main(argv=None) -> int:
     if args.xgmi_child:
         return xgmi_child_main(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
+    if args.gpus > 1 and os.environ.get("TORCHELASTIC_RUN_ID") and not os.environ.get("ONO_BENCH_RANK"):
+        # under torch.distributed.run: its local rank 0 becomes the GPU-free launcher of the N ranks (so that a
+        # failed headline can be measured again by fresh processes), the others leave at once, before any GPU call
+        if os.environ.get("LOCAL_RANK", "0") != "0":
+            return 0
         return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1208,8 +1257,12 @@ def main(argv=None) -> int:
     bucket_bytes = elems * 4
 
     def new_ring(wire: str, algo: str, size: int = elems):
-        if dry:
-            return DryRing()
+        if dry:  # (stubs: an RCCL ring that fails to come up, or never does)
+            if algo != "xgmi" and os.environ.get("ONO_BENCH_DRY_RING_FAIL"):
+                raise RuntimeError("RcclError: ncclCommInitRank failed (dry-run stub)")
+            if algo != "xgmi" and os.environ.get("ONO_BENCH_DRY_RING_HANG"):
+                time.sleep(1e6)
+            return DryRing("xgmi" if algo == "xgmi" else "dry")
         if algo == "xgmi" and world > 1:  # no communicator: IPC handles over the control plane
             return ono_amd.WorkerRingManager.over_xgmi(rank, world, size, ctl.allgather_bytes, wire=wire,
                                                        device=local_rank)
@@ -1217,9 +1270,24 @@ def main(argv=None) -> int:
         uid = ctl.bcast_bytes(uid) if world > 1 else None
         return ono_amd.WorkerRingManager(rank, world, size, uid=uid, wire=wire, device=local_rank, algo=algo)
 
-    # ---- the headline first: measured, checked and in the line before any informational leg
-    ring = new_ring(args.wire, args.algo)
-    ring.set_pipeline(args.segments)
+    # ---- the headline first: measured, checked and in the line before any informational leg.  If its ring cannot
+    # be created (RCCL), or the headline does not finish in time, rank 0 reports it and the process ends: the
+    # launcher measures the headline again on the xGMI schedule in fresh processes (launch_ranks).
+    hl_timeout = float(os.environ.get("ONO_BENCH_HEADLINE_TIMEOUT_S", "180"))
+    watchdog = None
+    if world > 1:
+        watchdog = threading.Timer(hl_timeout, headline_abort,
+                                   (rank, f"the {args.algo} headline (ring creation, {args.steps} steps and the check) "
+                                          f"did not finish in {hl_timeout:.0f} s"))
+        watchdog.daemon = True
+        watchdog.start()
+    try:
+        ring = new_ring(args.wire, args.algo)
+        ring.set_pipeline(args.segments)
+    except Exception as e:  # noqa: BLE001
+        if world == 1:
+            raise
+        headline_abort(rank, f"{args.algo} ring creation failed: {type(e).__name__}: {e}")
     if dry:
         run = None
 
@@ -1236,6 +1304,8 @@ def main(argv=None) -> int:
     elapsed, tim = measure(ring)
 
     extra = {"check": {"ok": True, "dry_run": True} if dry else run.verify(args.wire)}
+    if watchdog is not None:
+        watchdog.cancel()
     if world == 1:
         avg_ms = tim["kernel_ms"] / max(tim["kernels"], 1)
         per_launch = 12 * elems  # read residual, write grad, write zeros (12 N)
@@ -1263,6 +1333,8 @@ def main(argv=None) -> int:
                           bucket_bytes=bucket_bytes, wire=args.wire, extra=extra)
     line = BOX.line
     line["config"]["schedule"] = ring.algo
+    if os.environ.get("ONO_BENCH_FALLBACK"):  # this headline replaces one that failed (launch_ranks)
+        line["headline_fallback"] = json.loads(os.environ["ONO_BENCH_FALLBACK"])
     if world > 1 and ring.algo == "xgmi":
         line["config"]["collective"] = "xGMI peer-access kernels over IPC-mapped peer HBM (no RCCL)"
     if world > 1 and args.wire == "f32" and ring.algo in ("auto", "allreduce"):

@@ -252,3 +252,53 @@ def test_two_self_launched_ranks_cut_together():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["deadline"]["cut"]
     assert took < 60
+
+
+def test_rccl_failure_falls_back_to_xgmi_in_fresh_ranks():
+    """the RCCL ring of the headline cannot be created (dry-run stub of a failing
+    ncclCommInitRank): rank 0 reports it, the launcher starts a fresh set of ranks on the xGMI schedule
+    (no RCCL) and relays one line that records headline_fallback {from, reason}, within the deadline."""
+    r, lines, took = _bench(["--gpus", "2", "--deadline", "60"], ONO_BENCH_DRY_RING_FAIL="1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["headline_fallback"]["from"] == "allreduce"
+    assert "ncclCommInitRank" in line["headline_fallback"]["reason"]
+    assert line["config"]["schedule"] == "xgmi" and line["value"] > 0 and line["check"]["ok"]
+    assert line["n_gpus"] == 2 and "headline_error" not in line
+    assert took < 60
+
+
+def test_hung_headline_falls_back_to_xgmi():
+    """The headline's ring never comes up (stub: ring creation sleeps): the rank's headline watchdog ends it
+    after ONO_BENCH_HEADLINE_TIMEOUT_S with a headline_error, and the xGMI fallback measures the line."""
+    r, lines, took = _bench(["--gpus", "2", "--deadline", "60"], ONO_BENCH_DRY_RING_HANG="1",
+                            ONO_BENCH_HEADLINE_TIMEOUT_S="4")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert "did not finish in 4 s" in line["headline_fallback"]["reason"]
+    assert line["config"]["schedule"] == "xgmi" and line["value"] > 0
+    assert took < 60
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_under_torchrun_one_gpu_free_launcher_prints_one_line(fail):
+    """Launched the way the driver launches N > 1 (torch.distributed.run --nproc-per-node 2): torchrun's local
+    rank 0 becomes the GPU-free launcher of the two ranks, the other torchrun process leaves at once; exactly one
+    JSON line comes out, with the xGMI fallback when the RCCL ring fails."""
+    port = _free_port()
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ONO_BENCH_DEADLINE")}
+    e.update(HIP_VISIBLE_DEVICES="")
+    if fail:
+        e["ONO_BENCH_DRY_RING_FAIL"] = "1"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1", "--deadline", "60"],
+                       capture_output=True, text=True, timeout=180, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert ("headline_fallback" in line) == fail
