@@ -772,10 +772,11 @@ int ono_xgmi_pool_release(size_t *freed_bytes, size_t *closed_imports) {
     if (closed_imports) *closed_imports = 0;
     int rc = ono_xgmi_pool_close_imports(closed_imports);
     if (rc) return rc;
-    // the peers close their imports of this process's regions in their own release: wait for them
-    // (bounded by the ring timeout's default; a region still mapped by a peer after it stays pooled)
-    const char *e = getenv("ONO_XGMI_TIMEOUT_S");
-    const double wait = e && atof(e) > 0 ? atof(e) : 600.0;
+    // the peers close their imports of this process's regions in their own release: wait for them a short
+    // while (ONO_XGMI_RELEASE_WAIT_S, 30 s by default; a region still mapped by a peer after it is kept, and
+    // retired from reuse)
+    const char *e = getenv("ONO_XGMI_RELEASE_WAIT_S");
+    const double wait = e && atof(e) > 0 ? atof(e) : 30.0;
     return ono_xgmi_pool_free_exports(freed_bytes, nullptr, wait);
 }
 

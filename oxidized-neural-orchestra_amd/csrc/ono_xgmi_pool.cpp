@@ -24,7 +24,8 @@ int XgmiPool::acquire(int device, size_t bytes, size_t alloc_bytes, uint64_t new
     std::lock_guard<std::mutex> lk(mu_);
     Region *best = nullptr;
     for (auto &r : regions_)
-        if (!r.busy && r.device == device && r.bytes >= bytes && (!best || r.bytes < best->bytes)) best = &r;
+        if (!r.busy && !r.retired && r.device == device && r.bytes >= bytes && (!best || r.bytes < best->bytes))
+            best = &r;
     *fresh = best == nullptr;
     if (!best) {
         Region r{};
@@ -117,24 +118,26 @@ int XgmiPool::close_imports(size_t *closed, std::string &msg) {
 }
 
 int XgmiPool::free_exports(double wait_s, size_t *freed_bytes, size_t *kept, std::string &msg) {
-    std::lock_guard<std::mutex> lk(mu_);
     if (freed_bytes) *freed_bytes = 0;
     if (kept) *kept = 0;
-    if (live_ > 0) {
-        msg = std::to_string(live_) + " xGMI ring(s) of this process are alive";
-        return ONO_E_ARG;
+    std::vector<Region> pending;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (live_ > 0) {
+            msg = std::to_string(live_) + " xGMI ring(s) of this process are alive";
+            return ONO_E_ARG;
+        }
+        // the idle regions leave the pool while they are polled (no ring can be handed one); the busy ones
+        // here are the quarantined.  Parked allocations stay allocated: freed, the allocator would hand the
+        // same blocks (and handles) back to the next fresh allocation.
+        std::vector<Region> keep;
+        for (auto &r : regions_) (r.busy ? keep : pending).push_back(r);
+        regions_.swap(keep);
     }
+    // polled without the lock: a peer that never closes costs this caller the wait, not every other call
     int rc = ONO_OK;
-    size_t freed = 0, still = 0;
-    for (auto &r : parked_) {  // never exported: nobody maps them
-        std::string m;
-        int e = ops_.free(r.device, r.ptr, m);
-        if (e && rc == ONO_OK) rc = e, msg = m;
-        freed += r.bytes;
-    }
-    parked_.clear();
-    std::vector<Region> keep, pending;
-    for (auto &r : regions_) (r.busy ? keep : pending).push_back(r);  // busy here = quarantined
+    size_t freed = 0;
+    std::vector<Region> kept_regions;
     const double t0 = ops_.now();
     for (;;) {
         std::vector<Region> later;
@@ -144,7 +147,7 @@ int XgmiPool::free_exports(double wait_s, size_t *freed_bytes, size_t *kept, std
             int e = ops_.read2(r.device, reinterpret_cast<const uint64_t *>(r.ptr + count_off_), c, m);
             if (e) {  // cannot tell whether a peer still maps it: keep it
                 if (rc == ONO_OK) rc = e, msg = m;
-                keep.push_back(r);
+                kept_regions.push_back(r);
             } else if (c[1] >= c[0]) {
                 if ((e = ops_.free(r.device, r.ptr, m)) && rc == ONO_OK) rc = e, msg = m;
                 freed += r.bytes;
@@ -156,9 +159,15 @@ int XgmiPool::free_exports(double wait_s, size_t *freed_bytes, size_t *kept, std
         if (pending.empty() || ops_.now() - t0 > wait_s) break;
         ops_.pause();
     }
-    for (auto &r : pending) keep.push_back(r);
-    still = pending.size();
-    regions_.swap(keep);
+    const size_t still = pending.size();
+    for (auto &r : pending) kept_regions.push_back(r);
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto &r : kept_regions) {
+            r.retired = true;  // its peers may have closed it: never exported to another ring
+            regions_.push_back(r);
+        }
+    }
     if (still && rc == ONO_OK) {
         msg = std::to_string(still) + " exchange region(s) still imported by a peer after " + std::to_string(wait_s) +
               " s: kept (call ono_xgmi_pool_close_imports on every rank first)";

@@ -7,8 +7,11 @@
 //     fits; a new one is allocated only when none does;
 //   * no IPC handle is handed out twice: a fresh allocation whose handle bytes
 //     repeat any handle this process obtained before is parked (kept
-//     allocated, never exported) and another is allocated — round 3 traced a
-//     wrong result to a re-import whose handle repeated an earlier one;
+//     allocated for the life of the process, never exported — freeing it would
+//     hand the allocator the same block back, so every release cycle would need
+//     one more discarded allocation than the last) and another is allocated —
+//     round 3 traced a wrong result to a re-import whose handle repeated an
+//     earlier one;
 //   * an importer never opens a handle whose bytes it opened before (the same
 //     hazard from the other side: ONO_E_IO instead of a stale mapping);
 //   * release is two-phase.  close_imports (every rank) marks each peer region
@@ -16,8 +19,10 @@
 //     and closes the import; then, after a collective step, free_exports
 //     (every rank) frees a region only once its close counter has caught up
 //     with its open counter (every importer bumped the open counter when it
-//     mapped the region), waiting a bounded time; a region some peer still
-//     maps is kept, never freed under it;
+//     mapped the region), waiting a bounded time without holding the pool's
+//     lock; a region some peer still maps is kept — never freed under it,
+//     never handed to a later ring (its peers may have closed it), retried by
+//     the next free_exports;
 //   * a ring's liveness count moves only for rings that obtained a region, so
 //     an allocation that failed cannot let a release free a region in use.
 #pragma once
@@ -61,6 +66,7 @@ public:
         IpcBytes handle;
         bool busy;         // a ring uses it
         bool quarantined;  // a ring's teardown ended without every peer's marker: never reused, never freed
+        bool retired;      // a free_exports found it still imported: never reused, freed by a later free_exports
     };
     struct Import {
         int device;
@@ -88,9 +94,9 @@ public:
     int map(int device, const IpcBytes &handle, uint64_t uid, size_t bytes, uint8_t **out, std::string &msg);
     // Release, phase 1: every import marked closed in its region, then closed.  Refused while a ring lives.
     int close_imports(size_t *closed, std::string &msg);
-    // Release, phase 2: every idle region freed once its importers have all closed it (waits up to
-    // wait_s), every parked allocation freed.  Regions still imported after the wait are kept
-    // (ONO_E_IO, *kept).  Refused while a ring lives.
+    // Release, phase 2: every idle region freed once its importers have all closed it (polls up to
+    // wait_s, the lock released in between).  Regions still imported after the wait are kept and
+    // retired (ONO_E_IO, *kept).  Parked allocations stay.  Refused while a ring lives.
     int free_exports(double wait_s, size_t *freed_bytes, size_t *kept, std::string &msg);
     Stats stats();
     int live();

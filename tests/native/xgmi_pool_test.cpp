@@ -14,8 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -49,6 +51,7 @@ struct Device {
         IpcBytes handle;
         int open_imports = 0;
         bool freed = false;
+        int owner = 0;  // the simulated process that allocated it (each process has its own allocator)
     };
     std::vector<std::unique_ptr<Alloc>> allocs;
     std::vector<IpcBytes> next_handles;  // handles the next allocations get (then fresh ones)
@@ -56,6 +59,12 @@ struct Device {
     int fail_next_alloc = 0;
     int frees_under_import = 0;
     double clock = 0;
+    // lifo: an allocation takes the most recently freed block that fits, with the handle it had (the
+    // deterministic reuse ADVICE r5 describes: every freed block comes back, named as before)
+    bool lifo = false;
+    int procs = 0;
+    std::vector<Alloc *> free_list;
+    std::function<void()> on_pause;  // (called between free_exports' polls)
 
     Alloc *by_ptr(const uint8_t *p) {
         for (auto &a : allocs)
@@ -77,17 +86,29 @@ IpcBytes handle_of(uint8_t tag) {
     return h;
 }
 
-XgmiPoolOps ops_for(Device &d) {
+XgmiPoolOps ops_for(Device &d, int owner) {
     XgmiPoolOps o;
-    o.alloc = [&d](int, size_t bytes, uint8_t **ptr, IpcBytes *h, std::string &msg) -> int {
+    o.alloc = [&d, owner](int, size_t bytes, uint8_t **ptr, IpcBytes *h, std::string &msg) -> int {
         if (d.fail_next_alloc > 0) {
             d.fail_next_alloc--;
             msg = "simulated allocation failure";
             return ONO_E_HIP;
         }
+        if (d.lifo)
+            for (size_t k = d.free_list.size(); k-- > 0;)
+                if (d.free_list[k]->owner == owner && d.free_list[k]->bytes >= bytes) {
+                    Device::Alloc *b = d.free_list[k];
+                    d.free_list.erase(d.free_list.begin() + (long)k);
+                    b->freed = false;
+                    std::memset(b->mem.get(), 0, b->bytes);
+                    *ptr = b->mem.get();
+                    *h = b->handle;
+                    return ONO_OK;
+                }
         auto a = std::make_unique<Device::Alloc>();
         a->mem.reset(new uint8_t[bytes]());
         a->bytes = bytes;
+        a->owner = owner;
         if (!d.next_handles.empty()) {
             a->handle = d.next_handles.front();
             d.next_handles.erase(d.next_handles.begin());
@@ -107,6 +128,7 @@ XgmiPoolOps ops_for(Device &d) {
         }
         if (a->open_imports > 0) d.frees_under_import++;
         a->freed = true;
+        d.free_list.push_back(a);
         return ONO_OK;
     };
     o.open = [&d](int, const IpcBytes &h, uint8_t **ptr, std::string &msg) -> int {
@@ -137,7 +159,10 @@ XgmiPoolOps ops_for(Device &d) {
         out[1] = p[1];
         return ONO_OK;
     };
-    o.pause = [&d] { d.clock += 0.001; };
+    o.pause = [&d] {
+        d.clock += 0.001;
+        if (d.on_pause) d.on_pause();
+    };
     o.now = [&d] { return d.clock; };
     return o;
 }
@@ -145,7 +170,7 @@ XgmiPoolOps ops_for(Device &d) {
 struct Proc {
     XgmiPool pool;
     XgmiPool::Region reg{};
-    explicit Proc(Device &d) : pool(ops_for(d), kCountOff) {}
+    explicit Proc(Device &d) : pool(ops_for(d, ++d.procs), kCountOff) {}
 };
 
 // n processes each create one ring region and map every peer's (connect); then all rings are destroyed
@@ -245,8 +270,90 @@ void test_repeated_handles() {
     ps[0]->pool.release_ring(r0.ptr, true);  // (the first acquire's ring)
     ps[1]->pool.release_ring(r1.ptr, true);
     for (auto &q : ps) q->pool.close_imports(&closed, msg);
-    CHECK(ps[0]->pool.free_exports(0.0, &freed, &kept, msg) == ONO_OK && ps[0]->pool.stats().parked == 0,
-          "parked allocations not freed: %s", msg.c_str());
+    // parked allocations stay allocated (freed, the allocator would hand the same blocks back)
+    CHECK(ps[0]->pool.free_exports(0.0, &freed, &kept, msg) == ONO_OK && ps[0]->pool.stats().parked == 9,
+          "parked allocations freed: %s (%zu parked)", msg.c_str(), ps[0]->pool.stats().parked);
+}
+
+// an allocator that reuses every freed block in LIFO order, handle and all.  Over 12 release
+// cycles every ring still gets a region whose handle was never handed out before (at most one repeat per
+// cycle: the parked blocks stay out of the allocator), no region is freed while imported, and the pool
+// holds at most one parked block per cycle.
+void test_release_cycles_lifo() {
+    Device d;
+    d.lifo = true;
+    std::vector<std::unique_ptr<Proc>> ps;
+    for (int i = 0; i < 3; i++) ps.push_back(std::make_unique<Proc>(d));
+    std::string msg;
+    std::set<IpcBytes> seen;
+    for (int cycle = 0; cycle < 12; cycle++) {
+        std::vector<IpcBytes> got;
+        for (size_t i = 0; i < ps.size(); i++) {
+            bool fresh = false;
+            int rc = ps[i]->pool.acquire(0, 8192, 8192, 1000 + 10 * (uint64_t)cycle + i, &ps[i]->reg, &fresh, msg);
+            CHECK(rc == ONO_OK && fresh, "cycle %d rank %zu acquire: rc %d %s", cycle, i, rc, msg.c_str());
+            if (rc) return;
+            CHECK(!seen.count(ps[i]->reg.handle), "cycle %d rank %zu: a handle handed out before", cycle, i);
+            got.push_back(ps[i]->reg.handle);
+        }
+        for (auto &h : got) seen.insert(h);
+        for (size_t i = 0; i < ps.size(); i++)
+            for (size_t j = 0; j < ps.size(); j++) {
+                if (i == j) continue;
+                uint8_t *p = nullptr;
+                int rc = ps[i]->pool.map(0, ps[j]->reg.handle, ps[j]->reg.uid, ps[j]->reg.bytes, &p, msg);
+                CHECK(rc == ONO_OK && p == ps[j]->reg.ptr, "cycle %d map: %s", cycle, msg.c_str());
+            }
+        for (auto &p : ps) p->pool.release_ring(p->reg.ptr, true);
+        size_t closed, freed, kept;
+        for (auto &p : ps) CHECK(p->pool.close_imports(&closed, msg) == ONO_OK, "%s", msg.c_str());
+        for (auto &p : ps)
+            CHECK(p->pool.free_exports(0.0, &freed, &kept, msg) == ONO_OK && freed == 8192, "cycle %d free: %s",
+                  cycle, msg.c_str());
+    }
+    size_t parked = 0;
+    for (auto &p : ps) parked += p->pool.stats().parked;
+    // every cycle after the first: the freed block came back first (one repeat, parked) — the case exercised
+    CHECK(parked == 11 * ps.size(), "%zu parked blocks after 12 cycles of 3 processes", parked);
+    CHECK(d.frees_under_import == 0, "%d regions freed while imported", d.frees_under_import);
+}
+
+// free_exports waits for a peer without holding the pool's lock: during its polls the same pool
+// answers stats() and hands a new ring a region; the region it gave up on is kept, retired (not handed out),
+// and freed by the next free_exports once the peer has closed.
+void test_free_exports_polls_unlocked() {
+    Device d;
+    std::vector<std::unique_ptr<Proc>> ps;
+    for (int i = 0; i < 2; i++) ps.push_back(std::make_unique<Proc>(d));
+    rings(ps, 4096, 700);
+    std::string msg;
+    size_t closed = 0, freed = 0, kept = 0;
+    CHECK(ps[0]->pool.close_imports(&closed, msg) == ONO_OK, "%s", msg.c_str());
+    int polls = 0, acquired = 0;
+    XgmiPool::Region other{};
+    d.on_pause = [&] {
+        polls++;
+        (void)ps[0]->pool.stats();  // would deadlock if free_exports held the lock
+        if (polls == 3) {
+            bool fresh = false;
+            std::string m;
+            if (ps[0]->pool.acquire(0, 4096, 4096, 777, &other, &fresh, m) == ONO_OK) acquired = fresh ? 1 : -1;
+        }
+    };
+    int rc = ps[0]->pool.free_exports(0.01, &freed, &kept, msg);
+    d.on_pause = nullptr;
+    CHECK(rc == ONO_E_IO && kept == 1 && polls >= 3, "rc %d kept %zu polls %d", rc, kept, polls);
+    CHECK(acquired == 1 && other.ptr != ps[0]->reg.ptr, "acquire during the polls: %d", acquired);
+    ps[0]->pool.release_ring(other.ptr, true);
+    XgmiPool::Region again{};
+    bool fresh = false;
+    CHECK(ps[0]->pool.acquire(0, 4096, 4096, 778, &again, &fresh, msg) == ONO_OK && again.ptr != ps[0]->reg.ptr,
+          "the kept region was handed to another ring");
+    ps[0]->pool.release_ring(again.ptr, true);
+    CHECK(ps[1]->pool.close_imports(&closed, msg) == ONO_OK, "%s", msg.c_str());
+    CHECK(ps[0]->pool.free_exports(0.0, &freed, &kept, msg) == ONO_OK && kept == 0 && freed >= 4096,
+          "the retired region was not freed once closed: %s", msg.c_str());
+    CHECK(d.frees_under_import == 0, "%d regions freed while imported", d.frees_under_import);
 }
 
 void test_liveness() {
@@ -279,6 +386,8 @@ int main() {
     test_free_before_peer_closes_is_kept();
     test_repeated_handles();
     test_liveness();
+    test_release_cycles_lifo();
+    test_free_exports_polls_unlocked();
     if (g_fail) {
         fprintf(stderr, "%d of %d checks failed\n", g_fail, g_checks);
         return 1;
