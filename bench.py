@@ -273,8 +273,47 @@ def cpu_baseline(bucket_elems: int, ranks: int, rounds: int) -> dict:
                                  "sample": f"BlockingStore: {ps['workers']} accumulates + 1 update (÷n, GD) of "
                                            f"{ps['len']} params, {ps['shards']} shards on {ps['threads']} pinned cores"},
         "march_native": native,
+        "ring_by_ranks": ring_by_ranks(bucket_elems, ranks),
         "sparse_ring": sparse_ring_baseline(),
     }
+
+
+def usable_cpus() -> int:
+    """CPUs this process may keep busy: its affinity set, capped by the cgroup's
+    cpu.max quota (a GPU box grants 16 CPUs of a 256-CPU host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def ring_by_ranks(bucket_elems: int, done: int, ranks=(2, 4, 8), rounds: int = 2) -> dict:
+    """BASELINE.md's CPU plan at every GPU count of the scaling line: the reference-style CPU ring with n = 2, 4,
+    8 workers (one pinned core each, as docker/gen_compose.py:9 deploys them) on the same 256 MiB bucket per
+    worker, so the N = 2 / 4 / 8 GPU lines have a same-n CPU figure from one run.  An n is run only when the
+    process may use n + 1 CPUs (n pinned workers and the driver); the cores used are recorded."""
+    from oracle import oracle as O  # noqa: WPS433 (cpu_baseline leg only)
+    cpus = usable_cpus()
+    out = {"usable_cpus": cpus}
+    for n in ranks:
+        if n == done:
+            continue  # (the line's own cpu_baseline)
+        if n + 1 > cpus:
+            out[str(n)] = {"skipped": f"needs {n + 1} CPUs, the process may use {cpus}"}
+            continue
+        try:
+            r = O.cpu_ring(n, bucket_elems, rounds, check=False, pin=True, timeout=600)
+            out[str(n)] = {"gib_s_per_worker": round(r["gib_s"], 4), "s_per_round": round(r["s_per_round"], 4),
+                           "cores": n, "workers_pinned": r.get("workers_pinned"), "rounds": rounds,
+                           "aggregate_gib_s": round(r["gib_s"] * n, 4)}
+        except Exception as e:  # noqa: BLE001
+            out[str(n)] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    return out
 
 
 def sparse_ring_baseline(ratio: float = 0.1, rounds: int = 20) -> dict:
@@ -1393,7 +1432,7 @@ def main(argv=None) -> int:
             leg("sparse_codec", 25, lambda: sparse_codec(torch, ono_amd))
             leg("copy_ceiling", 15, lambda: copy_ceiling(torch, ono_amd, max(args.steps, 10), max(args.warmup, 2)))
         if not args.no_cpu_baseline:
-            leg("cpu_baseline", 60, lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
+            leg("cpu_baseline", 80, lambda: cpu_baseline(elems, args.cpu_ranks, args.cpu_rounds))
         with BOX.lock:
             n1_roofline_summary(line["roofline"], line.get("local_reduce"), line.get("copy_ceiling"))
 

@@ -176,12 +176,19 @@ static size_t recv_grad(const uint8_t *b, size_t got, float *dec, size_t cap) {
 
 static void *worker_main(void *arg) {
     worker_t *w = (worker_t *)arg;
-    if (w->pin) {
-        long nc = sysconf(_SC_NPROCESSORS_ONLN);
-        cpu_set_t cs;
+    if (w->pin) {  /* the rank-th CPU this process may run on (a box's cpuset need not start at CPU 0) */
+        cpu_set_t allowed, cs;
         CPU_ZERO(&cs);
-        CPU_SET(w->rank % (nc > 0 ? nc : 1), &cs);
-        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+        if (sched_getaffinity(0, sizeof allowed, &allowed) == 0 && CPU_COUNT(&allowed) > 0) {
+            int k = w->rank % CPU_COUNT(&allowed), c = 0;
+            for (; c < CPU_SETSIZE; c++)
+                if (CPU_ISSET(c, &allowed) && k-- == 0) break;
+            CPU_SET(c, &cs);
+        } else {
+            long nc = sysconf(_SC_NPROCESSORS_ONLN);
+            CPU_SET(w->rank % (nc > 0 ? nc : 1), &cs);
+        }
+        if (pthread_setaffinity_np(pthread_self(), sizeof cs, &cs) != 0) w->pin = 0;  /* reported: not pinned */
     }
     int n = w->n;
     int fd_next = -1, fd_prev = -1;
@@ -376,8 +383,10 @@ int main(int argc, char **argv) {
         free(res); free(gr);
     }
     double spr = g_total / rounds;
-    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"pinned\": %d, \"s_per_round\": %.9f, "
-           "\"gib_s\": %.6f, \"check\": %d}\n",
-           n, len, rounds, pin, spr, (double)len * 4.0 / spr / (double)(1ull << 30), ok);
+    int pinned = 0;  /* workers whose thread really got its one core */
+    for (int r = 0; r < n; r++) pinned += w[r].pin;
+    printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"pinned\": %d, \"workers_pinned\": %d, "
+           "\"s_per_round\": %.9f, \"gib_s\": %.6f, \"check\": %d}\n",
+           n, len, rounds, pin, pinned, spr, (double)len * 4.0 / spr / (double)(1ull << 30), ok);
     return ok == 0 ? 4 : 0;
 }
