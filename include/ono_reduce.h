@@ -148,17 +148,37 @@ int ono_sparse_sample_default(uint64_t *state, size_t len, uint32_t *idx, size_t
  * gradient seen and never shrunk: above 256 tiles of 2048 values about 2.1
  * bytes per value (the keep flags and a f16 slot per tile for the kept
  * values) plus 16 bytes per tile; up to 256 tiles 32 bytes per tile.
- * Neither drop can be captured into a HIP graph (ONO_E_ARG): the launches
- * keep host-side state between calls that a replay would not follow.       */
+ * No writer stores past buf + cap: a tile whose range would pass it (only
+ * possible with corrupt or stale scratch) stores nothing, and the call fails
+ * with ONO_E_IO (blocking) or reports it through ono_sparse_drop_check and the
+ * next drop on the stream (stream-ordered; its *nbytes_dev reads ~0 when the
+ * totals pass cap).  The blocking drop cannot be captured into a HIP graph
+ * (ONO_E_ARG: it waits for its result); ono_sparse_drop_async can (see there). */
 int ono_sparse_drop(uint8_t *buf_dev, size_t cap, size_t *nbytes, const float *g_dev, size_t n,
                     float threshold, void *stream);
 /* The stream-ordered drop: the same bytes, nothing waits on the host; the
  * wire length lands in *nbytes_dev (device or host-mapped u64) when the
  * stream reaches it.  cap must be ono_sparse_max_bytes(n) (ONO_E_SIZE
  * otherwise).  For a device-side consumer of the stream (an RCCL send of the
- * frame, a device lift) and for back-to-back timing.                      */
+ * frame, a device lift) and for back-to-back timing.
+ * It can be captured into a HIP graph once an uncaptured call on the same
+ * stream has made its scratch for that size (else ONO_E_ARG; nothing is
+ * allocated or zeroed under capture): captured, it always takes the two
+ * launches, whose state between calls (the chunk aggregates' parity) lives on
+ * the device.  The graph holds that stream's scratch: replay it ordered with
+ * the stream's other drops (on the stream, or after it).                    */
 int ono_sparse_drop_async(uint8_t *buf_dev, size_t cap, uint64_t *nbytes_dev, const float *g_dev, size_t n,
                           float threshold, void *stream);
+/* Synchronizes the stream, then reports (and clears) an error a stream-ordered
+ * drop on it left: ONO_E_IO when a writer found its range past the buffer or
+ * the chunk aggregates disagreeing with the tile records; ONO_OK otherwise.  */
+int ono_sparse_drop_check(void *stream);
+/* Test hook: adds `add` to the kept-value and run counts of every chunk
+ * aggregate that the stream's next two-launch drop will sum into — the
+ * "aggregate not zero when the call began" fault — so that tests can show it
+ * ends in ONO_E_IO, not an out-of-bounds store.  ONO_E_ARG before the first
+ * two-launch drop on the stream.                                             */
+int ono_sparse_drop_debug_stale(void *stream, uint32_t add);
 int ono_sparse_lift(float *g_dev, size_t cap, size_t *out_len, const uint8_t *buf_host, size_t nbytes,
                     void *stream);
 /* lift of a stream already in HBM (e.g. ono_sparse_drop's output or a frame
@@ -319,7 +339,11 @@ typedef enum {
  *              device-side flag barriers (timeout: ono_ring_set_xgmi_timeout,
  *              default 600 s -> ONO_E_IO).  Bit-exact for both wires; ranks of
  *              one node; n <= ONO_MAX_INPUTS.  On an RCCL ring the exchange
- *              regions are connected over the communicator on first use.    */
+ *              regions are connected over the communicator on first use.
+ *              One ring's rounds must run in issue order (one stream, or
+ *              streams ordered by events): a barrier takes a peer's flag more
+ *              than one epoch ahead as foreign and fails the round (ONO_E_IO),
+ *              which two unordered rounds of one ring could produce.        */
 int ono_ring_set_algo(ono_ring *ring, int algo);
 /* A ring with no collective library at all (ONO_ALGO_XGMI only): create,
  * export this rank's handle, pass every rank's handle (nranks x
@@ -350,12 +374,15 @@ int ono_ring_xgmi_connect(ono_ring *ring, const uint8_t *handles);
  *   3. ono_xgmi_pool_free_exports on every rank: each idle region is freed
  *      once its close counter has reached its open counter (each importer
  *      bumped the open counter when it mapped the region), waiting up to wait_s
- *      seconds; a region some peer still maps is kept (ONO_E_IO, *kept > 0)
- *      and parked allocations are freed.  So no region is freed while a peer
- *      still maps it.  Quarantined regions stay.
+ *      seconds (other pool calls are not held up meanwhile); a region some
+ *      peer still maps is kept (ONO_E_IO, *kept > 0), never handed to a later
+ *      ring, and freed by a later free_exports once its peers closed it.  So no
+ *      region is freed while a peer still maps it.  Quarantined regions and
+ *      parked allocations (fresh ones whose handle repeated an earlier one:
+ *      freed, the allocator would return the same block and handle) stay.
  * Rings created afterwards export and import fresh regions (verified at
  * connect as always).  ono_xgmi_pool_release = phase 1 then phase 3 in one
- * call, waiting (ONO_XGMI_TIMEOUT_S, default 600 s) for the peers' phase 1:
+ * call, waiting up to 30 s (env ONO_XGMI_RELEASE_WAIT_S) for the peers' phase 1:
  * the counters still order the frees after the peers' close marks, but the
  * mark precedes its import's close by one host call, so multi-process callers
  * should use the two phases with the collective step between.               */

@@ -197,6 +197,18 @@ constexpr int kSlotU16 = 5128;  // the largest tile image, 3 S + 2049 <= 5121 un
 static_assert((kSlotU16 * 2) % 16 == 0, "slots are 16-B aligned");
 constexpr int kRecChunk = 128;  // tiles per chunk of the aggregates: two records per lane of the move's wave
 constexpr int kAggStride = 8;   // one chunk aggregate per 128-B line (uint4 units): atomics of different chunks never share one
+// The two aggregate arrays that calls alternate between share each chunk's line: array h at uint4 h * kAggHalf
+// of it, so a reader that loads both (sp_emit: the parity comes with the records) asks for no more lines
+constexpr int kAggHalf = 4;
+static_assert(2 * kAggHalf <= kAggStride, "both arrays in the chunk's line");
+// The encoders' error word (host_tot[3], host-mapped): a writer whose range would pass the buffer's end
+// stores nothing and leaves kDropErrRange; aggregates that disagree with their records (not zero when
+// the call began) kDropErrStale.  The blocking call returns it (ONO_E_IO); a stream-ordered call's
+// length reads ~0 when the totals pass the buffer, and ono_sparse_drop_check reports the word.
+constexpr uint64_t kDropErrRange = 1, kDropErrStale = 2;
+__device__ __forceinline__ void drop_error(uint64_t *host_tot, uint64_t code) {
+    __hip_atomic_store(host_tot + 3, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Block-wide scans over the threads of a tile (tile-local indices): the
 // exclusive prefix of (kept, runs), the last kept index + 1 before the thread
@@ -575,8 +587,51 @@ __device__ __forceinline__ uint2 chunk_totals(const uint4 *agg, uint32_t G) {
 // four waves then share one set of loads: every wave of the grid reads the same few aggregate lines
 // at the same moment, and a quarter of the requests shortens that phase.
 constexpr int kGP = kSB / 64;  // tiles per group_prefix (sp_emit's workgroup, sp_count's kCountTpw)
-__device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg, size_t ntiles, uint32_t G, size_t tb,
-                                             uint32_t n, uint4 (&pre)[kGP], uint2 (&own)[kGP]) {
+// sp_count's records carry the call's aggregate parity in bit 31 of .x (kept | runs << 16 | parity << 31:
+// runs <= 1024 fit 15 bits), so sp_emit learns which of the two aggregate arrays holds this call's sums
+// from records it loads anyway — no hot parity word read by every workgroup at once
+constexpr uint32_t kRecRunsMask = 0x7FFFu;
+__device__ __forceinline__ uint32_t rec_runs(uint32_t x) { return (x >> 16) & kRecRunsMask; }
+__device__ __forceinline__ uint32_t wsum_dpp(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(v), 63); }
+__device__ __forceinline__ uint32_t wmax_dpp(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(v), 63); }
+__device__ __forceinline__ uint32_t wmin_dpp(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(v), 63); }
+__device__ __forceinline__ uint4 readlane4(uint4 v, int l) {
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
+                      (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l));
+}
+// The chunk's aggregate against its tiles' records (every record of the chunk is in r[], two per lane):
+// sp_count adds exactly the records' kept values and runs and takes the maxima of their edges, so any
+// difference means an aggregate that was not zero when sp_count began (or was written since) — the
+// stale-aggregate case in which every later place in the wire would be wrong.
+__device__ __forceinline__ bool chunk_agrees(const uint2 (&r)[kRecChunk / 64], uint32_t cs, uint32_t m, uint4 oc) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t f = 0, s = 0, lk = 0, fu = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < kRecChunk / 64; k++) {
+        const uint32_t j = lane + 64 * k, t0 = (cs + j) * (uint32_t)kTile;
+        if (j < m) {
+            const uint32_t F = r[k].x & 0xFFFFu, L1 = r[k].y & 0xFFFFu, FU = r[k].y >> 16;
+            f += F;
+            s += rec_runs(r[k].x);
+            if (F) lk = max(lk, t0 + L1);
+            if (FU < (uint32_t)kTile) fu = min(fu, t0 + FU);
+        }
+    }
+    const uint32_t F = wsum_dpp(f), S = wsum_dpp(s), LK = wmax_dpp(lk), FUm = wmin_dpp(fu);
+    return oc.x == F && oc.y == S && oc.z == LK && oc.w == (FUm != 0xFFFFFFFFu ? ~FUm : 0u);
+}
+// agg2: the two aggregate arrays (kAggHalf apart in each chunk's line); *par: which one this call's sp_count
+// filled (from the records);
+// *ok: the chunk's aggregate agrees with its records (chunk_agrees)
+// DEVPAR false: the host knows the parity (hpar; every call on the stream so far was uncaptured) and one array's
+// lines are loaded, four 64-chunk instructions as in round 5; true (a graph may have replayed calls on this
+// stream, so only the device knows it): both arrays, paired lanes, the parity taken from the records.  The
+// paired form holds twice the load registers (66 VGPRs: 7 waves per SIMD, and 8192 waves of a 64 MiB drop
+// no longer fit at once: +2.8 us per drop, profiles/r06_s4_*), so it is kept to the streams that need it.
+template <bool DEVPAR>
+__device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg2, uint32_t hpar, size_t ntiles,
+                                             uint32_t G, size_t tb, uint32_t n, uint4 (&pre)[kGP], uint2 (&own)[kGP],
+                                             uint32_t &par, bool &ok) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = (uint32_t)(tb / kRecChunk), cs = c * (uint32_t)kRecChunk;
     const uint32_t i0 = (uint32_t)tb - cs, m = (uint32_t)min((size_t)kRecChunk, ntiles - cs);
@@ -586,15 +641,37 @@ __device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg
 #if defined(ONO_EXP_EMIT) && ONO_EXP_EMIT == 6  // measurement only (tools/sp_phases_e6): no records, wrong wire
     r[0] = r[1] = make_uint2(0u, 0u);
 #endif
-    uint4 a[4];
+    // both arrays (DEVPAR), issued with the records (the parity comes with them: no load waits for another):
+    // lanes 2 i and 2 i + 1 take chunk j0 + i's two aggregates, one line; or this call's array alone, a chunk
+    // per lane.  The own chunk's line too, for the check.
+    constexpr int kAL = DEVPAR ? 8 : 4;     // instructions over the first 256 chunks
+    constexpr int kCPI = DEVPAR ? 32 : 64;  // chunks per instruction
+    uint4 a[kAL];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t j = 64 * k + lane;
+    for (int k = 0; k < kAL; k++) {
+        const uint32_t j = kCPI * k + (DEVPAR ? lane >> 1 : lane);
         a[k] = make_uint4(0u, 0u, 0u, 0u);
 #if !defined(ONO_EXP_EMIT) || ONO_EXP_EMIT != 5  // (measurement only, tools/sp_phases_e5: no aggregates, wrong wire)
-        if (64 * k < G && (j < c || j == c + 1) && j < G) a[k] = agg[(size_t)j * kAggStride];
+        if (kCPI * k < G && kCPI * k <= c + 1 && j <= c + 1 && j < G)
+            a[k] = agg2[(size_t)j * kAggStride + (DEVPAR ? (lane & 1) : hpar) * kAggHalf];
 #endif
     }
+    par = DEVPAR ? (uint32_t)__builtin_amdgcn_readfirstlane((int)r[0].x) >> 31 : hpar;
+    const uint4 *agg = agg2 + par * kAggHalf;
+    const bool mine = !DEVPAR || (lane & 1u) == par;  // the lane holds this call's array
+    uint4 oc;  // the own chunk's aggregate
+    if (c < (uint32_t)(kCPI * kAL)) {
+        uint4 o4 = a[0];
+#pragma unroll
+        for (int k = 1; k < kAL; k++)
+            if (c / kCPI == (uint32_t)k) o4 = a[k];
+        oc = readlane4(o4, (int)(DEVPAR ? 2 * (c & 31) + par : c & 63));
+    } else {
+        uint32_t ca = c;
+        asm volatile("" : "+v"(ca));  // (a vector load)
+        oc = agg[(size_t)ca * kAggStride];
+    }
+    ok = chunk_agrees(r, cs, m, oc);
     uint32_t f = 0, s = 0, mx = 0, q = n;
     for (uint32_t j0 = 256; j0 < c; j0 += 64) {  // chunks before past the first 256 (G > 256: n > 2^26)
         const uint32_t j = j0 + lane;
@@ -608,13 +685,13 @@ __device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg
         q = w ? ~w : q;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t j = 64 * k + lane;
-        const bool before = j < c;
+    for (int k = 0; k < kAL; k++) {
+        const uint32_t j = kCPI * k + (DEVPAR ? lane >> 1 : lane);
+        const bool before = mine && j < c;
         f += before ? a[k].x : 0u;
         s += before ? a[k].y : 0u;
         mx = max(mx, before ? a[k].z : 0u);
-        q = min(q, j == c + 1 && a[k].w ? ~a[k].w : q);
+        q = min(q, mine && j == c + 1 && a[k].w ? ~a[k].w : q);
     }
     const uint32_t ilast = i0 + kGP - 1;
 #pragma unroll
@@ -622,7 +699,7 @@ __device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg
         const uint32_t j = lane + 64 * k, t0 = (cs + j) * (uint32_t)kTile;
         if (j < i0) {
             f += r[k].x & 0xFFFFu;
-            s += r[k].x >> 16;
+            s += rec_runs(r[k].x);
             const uint32_t l1 = r[k].y & 0xFFFFu;
             if (l1) mx = max(mx, t0 + l1);
         } else if (j > ilast && j < m) {
@@ -665,7 +742,7 @@ __device__ __forceinline__ void group_prefix(const uint2 *recA, const uint4 *agg
         pre[k] = make_uint4(F, S, MX, Qk[k]);
         const uint32_t l1 = rg[k].y & 0xFFFFu;
         F += rg[k].x & 0xFFFFu;
-        S += rg[k].x >> 16;
+        S += rec_runs(rg[k].x);
         if (l1) MX = max(MX, (cs + i0 + k) * (uint32_t)kTile + l1);
     }
 }
@@ -686,10 +763,6 @@ __device__ __forceinline__ uint4 ldn4(const uint4 *p) {
 }
 __device__ __forceinline__ uint4 lane_before4(uint4 v) {
     return make_uint4(lane_before(v.x), lane_before(v.y), lane_before(v.z), lane_before(v.w));
-}
-__device__ __forceinline__ uint4 readlane4(uint4 v, int l) {
-    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
-                      (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l));
 }
 template <int O>
 __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveBatch], uint32_t nu16, uint16_t *base16) {
@@ -737,7 +810,8 @@ __device__ __forceinline__ void move_chunks(const uint4 *src4, uint4 (&v)[kMoveB
 // One tile's slot to its place (sp_move).
 __device__ __forceinline__ void move_tile(const uint16_t *__restrict__ img, const uint2 *__restrict__ recA,
                                           const uint2 *__restrict__ recB, const uint4 *__restrict__ agg, size_t ntiles,
-                                          uint32_t G, size_t n, uint8_t *__restrict__ buf, size_t tile) {
+                                          uint32_t G, size_t n, uint8_t *__restrict__ buf, size_t cap,
+                                          uint64_t *__restrict__ host_tot, size_t tile) {
     const uint32_t lane = threadIdx.x & 63;
     SP_CLOCK(sp_t0);
     const uint4 *src4 = (const uint4 *)(img + tile * kSlotU16);
@@ -758,6 +832,10 @@ __device__ __forceinline__ void move_tile(const uint16_t *__restrict__ img, cons
     const uint32_t lenl = (hb.y >> 16) + (tile0 + (a.y & 0xFFFFu) == tend ? p.w - tend : 0u);
     const uint32_t c0 = hb.x & 0xFFFFu, hl = hb.x >> 16;
     uint8_t *dst = buf + 8 + 8 * (size_t)p.y + 2 * (size_t)p.x;
+    if (8 + 8 * (size_t)p.y + 2 * ((size_t)p.x + nu16) > cap) {  // never past the buffer (uniform)
+        if (lane == 0) drop_error(host_tot, kDropErrRange);
+        return;
+    }
     const uint32_t O = (uint32_t)__builtin_amdgcn_readfirstlane((int)(((uintptr_t)dst & 15u) >> 1));
     uint16_t *base16 = (uint16_t *)(dst - 2 * O);
     switch (O) {
@@ -836,16 +914,17 @@ __device__ __forceinline__ void stage_out(const lds_u4 *src4, uint32_t nu16, uin
 // Block 0 also writes the u64 total length and publishes the wire length.
 __global__ __launch_bounds__(kSB) void sp_move(
     const uint16_t *__restrict__ img, const uint2 *__restrict__ recA, const uint2 *__restrict__ recB,
-    const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, uint64_t *__restrict__ host_tot,
-    uint64_t *__restrict__ nbytes_out) {
+    const uint4 *__restrict__ agg, size_t ntiles, size_t n, uint8_t *__restrict__ buf, size_t cap,
+    uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
         const uint2 t = chunk_totals(agg, G);
         if (threadIdx.x == 0) {
             for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
-            const uint64_t F = t.x, R = t.y;
+            const uint64_t F = t.x, R = t.y, nb = 8 + 8 * R + 2 * F;
+            if (nb > cap) drop_error(host_tot, kDropErrRange);
             if (nbytes_out) {
-                *nbytes_out = 8 + 8 * R + 2 * F;  // the stream-ordered form: nothing crosses PCIe
+                *nbytes_out = nb <= cap ? nb : ~0ull;  // the stream-ordered form: nothing crosses PCIe
             } else {
                 host_tot[0] = F;  // the blocking form: the wire length's terms for the host (host-mapped)
                 host_tot[1] = R;
@@ -854,7 +933,7 @@ __global__ __launch_bounds__(kSB) void sp_move(
     }
     // wave-uniform (readfirstlane): scalar base addresses and branches
     const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kSB / 64) + (threadIdx.x >> 6)));
-    if (tile < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, tile);
+    if (tile < ntiles) move_tile(img, recA, recB, agg, ntiles, G, n, buf, cap, host_tot, tile);
 }
 
 
@@ -912,8 +991,8 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {  // v_cvt_pk_f16_
 }
 __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, size_t n, size_t ntiles, float t,
                                                 const float *t_dev, bool vec, uint32_t *__restrict__ mask,
-                                                uint16_t *__restrict__ cv, uint2 *__restrict__ recA, uint4 *agg,
-                                                uint4 *agg_next, uint32_t gcap) {
+                                                uint16_t *__restrict__ cv, uint2 *__restrict__ recA, uint4 *agg2,
+                                                uint32_t gcap, uint32_t *state) {
     // per round's parity (thread 0 reads one round's while a faster wave writes the next one's)
     __shared__ uint32_t s_fr[2][kCountTpw][2], s_lk[2][kCountTpw], s_fu[2][kCountTpw];
     // a wave's compact values (+ a dummy slot per lane)
@@ -921,8 +1000,11 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
     __shared__ __attribute__((aligned(16))) uint16_t s_row[kCountTpw][64 * kCRow];  // the lanes' values as f16
     SP_CLOCK(sp_t0);
     if (t_dev) t = *t_dev;
-    for (size_t i = (size_t)blockIdx.x * kSB + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kSB)
-        agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
+    // The two aggregate arrays alternate by a parity kept on the device (state[0], flipped by sp_emit's
+    // workgroup 0 once every wave has read this call's sums): this call adds into agg2[par] — zeroed by
+    // the previous call — and zeroes the other one for the next call.  A replayed graph follows it as
+    // an uncaptured call does (a host-side parity would be frozen into the graph).
+    // (read after the first tile's loads are issued: the word is one line every workgroup reads at once)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t step = (size_t)gridDim.x * kCountTpw;
 #ifdef ONO_SP_STAMP
@@ -941,6 +1023,11 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
     };
     size_t tile = (size_t)blockIdx.x * kCountTpw + wave;
     load(tile);
+    const uint32_t apar = state[0] & 1u;
+    uint4 *agg = agg2 + apar * kAggHalf, *agg_next = agg2 + (apar ^ 1u) * kAggHalf;
+    if (blockIdx.x == 0 && threadIdx.x == 0) state[1] = apar;  // (sp_totals_out's)
+    for (size_t i = (size_t)blockIdx.x * kSB + threadIdx.x; i < gcap; i += (size_t)gridDim.x * kSB)
+        agg_next[i * kAggStride] = make_uint4(0u, 0u, 0u, 0u);
     int par = 0;
     for (size_t b0 = (size_t)blockIdx.x * kCountTpw; b0 < ntiles; b0 += step, tile += step) {
         uint32_t F = 0, R = 0, LK = 0, FU = kTile;
@@ -1007,7 +1094,7 @@ __global__ __launch_bounds__(kSB) void sp_count(const float *__restrict__ g, siz
             R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp((uint32_t)__popc(start)), 63);
             LK = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(keep ? lo + 32u - (uint32_t)__clz(keep) : 0u), 63);
             FU = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_min_dpp(unk ? lo + (uint32_t)(__ffs(unk) - 1) : (uint32_t)kTile), 63);
-            if (lane == 0) recA[tile] = make_uint2(F | R << 16, LK | FU << 16);
+            if (lane == 0) recA[tile] = make_uint2(F | R << 16 | apar << 31, LK | FU << 16);  // (group_prefix)
         }
         if (lane == 0) {
             s_fr[par][wave][0] = F;
@@ -1053,25 +1140,32 @@ constexpr int kEmitVals = 1024;
 #define ONO_EMIT_SPEC 256
 #endif
 constexpr int kEmitSpec = ONO_EMIT_SPEC;  // values loaded speculatively (10 % kept: 205 +- 14 per tile)
-template <bool STAGE>
-__global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
+template <bool STAGE, bool DEVPAR>
+__global__ __launch_bounds__(kSB) __attribute__((amdgpu_waves_per_eu(8))) void sp_emit(const uint16_t *__restrict__ cv, size_t n, size_t ntiles,
                                                const uint32_t *__restrict__ mask, const uint2 *__restrict__ recA,
-                                               const uint4 *__restrict__ agg, uint8_t *__restrict__ buf,
+                                               const uint4 *__restrict__ agg2, uint32_t *__restrict__ state,
+                                               uint32_t hpar, uint8_t *__restrict__ buf, size_t cap,
                                                uint64_t *__restrict__ host_tot, uint64_t *__restrict__ nbytes_out) {
     __shared__ __attribute__((aligned(16))) uint16_t vals[kSB / 64][kEmitVals];  // per wave: the tile's compact values
     __shared__ __attribute__((aligned(16))) uint16_t stage[STAGE ? kSB / 64 : 1][STAGE ? kEmitStage + 16 : 8];
     SP_CLOCK(sp_t0);
     const uint32_t G = (uint32_t)((ntiles + kRecChunk - 1) / kRecChunk);
-    if (blockIdx.x == 0 && threadIdx.x < 64) {  // u64 LE total length, as four 2-byte stores (buf is 2-B aligned)
-        const uint2 t = chunk_totals(agg, G);
-        if (threadIdx.x == 0) {
+    const int wave = threadIdx.x >> 6;
+    // block 0's first wave, first: the totals, the header and the parity flip (the array: the host's parity,
+    // or the one sp_count's workgroup 0 named in state[1])
+    if (blockIdx.x == 0 && wave == 0) {
+        const uint32_t par = DEVPAR ? state[1] & 1u : hpar;
+        const uint2 t = chunk_totals(agg2 + par * kAggHalf, G);
+        if ((threadIdx.x & 63) == 0) {  // u64 LE total length, as four 2-byte stores (buf 2-B aligned, cap >= 8)
             for (int q = 0; q < 4; q++) *(uint16_t *)(buf + 2 * q) = (uint16_t)((uint64_t)n >> (16 * q));
-            const uint64_t F = t.x, R = t.y;
-            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;
+            const uint64_t F = t.x, R = t.y, nb = 8 + 8 * R + 2 * F;
+            const bool good = nb <= cap;  // (a wire past the buffer: no length, an error)
+            if (nbytes_out) *nbytes_out = good ? nb : ~0ull;
             else { host_tot[0] = F; host_tot[1] = R; }
+            if (!good) drop_error(host_tot, kDropErrRange);
+            state[0] = par ^ 1u;  // the next call's sp_count adds into the other array (sp_emit reads none)
         }
     }
-    const int wave = threadIdx.x >> 6;
     const size_t tb = (size_t)blockIdx.x * kCountTpw;  // the workgroup's first tile (< ntiles)
     const size_t tile = (size_t)__builtin_amdgcn_readfirstlane((int)(tb + wave));
     const bool live = tile < ntiles;  // (wave-uniform; every wave reaches the barrier below)
@@ -1091,17 +1185,22 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     // the prefixes of the workgroup's tiles (F0, R0, P, Q) and their records, by wave 0, through LDS
     __shared__ uint4 s_pre[kCountTpw];
     __shared__ uint2 s_own[kCountTpw];
+    __shared__ uint32_t s_ok;
     if (wave == 0) {
         uint4 pre[kCountTpw];
         uint2 ow[kCountTpw];
-        group_prefix(recA, agg, ntiles, G, tb, (uint32_t)n, pre, ow);
+        uint32_t par;
+        bool ok;
+        group_prefix<DEVPAR>(recA, agg2, hpar, ntiles, G, tb, (uint32_t)n, pre, ow, par, ok);
         if (lane == 0) {
 #pragma unroll
             for (int k = 0; k < kCountTpw; k++) {
                 s_pre[k] = pre[k];
                 s_own[k] = ow[k];
             }
+            s_ok = ok;
         }
+        (void)par;
     }
     const uint32_t valid = valid_w32(n, tile), unk = valid & ~keep;
     uint32_t prev = lane_before(keep >> 31);
@@ -1125,6 +1224,15 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     if (!live) return;  // (no barrier below)
     const uint4 p = s_pre[wave];
     const uint2 own = s_own[wave];
+    // the tile's range inside the buffer, from aggregates that agree with their records — else no store
+    // at all (a wrong prefix never becomes an address), and the call reports the error (uniform)
+    {
+        const size_t end = 8 + 2 * (4 * (size_t)p.y + (size_t)p.x + 4 * (size_t)rec_runs(own.x) + (own.x & 0xFFFFu));
+        if (!s_ok || end > cap) {
+            if (lane == 0) drop_error(host_tot, s_ok ? kDropErrRange : kDropErrStale);
+            return;
+        }
+    }
     // the tile's compact values (sp_count's slot) into LDS in 16-B pieces, read below by position: the
     // lane's k-th kept value is the tile's (ef + k)-th
     const uint32_t Ft = own.x & 0xFFFFu;
@@ -1146,7 +1254,7 @@ __global__ __launch_bounds__(kSB) void sp_emit(const uint16_t *__restrict__ cv, 
     const uint16_t *g16 = cv + tile * kTile + ef;
     uint16_t *w16 = (uint16_t *)(buf + 8);
     const size_t U0 = 4 * (size_t)p.y + (size_t)p.x;  // the tile's first unit
-    const uint32_t nu16 = 4 * (own.x >> 16) + (own.x & 0xFFFFu);
+    const uint32_t nu16 = 4 * rec_runs(own.x) + (own.x & 0xFFFFu);
     if (STAGE && fits && nu16 <= (uint32_t)kEmitStage) {  // (uniform)
         typedef __attribute__((address_space(3))) uint16_t lds_u16;
         lds_u16 *st = (lds_u16 *)stage[STAGE ? wave : 0];
@@ -1352,10 +1460,36 @@ __device__ __forceinline__ void st_u32_2b(uint8_t *p, uint32_t v) {  // a 2-B al
     st_u16(p + 2, (uint16_t)(v >> 16));
 }
 
+// The blocking one-launch drop's completion, in the kernel (no signal launch behind it, no stream wait): every
+// wave waits for its stores to be acknowledged, the workgroup meets, and thread 0 releases at system scope (the
+// wire in pinned coherent memory can sit dirty in its XCD's L2 until written back: without this fence the TCP
+// ring sent frames the host read before their last bytes landed — tools/ono_tcp_bench, profiles/r06_s4_*) and
+// counts the workgroup in; the one whose returned count is the call's `target` (the last of the grid to
+// arrive: every other workgroup's stores are then out) stores the call's tag into host_tot[2], which the host
+// spins on.  The count only grows (the host adds each call's grid to its target), so it is never reset.
+__device__ __forceinline__ void drop1_complete(uint64_t *host_tot, uint64_t *arrive, uint64_t target, uint32_t sig) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);  // (system scope: this XCD's L2 written back)
+        const uint64_t old = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == target) __hip_atomic_store(host_tot + 2, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+// measurement A/B (round 6): ONO_DROP1_SIGNAL=0 waits for the blocking one launch by a signal kernel behind it
+bool drop1_signal_in_kernel() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_DROP1_SIGNAL");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
+}
+
 __global__ __launch_bounds__(kIT) void sp_drop1(const float *__restrict__ g, size_t n, size_t ntiles, float t,
                                                 const float *t_dev, bool vec, uint64_t *desc, uint32_t epoch,
-                                                uint32_t fb_polls, uint8_t *buf, uint64_t *host_tot,
-                                                uint64_t *nbytes_out) {
+                                                uint32_t fb_polls, uint8_t *buf, size_t cap, uint64_t *host_tot,
+                                                uint64_t *nbytes_out, uint64_t *arrive, uint64_t target,
+                                                uint32_t sig) {
     __shared__ uint32_t s_pre[4];
     SP_CLOCK(sp_t0);
     if (t_dev) t = *t_dev;
@@ -1368,6 +1502,7 @@ __global__ __launch_bounds__(kIT) void sp_drop1(const float *__restrict__ g, siz
             if (nbytes_out) *nbytes_out = 8;
             else { host_tot[0] = 0; host_tot[1] = 0; }
         }
+        if (sig) drop1_complete(host_tot, arrive, target, sig);
         return;
     }
     const size_t tile0 = tile * kTile;
@@ -1470,7 +1605,11 @@ __global__ __launch_bounds__(kIT) void sp_drop1(const float *__restrict__ g, siz
     };
     const uint32_t O = (uint32_t)(((uintptr_t)dst & 15u) >> 1);  // the range starts O units into a 16-B chunk
     uint16_t *base16 = (uint16_t *)(dst - 2 * O);
-    const uint32_t nch = nu16 ? (O + nu16 + 7) / 8 : 0;
+    // the range inside the buffer, else no store (uniform; the prefix is a look-back over tagged
+    // granules, so this is the bound that keeps any wrong prefix from becoming an address)
+    const bool in_buf = 8 + 8 * (size_t)R0 + 2 * ((size_t)F0 + nu16) <= cap;
+    if (!in_buf && threadIdx.x == 0) drop_error(host_tot, kDropErrRange);
+    const uint32_t nch = nu16 && in_buf ? (O + nu16 + 7) / 8 : 0;
     for (uint32_t c = threadIdx.x; c < nch; c += kIT) {
         uint16_t v[8];
         bool all = true, any = false;
@@ -1501,15 +1640,18 @@ __global__ __launch_bounds__(kIT) void sp_drop1(const float *__restrict__ g, siz
             const uint32_t end = ti.first_unkept < (uint32_t)kTile && (uint32_t)tile0 + ti.first_unkept < tend
                                      ? (uint32_t)tile0 + ti.first_unkept : (uint32_t)n;
             const size_t hpos = 8 + 8 * (size_t)(R0 - 1) + 2 * (size_t)(F0 - ((uint32_t)tile0 - s0));
-            st_u32_2b(buf + hpos + 4, end - s0);
+            if (hpos + 8 <= cap) st_u32_2b(buf + hpos + 4, end - s0);
+            else drop_error(host_tot, kDropErrRange);
         }
-        if (tile + 1 == ntiles) {  // the total (u64 LE, 2-B aligned buf) and the wire length
+        if (tile + 1 == ntiles) {  // the total (u64 LE, 2-B aligned buf, cap >= 8) and the wire length
             for (int q = 0; q < 4; q++) st_u16(buf + 2 * q, (uint16_t)((uint64_t)n >> (16 * q)));
-            const uint64_t F = F0 + ti.F, R = R0 + ti.R;
-            if (nbytes_out) *nbytes_out = 8 + 8 * R + 2 * F;
+            const uint64_t F = F0 + ti.F, R = R0 + ti.R, nb = 8 + 8 * R + 2 * F;
+            if (nbytes_out) *nbytes_out = nb <= cap ? nb : ~0ull;
             else { host_tot[0] = F; host_tot[1] = R; }
+            if (nb > cap) drop_error(host_tot, kDropErrRange);
         }
     }
+    if (sig) drop1_complete(host_tot, arrive, target, sig);
 #ifdef ONO_SP_STAMP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -3245,7 +3387,9 @@ __global__ void sp_signal(uint64_t *host_word, uint32_t epoch) {
 }
 
 // the totals into the host-mapped words (the exact-size path of a small buffer), one wave
-__global__ void sp_totals_out(const uint4 *agg, uint32_t G, uint64_t *host_tot) {
+// (agg: the call's aggregates; state != NULL: the count + emit form, whose array sp_count named in state[1])
+__global__ void sp_totals_out(const uint4 *agg, size_t half, const uint32_t *state, uint32_t G, uint64_t *host_tot) {
+    if (state && (state[1] & 1u)) agg += half;
     const uint2 t = chunk_totals(agg, G);
     if (threadIdx.x == 0) {
         host_tot[0] = t.x;
@@ -3272,12 +3416,29 @@ struct Scratch {
     uint32_t *mask = nullptr;  // mask_cap tiles of 64 keep words (N / 8 bytes): sp_count / sp_emit
     uint16_t *cv = nullptr;    // mask_cap tile slots of kTile f16 (the kept values, compact): sp_count / sp_emit
     size_t mask_cap = 0;
-    uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;  // [F, R, the completion tag, spare]
+    uint64_t *host_tot = nullptr, *host_tot_dev = nullptr;  // [F, R, the completion tag, the error word]
     // the one-launch form (sp_drop1): 4 granules per tile and per group of tiles (zeroed when
     // allocated, and when the epoch wraps), the call's epoch
     uint64_t *desc = nullptr;
     size_t desc_cap = 0;
     uint32_t depoch = 0;
+    // the blocking one launch's in-kernel completion: workgroups counted in (device, never reset), and the
+    // count the call before this one ended at
+    uint64_t *arrive = nullptr;
+    uint64_t arrive_base = 0;
+    // count + emit: the aggregate parity on the device ([0] the array sp_count adds into, flipped by
+    // sp_emit; [1] the array of the call in flight, for sp_totals_out), zeroed with agg
+    uint32_t *state = nullptr;
+    // the host's copy of state[0] while every call on the stream was uncaptured (par_known): sp_emit then takes
+    // it as an argument and loads one array; after a capture only the device knows it (sp_emit<.., true>)
+    bool par_known = true;
+    uint32_t hpar = 0;
+    // a graph captured a call on this stream: its kernels hold these arrays, so they are never freed or
+    // regrown in place (a larger call moves them to `retired` and allocates new ones)
+    bool captured = false;
+    // sp_count ran without its sp_emit (a failed launch): the aggregates are re-zeroed before the next call
+    bool dirty = false;
+    std::vector<void *> retired;
 };
 std::mutex g_scratch_mu;
 std::map<std::pair<int, hipStream_t>, Scratch> g_scratch;
@@ -3292,6 +3453,11 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = t
         ONO_HIP(hipHostGetDevicePointer((void **)&sc.host_tot_dev, sc.host_tot, 0));
         sc.host_tot[3] = 0;
     }
+    if (!sc.arrive) {
+        ONO_HIP(hipMalloc((void **)&sc.arrive, 64));
+        ONO_HIP(hipMemsetAsync(sc.arrive, 0, 64, stream));
+        sc.arrive_base = 0;
+    }
     if (!image) {  // sp_drop1's granules instead of the slot image
         const size_t want = std::max<size_t>(ntiles + (ntiles + kDropGroup - 1) / kDropGroup, 1);  // tiles, groups
         if (want > sc.desc_cap) {
@@ -3305,39 +3471,65 @@ int scratch_for(size_t ntiles, hipStream_t stream, Scratch **out, bool image = t
         *out = &sc;
         return ONO_OK;
     }
-    if (ntiles > sc.tiles_cap) {
-        (void)hipFree(sc.rec);
-        (void)hipFree(sc.agg);
+    // a captured graph's arrays are retired, not freed (the graph may be replayed as long as it exists)
+    auto drop_arr = [&sc](void *p) {
+        if (!p) return;
+        if (sc.captured) sc.retired.push_back(p);
+        else (void)hipFree(p);
+    };
+    if (ntiles > sc.tiles_cap || !sc.state) {
+        drop_arr(sc.rec);
+        drop_arr(sc.agg);
+        drop_arr(sc.state);
         sc.rec = nullptr;
         sc.agg = nullptr;
+        sc.state = nullptr;
         sc.tiles_cap = sc.agg_cap = 0;
-        const size_t gcap = (ntiles + kRecChunk - 1) / kRecChunk;
-        ONO_HIP(hipMalloc((void **)&sc.rec, 2 * ntiles * sizeof(uint2)));
-        ONO_HIP(hipMalloc((void **)&sc.agg, 2 * gcap * kAggStride * sizeof(uint4)));
-        ONO_HIP(hipMemsetAsync(sc.agg, 0, 2 * gcap * kAggStride * sizeof(uint4), stream));
-        sc.tiles_cap = ntiles;
+        const size_t tc = std::max<size_t>(ntiles, 1), gcap = (tc + kRecChunk - 1) / kRecChunk;
+        ONO_HIP(hipMalloc((void **)&sc.rec, 2 * tc * sizeof(uint2)));
+        ONO_HIP(hipMalloc((void **)&sc.agg, gcap * kAggStride * sizeof(uint4)));  // (both arrays: kAggHalf)
+        ONO_HIP(hipMemsetAsync(sc.agg, 0, gcap * kAggStride * sizeof(uint4), stream));
+        ONO_HIP(hipMalloc((void **)&sc.state, 16 * sizeof(uint32_t)));
+        ONO_HIP(hipMemsetAsync(sc.state, 0, 16 * sizeof(uint32_t), stream));
+        sc.tiles_cap = tc;
         sc.agg_cap = gcap;
         sc.parity = 0;
+        sc.dirty = false;
+        sc.par_known = true;
+        sc.hpar = 0;
     }
     if (!emit && ntiles > sc.img_cap) {
-        (void)hipFree(sc.img);
+        drop_arr(sc.img);
         sc.img = nullptr;
         sc.img_cap = 0;
         ONO_HIP(hipMalloc((void **)&sc.img, ntiles * kSlotU16 * sizeof(uint16_t)));
         sc.img_cap = ntiles;
     }
-    if (emit && ntiles > sc.mask_cap) {
-        (void)hipFree(sc.mask);
-        (void)hipFree(sc.cv);
+    if (emit && (ntiles > sc.mask_cap || !sc.mask)) {
+        drop_arr(sc.mask);
+        drop_arr(sc.cv);
         sc.mask = nullptr;
         sc.cv = nullptr;
         sc.mask_cap = 0;
-        ONO_HIP(hipMalloc((void **)&sc.mask, ntiles * 64 * sizeof(uint32_t)));
-        ONO_HIP(hipMalloc((void **)&sc.cv, ntiles * kTile * sizeof(uint16_t)));
-        sc.mask_cap = ntiles;
+        const size_t tc = std::max<size_t>(ntiles, 1);
+        ONO_HIP(hipMalloc((void **)&sc.mask, tc * 64 * sizeof(uint32_t)));
+        ONO_HIP(hipMalloc((void **)&sc.cv, tc * kTile * sizeof(uint16_t)));
+        sc.mask_cap = tc;
     }
     *out = &sc;
     return ONO_OK;
+}
+// Under stream capture nothing may be allocated or zeroed (a memset would become a graph node that every
+// replay runs; an allocation is not allowed while the stream captures): the call's arrays must exist from
+// an earlier uncaptured call on the stream.  Returns the scratch, or NULL.
+Scratch *scratch_ready(size_t ntiles, hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    auto it = g_scratch.find({dev, stream});
+    if (it == g_scratch.end()) return nullptr;
+    Scratch &sc = it->second;
+    if (!sc.host_tot || !sc.state || !sc.mask || sc.dirty || ntiles > sc.tiles_cap || ntiles > sc.mask_cap) return nullptr;
+    return &sc;
 }
 
 struct LiftScratch {
@@ -3488,12 +3680,18 @@ int lift_host_path(float *g, const uint8_t *hbuf, const uint8_t *dbuf, size_t nb
 // wake-up is the larger part of a blocking call's host time otherwise: 38.3-
 // 39.0 against 42.4-42.7 us per 64 MiB lift, same box); after ~2 s without the
 // signal (a faulted kernel) the stream synchronisation reports the error.
+hipError_t host_spin(hipStream_t s, uint64_t *word_host, uint32_t epoch);
 hipError_t host_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uint32_t epoch) {
     volatile uint64_t *w = word_host;
     *w = 0;  // (a lift may wait more than once under one epoch)
     hipLaunchKernelGGL(sp_signal, dim3(1), dim3(64), 0, s, word_dev, epoch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    return host_spin(s, word_host, epoch);
+}
+// the spin of host_wait, on a word the stream's own kernel stores (sp_drop1's in-kernel completion)
+hipError_t host_spin(hipStream_t s, uint64_t *word_host, uint32_t epoch) {
+    volatile uint64_t *w = word_host;
     // A tight spin for the lift's own few tens of microseconds; beyond that the
     // stream had other work queued ahead of the call (training kernels before a
     // TCP hop's drop or lift), so the thread backs off — pause, then yield —
@@ -3702,7 +3900,9 @@ __device__ __forceinline__ void transpose32(uint32_t (&A)[32]) {
         }
     }
 }
-// keys: the gathered keys, or NULL: the sample is g[0, m) itself
+// keys: the gathered keys, or NULL: the sample is g[0, m) itself.  (Round 6 measured gathering g[idx[i]] here
+// instead of in sp_gather_keys, one launch less: +10 us per SparseCapable push of the config-1 TCP ring — one
+// workgroup's 16384 scattered loads cost more than the gather's launch; profiles/r06_s4_tcp_variants.jsonl.)
 __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, const float *g, uint32_t m, uint32_t k,
                                                       float *t_out) {
     __shared__ uint32_t wc[2][kThrT / 64][2];
@@ -3760,7 +3960,7 @@ __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, cons
     }
 }
 // the select over g[0, m) (idx NULL) or over g[idx[i]] (keys: m device words for the gathered keys; idx
-// may be the same buffer)
+// may be the same buffer; in HBM or pinned host memory)
 hipError_t launch_threshold(const float *g, const uint32_t *idx, uint32_t *keys, uint32_t m, uint32_t k, float *t_out,
                             hipStream_t s) {
     if (idx)
@@ -3854,6 +4054,18 @@ size_t drop_one_launch_tiles() {
     return v;
 }
 
+// the error word an encoder left (host_tot[3]), cleared
+int take_drop_error(Scratch *sc, const char *when) {
+    volatile uint64_t *w = sc->host_tot;
+    const uint64_t code = w[3];
+    if (!code) return ONO_OK;
+    w[3] = 0;
+    return set_error(ONO_E_IO, "sparse drop%s: %s", when,
+                     code == kDropErrStale ? "chunk aggregates disagree with their tile records (not zero when the "
+                                             "call began); nothing was written past the buffer"
+                                           : "a tile's range would pass the end of the buffer; it was not written");
+}
+
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s, const float *t_dev = nullptr) {
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
@@ -3861,12 +4073,51 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
     std::lock_guard<std::mutex> lk(g_scratch_mu);  // the host side of one call at a time
     Scratch *sc = nullptr;
+    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cap_st) == hipSuccess && cap_st != hipStreamCaptureStatusNone;
+    if (capturing) {
+        // Captured: the stream-ordered two launches (count + emit), whose only state between calls is on
+        // the device (the aggregate parity), over arrays an earlier uncaptured call on this stream made.
+        // Not the one launch (a replay would repeat its epoch), not a blocking call (it waits for its
+        // result), no allocation or memset (r05: a captured form with memset nodes faulted on replay).
+        if (!nbytes_dev) return set_error(ONO_E_ARG, "the blocking sparse drop cannot be captured (use the stream-ordered one)");
+        if (!drop_emit()) return set_error(ONO_E_ARG, "the image-form drop (ONO_DROP_FORM=image) cannot be captured");
+        if (ntiles == 0) {  // the total alone (sp_drop1's empty case reads no descriptor and no scratch)
+            hipLaunchKernelGGL(sp_drop1, dim3(1), dim3(kIT), 0, s, g, n, (size_t)0, threshold, t_dev, vec,
+                               (uint64_t *)nullptr, 0u, 0u, buf, cap, (uint64_t *)nullptr, nbytes_dev,
+                               (uint64_t *)nullptr, (uint64_t)0, 0u);
+            ONO_HIP(hipGetLastError());
+            return ONO_OK;
+        }
+        sc = scratch_ready(ntiles, s);
+        if (!sc)
+            return set_error(ONO_E_ARG, "sparse drop under capture: call it once on this stream outside the capture "
+                                        "first (its scratch for %zu tiles is made there)", ntiles);
+        sc->captured = true;
+        sc->par_known = false;  // from now on replays flip the device parity behind the host's back
+    }
+    const bool emit = drop_emit();
+    if (!capturing) {
+        // the two-launch arrays whatever the form this call takes, so that a capture on this stream finds
+        // them (up to 256 tiles ~1.1 MB)
+        int rc = scratch_for(ntiles, s, &sc, true, emit);
+        if (rc) return rc;
+        if ((rc = take_drop_error(sc, " (an earlier call on this stream)"))) return rc;
+        if (sc->dirty) {  // an earlier sp_count without its sp_emit: both arrays and the parity from zero
+            ONO_HIP(hipMemsetAsync(sc->agg, 0, sc->agg_cap * kAggStride * sizeof(uint4), s));
+            ONO_HIP(hipMemsetAsync(sc->state, 0, 16 * sizeof(uint32_t), s));
+            sc->dirty = false;
+            sc->parity = 0;
+            if (!sc->captured) {  // (a graph's replays still flip the device parity)
+                sc->par_known = true;
+                sc->hpar = 0;
+            }
+        }
+    }
     // the one-launch form when the buffer holds the worst case (it writes as it goes) and the stream is
     // not being captured (a replayed graph would repeat the epoch: the last replay's descriptors would
     // read as this one's)
-    hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
-    const bool capturing = hipStreamIsCapturing(s, &cap_st) == hipSuccess && cap_st != hipStreamCaptureStatusNone;
-    if (drop_fused() && worst_case_fits && !capturing && ntiles <= drop_one_launch_tiles()) {
+    if (!capturing && drop_fused() && worst_case_fits && ntiles <= drop_one_launch_tiles()) {
         int rc = scratch_for(ntiles, s, &sc, false);
         if (rc) return rc;
         if (++sc->depoch == 0 || sc->depoch >= 0x7FFFFFFFu) {  // tags 2 e, 2 e + 1 stay nonzero and distinct
@@ -3874,36 +4125,49 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
             sc->depoch = 1;
         }
         const uint32_t grid = (uint32_t)std::max<size_t>(ntiles, 1);
+        // blocking: the kernel signals its own completion (drop1_complete) — no signal launch, no stream wait
+        uint32_t sig = 0;
+        uint64_t target = 0;
+        const bool in_kernel = drop1_signal_in_kernel();
+        if (!nbytes_dev && in_kernel) {
+            if (++sc->calls == 0) sc->calls = 1;
+            sig = sc->calls;
+            target = sc->arrive_base + grid - 1;
+            *(volatile uint64_t *)(sc->host_tot + 2) = 0;
+        }
         hipLaunchKernelGGL(sp_drop1, dim3(grid), dim3(kIT), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->desc,
-                           sc->depoch, drop_fallback_polls(), buf, sc->host_tot_dev, nbytes_dev);
+                           sc->depoch, drop_fallback_polls(), buf, cap, sc->host_tot_dev, nbytes_dev, sc->arrive,
+                           target, sig);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
         if (nbytes_dev) return ONO_OK;
         volatile uint64_t *tot = sc->host_tot;
-        if (++sc->calls == 0) sc->calls = 1;
-        e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
+        if (in_kernel) {
+            sc->arrive_base += grid;
+            e = host_spin(s, sc->host_tot + 2, sig);
+        } else {
+            if (++sc->calls == 0) sc->calls = 1;
+            e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
+        }
         if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
+        if ((rc = take_drop_error(sc, ""))) return rc;
         *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
         return ONO_OK;
     }
-    // not under stream capture: the two launches keep host-side state between calls (which chunk
-    // aggregates are zero), which a replayed graph would not follow
-    if (capturing) return set_error(ONO_E_ARG, "the sparse drop cannot be captured into a graph");
-    const bool emit = drop_emit();
-    int rc = scratch_for(ntiles, s, &sc, true, emit);
-    if (rc) return rc;
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
     const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
-    uint4 *agg = sc->agg + sc->parity * sc->agg_cap * kAggStride;
-    uint4 *agg_next = sc->agg + (1 - sc->parity) * sc->agg_cap * kAggStride;
+    const size_t half = kAggHalf;  // (the second array, within each chunk's line)
+    // the image form keeps its parity on the host (it is never captured); count + emit on the device
+    uint4 *agg = sc->agg + sc->parity * half;
+    uint4 *agg_next = sc->agg + (1 - sc->parity) * half;
     volatile uint64_t *tot = sc->host_tot;  // pinned, written by the device
     if (!nbytes_dev) tot[0] = tot[1] = 0;
     hipError_t e = hipSuccess;
     if (ntiles && emit) {
         hipLaunchKernelGGL(sp_count, dim3((unsigned)count_grid(ntiles)), dim3(kSB), 0, s, g, n, ntiles, threshold, t_dev, vec,
-                           sc->mask, sc->cv, recA, agg, agg_next, (uint32_t)sc->agg_cap);
+                           sc->mask, sc->cv, recA, sc->agg, (uint32_t)sc->agg_cap, sc->state);
         e = hipGetLastError();
-        if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
+        if (e == hipSuccess) sc->dirty = true;  // until its sp_emit is launched
     } else if (ntiles) {
         const size_t grid = (ntiles + kImageTpw - 1) / kImageTpw;
         hipLaunchKernelGGL(sp_image, dim3((unsigned)grid), dim3(kIT), 0, s, g, n, ntiles, (uint32_t)kImageTpw, threshold,
@@ -3911,9 +4175,11 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
         e = hipGetLastError();
         if (e == hipSuccess) sc->parity ^= 1;  // agg_next is zeroed for the next call
     }
-    if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip)
-        hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, agg, (uint32_t)nchunks, sc->host_tot_dev);
+    if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip; never captured)
+        hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, emit ? sc->agg : agg, half,
+                           emit ? (const uint32_t *)sc->state : nullptr, (uint32_t)nchunks, sc->host_tot_dev);
         e = hipStreamSynchronize(s);
+        // (count + emit: no sp_emit follows, so the call stays `dirty` and the next one re-zeroes)
         if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
             return set_error(ONO_E_SIZE, "sparse encoding needs %zu bytes, buffer holds %zu",
                              (size_t)(8 + 8 * tot[1] + 2 * tot[0]), cap);
@@ -3923,23 +4189,44 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
 #ifdef ONO_EXP_COUNT
     if (emit) return 0;  // measurement builds: sp_count alone
 #endif
-    if (emit && emit_stage())
-        hipLaunchKernelGGL(sp_emit<true>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA,
-                           agg, buf, sc->host_tot_dev, nbytes_dev);
-    else if (emit)
-        hipLaunchKernelGGL(sp_emit<false>, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA,
-                           agg, buf, sc->host_tot_dev, nbytes_dev);
+    const bool dp = !sc->par_known;
+    const uint32_t hp = sc->hpar;
+    if (emit) {
+        auto k = emit_stage() ? (dp ? sp_emit<true, true> : sp_emit<true, false>)
+                              : (dp ? sp_emit<false, true> : sp_emit<false, false>);
+        hipLaunchKernelGGL(k, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->cv, n, ntiles, sc->mask, recA, sc->agg,
+                           sc->state, hp, buf, cap, sc->host_tot_dev, nbytes_dev);
+    }
     else
         hipLaunchKernelGGL(sp_move, dim3((unsigned)mblocks), dim3(kSB), 0, s, sc->img, recA, recB, agg, ntiles, n, buf,
-                           sc->host_tot_dev, nbytes_dev);
+                           cap, sc->host_tot_dev, nbytes_dev);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
+    if (emit) {
+        sc->dirty = false;
+        sc->hpar ^= 1u;  // (sp_emit flipped state[0])
+    }
     if (nbytes_dev) return ONO_OK;
     if (++sc->calls == 0) sc->calls = 1;
     e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
+    int rc = take_drop_error(sc, "");
+    if (rc) return rc;
     *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
     return ONO_OK;
+}
+
+// Test hook (ono_sparse_drop_debug_stale): adds `add` to the kept values and runs of every chunk aggregate
+// in the array the stream's next sp_count adds into — an aggregate that was not zero when the call began,
+// the hazard the writers' bounds and sp_emit's record check exist for.
+__global__ void sp_poison(uint4 *agg2, size_t half, const uint32_t *state, uint32_t G, uint32_t add) {
+    uint4 *agg = agg2 + (size_t)(state[0] & 1u) * half;
+    for (uint32_t j = threadIdx.x; j < G; j += blockDim.x) {
+        uint4 a = agg[(size_t)j * kAggStride];
+        a.x += add;
+        a.y += add;
+        agg[(size_t)j * kAggStride] = a;
+    }
 }
 
 int drop_args(const float *g, size_t n, const uint8_t *buf, size_t cap) {
@@ -3970,6 +4257,32 @@ int ono_sparse_drop_async(uint8_t *buf, size_t cap, uint64_t *nbytes_dev, const 
         return set_error(ONO_E_SIZE, "the stream-ordered drop needs the worst-case buffer (%zu bytes, have %zu)",
                          ono_sparse_max_bytes(n), cap);
     return drop_launch(buf, cap, nullptr, nbytes_dev, g, n, threshold, reinterpret_cast<hipStream_t>(stream));
+}
+
+int ono_sparse_drop_check(void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ONO_HIP(hipStreamSynchronize(s));
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    auto it = g_scratch.find({dev, s});
+    if (it == g_scratch.end() || !it->second.host_tot) return ONO_OK;
+    return take_drop_error(&it->second, "");
+}
+
+int ono_sparse_drop_debug_stale(void *stream, uint32_t add) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    int dev = 0;
+    ONO_HIP(hipGetDevice(&dev));
+    auto it = g_scratch.find({dev, s});
+    if (it == g_scratch.end() || !it->second.state)
+        return set_error(ONO_E_ARG, "no count + emit drop has run on this stream");
+    Scratch &sc = it->second;
+    hipLaunchKernelGGL(sp_poison, dim3(1), dim3(256), 0, s, sc.agg, (size_t)kAggHalf, (const uint32_t *)sc.state,
+                       (uint32_t)sc.agg_cap, add);
+    ONO_HIP(hipGetLastError());
+    return ONO_OK;
 }
 
 int ono_sparse_lift(float *g, size_t cap, size_t *out_len, const uint8_t *buf, size_t nbytes, void *stream) {

@@ -71,6 +71,21 @@ constexpr size_t kSampleMax = 16384;              // SAMPLE_SIZE (protocol.rs:13
 // a SparseGrad push whose worst-case stream fits this is encoded straight into a pinned frame (the drop's
 // own wait covers it: no D2H and no second wait); larger ones come down in pieces beside the send
 constexpr size_t kSparseZeroCopy = size_t(4) << 20;
+// measurement A/B (round 6), read once: ONO_TCP_LIFT_PINNED=0 copies a received SparseGrad into HBM before the
+// lift (round 5's form) instead of lifting from the pinned frame; ONO_THR_HBM=0 gathers the sample's keys
+// from the pinned indices even when the helper thread put them in HBM
+bool env_on(const char *name) {
+    const char *e = getenv(name);
+    return !(e && !strcmp(e, "0"));
+}
+bool lift_pinned() {
+    static const bool v = env_on("ONO_TCP_LIFT_PINNED");
+    return v;
+}
+bool thr_hbm() {
+    static const bool v = env_on("ONO_THR_HBM");
+    return v;
+}
 
 enum : uint32_t {
     KIND_CONTROL = 0,
@@ -138,7 +153,11 @@ struct Incoming {
     uint8_t *dense_dev = nullptr;
     uint32_t kind = 0;  // result: KIND_DENSE, KIND_DENSE_OTHER, KIND_SPARSE, or the kind byte 0 / 5 / 6
     size_t bytes = 0;   // result: payload bytes
+    bool sparse_dev = false;  // result: a large SparseGrad also went up to r->sp_rx_dev piece by piece
 };
+// a SparseGrad longer than this goes up to HBM in pieces while it is still on the socket (as a dense payload
+// does), so that its lift starts at its last byte; shorter ones are lifted from the pinned frame
+constexpr size_t kSparseUpload = size_t(1) << 20;
 
 // Wait until `fd` is ready for `ev`; false (with e set) on abort, stop or poll error.
 bool tcp_wait(ono_ring *r, int fd, short ev, const std::atomic<bool> &stop, TcpErr &e) {
@@ -210,11 +229,26 @@ struct TcpRecv {
             in.kind = (kind == KIND_SPARSE || kind == KIND_SPARSE_LAST) ? KIND_SPARSE : kind;
         }
         if (!dst) {  // the whole payload to host memory
-            // (+8: the hop's copy kernel moves whole 4-byte words, up to 3 bytes past the payload)
-            if (int rc = grow_pinned(&r->sp_rx, &r->sp_rx_cap, std::max<size_t>(pay, 8) + 8)) {
+            // (+64: the lift reads the frame in place in whole 8-byte words, the copy kernel in 4-byte ones)
+            if (int rc = grow_pinned(&r->sp_rx, &r->sp_rx_cap, std::max<size_t>(pay, 8) + 64)) {
                 e.code = rc; snprintf(e.msg, sizeof e.msg, "%s", ono_last_error()); return false;
             }
             dst = r->sp_rx;
+            if (in.kind == KIND_SPARSE && pay > kSparseUpload) {  // and up to HBM piece by piece (the lift's input)
+                const size_t want = (size_t)pay + 64;
+                if (r->sp_rx_dev_cap < want) {
+                    (void)hipFree(r->sp_rx_dev);
+                    r->sp_rx_dev = nullptr;
+                    r->sp_rx_dev_cap = 0;
+                    if (hipMalloc((void **)&r->sp_rx_dev, want) != hipSuccess) {
+                        e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "device buffer for a SparseGrad frame");
+                        return false;
+                    }
+                    r->sp_rx_dev_cap = want;
+                }
+                dev = r->sp_rx_dev;
+                in.sparse_dev = true;
+            }
         }
         in.bytes = (size_t)pay;
         need = 12 + (size_t)pay;
@@ -332,10 +366,13 @@ namespace ono {
 struct SampleAhead {
     std::mutex mu;
     std::condition_variable cv;
-    bool stop = false, job = false, busy = false, ready = false;
+    bool stop = false, job = false, busy = false, ready = false, up = false;
     uint64_t st_in = 0, st_out = 0;
     size_t len = 0, m = 0;
-    uint32_t *buf = nullptr;  // pinned, kSampleMax indices
+    uint32_t *buf = nullptr;   // pinned, kSampleMax indices
+    uint32_t *dbuf = nullptr;  // the same draw in HBM (uploaded by this thread on its own stream)
+    int device = 0;
+    hipStream_t ust = nullptr;  // (non-blocking: no implicit order with the ring's stream)
     int rc = ONO_OK;
     std::thread th;
 
@@ -347,12 +384,20 @@ struct SampleAhead {
             job = false;
             uint64_t st = st_in;
             const size_t L = len, mm = m;
-            uint32_t *b = buf;
+            uint32_t *b = buf, *db = dbuf;
             lk.unlock();
             const int e = ono_sparse_sample_default(&st, L, b, mm);
+            // the indices up to HBM here, off the push's path: the push's threshold then reads them there
+            // (read in place from pinned memory they cost the gather ~6 us per push; an upload on the
+            // ring's stream ~30 us of copy-engine hand-off)
+            bool u = false;
+            if (e == ONO_OK && db && ust && hipSetDevice(device) == hipSuccess &&
+                hipMemcpyAsync(db, b, mm * sizeof(uint32_t), hipMemcpyHostToDevice, ust) == hipSuccess)
+                u = hipStreamSynchronize(ust) == hipSuccess;
             lk.lock();
             st_out = st;
             rc = e;
+            up = u;
             ready = true;
             cv.notify_all();
         }
@@ -366,14 +411,20 @@ struct SampleAhead {
         ready = false;
         cv.notify_all();
     }
-    // the draw for (st, L, mm) if it was made ahead: *idx swapped with the spare buffer, *st advanced
-    bool take(uint64_t *st, size_t L, size_t mm, uint32_t **idx) {
+    // the draw for (st, L, mm) if it was made ahead: *idx swapped with the spare buffer, *st advanced; when
+    // it is also in HBM, *didx swapped with the spare device buffer and *in_hbm set
+    bool take(uint64_t *st, size_t L, size_t mm, uint32_t **idx, uint32_t **didx, bool *in_hbm) {
         std::unique_lock<std::mutex> lk(mu);
+        *in_hbm = false;
         if (!busy) return false;
         cv.wait(lk, [&] { return ready; });
         busy = false;
         if (rc != ONO_OK || st_in != *st || len != L || m != mm) return false;
         std::swap(*idx, buf);
+        if (up && didx && *didx) {
+            std::swap(*didx, dbuf);
+            *in_hbm = true;
+        }
         *st = st_out;
         return true;
     }
@@ -388,6 +439,8 @@ void sample_ahead_free(SampleAhead *a) {
     }
     if (a->th.joinable()) a->th.join();
     if (a->buf) (void)hipHostFree(a->buf);
+    if (a->dbuf) (void)hipFree(a->dbuf);
+    if (a->ust) (void)hipStreamDestroy(a->ust);
     delete a;
 }
 
@@ -401,6 +454,7 @@ int alloc_sample(ono_ring *r) {
     DeviceGuard g(r->device);
     ONO_HIP(hipHostMalloc((void **)&r->sample_idx, kSampleMax * sizeof(uint32_t), hipHostMallocDefault));
     ONO_HIP(hipMalloc((void **)&r->sp_idx_dev, kSampleMax * sizeof(uint32_t)));
+    ONO_HIP(hipMalloc((void **)&r->sample_idx_hbm, kSampleMax * sizeof(uint32_t)));
     ONO_HIP(hipMalloc((void **)&r->sp_t_dev, sizeof(float)));
     ONO_HIP(hipHostMalloc((void **)&r->sp_status, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
     *r->sp_status = 0;
@@ -547,13 +601,13 @@ private:
     // it there (no host round trip; the host never needs the value)
     int threshold(const float *chunk, size_t L, size_t next_L) {
         const size_t m = std::min(L, kSampleMax);
-        bool sampled = false;
+        bool sampled = false, in_hbm = false;
         if (r_->sampler) {
             if (r_->sampler(r_->sampler_ctx, L, r_->sample_idx, m) != 0)
                 return set_error(ONO_E_OTHER, "the sampler failed for a chunk of %zu values", L);
             sampled = L > kSampleMax;
         } else if (L > kSampleMax) {
-            if (!r_->ahead || !r_->ahead->take(&r_->sample_state, L, m, &r_->sample_idx)) {
+            if (!r_->ahead || !r_->ahead->take(&r_->sample_state, L, m, &r_->sample_idx, &r_->sample_idx_hbm, &in_hbm)) {
                 int rc = ono_sparse_sample_default(&r_->sample_state, L, r_->sample_idx, m);
                 if (rc) return rc;
             }
@@ -561,10 +615,13 @@ private:
             if (next_L > kSampleMax) {  // the next push's draw, while this one's frame is made and sent
                 if (!r_->ahead) {
                     auto *a = new SampleAhead();
+                    a->device = r_->device;
                     if (hipHostMalloc((void **)&a->buf, kSampleMax * sizeof(uint32_t), hipHostMallocDefault) !=
-                        hipSuccess) {
-                        delete a;
-                        return set_error(ONO_E_HIP, "pinned sample buffer");
+                            hipSuccess ||
+                        hipMalloc((void **)&a->dbuf, kSampleMax * sizeof(uint32_t)) != hipSuccess ||
+                        hipStreamCreateWithFlags(&a->ust, hipStreamNonBlocking) != hipSuccess) {
+                        sample_ahead_free(a);
+                        return set_error(ONO_E_HIP, "sample buffers");
                     }
                     a->th = std::thread([a] { a->loop(); });
                     r_->ahead = a;
@@ -577,8 +634,10 @@ private:
                 if (r_->sample_idx[i] >= L) return set_error(ONO_E_ARG, "sample index %u out of %zu", r_->sample_idx[i], L);
         // the gather kernel reads the pinned indices in place (an upload by the copy engine cost ~30 us
         // of cross-engine hand-off per push); the buffer is not rewritten before this push's drop returns
+        // — unless the helper thread already put the draw in HBM, where the gather reads it
         uint32_t *idx_dev = nullptr;
-        if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, r_->sample_idx, 0));
+        if (sampled && in_hbm && thr_hbm()) idx_dev = r_->sample_idx_hbm;
+        else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, r_->sample_idx, 0));
         return sparse_threshold_dev(r_->sp_t_dev, chunk, L, idx_dev, r_->sp_idx_dev, m, r_->sparse_r, s_);
     }
 
@@ -657,7 +716,7 @@ private:
             return ONO_OK;
         }
         const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
-        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes); });
+        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes, in.sparse_dev); });
         // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
         if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
         if (rc) return rc;
@@ -666,27 +725,45 @@ private:
         return ONO_OK;
     }
 
-    // grad_lift_into of the received stream (r->sp_rx, host): uploaded, then the stream-ordered lift
-    // (ono_sparse_lift_dev_async: the pattern path, one or two launches); a stream it refuses (not
-    // drop-shaped, malformed) goes to the blocking device lift, which parses anything and returns the
+    // grad_lift_into of the received stream (r->sp_rx, pinned host): the stream-ordered lift
+    // (ono_sparse_lift_dev_async: the pattern path, one or two launches) reads the frame in place through
+    // its device mapping — no copy of the frame into HBM in the hop; a stream it refuses (not drop-shaped,
+    // malformed) goes up to HBM and to the blocking device lift, which parses anything and returns the
     // reference's errors.  *got = the stream's total.
-    int lift(float *out, size_t cap, size_t *got, size_t nbytes) {
+    int lift(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev) {
         if (nbytes < 8) return ono_sparse_lift(out, cap, got, r_->sp_rx, nbytes, s_);
-        const size_t words = (nbytes + 3) & ~size_t(3);  // whole words for the copy kernel
-        if (r_->sp_rx_dev_cap < words) {
-            (void)hipFree(r_->sp_rx_dev);
-            r_->sp_rx_dev = nullptr;
-            r_->sp_rx_dev_cap = 0;
-            const size_t c2 = std::max(words, ono_sparse_max_bytes(r_->maxc) + 8);
-            ONO_HIP(hipMalloc((void **)&r_->sp_rx_dev, c2));
-            r_->sp_rx_dev_cap = c2;
+        if (in_dev) {  // a large frame already went up piece by piece (TcpRecv): lifted from HBM
+            uint64_t ticket = 0;
+            int rc = ono_sparse_lift_dev_async(out, cap, r_->sp_rx_dev, nbytes, r_->sp_status, &ticket, s_);
+            if (rc || (rc = wait())) return rc;
+            if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
+                uint64_t total = 0;
+                memcpy(&total, r_->sp_rx, 8);  // (little endian, protocol.rs:102-106)
+                *got = (size_t)total;
+                return ONO_OK;
+            }
+            return ono_sparse_lift_dev(out, cap, got, r_->sp_rx_dev, nbytes, s_);
         }
-        // up by the library's copy kernel reading the pinned frame in place: no copy engine in the hop
         const uint8_t *src = nullptr;
         ONO_HIP(hipHostGetDevicePointer((void **)&src, r_->sp_rx, 0));
-        ONO_HIP(dev_copy(r_->sp_rx_dev, src, words, s_));
+        const size_t words = (nbytes + 3) & ~size_t(3);  // whole words for the copy kernel
+        auto up = [&]() -> int {
+            if (r_->sp_rx_dev_cap < words) {
+                (void)hipFree(r_->sp_rx_dev);
+                r_->sp_rx_dev = nullptr;
+                r_->sp_rx_dev_cap = 0;
+                const size_t c2 = std::max(words, ono_sparse_max_bytes(r_->maxc) + 8);
+                ONO_HIP(hipMalloc((void **)&r_->sp_rx_dev, c2));
+                r_->sp_rx_dev_cap = c2;
+            }
+            ONO_HIP(dev_copy(r_->sp_rx_dev, src, words, s_));
+            return ONO_OK;
+        };
+        const bool pinned = lift_pinned();
+        int rc = pinned ? ONO_OK : up();
+        if (rc) return rc;
         uint64_t ticket = 0;
-        int rc = ono_sparse_lift_dev_async(out, cap, r_->sp_rx_dev, nbytes, r_->sp_status, &ticket, s_);
+        rc = ono_sparse_lift_dev_async(out, cap, pinned ? src : r_->sp_rx_dev, nbytes, r_->sp_status, &ticket, s_);
         if (rc || (rc = wait())) return rc;
         if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
             uint64_t total = 0;
@@ -694,6 +771,7 @@ private:
             *got = (size_t)total;
             return ONO_OK;
         }
+        if (pinned && (rc = up())) return rc;
         return ono_sparse_lift_dev(out, cap, got, r_->sp_rx_dev, nbytes, s_);
     }
 

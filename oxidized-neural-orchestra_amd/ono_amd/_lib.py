@@ -110,6 +110,8 @@ _SIGS = {
     "ono_sparse_max_bytes": (_sz, [_sz]),
     "ono_sparse_drop": (_i, [_vp, _sz, C.POINTER(C.c_size_t), _fp, _sz, C.c_float, _vp]),
     "ono_sparse_drop_async": (_i, [_vp, _sz, _vp, _fp, _sz, C.c_float, _vp]),
+    "ono_sparse_drop_check": (_i, [_vp]),
+    "ono_sparse_drop_debug_stale": (_i, [_vp, C.c_uint32]),
     "ono_sparse_lift": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_dev": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_fallbacks": (_sz, []),

@@ -104,6 +104,19 @@ def grad_drop_async(g: torch.Tensor, threshold: float, buf: torch.Tensor, nbytes
          float(threshold), kernels.stream_handle(stream))
 
 
+def drop_check(stream=None) -> None:
+    """ono_sparse_drop_check: synchronizes the stream and raises IoError if a
+    stream-ordered drop on it found a range past its buffer or stale chunk
+    aggregates (nothing was stored out of bounds either way)."""
+    call("ono_sparse_drop_check", kernels.stream_handle(stream))
+
+
+def drop_debug_stale(add: int, stream=None) -> None:
+    """Test hook (ono_sparse_drop_debug_stale): the stream's next two-launch
+    drop starts from chunk aggregates that are not zero."""
+    call("ono_sparse_drop_debug_stale", kernels.stream_handle(stream), int(add))
+
+
 def grad_lift_dev(buf: torch.Tensor, cap: int | None = None, stream=None) -> torch.Tensor:
     """grad_lift of wire bytes already in HBM (ono_sparse_lift_dev)."""
     assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()

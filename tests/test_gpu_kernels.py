@@ -190,22 +190,24 @@ def test_synth_matches_oracle(n, seed, rank, offset):
         assert_bitexact(host(t), O.synth(n, seed, rank, offset))
 
 
-def test_full_size_sum_scale_property():
-    """64 MiB bucket (BASELINE config 2), k = 4: the kernel equals the oracle
-    on a strided sample and sum(out) * 4 == sum of the inputs' sums within
-    f32 re-association bounds."""
+@pytest.mark.parametrize("k", [2, 4, 8])
+def test_full_size_sum_scale_property(k):
+    """64 MiB bucket (BASELINE config 2), k = 2 / 4 / 8 inputs (each k its own
+    SumScaleOp instantiation), divisor k: the kernel equals the oracle on a
+    strided sample and then on all 16 M elements
+    (worker_ring.rs:141-143 summed in input order, param_manager.rs:183-188 ÷n)."""
     n = 1 << 24
-    ins = [torch.empty(n, dtype=torch.float32, device=DEV) for _ in range(4)]
+    ins = [torch.empty(n, dtype=torch.float32, device=DEV) for _ in range(k)]
     for r, t in enumerate(ins):
         K.synth(t, SEED, r)
     out = torch.empty(n, dtype=torch.float32, device=DEV)
-    K.sum_scale(out, ins, 4.0)
+    K.sum_scale(out, ins, float(k))
     idx = np.arange(0, n, 4097)
     got = host(out)[idx]
     hs = [host(t)[idx] for t in ins]
-    assert_bitexact(got, O.sum_scale(hs, 4.0))
+    assert_bitexact(got, O.sum_scale(hs, float(k)))
     full = [host(t) for t in ins]
-    assert_bitexact(host(out), O.sum_scale(full, 4.0), "all 16M elements")
+    assert_bitexact(host(out), O.sum_scale(full, float(k)), f"all 16M elements, k = {k}")
 
 
 @pytest.mark.parametrize("wire", ["f32", "f16"])
