@@ -108,14 +108,17 @@ struct TcpErr {
     char msg[192] = {0};
 };
 
-// pinned host buffer grown on demand (never while a transfer into it is pending)
+// pinned host buffer grown on demand (never while a transfer into it is pending), with a quarter of headroom:
+// SparseGrad frames differ in length from hop to hop, and pinning tens of MB costs milliseconds, so a buffer
+// sized to each new longest frame exactly was re-pinned round after round
 int grow_pinned(uint8_t **p, size_t *cap, size_t need, unsigned flags = hipHostMallocDefault) {
     if (*cap >= need) return ONO_OK;
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     *cap = 0;
-    ONO_HIP(hipHostMalloc((void **)p, need, flags));
-    *cap = need;
+    const size_t want = need + need / 4;
+    ONO_HIP(hipHostMalloc((void **)p, want, flags));
+    *cap = want;
     return ONO_OK;
 }
 
@@ -236,15 +239,15 @@ struct TcpRecv {
             dst = r->sp_rx;
             if (in.kind == KIND_SPARSE && pay > kSparseUpload) {  // and up to HBM piece by piece (the lift's input)
                 const size_t want = (size_t)pay + 64;
-                if (r->sp_rx_dev_cap < want) {
+                if (r->sp_rx_dev_cap < want) {  // (with headroom, as grow_pinned)
                     (void)hipFree(r->sp_rx_dev);
                     r->sp_rx_dev = nullptr;
                     r->sp_rx_dev_cap = 0;
-                    if (hipMalloc((void **)&r->sp_rx_dev, want) != hipSuccess) {
+                    if (hipMalloc((void **)&r->sp_rx_dev, want + want / 4) != hipSuccess) {
                         e.code = ONO_E_HIP; snprintf(e.msg, sizeof e.msg, "device buffer for a SparseGrad frame");
                         return false;
                     }
-                    r->sp_rx_dev_cap = want;
+                    r->sp_rx_dev_cap = want + want / 4;
                 }
                 dev = r->sp_rx_dev;
                 in.sparse_dev = true;
@@ -988,6 +991,12 @@ int ono_ring_set_sparse(ono_ring *r, float ratio, uint64_t seed) {
         return set_error(ONO_E_ARG, "the SparseCapable serializer is a TCP-wire format: TCP rings only");
     std::lock_guard<std::mutex> lk(r->mu);
     if (int rc = alloc_sample(r)) return rc;
+    // the SparseGrad receive frame at the size no sparse push exceeds (a stream above 2 bytes per value goes
+    // dense: compressor.rs:79), pinned once here rather than re-pinned as the hops' frames grow
+    if (ratio > 0.0f && r->fd_prev >= 0) {
+        DeviceGuard g(r->device);
+        if (int rc = grow_pinned(&r->sp_rx, &r->sp_rx_cap, 2 * (r->maxc + 4) + 64)) return rc;
+    }
     r->sparse_r = ratio;
     r->sample_state = seed;
     return ONO_OK;
