@@ -582,7 +582,6 @@ int ono_ring_destroy(ono_ring *r) {
         sample_ahead_free(r->ahead);  // (joins its thread before its buffer goes)
         if (r->sample_idx) (void)hipHostFree(r->sample_idx);
         (void)hipFree(r->sp_idx_dev);
-        (void)hipFree(r->sample_idx_hbm);
         (void)hipFree(r->sp_t_dev);
         (void)hipFree(r->sp_rx_dev);
         if (r->sp_status) (void)hipHostFree(r->sp_status);

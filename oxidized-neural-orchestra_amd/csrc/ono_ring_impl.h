@@ -140,8 +140,7 @@ struct ono_ring {
     void *sampler_ctx = nullptr;
     uint32_t *sample_idx = nullptr;   // pinned host: the sampler's output, uploaded in stream order
     uint32_t *sp_idx_dev = nullptr;   // the gathered keys on the device (the threshold's scratch)
-    uint32_t *sample_idx_hbm = nullptr;  // the sample indices in HBM when the helper thread drew them ahead
-    ono::SampleAhead *ahead = nullptr;  // the default sampler's next draw (a helper thread)
+    ono::SampleAhead *ahead = nullptr;  // the default sampler's coming draws (a helper thread, a queue)
     float *sp_t_dev = nullptr;        // the push's threshold on the device (sparse_threshold_dev)
     uint8_t *sp_rx_dev = nullptr;     // a received SparseGrad, uploaded for the stream-ordered lift
     size_t sp_rx_dev_cap = 0;

@@ -51,6 +51,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdlib>
@@ -72,8 +73,8 @@ constexpr size_t kSampleMax = 16384;              // SAMPLE_SIZE (protocol.rs:13
 // own wait covers it: no D2H and no second wait); larger ones come down in pieces beside the send
 constexpr size_t kSparseZeroCopy = size_t(4) << 20;
 // measurement A/B (round 6), read once: ONO_TCP_LIFT_PINNED=0 copies a received SparseGrad into HBM before the
-// lift (round 5's form) instead of lifting from the pinned frame; ONO_THR_HBM=0 gathers the sample's keys
-// from the pinned indices even when the helper thread put them in HBM
+// lift (round 5's form) instead of lifting from the pinned frame; ONO_THR_HBM=1 has the sampler's helper
+// thread upload each draw to HBM for the gather (measured no gain: profiles/r06_s5_tcp_variants.jsonl)
 bool env_on(const char *name) {
     const char *e = getenv(name);
     return !(e && !strcmp(e, "0"));
@@ -82,8 +83,62 @@ bool lift_pinned() {
     static const bool v = env_on("ONO_TCP_LIFT_PINNED");
     return v;
 }
-bool thr_hbm() {
-    static const bool v = env_on("ONO_THR_HBM");
+bool thr_hbm() {  // (default off: no gain measured, and the upload lengthened every draw of the queue)
+    static const bool v = [] {
+        const char *e = getenv("ONO_THR_HBM");
+        return e && !strcmp(e, "1");
+    }();
+    return v;
+}
+// ONO_TCP_TRACE=1 (measurement): host time per step of every SparseCapable hop, summed over the process's
+// rings and printed to stderr at exit — sample (taken from the queue or drawn) / threshold (its launches) /
+// drop (launch + wait) / mask / exchange / incoming (lift + wait) / add — for where a config-1 round's time
+// goes between the kernels
+struct HopTrace {
+    static constexpr int kSteps = 7;
+    std::atomic<uint64_t> ns[kSteps] = {}, hops{0}, draw_ns{0}, draws{0}, wait_ns{0}, waits{0}, misses{0},
+        take_ns{0}, takes{0};
+    ~HopTrace() {
+        const uint64_t h = hops.load();
+        if (!h) return;
+        if (draws.load())
+            fprintf(stderr, "ONO_TCP_TRACE the sampler queue's draws: %llu, %.2f us each; takes that waited: %llu, "
+                    "%.2f us each; misses (drawn inline): %llu\n",
+                    (unsigned long long)draws.load(), draw_ns.load() / 1e3 / (double)draws.load(),
+                    (unsigned long long)waits.load(), waits.load() ? wait_ns.load() / 1e3 / (double)waits.load() : 0.0,
+                    (unsigned long long)misses.load());
+        if (takes.load())
+            fprintf(stderr, "ONO_TCP_TRACE take() calls: %llu, %.2f us each\n", (unsigned long long)takes.load(),
+                    take_ns.load() / 1e3 / (double)takes.load());
+        static const char *names[kSteps] = {"threshold", "drop", "mask", "exchange", "incoming", "add", "sample"};
+        fprintf(stderr, "ONO_TCP_TRACE %llu hops, us per hop:", (unsigned long long)h);
+        for (int k = 0; k < kSteps; k++) fprintf(stderr, " %s %.2f", names[k], ns[k].load() / 1e3 / (double)h);
+        fprintf(stderr, "\n");
+    }
+};
+HopTrace g_hop_trace;
+bool trace_on() {
+    static const bool v = getenv("ONO_TCP_TRACE") != nullptr;
+    return v;
+}
+std::atomic<uint64_t> g_hops_seen{0};
+struct HopClock {  // one hop's step times into g_hop_trace (a no-op unless ONO_TCP_TRACE; the process's first
+                   // 64 hops are left out: they hold the one-time allocations of the warmup round)
+    bool on = trace_on() && g_hops_seen++ >= 64;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void step(int k) {
+        if (!on) return;
+        const auto u = std::chrono::steady_clock::now();
+        g_hop_trace.ns[k] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(u - t).count();
+        t = u;
+    }
+    void done() {
+        if (on) g_hop_trace.hops++;
+    }
+};
+// ONO_TCP_MASK_EARLY=0: a sparse push's mask after the exchange (round 5) instead of before it
+bool mask_early() {
+    static const bool v = env_on("ONO_TCP_MASK_EARLY");
     return v;
 }
 
@@ -360,75 +415,137 @@ int tcp_exchange(ono_ring *r, const Outgoing &out, Incoming &in, hipStream_t s) 
 
 namespace ono {
 
-// The default sampler one push ahead.  Its draws depend only on the state and
-// the chunk length (ono_sparse_sample_default), and a ring's pushes take their
-// chunks in a fixed order, so a helper thread draws the next push's sample into
-// a spare pinned buffer while this push's frame is encoded and on the socket.
-// A push whose state or length is not the one drawn ahead (ono_ring_set_sparse
-// reset the state) draws inline; a caller's sampler is never called ahead.
+// The default sampler, run ahead by a helper thread.  Its draws depend only on the state and the chunk length
+// (ono_sparse_sample_default), and a ring's pushes take their chunks in a fixed cyclic order (its round's
+// pushes, then the next round's), so the helper draws the coming pushes' samples into a queue of kDepth slots
+// — each in pinned memory and uploaded to HBM on the helper's own non-blocking stream — while the ring makes
+// and sends its frames.  Round 5 drew one push ahead: a draw (16384 of 54,693 values, 64-bit modulo per
+// index) plus its upload outlasts a config-1 hop, and the push waited ~30 us for it (ONO_TCP_TRACE,
+// profiles/r06_s8_trace.txt).  A push whose state or length is not the queue's next (ono_ring_set_sparse reset
+// the state, the first push) draws inline and re-plans the queue; a caller's sampler is never called ahead.
 struct SampleAhead {
+    static constexpr int kDepth = 4;
+    struct Slot {
+        uint64_t st_in = 0, st_out = 0;
+        size_t len = 0, m = 0;
+        uint32_t *buf = nullptr;   // pinned, kSampleMax indices
+        uint32_t *dbuf = nullptr;  // the same draw in HBM
+        bool ready = false, up = false;
+        int rc = ONO_OK;
+    };
     std::mutex mu;
     std::condition_variable cv;
-    bool stop = false, job = false, busy = false, ready = false, up = false;
-    uint64_t st_in = 0, st_out = 0;
-    size_t len = 0, m = 0;
-    uint32_t *buf = nullptr;   // pinned, kSampleMax indices
-    uint32_t *dbuf = nullptr;  // the same draw in HBM (uploaded by this thread on its own stream)
+    bool stop = false;
+    Slot slot[kDepth];
+    int head = 0, tail = 0, count = 0;  // slots [head, head + count) drawn or being drawn, in push order
+    int held = -1;                      // the slot the ring's current push reads (freed at its next take)
+    uint64_t gen = 0;                   // a re-plan discards a draw in flight
+    // the plan: the next draw's state, and the cyclic push lengths from plan_pos on
+    bool planned = false;
+    uint64_t plan_st = 0;
+    std::vector<size_t> plan_len;
+    size_t plan_pos = 0;
     int device = 0;
     hipStream_t ust = nullptr;  // (non-blocking: no implicit order with the ring's stream)
-    int rc = ONO_OK;
+    bool upload = false;        // ONO_THR_HBM=1: each draw also goes up to HBM for the gather
     std::thread th;
 
     void loop() {
         std::unique_lock<std::mutex> lk(mu);
+        (void)hipSetDevice(device);
         for (;;) {
-            cv.wait(lk, [&] { return stop || job; });
+            cv.wait(lk, [&] { return stop || (planned && count + (held >= 0) < kDepth); });
             if (stop) return;
-            job = false;
-            uint64_t st = st_in;
-            const size_t L = len, mm = m;
-            uint32_t *b = buf, *db = dbuf;
+            // the next push that draws (a chunk of at most kSampleMax values is its own sample: no draw)
+            size_t L = 0;
+            for (size_t k = 0; k < plan_len.size(); k++) {
+                L = plan_len[plan_pos % plan_len.size()];
+                if (L > kSampleMax) break;
+                plan_pos++;
+            }
+            if (L <= kSampleMax) {  // (no push of this ring ever draws)
+                planned = false;
+                continue;
+            }
+            const int q = tail;
+            Slot &sl = slot[q];
+            sl.st_in = plan_st;
+            sl.len = L;
+            sl.m = kSampleMax;
+            sl.ready = false;
+            tail = (tail + 1) % kDepth;
+            count++;
+            const uint64_t g = gen;
+            uint64_t st = plan_st;
+            uint32_t *b = sl.buf, *db = sl.dbuf;
             lk.unlock();
-            const int e = ono_sparse_sample_default(&st, L, b, mm);
-            // the indices up to HBM here, off the push's path: the push's threshold then reads them there
-            // (read in place from pinned memory they cost the gather ~6 us per push; an upload on the
-            // ring's stream ~30 us of copy-engine hand-off)
+            const auto t0 = std::chrono::steady_clock::now();
+            const int e = ono_sparse_sample_default(&st, L, b, kSampleMax);
             bool u = false;
-            if (e == ONO_OK && db && ust && hipSetDevice(device) == hipSuccess &&
-                hipMemcpyAsync(db, b, mm * sizeof(uint32_t), hipMemcpyHostToDevice, ust) == hipSuccess)
+            if (upload && e == ONO_OK && db && ust &&
+                hipMemcpyAsync(db, b, kSampleMax * sizeof(uint32_t), hipMemcpyHostToDevice, ust) == hipSuccess)
                 u = hipStreamSynchronize(ust) == hipSuccess;
+            if (trace_on()) {
+                g_hop_trace.draw_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                           std::chrono::steady_clock::now() - t0).count();
+                g_hop_trace.draws++;
+            }
             lk.lock();
-            st_out = st;
-            rc = e;
-            up = u;
-            ready = true;
+            if (g != gen) continue;  // re-planned meanwhile: the slot was dropped
+            sl.st_out = st;
+            sl.rc = e;
+            sl.up = u;
+            sl.ready = true;
+            plan_st = st;
+            plan_pos++;
+            if (e != ONO_OK) planned = false;
             cv.notify_all();
         }
     }
-    void submit(uint64_t st, size_t L, size_t mm) {
+    // the queue restarts at state st with the ring's cyclic push lengths from position pos
+    void plan(uint64_t st, const std::vector<size_t> &lens, size_t pos) {
         std::lock_guard<std::mutex> lk(mu);
-        st_in = st;
-        len = L;
-        m = mm;
-        job = busy = true;
-        ready = false;
+        gen++;
+        head = tail = (held >= 0 ? (held + 1) % kDepth : 0);
+        count = 0;
+        plan_st = st;
+        plan_len = lens;
+        plan_pos = pos;
+        planned = !lens.empty();
         cv.notify_all();
     }
-    // the draw for (st, L, mm) if it was made ahead: *idx swapped with the spare buffer, *st advanced; when
-    // it is also in HBM, *didx swapped with the spare device buffer and *in_hbm set
+    // the next push's draw for (st, L, mm) if the queue made it: *idx / *didx point at the slot (valid until
+    // the next take), *st advanced, *in_hbm when the HBM copy is there.  The slot the previous push read is
+    // freed first (its drop, which read the sample, has returned).
     bool take(uint64_t *st, size_t L, size_t mm, uint32_t **idx, uint32_t **didx, bool *in_hbm) {
         std::unique_lock<std::mutex> lk(mu);
         *in_hbm = false;
-        if (!busy) return false;
-        cv.wait(lk, [&] { return ready; });
-        busy = false;
-        if (rc != ONO_OK || st_in != *st || len != L || m != mm) return false;
-        std::swap(*idx, buf);
-        if (up && didx && *didx) {
-            std::swap(*didx, dbuf);
-            *in_hbm = true;
+        if (held >= 0) {
+            held = -1;
+            cv.notify_all();
         }
-        *st = st_out;
+        if (!count || slot[head].st_in != *st || slot[head].len != L || slot[head].m != mm) {
+            if (trace_on()) g_hop_trace.misses++;
+            return false;
+        }
+        Slot &sl = slot[head];
+        if (!sl.ready && trace_on()) {
+            const auto t0 = std::chrono::steady_clock::now();
+            cv.wait(lk, [&] { return sl.ready; });
+            g_hop_trace.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                       std::chrono::steady_clock::now() - t0).count();
+            g_hop_trace.waits++;
+        }
+        cv.wait(lk, [&] { return sl.ready; });
+        if (sl.rc != ONO_OK) return false;
+        held = head;
+        head = (head + 1) % kDepth;
+        count--;
+        *idx = sl.buf;
+        *didx = sl.dbuf;
+        *in_hbm = sl.up;
+        *st = sl.st_out;
+        cv.notify_all();
         return true;
     }
 };
@@ -441,8 +558,10 @@ void sample_ahead_free(SampleAhead *a) {
         a->cv.notify_all();
     }
     if (a->th.joinable()) a->th.join();
-    if (a->buf) (void)hipHostFree(a->buf);
-    if (a->dbuf) (void)hipFree(a->dbuf);
+    for (auto &sl : a->slot) {
+        if (sl.buf) (void)hipHostFree(sl.buf);
+        if (sl.dbuf) (void)hipFree(sl.dbuf);
+    }
     if (a->ust) (void)hipStreamDestroy(a->ust);
     delete a;
 }
@@ -457,7 +576,6 @@ int alloc_sample(ono_ring *r) {
     DeviceGuard g(r->device);
     ONO_HIP(hipHostMalloc((void **)&r->sample_idx, kSampleMax * sizeof(uint32_t), hipHostMallocDefault));
     ONO_HIP(hipMalloc((void **)&r->sp_idx_dev, kSampleMax * sizeof(uint32_t)));
-    ONO_HIP(hipMalloc((void **)&r->sample_idx_hbm, kSampleMax * sizeof(uint32_t)));
     ONO_HIP(hipMalloc((void **)&r->sp_t_dev, sizeof(float)));
     ONO_HIP(hipHostMalloc((void **)&r->sp_status, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
     *r->sp_status = 0;
@@ -557,10 +675,10 @@ private:
     int out_sparse(float *chunk, int c, bool zero_chunk, float &t, bool &sparse, Outgoing &o) {
         const size_t L = len(c);
         (void)t;  // (the threshold stays on the device: r_->sp_t_dev)
-        const size_t next_L = push_len_.empty() ? 0 : push_len_[(push_k_ + 1) % push_len_.size()];
-        push_k_++;
-        int rc = codec([&] { return threshold(chunk, L, next_L); });
+        const size_t k_push = push_k_++;
+        int rc = codec([&] { return threshold(chunk, L, k_push); });
         if (rc) return rc;
+        if (clk_) clk_->step(0);
         const size_t cap = ono_sparse_max_bytes(L);
         const bool zc = cap <= kSparseZeroCopy;
         uint8_t *dst = nullptr;
@@ -579,6 +697,7 @@ private:
         }
         size_t nb = 0;
         if ((rc = codec([&] { return sparse_drop_tdev(dst, cap, &nb, chunk, L, r_->sp_t_dev, s_); }))) return rc;
+        if (clk_) clk_->step(1);
         sparse = nb <= 2 * L;
         if (!sparse) {
             if (zero_chunk) ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, c), chunk, L, s_));
@@ -602,36 +721,52 @@ private:
     // calculate_threshold over the sample the sampler draws (all values up to SAMPLE_SIZE; above, the
     // caller's sampler or the default one), into r->sp_t_dev in stream order: the drop and the masks read
     // it there (no host round trip; the host never needs the value)
-    int threshold(const float *chunk, size_t L, size_t next_L) {
+    int threshold(const float *chunk, size_t L, size_t k_push) {
         const size_t m = std::min(L, kSampleMax);
         bool sampled = false, in_hbm = false;
+        uint32_t *idx_host = r_->sample_idx, *idx_hbm = nullptr;
         if (r_->sampler) {
             if (r_->sampler(r_->sampler_ctx, L, r_->sample_idx, m) != 0)
                 return set_error(ONO_E_OTHER, "the sampler failed for a chunk of %zu values", L);
             sampled = L > kSampleMax;
         } else if (L > kSampleMax) {
-            if (!r_->ahead || !r_->ahead->take(&r_->sample_state, L, m, &r_->sample_idx, &r_->sample_idx_hbm, &in_hbm)) {
+            if (!r_->ahead) {
+                auto *a = new SampleAhead();
+                a->device = r_->device;
+                a->upload = thr_hbm();
+                bool ok = hipStreamCreateWithFlags(&a->ust, hipStreamNonBlocking) == hipSuccess;
+                for (auto &sl : a->slot)
+                    ok = ok &&
+                         hipHostMalloc((void **)&sl.buf, kSampleMax * sizeof(uint32_t), hipHostMallocDefault) ==
+                             hipSuccess &&
+                         hipMalloc((void **)&sl.dbuf, kSampleMax * sizeof(uint32_t)) == hipSuccess;
+                if (!ok) {
+                    sample_ahead_free(a);
+                    return set_error(ONO_E_HIP, "sample buffers");
+                }
+                a->th = std::thread([a] { a->loop(); });
+                r_->ahead = a;
+            }
+            uint32_t *qi = nullptr, *qd = nullptr;
+            const auto tk0 = std::chrono::steady_clock::now();
+            const bool took = r_->ahead->take(&r_->sample_state, L, m, &qi, &qd, &in_hbm);
+            if (trace_on()) {
+                g_hop_trace.take_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                           std::chrono::steady_clock::now() - tk0).count();
+                g_hop_trace.takes++;
+            }
+            if (took) {
+                idx_host = qi;
+                idx_hbm = qd;
+            } else {  // not the queue's next draw: drawn here, and the queue re-planned from the state after it
                 int rc = ono_sparse_sample_default(&r_->sample_state, L, r_->sample_idx, m);
                 if (rc) return rc;
+                in_hbm = false;
+                r_->ahead->plan(r_->sample_state, push_len_, k_push + 1);
             }
             sampled = true;
-            if (next_L > kSampleMax) {  // the next push's draw, while this one's frame is made and sent
-                if (!r_->ahead) {
-                    auto *a = new SampleAhead();
-                    a->device = r_->device;
-                    if (hipHostMalloc((void **)&a->buf, kSampleMax * sizeof(uint32_t), hipHostMallocDefault) !=
-                            hipSuccess ||
-                        hipMalloc((void **)&a->dbuf, kSampleMax * sizeof(uint32_t)) != hipSuccess ||
-                        hipStreamCreateWithFlags(&a->ust, hipStreamNonBlocking) != hipSuccess) {
-                        sample_ahead_free(a);
-                        return set_error(ONO_E_HIP, "sample buffers");
-                    }
-                    a->th = std::thread([a] { a->loop(); });
-                    r_->ahead = a;
-                }
-                r_->ahead->submit(r_->sample_state, next_L, std::min(next_L, kSampleMax));
-            }
         }
+        if (clk_) clk_->step(6);  // (the sample: taken from the queue or drawn here)
         if (sampled && r_->sampler)  // a caller's indices are checked; the default sampler's are in range
             for (size_t i = 0; i < m; i++)
                 if (r_->sample_idx[i] >= L) return set_error(ONO_E_ARG, "sample index %u out of %zu", r_->sample_idx[i], L);
@@ -639,8 +774,8 @@ private:
         // of cross-engine hand-off per push); the buffer is not rewritten before this push's drop returns
         // — unless the helper thread already put the draw in HBM, where the gather reads it
         uint32_t *idx_dev = nullptr;
-        if (sampled && in_hbm && thr_hbm()) idx_dev = r_->sample_idx_hbm;
-        else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, r_->sample_idx, 0));
+        if (sampled && in_hbm && thr_hbm()) idx_dev = idx_hbm;
+        else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, idx_host, 0));
         return sparse_threshold_dev(r_->sp_t_dev, chunk, L, idx_dev, r_->sp_idx_dev, m, r_->sparse_r, s_);
     }
 
@@ -850,17 +985,29 @@ private:
             const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            if ((rc = out_sparse(res + off(cs), cs, true, t, sparse, o)) || (rc = xchg(o, in))) return rc;
-            // :126-132 sent values leave; a dense push (:133) zeroed the chunk in its encoder
-            if (sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
+            // :126-132 sent values leave; a dense push (:133) zeroed the chunk in its encoder.  The frame is
+            // complete when out_sparse returns, so the mask runs on the device while the frame is on the socket
+            const bool early = mask_early();
+            HopClock clk;
+            clk_ = &clk;
+            if ((rc = out_sparse(res + off(cs), cs, true, t, sparse, o))) return rc;
+            if (early && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
+            clk.step(2);
+            if ((rc = xchg(o, in))) return rc;
+            clk.step(3);
+            if (!early && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
             if (in.kind == KIND_DENSE) {
                 ONO_K(r_, s_, launch_decode_add<uint16_t>(res + off(cr), slot(1, cr), len(cr), s_));
             } else {
                 const float *v = nullptr;
                 size_t k = 0;
                 if ((rc = incoming(in, cr, false, &v, &k))) return rc;
+                clk.step(4);
                 ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
             }
+            clk.step(5);
+            clk.done();
+            clk_ = nullptr;
         }
         const int own = mod(pos_ + 1);  // gather (:155-204)
         ONO_HIP(dev_copy(grad + off(own), res + off(own), len(own) * sizeof(float), s_));  // :166
@@ -868,9 +1015,16 @@ private:
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            if ((rc = out_sparse(grad + off(cs), cs, false, t, sparse, o)) || (rc = xchg(o, in))) return rc;
+            const bool early = mask_early();
+            HopClock clk;
+            clk_ = &clk;
+            if ((rc = out_sparse(grad + off(cs), cs, false, t, sparse, o))) return rc;
+            if (early && sparse && (rc = mask(grad + off(cs), len(cs), 0))) return rc;  // (during the exchange)
+            clk.step(2);
+            if ((rc = xchg(o, in))) return rc;
+            clk.step(3);
             if (sparse) {  // :177-190: keep the sent values; the owned residual stays (:178-184 commented out)
-                if ((rc = mask(grad + off(cs), len(cs), 0))) return rc;
+                if (!early && (rc = mask(grad + off(cs), len(cs), 0))) return rc;
             } else if (j == 0) {  // :191-193
                 ONO_HIP(dev_zero(res + off(own), len(own) * sizeof(float), s_));
             }
@@ -880,8 +1034,12 @@ private:
                 const float *v = nullptr;
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
+                clk.step(4);
                 ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
             }
+            clk.step(5);
+            clk.done();
+            clk_ = nullptr;
         }
         ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105
         return ONO_OK;
@@ -906,6 +1064,7 @@ private:
     bool zc_;
     std::vector<size_t> push_len_;
     size_t push_k_ = 0;
+    HopClock *clk_ = nullptr;  // (ONO_TCP_TRACE: the hop in progress)
 };
 
 }  // namespace

@@ -9,6 +9,9 @@
 // the line then also carries rank 0's per-round phase split (ono_ring_timing_phases:
 // kernels, socket exchange, sparse codec) and the codec's share of the round.
 //
+// --phases 0: no phase timing (rank 0's per-launch event pairs cost host time inside every round, and the
+// peers wait for rank 0: the round time without them is the one to quote; the phase split needs them).
+//
 // --dump PATH: rank 0's grad and residual after the last round (2 x len f32), for a checker to
 // replay the rounds (residual k = synth(len, 0x0402026 + k, rank) for k = 0..rounds, sampler seed
 // 0x5EED0000 + rank, carried across rounds).
@@ -73,12 +76,14 @@ int main(int argc, char **argv) {
     size_t len = 109386;
     float sparse = 0.0f;
     const char *dump = nullptr;
+    int phases = 1;
     for (int a = 1; a < argc; a++) {
         if (!strcmp(argv[a], "--ranks") && a + 1 < argc) n = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--len") && a + 1 < argc) len = strtoull(argv[++a], nullptr, 10);
         else if (!strcmp(argv[a], "--rounds") && a + 1 < argc) rounds = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--sparse") && a + 1 < argc) sparse = (float)atof(argv[++a]);
         else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
+        else if (!strcmp(argv[a], "--phases") && a + 1 < argc) phases = atoi(argv[++a]);
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
     if (n < 2 || rounds < 1 || len < (size_t)n) { fprintf(stderr, "need ranks >= 2, len >= ranks\n"); return 1; }
@@ -106,7 +111,7 @@ int main(int argc, char **argv) {
             int e = ono_ring_create_tcp(&ring, r, n, len, 0, prv, nxt);
             if (e == ONO_OK && sparse > 0.0f) e = ono_ring_set_sparse(ring, sparse, 0x5EED0000ull + (uint64_t)r);
             for (int k = 0; k <= rounds && e == ONO_OK; k++) {  // round 0 is warmup
-                if (k == 1 && r == 0) e = ono_ring_timing_enable(ring, 1);
+                if (k == 1 && r == 0 && phases) e = ono_ring_timing_enable(ring, 1);
                 e = ono_synth_f32(ono_ring_residual(ring), len, 0x0402026 + k, (uint64_t)r, 0, s);
                 if (e == ONO_OK) e = hipStreamSynchronize(s) == hipSuccess ? ONO_OK : ONO_E_HIP;
                 pthread_barrier_wait(&bar);
@@ -121,7 +126,7 @@ int main(int argc, char **argv) {
                 fprintf(stderr, "worker %d: %s\n", r, ono_last_error());
                 _exit(2);
             }
-            if (r == 0 && e == ONO_OK) e = ono_ring_timing_phases(ring, ph_ms, ph_n);
+            if (r == 0 && e == ONO_OK && phases) e = ono_ring_timing_phases(ring, ph_ms, ph_n);
             if (r == 0 && e == ONO_OK && dump) {
                 std::vector<float> h(2 * len);
                 if (hipMemcpy(h.data(), ono_ring_grad(ring), len * 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -152,8 +157,8 @@ int main(int argc, char **argv) {
     printf("{\"ranks\": %d, \"len\": %zu, \"rounds\": %d, \"sparse_r\": %g, \"s_per_round\": %.9f, "
            "\"s_per_round_mean\": %.9f, \"gib_s\": %.6f, \"phase_ms_per_round\": {\"kernel\": %.5f, "
            "\"exchange\": %.5f, \"sparse_codec\": %.5f}, \"codec_calls_per_round\": %.2f, "
-           "\"codec_share_of_round\": %.4f}\n",
+           "\"codec_share_of_round\": %.4f, \"phases_timed\": %d}\n",
            n, len, rounds, (double)sparse, med, mean, (double)len * 4.0 / med / (double)(1ull << 30), kern, xchg, codec,
-           (double)ph_n[ONO_PHASE_SPARSE_CODEC] / rounds, codec * 1e-3 / mean);
+           (double)ph_n[ONO_PHASE_SPARSE_CODEC] / rounds, codec * 1e-3 / mean, phases);
     return 0;
 }
