@@ -907,8 +907,8 @@ def tcp_edge_native(elems: int, rounds: int, ranks: int = 2) -> dict | None:
         return None
     import subprocess
     try:
-        out = subprocess.run([exe, "--ranks", str(ranks), "--len", str(elems), "--rounds", str(rounds)],
-                             capture_output=True, text=True, timeout=300, check=True)
+        out = subprocess.run([exe, "--ranks", str(ranks), "--len", str(elems), "--rounds", str(rounds),
+                              "--phases", "0"], capture_output=True, text=True, timeout=300, check=True)
         d = json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001 — reported in the line
         return {"error": f"{type(e).__name__}: {e}"[:200]}
@@ -929,19 +929,24 @@ def tcp_sparse_native(elems: int, rounds: int, ranks: int, ratio: float, dump: s
     cmd = [exe, "--ranks", str(ranks), "--len", str(elems), "--rounds", str(rounds), "--sparse",
            repr(float(np.float32(ratio)))] + (["--dump", dump] if dump else [])
     try:
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        # ms from an untimed run: rank 0's per-launch event pairs of the phase split cost host time inside
+        # every round (config 1: ~0.04 ms of a ~0.2 ms round), so the split comes from a second, timed run
+        out = subprocess.run(cmd + ["--phases", "0"], capture_output=True, text=True, timeout=300, check=True)
         d = json.loads(out.stdout.strip().splitlines()[-1])
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
+        t = json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # noqa: BLE001 — reported in the line
         return {"error": f"{type(e).__name__}: {e}"[:200]}
     return {"ranks": ranks, "elems": elems, "ratio": ratio, "ms": round(d["s_per_round"] * 1e3, 4),
-            "gib_s": round(d["gib_s"], 3), "phase_ms_per_round": d["phase_ms_per_round"],
-            "codec_share_of_round": d["codec_share_of_round"]}
+            "gib_s": round(d["gib_s"], 3), "timed_run_ms": round(t["s_per_round"] * 1e3, 4),
+            "phase_ms_per_round": t["phase_ms_per_round"], "codec_share_of_round": t["codec_share_of_round"]}
 
 
 def tcp_sparse_legs() -> dict:
     """SURVEY §8(f) row 3 on the product path: the sparse ring end to end."""
     out = {"workload": "pull_grads over loopback TCP with SparseCapable{r} workers (SparseGrad frames, "
-                       "reference framing), C++ host threads on one GPU; ms per round, rank 0's phase split"}
+                       "reference framing), C++ host threads on one GPU; ms per round of an untimed run, rank 0's phase split from a second, "
+                       "timed run (timed_run_ms: its round, the event pairs' host cost included)"}
     for key, e, n, r, k in (("config1_2_ranks_r0.1", CONFIG1_ELEMS, 2, 0.1, 200),
                             ("config1_2_ranks_r0.01", CONFIG1_ELEMS, 2, 0.01, 200),
                             ("config1_4_ranks_r0.1", CONFIG1_ELEMS, 4, 0.1, 200),
