@@ -78,6 +78,19 @@ hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int z
 // that a one-lane kernel sets to `epoch` (a stream synchronisation's wake-up
 // costs several microseconds more; used on the TCP ring's hops).
 hipError_t stream_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uint32_t epoch);
+// the spin of stream_wait alone, on a word the stream's own kernel stores
+hipError_t stream_spin(hipStream_t s, uint64_t *word_host, uint32_t epoch);
+// ono_sparse_lift_dev_async with an in-kernel completion: when the lift is one launch its last workgroup
+// stores `sig` into the host-mapped word (word_host / word_dev) and in_kernel is set; else the caller waits.
+// zero_refused: a refused one-launch lift leaves its output [0, min(total, cap)) zero (the pipelined hop)
+struct LiftDone {
+    uint64_t *word_host = nullptr, *word_dev = nullptr;
+    uint32_t sig = 0;
+    bool zero_refused = false;
+    bool in_kernel = false;
+};
+int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status, uint64_t *ticket,
+                   hipStream_t s, LiftDone *done);
 // a SparseGrad's values [0, min(total, L)) on the host after the reference's
 // sequential parse of the whole stream (ono_sparse.hip); *got = its total
 int sparse_lift_prefix_host(const uint8_t *buf, size_t nbytes, float *out, size_t L, size_t *got);

@@ -1467,14 +1467,18 @@ __device__ __forceinline__ void st_u32_2b(uint8_t *p, uint32_t v) {  // a 2-B al
 // counts the workgroup in; the one whose returned count is the call's `target` (the last of the grid to
 // arrive: every other workgroup's stores are then out) stores the call's tag into host_tot[2], which the host
 // spins on.  The count only grows (the host adds each call's grid to its target), so it is never reset.
-__device__ __forceinline__ void drop1_complete(uint64_t *host_tot, uint64_t *arrive, uint64_t target, uint32_t sig) {
+// (pl_fused's completion for the TCP ring's lift is the same, into the ring's word)
+__device__ __forceinline__ void grid_complete(uint64_t *word, uint64_t *arrive, uint64_t target, uint32_t sig) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __atomic_thread_fence(__ATOMIC_RELEASE);  // (system scope: this XCD's L2 written back)
         const uint64_t old = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == target) __hip_atomic_store(host_tot + 2, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (old == target) __hip_atomic_store(word, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+__device__ __forceinline__ void drop1_complete(uint64_t *host_tot, uint64_t *arrive, uint64_t target, uint32_t sig) {
+    grid_complete(host_tot + 2, arrive, target, sig);
 }
 // measurement A/B (round 6): ONO_DROP1_SIGNAL=0 waits for the blocking one launch by a signal kernel behind it
 bool drop1_signal_in_kernel() {
@@ -3045,6 +3049,35 @@ struct FusedGrid {
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// pl_fused's completion for the TCP ring's hop (grid_complete's counted arrival): the last workgroup to finish
+// stores `sig` into the host-mapped word.  zero_refused (the ring's pipelined hop, which enqueues the kernels
+// that read the lift's output before it knows whether the lift was refused): a refused call's output
+// [0, n) is zeroed first by that workgroup, so that an add of it changes no value (x + 0 is x, and -0 + 0 the
+// +0 the reference's own add of an unkept value gives) until the host lifts the stream its way and replays
+// the work behind it.
+__device__ void lift_complete(float *g, uint64_t n, const uint64_t *badw, uint32_t epoch, uint64_t *word,
+                              uint64_t *arrive, uint64_t target, uint32_t sig, int zero_refused) {
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);  // (system scope: the refusal word and the stores out)
+        const uint64_t old = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == target ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (zero_refused &&
+        __hip_atomic_load(badw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == (uint64_t)epoch) {
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) g[i] = 0.0f;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __hip_atomic_store(word, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 // pl_fused's staging (an 8-B aligned stream), 8 B per load: every tile's loads issued up front,
 // the first tile's first (a scheduling barrier keeps them ahead: the wait for them lets the later
 // tiles' loads stay in flight while the first tile is indexed and published), unconditional and
@@ -3146,7 +3179,9 @@ template <int TPW>
 __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void pl_fused(
     float *g, const uint8_t *b, size_t M, size_t T, size_t cap, int vec,
                                                   uint64_t *frec, uint64_t *fchunk, uint64_t *fchunk_next,
-                                                  uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch, uint64_t *arrive, uint64_t arrive_target) {
+                                                  uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch, uint64_t *arrive, uint64_t arrive_target,
+                                                  uint64_t *done_word, uint64_t *done_arrive, uint64_t done_target, uint32_t done_sig,
+                                                  int zero_refused, int force_bad) {
     __shared__ uint4 img16[kPatImg / 8];  // a range as f16 bits (12 KiB), widened on the way out
     __shared__ uint4 lw4[TPW][kStageU4];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -3163,6 +3198,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         s_bad = 0;
     }
     const uint32_t tagv = epoch;  // (never 0: frec starts zeroed)
+    if (force_bad && blockIdx.x == 0 && threadIdx.x == 0) raise_bad(badw, epoch);  // (ono_sparse_lift_debug_refuse)
     uint2 v[TPW][kStageK];
     uint32_t n16[TPW];
     // the total (b is 8-B aligned: the host launches pl_fused for no other stream), issued first, from a
@@ -3236,6 +3272,8 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         // and a line left holding this launch's counts would look complete to the next-but-one launch
         for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
             fchunk_next[(size_t)i * kFusedLine] = 0;
+        if (done_word) lift_complete(g, min(total, (uint64_t)cap), badw, epoch, done_word, done_arrive, done_target,
+                                     done_sig, zero_refused);
         return;
     }
     const uint32_t total32 = (uint32_t)total;
@@ -3355,6 +3393,9 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
     // end: a store loop ahead of the first waits would make them wait for every load in flight)
     for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
         fchunk_next[(size_t)i * kFusedLine] = 0;
+    // the TCP ring's lift: the last workgroup to finish tells the host (with every refusal before it)
+    if (done_word) lift_complete(g, min(total, (uint64_t)cap), badw, epoch, done_word, done_arrive, done_target,
+                                 done_sig, zero_refused);
 #ifdef ONO_SP_STAMP
     SP_CLOCK(sp_tm);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3565,9 +3606,12 @@ struct PatScratch {
     int fpar = 0;
     uint64_t *arrive = nullptr;  // pl_fused's arrival count: kArriveShards lines + the top word (zeroed once)
     uint64_t arrive_base = 0;    // the top word once every earlier launch's grid has started
+    uint64_t *done_arrive = nullptr;  // pl_fused's completion count (a caller's word; grows, never reset)
+    uint64_t done_base = 0;
 };
 std::map<std::pair<int, hipStream_t>, PatScratch> g_pat;
 std::atomic<size_t> g_lift_fallbacks{0};      // lifts the host parsed (walk path refuted, or malformed)
+std::atomic<uint32_t> g_lift_force_refuse{0};  // one-launch lifts still to be refused (a test hook)
 std::atomic<size_t> g_lift_pattern_misses{0}; // lifts the pattern path handed to the walk path
 std::atomic<int> g_lift_mode{0};              // 0: pattern, then walk, then host; 1: walk, then host
 
@@ -4323,6 +4367,7 @@ static size_t threshold_rank(size_t m, float r) {
 hipError_t stream_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, uint32_t epoch) {
     return host_wait(s, word_host, word_dev, epoch);
 }
+hipError_t stream_spin(hipStream_t s, uint64_t *word_host, uint32_t epoch) { return host_spin(s, word_host, epoch); }
 
 int sparse_threshold_dev(float *t_dev, const float *g, size_t n, const uint32_t *idx, uint32_t *keys, size_t m, float r,
                          hipStream_t s) {
@@ -4417,33 +4462,66 @@ size_t fused_slots(int tpw) {
     memo[{dev, tpw}] = slots;
     return slots;
 }
-// One one-launch lift in flight per device: its grid needs the whole device, so a second stream's
-// lift queued while the first may still run takes the two launches (else both grids would hold slots
-// the other waits for, until a poll times out and both are refused).  While one stream alone uses the
-// form nothing is recorded (an event after every launch measured 26.5 vs 22.7 us per lift back to
-// back); the first call from a second stream takes the two launches, and from then on every
-// one-launch lift on the device is followed by an event that the other streams query.
-struct FusedLast {
-    hipStream_t s = nullptr;
-    hipEvent_t ev = nullptr;
-    bool multi = false, recorded = false;
-};
-std::map<int, FusedLast> g_fused_last;  // (under g_scratch_mu)
-bool fused_device_free(int dev, hipStream_t s) {
-    auto it = g_fused_last.find(dev);
-    if (it == g_fused_last.end() || it->second.s == s) return true;
-    FusedLast &f = it->second;
-    if (!f.multi) {  // a second stream: the first one's last lift may still run, and nothing says
-        f.multi = true;
-        return false;
-    }
-    return f.recorded && hipEventQuery(f.ev) == hipSuccess;
+// The one-launch lifts of different streams must not hold slots the others wait for: a tile waits for
+// tiles of higher workgroups, so grids that together overfill the device could each wait for workgroups
+// that cannot start until a poll times out (~10 ms) and the calls are refused.  Each stream's last
+// one-launch grid is remembered; while one stream alone uses the form nothing is recorded (an event after
+// every launch measured 26.5 vs 22.7 us per lift back to back).  A stream's launch takes the one launch
+// when the grids of the other streams that may still run (no event yet, or one not reached) and its own
+// fit in half the device's slots together — round 5 allowed one such lift per device, so two workers
+// sharing a GPU (the TCP bench, the ring tests) lifted every other frame in two launches, 17-19 vs 8-9 us
+// for a config-1 frame (profiles/r06_s17); ONO_LIFT_FUSED_SHARE=0 restores that rule (measurement).
+bool lift_fused_share() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_LIFT_FUSED_SHARE");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
 }
-void fused_device_mark(int dev, hipStream_t s) {
-    FusedLast &f = g_fused_last[dev];
-    f.s = s;
+struct FusedLast {
+    hipEvent_t ev = nullptr;
+    bool recorded = false;
+    size_t grid = 0;
+};
+struct FusedDev {
+    std::map<hipStream_t, FusedLast> last;
+    bool multi = false;
+};
+std::map<int, FusedDev> g_fused_last;  // (under g_scratch_mu)
+bool fused_device_free(int dev, hipStream_t s, size_t grid, size_t slots) {
+    FusedDev &D = g_fused_last[dev];
+    size_t busy = 0, others = 0;
+    for (auto it = D.last.begin(); it != D.last.end();) {
+        FusedLast &f = it->second;
+        if (it->first == s || !f.grid) { ++it; continue; }
+        others++;
+        const bool done = f.recorded && hipEventQuery(f.ev) != hipErrorNotReady;
+        if (done) {
+            f.grid = 0;
+            if (D.last.size() > 64) {  // streams come and go: forget the finished ones
+                (void)hipEventDestroy(f.ev);
+                it = D.last.erase(it);
+                continue;
+            }
+        } else {
+            busy += f.grid;
+        }
+        ++it;
+    }
+    if (!others) return true;
+    if (!D.multi) {  // a second stream: from now on every one-launch lift on the device is recorded
+        D.multi = true;
+        if (!lift_fused_share()) return false;
+    }
+    if (!lift_fused_share()) return busy == 0;
+    return busy + grid <= slots / 2;
+}
+void fused_device_mark(int dev, hipStream_t s, size_t grid) {
+    FusedDev &D = g_fused_last[dev];
+    FusedLast &f = D.last[s];
+    f.grid = grid;
     f.recorded = false;
-    if (!f.multi) return;
+    if (!D.multi) return;
     if (!f.ev && hipEventCreateWithFlags(&f.ev, hipEventDisableTiming) != hipSuccess) {
         f.ev = nullptr;
         return;
@@ -4455,9 +4533,21 @@ extern "C" {
 
 int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status,
                               uint64_t *ticket, void *stream) {
+    return ono::lift_dev_async(g, cap, buf_dev, nbytes, status, ticket, reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+}  // extern "C"
+
+namespace ono {
+
+// ono_sparse_lift_dev_async; done (the TCP ring's hop): when the lift is one launch, its last workgroup
+// stores done->sig into done->word (host-mapped, zeroed here) and done->in_kernel is set — the caller spins on
+// the word instead of a signal launch behind the lift
+int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status, uint64_t *ticket,
+                   hipStream_t s, LiftDone *done) {
+    if (done) done->in_kernel = false;
     if (!status || !ticket || (!buf_dev && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
     if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
@@ -4501,8 +4591,10 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
     const bool capturing = lift_fused_mode() != 2 && hipStreamIsCapturing(s, &cap_st) == hipSuccess &&
                            cap_st != hipStreamCaptureStatusNone;
+    const bool one = T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX);
+    const size_t grid = one ? T : (T + 2) / 3;
     if (T <= kPatDirect && ((uintptr_t)buf_dev & 7) == 0 && lift_fused() && !capturing &&
-        (T + 2) / 3 <= fused_slots(3) && fused_device_free(dev, s)) {
+        (T + 2) / 3 <= fused_slots(3) && fused_device_free(dev, s, grid, one ? fused_slots(1) : fused_slots(3))) {
         if (T > P.fcap) {
             const size_t gc = (T + kPatChunk - 1) / kPatChunk;
             (void)hipFree(P.frec);
@@ -4523,19 +4615,38 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
         }
         uint64_t *cur = P.fchunk + (size_t)P.fpar * kFusedRep * P.fgcap * kFusedLine;
         uint64_t *next = P.fchunk + (size_t)(1 - P.fpar) * kFusedRep * P.fgcap * kFusedLine;
-        const bool one = T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX);
-        const size_t grid = one ? T : (T + 2) / 3;
         const uint64_t target = P.arrive_base + std::min<size_t>(grid, kArriveShards);  // complete lines
+        int force = 0;
+        for (uint32_t k = g_lift_force_refuse.load(); k && !force;)
+            if (g_lift_force_refuse.compare_exchange_weak(k, k - 1)) force = 1;
+        uint64_t *dw = nullptr, dtarget = 0;
+        uint32_t dsig = 0;
+        if (done && done->word_dev) {
+            if (!P.done_arrive) {
+                ONO_HIP(hipMalloc((void **)&P.done_arrive, 16 * sizeof(uint64_t)));
+                ONO_HIP(hipMemsetAsync(P.done_arrive, 0, 16 * sizeof(uint64_t), s));
+            }
+            dw = done->word_dev;
+            dsig = done->sig;
+            dtarget = P.done_base + grid - 1;
+            *(volatile uint64_t *)done->word_host = 0;
+        }
         if (one)
             hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
-                               cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target);
+                               cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target, dw, P.done_arrive,
+                               dtarget, dsig, done && done->zero_refused ? 1 : 0, force);
         else
             hipLaunchKernelGGL(pl_fused<3>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec,
-                               P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target);
+                               P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target, dw,
+                               P.done_arrive, dtarget, dsig, done && done->zero_refused ? 1 : 0, force);
         ONO_HIP(hipGetLastError());
         P.arrive_base = target;
+        if (dw) {
+            P.done_base += grid;
+            done->in_kernel = true;
+        }
         P.fpar ^= 1;
-        fused_device_mark(dev, s);
+        fused_device_mark(dev, s, grid);
         return ONO_OK;
     }
     ONO_HIP(launch_pl_index(buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw, status, epoch, s));
@@ -4547,7 +4658,14 @@ int ono_sparse_lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size
     return ONO_OK;
 }
 
+}  // namespace ono
+
+extern "C" {
+
 size_t ono_sparse_lift_fallbacks(void) { return g_lift_fallbacks.load(); }
+int ono_sparse_lift_debug_refuse(uint32_t count) {
+    return (int)std::min<uint32_t>(g_lift_force_refuse.exchange(count), 0x7FFFFFFFu);
+}
 size_t ono_sparse_lift_pattern_misses(void) { return g_lift_pattern_misses.load(); }
 int ono_sparse_lift_set_mode(int mode) {
     if (mode != 0 && mode != 1) return set_error(ONO_E_ARG, "lift mode %d (0: pattern path first, 1: walk path)", mode);

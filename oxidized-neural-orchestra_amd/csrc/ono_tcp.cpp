@@ -52,6 +52,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdlib>
@@ -136,6 +137,17 @@ struct HopClock {  // one hop's step times into g_hop_trace (a no-op unless ONO_
         if (on) g_hop_trace.hops++;
     }
 };
+// ONO_TCP_SPIN_US (measurement, default 0): an inline exchange tries its socket calls without blocking for up
+// to this long before it sleeps in poll(2).  200 us measured slower, not faster: config 1 sparse 0.218 / 0.233
+// vs 0.200 / 0.186 ms per round, dense 0.095 / 0.120 vs 0.092 / 0.088 (profiles/r06_s18_variants.txt) — the
+// spinning threads take CPU time from the process's quota that the peer's thread and the host waits need
+int tcp_spin_us() {
+    static const int v = [] {
+        const char *e = getenv("ONO_TCP_SPIN_US");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    return v;
+}
 // ONO_TCP_MASK_EARLY=0: a sparse push's mask after the exchange (round 5) instead of before it
 bool mask_early() {
     static const bool v = env_on("ONO_TCP_MASK_EARLY");
@@ -369,6 +381,18 @@ int tcp_exchange_inline(ono_ring *r, const Outgoing &out, Incoming &in, hipStrea
     size_t sent = 0;
     TcpRecv rv(in);
     TcpErr e;
+    const int spin = tcp_spin_us();
+    if (spin > 0) {  // non-blocking calls first: most small frames are done before a poll would wake
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin);
+        for (unsigned it = 0; sent < total || !rv.done(); it++) {
+            if (sent < total && !tcp_send_some(r, out.frame, sent, total, e)) return set_error(e.code, "%s", e.msg);
+            if (!rv.done() && !rv.step(r, s, e)) return set_error(e.code, "%s", e.msg);
+            if ((it & 15) == 15) {
+                if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
+                if (std::chrono::steady_clock::now() >= until) break;
+            }
+        }
+    }
     while (sent < total || !rv.done()) {
         if (r->aborted.load()) return set_error(ONO_E_ABORTED, "ring aborted");
         struct pollfd p[2];
@@ -697,6 +721,12 @@ private:
         }
         size_t nb = 0;
         if ((rc = codec([&] { return sparse_drop_tdev(dst, cap, &nb, chunk, L, r_->sp_t_dev, s_); }))) return rc;
+        // the previous hop's lift, if still pending, has run (stream order): refused, its replay re-made this
+        // push's threshold and the push is dropped again
+        bool again = false;
+        if ((rc = resolve(false, &again))) return rc;
+        if (again && (rc = codec([&] { return sparse_drop_tdev(dst, cap, &nb, chunk, L, r_->sp_t_dev, s_); })))
+            return rc;
         if (clk_) clk_->step(1);
         sparse = nb <= 2 * L;
         if (!sparse) {
@@ -776,7 +806,13 @@ private:
         uint32_t *idx_dev = nullptr;
         if (sampled && in_hbm && thr_hbm()) idx_dev = idx_hbm;
         else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, idx_host, 0));
-        return sparse_threshold_dev(r_->sp_t_dev, chunk, L, idx_dev, r_->sp_idx_dev, m, r_->sparse_r, s_);
+        // (behind a pending lift the launches are kept: the sample's buffer stays until the next push's take)
+        ono_ring *r = r_;
+        const float ratio = r_->sparse_r;
+        hipStream_t s = s_;
+        return enq([=]() -> int {
+            return sparse_threshold_dev(r->sp_t_dev, chunk, L, idx_dev, r->sp_idx_dev, m, ratio, s);
+        });
     }
 
     Incoming in_for(int c, int b) const {
@@ -854,7 +890,7 @@ private:
             return ONO_OK;
         }
         const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
-        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes, in.sparse_dev); });
+        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes, in.sparse_dev, r_->sparse_r > 0.0f); });
         // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
         if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
         if (rc) return rc;
@@ -867,49 +903,78 @@ private:
     // (ono_sparse_lift_dev_async: the pattern path, one or two launches) reads the frame in place through
     // its device mapping — no copy of the frame into HBM in the hop; a stream it refuses (not drop-shaped,
     // malformed) goes up to HBM and to the blocking device lift, which parses anything and returns the
-    // reference's errors.  *got = the stream's total.
-    int lift(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev) {
+    // reference's errors.  *got = the stream's total.  pipe (the SparseCapable hop): a one-launch lift is not
+    // waited for — its refusal is looked at once later stream work has been waited for (resolve), and the
+    // work enqueued behind it in between is replayed after a refusal; ONO_TCP_PIPE=0 waits here (measurement).
+    int lift(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev, bool pipe = false) {
         if (nbytes < 8) return ono_sparse_lift(out, cap, got, r_->sp_rx, nbytes, s_);
-        if (in_dev) {  // a large frame already went up piece by piece (TcpRecv): lifted from HBM
-            uint64_t ticket = 0;
-            int rc = ono_sparse_lift_dev_async(out, cap, r_->sp_rx_dev, nbytes, r_->sp_status, &ticket, s_);
-            if (rc || (rc = wait())) return rc;
-            if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
-                uint64_t total = 0;
-                memcpy(&total, r_->sp_rx, 8);  // (little endian, protocol.rs:102-106)
-                *got = (size_t)total;
-                return ONO_OK;
+        const uint8_t *src = in_dev ? r_->sp_rx_dev : nullptr;
+        if (!in_dev) {
+            ONO_HIP(hipHostGetDevicePointer((void **)&src, r_->sp_rx, 0));
+            if (!lift_pinned()) {
+                int rc = up_frame(nbytes);
+                if (rc) return rc;
+                src = r_->sp_rx_dev;
             }
-            return ono_sparse_lift_dev(out, cap, got, r_->sp_rx_dev, nbytes, s_);
         }
-        const uint8_t *src = nullptr;
-        ONO_HIP(hipHostGetDevicePointer((void **)&src, r_->sp_rx, 0));
-        const size_t words = (nbytes + 3) & ~size_t(3);  // whole words for the copy kernel
-        auto up = [&]() -> int {
-            if (r_->sp_rx_dev_cap < words) {
-                (void)hipFree(r_->sp_rx_dev);
-                r_->sp_rx_dev = nullptr;
-                r_->sp_rx_dev_cap = 0;
-                const size_t c2 = std::max(words, ono_sparse_max_bytes(r_->maxc) + 8);
-                ONO_HIP(hipMalloc((void **)&r_->sp_rx_dev, c2));
-                r_->sp_rx_dev_cap = c2;
-            }
-            ONO_HIP(dev_copy(r_->sp_rx_dev, src, words, s_));
-            return ONO_OK;
-        };
-        const bool pinned = lift_pinned();
-        int rc = pinned ? ONO_OK : up();
-        if (rc) return rc;
+        uint64_t total = 0;
+        memcpy(&total, r_->sp_rx, 8);  // (little endian, protocol.rs:102-106)
+        static const bool pipe_on = env_on("ONO_TCP_PIPE");
+        pipe = pipe && pipe_on;
         uint64_t ticket = 0;
-        rc = ono_sparse_lift_dev_async(out, cap, pinned ? src : r_->sp_rx_dev, nbytes, r_->sp_status, &ticket, s_);
-        if (rc || (rc = wait())) return rc;
-        if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
-            uint64_t total = 0;
-            memcpy(&total, r_->sp_rx, 8);  // (little endian, protocol.rs:102-106)
+        LiftDone d;
+        static const bool in_kernel = env_on("ONO_LIFT_SIGNAL");
+        if (in_kernel || pipe) {
+            if (++r_->tcp_epoch == 0) r_->tcp_epoch = 1;
+            d.word_host = lift_word();
+            d.word_dev = r_->tcp_word_dev + 2;
+            d.sig = r_->tcp_epoch;
+            d.zero_refused = pipe;
+        }
+        int rc = lift_dev_async(out, cap, src, nbytes, r_->sp_status, &ticket, s_, d.word_host ? &d : nullptr);
+        if (rc) return rc;
+        if (d.in_kernel && pipe) {
+            pend_.on = true;
+            pend_.ticket = ticket;
+            pend_.sig = d.sig;
+            pend_.out = out;
+            pend_.cap = cap;
+            pend_.nbytes = nbytes;
+            pend_.in_dev = in_dev;
             *got = (size_t)total;
             return ONO_OK;
         }
-        if (pinned && (rc = up())) return rc;
+        if (d.in_kernel) ONO_HIP(stream_spin(s_, lift_word(), d.sig));
+        else if ((rc = wait())) return rc;
+        if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
+            *got = (size_t)total;
+            return ONO_OK;
+        }
+        return lift_fallback(out, cap, got, nbytes, in_dev);
+    }
+    // the received frame's whole words into r->sp_rx_dev by the library's copy kernel (in stream order)
+    int up_frame(size_t nbytes) {
+        const uint8_t *src = nullptr;
+        ONO_HIP(hipHostGetDevicePointer((void **)&src, r_->sp_rx, 0));
+        const size_t words = (nbytes + 3) & ~size_t(3);
+        if (r_->sp_rx_dev_cap < words) {
+            (void)hipFree(r_->sp_rx_dev);
+            r_->sp_rx_dev = nullptr;
+            r_->sp_rx_dev_cap = 0;
+            const size_t c2 = std::max(words, ono_sparse_max_bytes(r_->maxc) + 8);
+            ONO_HIP(hipMalloc((void **)&r_->sp_rx_dev, c2));
+            r_->sp_rx_dev_cap = c2;
+        }
+        ONO_HIP(dev_copy(r_->sp_rx_dev, src, words, s_));
+        return ONO_OK;
+    }
+    // a stream the pattern path refused: the blocking device lift from HBM (it parses anything, with the
+    // reference's errors); a frame lifted from its pinned mapping goes up first
+    int lift_fallback(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev) {
+        if (!in_dev && lift_pinned()) {
+            int rc = up_frame(nbytes);
+            if (rc) return rc;
+        }
         return ono_sparse_lift_dev(out, cap, got, r_->sp_rx_dev, nbytes, s_);
     }
 
@@ -1003,14 +1068,28 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, false, &v, &k))) return rc;
                 clk.step(4);
-                ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
+                float *dst = res + off(cr);
+                if ((rc = enq([=]() -> int {
+                         ONO_K(r_, s_, launch_acc(dst, v, k, s_, true));  // :141-143
+                         return ONO_OK;
+                     })))
+                    return rc;
             }
             clk.step(5);
             clk.done();
             clk_ = nullptr;
         }
         const int own = mod(pos_ + 1);  // gather (:155-204)
-        ONO_HIP(dev_copy(grad + off(own), res + off(own), len(own) * sizeof(float), s_));  // :166
+        {
+            float *dst = grad + off(own);
+            const float *src = res + off(own);
+            const size_t bytes = len(own) * sizeof(float);
+            if ((rc = enq([=]() -> int {
+                     ONO_HIP(dev_copy(dst, src, bytes, s_));  // :166
+                     return ONO_OK;
+                 })))
+                return rc;
+        }
         for (int j = 0; j < n_ - 1; j++) {
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
@@ -1035,12 +1114,19 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
                 clk.step(4);
-                ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
+                float *dst = grad + off(cr);
+                const size_t bytes = len(cr) * sizeof(float);
+                if ((rc = enq([=]() -> int {
+                         ONO_HIP(dev_copy(dst, v, bytes, s_));
+                         return ONO_OK;
+                     })))
+                    return rc;
             }
             clk.step(5);
             clk.done();
             clk_ = nullptr;
         }
+        if ((rc = resolve(true))) return rc;  // (the last hop's lift, before the division reads its copy)
         ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105
         return ONO_OK;
     }
@@ -1058,6 +1144,44 @@ private:
         });
     }
 
+    // A received SparseGrad's one-launch lift whose refusal the host has not looked at yet (the pipelined hop):
+    // the stream work enqueued behind it is kept, to run again after the host's own lift if it was refused.
+    struct PendingLift {
+        bool on = false;
+        uint64_t ticket = 0;
+        uint32_t sig = 0;
+        float *out = nullptr;
+        size_t cap = 0, nbytes = 0;
+        bool in_dev = false;
+        std::vector<std::function<int()>> ops;
+    };
+    // stream work behind a pending lift: run now, and kept for a replay
+    int enq(std::function<int()> f) {
+        if (pend_.on) pend_.ops.push_back(f);
+        return f();
+    }
+    // the pending lift looked at (spin: wait for its completion word first; otherwise the caller waited for
+    // later stream work): nothing to do if it was accepted; refused — its output is zero (lift_complete) and
+    // every add of it changed nothing — the host's lift of the stream, then the work behind it again, in order
+    // (*replayed).  A malformed stream is the lift's io::Error here, as in incoming().
+    int resolve(bool spin, bool *replayed = nullptr) {
+        if (replayed) *replayed = false;
+        if (!pend_.on) return ONO_OK;
+        PendingLift p = std::move(pend_);
+        pend_ = PendingLift{};
+        if (spin) ONO_HIP(stream_spin(s_, lift_word(), p.sig));
+        if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != p.ticket) return ONO_OK;
+        size_t got = 0;
+        int rc = codec([&] { return lift_fallback(p.out, p.cap, &got, p.nbytes, p.in_dev); });
+        if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
+        if (rc) return rc;
+        for (auto &f : p.ops)
+            if ((rc = f())) return rc;
+        if (replayed) *replayed = true;
+        return ONO_OK;
+    }
+    uint64_t *lift_word() const { return r_->tcp_word + 2; }
+
     ono_ring *r_;
     hipStream_t s_;
     int n_, pos_;
@@ -1065,6 +1189,7 @@ private:
     std::vector<size_t> push_len_;
     size_t push_k_ = 0;
     HopClock *clk_ = nullptr;  // (ONO_TCP_TRACE: the hop in progress)
+    PendingLift pend_;
 };
 
 }  // namespace
@@ -1125,7 +1250,8 @@ int ono_ring_create_tcp(ono_ring **out, int pos, int nranks, size_t size, int de
                 return hip_error(e, "zero-copy frame allocation", __FILE__, __LINE__);
             }
     r->tcp_block = tcp_block_bytes();
-    if ((e = hipHostMalloc((void **)&r->tcp_word, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+    // (word 0: the hops' waits; word 2: the SparseCapable hop's lift completion)
+    if ((e = hipHostMalloc((void **)&r->tcp_word, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&r->tcp_word_dev, r->tcp_word, 0)) != hipSuccess) {
         ono_ring_destroy(r);

@@ -115,6 +115,7 @@ _SIGS = {
     "ono_sparse_lift": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_dev": (_i, [_fp, _sz, C.POINTER(C.c_size_t), _vp, _sz, _vp]),
     "ono_sparse_lift_fallbacks": (_sz, []),
+    "ono_sparse_lift_debug_refuse": (_i, [C.c_uint32]),
     "ono_sparse_lift_pattern_misses": (_sz, []),
     "ono_sparse_lift_dev_async": (_i, [_fp, _sz, _vp, _sz, _vp, C.POINTER(C.c_uint64), _vp]),
     "ono_sparse_lift_set_mode": (_i, [_i]),

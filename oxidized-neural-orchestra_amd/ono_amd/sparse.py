@@ -117,6 +117,13 @@ def drop_debug_stale(add: int, stream=None) -> None:
     call("ono_sparse_drop_debug_stale", kernels.stream_handle(stream), int(add))
 
 
+def lift_debug_refuse(count: int) -> int:
+    """Test hook (ono_sparse_lift_debug_refuse): the process's next `count`
+    one-launch stream-ordered lifts are refused; 0 clears it.  Returns the
+    refusals of the previous setting not yet taken."""
+    return int(lib().ono_sparse_lift_debug_refuse(int(count)))
+
+
 def grad_lift_dev(buf: torch.Tensor, cap: int | None = None, stream=None) -> torch.Tensor:
     """grad_lift of wire bytes already in HBM (ono_sparse_lift_dev)."""
     assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()

@@ -478,6 +478,35 @@ def test_tcp_ring_sparse_socketpairs_vs_oracle(n, length, ratios, zero_copy, mon
         assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
 
 
+@pytest.mark.parametrize("n,length,ratios", [(2, 109386, [0.1, 0.1]), (3, 60000, [0.1, 0.15, 0.05])])
+@pytest.mark.parametrize("refuse", [1, 3, 10 ** 6])
+def test_tcp_ring_sparse_refused_lifts_replayed(n, length, ratios, refuse):
+    """The pipelined SparseCapable hop enqueues the add (or the gather's copy) and the next push's
+    threshold behind a one-launch lift it has not waited for; a refused lift leaves its output zero
+    and the hop lifts the stream on the host's path and replays that work before the push's frame
+    leaves.  Lifts refused by the test hook (the first one, three, or every one of the rings'): the
+    rings stay bit-exact with the restatement, and the refusals were taken."""
+    seeds = [91 + r for r in range(n)]
+    ins = inputs_for(n, length, 2, SEED + 45)
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(2)], *links[r], sparse=(ratios[r], seeds[r]))
+          for r in range(n)]
+    ono_amd.sparse.lift_debug_refuse(refuse)
+    left = None
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        left = ono_amd.sparse.lift_debug_refuse(0)
+        teardown(pairs, ws)
+    eg, er = oracle_rounds(ins, ratios, seeds)
+    for r in range(n):
+        assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
+    assert left < refuse and (refuse > 3 or left == 0), left  # (each ring round lifts at least 2 frames)
+
+
 def test_tcp_ring_sparse_host_fed_and_sampler_callback():
     """The host-fed form, and a caller-installed sampler (the boundary a Rust
     integration uses to draw rand's index::sample): here a Python sampler that
