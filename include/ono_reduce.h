@@ -214,9 +214,9 @@ int ono_sparse_lift_dev_async(float *g_dev, size_t cap, const uint8_t *buf_dev, 
 size_t ono_sparse_lift_fallbacks(void);
 /* test hook: the process's next `count` one-launch stream-ordered lifts are
  * refused (their status word set), whatever the stream — the path a caller
- * takes after a refusal (the blocking lift; the TCP ring's replay of the work
- * it enqueued behind a lift it had not waited for) is then exercised on
- * well-formed streams.  0 clears it.  Returns the count the call replaced
+ * takes after a refusal (the blocking lift, as the TCP ring's hop does) is
+ * then exercised on well-formed streams.  0 clears it.  Returns the count the
+ * call replaced
  * (the refusals not yet taken).                                              */
 int ono_sparse_lift_debug_refuse(uint32_t count);
 /* lifts so far (this process) that the pattern path handed to the walk path */

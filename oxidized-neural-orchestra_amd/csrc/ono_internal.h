@@ -81,12 +81,10 @@ hipError_t stream_wait(hipStream_t s, uint64_t *word_host, uint64_t *word_dev, u
 // the spin of stream_wait alone, on a word the stream's own kernel stores
 hipError_t stream_spin(hipStream_t s, uint64_t *word_host, uint32_t epoch);
 // ono_sparse_lift_dev_async with an in-kernel completion: when the lift is one launch its last workgroup
-// stores `sig` into the host-mapped word (word_host / word_dev) and in_kernel is set; else the caller waits.
-// zero_refused: a refused one-launch lift leaves its output [0, min(total, cap)) zero (the pipelined hop)
+// stores `sig` into the host-mapped word (word_host / word_dev) and in_kernel is set; else the caller waits
 struct LiftDone {
     uint64_t *word_host = nullptr, *word_dev = nullptr;
     uint32_t sig = 0;
-    bool zero_refused = false;
     bool in_kernel = false;
 };
 int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, uint64_t *status, uint64_t *ticket,

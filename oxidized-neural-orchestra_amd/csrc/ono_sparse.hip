@@ -1831,9 +1831,10 @@ __device__ __forceinline__ uint64_t stream_total(const uint8_t *b) {
     return total;
 }
 
-// A speculation refuted or a malformed stream: the host parses sequentially.
+// A speculation refuted or a malformed stream: the host parses sequentially.  (A system-scope store: the
+// word reaches host memory without waiting for an L2 write-back.)
 __device__ __forceinline__ void raise_bad(uint64_t *host_word, uint32_t epoch) {
-    *(volatile uint64_t *)host_word = epoch;
+    __hip_atomic_store(host_word, (uint64_t)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Segment s's speculative record start: the first 2-byte position whose next
@@ -3049,35 +3050,6 @@ struct FusedGrid {
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// pl_fused's completion for the TCP ring's hop (grid_complete's counted arrival): the last workgroup to finish
-// stores `sig` into the host-mapped word.  zero_refused (the ring's pipelined hop, which enqueues the kernels
-// that read the lift's output before it knows whether the lift was refused): a refused call's output
-// [0, n) is zeroed first by that workgroup, so that an add of it changes no value (x + 0 is x, and -0 + 0 the
-// +0 the reference's own add of an unkept value gives) until the host lifts the stream its way and replays
-// the work behind it.
-__device__ void lift_complete(float *g, uint64_t n, const uint64_t *badw, uint32_t epoch, uint64_t *word,
-                              uint64_t *arrive, uint64_t target, uint32_t sig, int zero_refused) {
-    __shared__ uint32_t s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __atomic_thread_fence(__ATOMIC_RELEASE);  // (system scope: the refusal word and the stores out)
-        const uint64_t old = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == target ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (zero_refused &&
-        __hip_atomic_load(badw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == (uint64_t)epoch) {
-        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) g[i] = 0.0f;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        __atomic_thread_fence(__ATOMIC_RELEASE);
-        __hip_atomic_store(word, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
 // pl_fused's staging (an 8-B aligned stream), 8 B per load: every tile's loads issued up front,
 // the first tile's first (a scheduling barrier keeps them ahead: the wait for them lets the later
 // tiles' loads stay in flight while the first tile is indexed and published), unconditional and
@@ -3181,7 +3153,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
                                                   uint64_t *frec, uint64_t *fchunk, uint64_t *fchunk_next,
                                                   uint32_t gcap, uint64_t *host_word, uint64_t *badw, uint32_t epoch, uint64_t *arrive, uint64_t arrive_target,
                                                   uint64_t *done_word, uint64_t *done_arrive, uint64_t done_target, uint32_t done_sig,
-                                                  int zero_refused, int force_bad) {
+                                                  int force_bad) {
     __shared__ uint4 img16[kPatImg / 8];  // a range as f16 bits (12 KiB), widened on the way out
     __shared__ uint4 lw4[TPW][kStageU4];
     __shared__ uint32_t lq[3 * kLQ], lqn;
@@ -3272,8 +3244,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
         // and a line left holding this launch's counts would look complete to the next-but-one launch
         for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
             fchunk_next[(size_t)i * kFusedLine] = 0;
-        if (done_word) lift_complete(g, min(total, (uint64_t)cap), badw, epoch, done_word, done_arrive, done_target,
-                                     done_sig, zero_refused);
+        if (done_word) grid_complete(done_word, done_arrive, done_target, done_sig);
         return;
     }
     const uint32_t total32 = (uint32_t)total;
@@ -3394,8 +3365,7 @@ __global__ __launch_bounds__(kPatT) __attribute__((amdgpu_waves_per_eu(6))) void
     for (uint32_t i = blockIdx.x * kPatT + threadIdx.x; i < kFusedRep * gcap; i += G * kPatT)
         fchunk_next[(size_t)i * kFusedLine] = 0;
     // the TCP ring's lift: the last workgroup to finish tells the host (with every refusal before it)
-    if (done_word) lift_complete(g, min(total, (uint64_t)cap), badw, epoch, done_word, done_arrive, done_target,
-                                 done_sig, zero_refused);
+    if (done_word) grid_complete(done_word, done_arrive, done_target, done_sig);
 #ifdef ONO_SP_STAMP
     SP_CLOCK(sp_tm);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3424,7 +3394,7 @@ __global__ __launch_bounds__(kPatT) void pl_wide(float *g, const uint8_t *b, siz
 // word once every earlier launch on the stream has finished; the host spins on
 // that word instead of a stream synchronisation (see host_wait).
 __global__ void sp_signal(uint64_t *host_word, uint32_t epoch) {
-    if (threadIdx.x == 0) *(volatile uint64_t *)host_word = epoch;
+    if (threadIdx.x == 0) __hip_atomic_store(host_word, (uint64_t)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the totals into the host-mapped words (the exact-size path of a small buffer), one wave
@@ -4634,11 +4604,11 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
         if (one)
             hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
                                cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target, dw, P.done_arrive,
-                               dtarget, dsig, done && done->zero_refused ? 1 : 0, force);
+                               dtarget, dsig, force);
         else
             hipLaunchKernelGGL(pl_fused<3>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec,
                                P.frec, cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target, dw,
-                               P.done_arrive, dtarget, dsig, done && done->zero_refused ? 1 : 0, force);
+                               P.done_arrive, dtarget, dsig, force);
         ONO_HIP(hipGetLastError());
         P.arrive_base = target;
         if (dw) {

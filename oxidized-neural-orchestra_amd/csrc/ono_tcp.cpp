@@ -52,7 +52,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <functional>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdlib>
@@ -721,12 +720,6 @@ private:
         }
         size_t nb = 0;
         if ((rc = codec([&] { return sparse_drop_tdev(dst, cap, &nb, chunk, L, r_->sp_t_dev, s_); }))) return rc;
-        // the previous hop's lift, if still pending, has run (stream order): refused, its replay re-made this
-        // push's threshold and the push is dropped again
-        bool again = false;
-        if ((rc = resolve(false, &again))) return rc;
-        if (again && (rc = codec([&] { return sparse_drop_tdev(dst, cap, &nb, chunk, L, r_->sp_t_dev, s_); })))
-            return rc;
         if (clk_) clk_->step(1);
         sparse = nb <= 2 * L;
         if (!sparse) {
@@ -806,13 +799,7 @@ private:
         uint32_t *idx_dev = nullptr;
         if (sampled && in_hbm && thr_hbm()) idx_dev = idx_hbm;
         else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, idx_host, 0));
-        // (behind a pending lift the launches are kept: the sample's buffer stays until the next push's take)
-        ono_ring *r = r_;
-        const float ratio = r_->sparse_r;
-        hipStream_t s = s_;
-        return enq([=]() -> int {
-            return sparse_threshold_dev(r->sp_t_dev, chunk, L, idx_dev, r->sp_idx_dev, m, ratio, s);
-        });
+        return sparse_threshold_dev(r_->sp_t_dev, chunk, L, idx_dev, r_->sp_idx_dev, m, r_->sparse_r, s_);
     }
 
     Incoming in_for(int c, int b) const {
@@ -890,7 +877,7 @@ private:
             return ONO_OK;
         }
         const size_t cap = in.bytes >= 8 ? (size_t)total : 0;
-        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes, in.sparse_dev, r_->sparse_r > 0.0f); });
+        rc = codec([&] { return lift(tmp_for(c), cap, &got, in.bytes, in.sparse_dev); });
         // a malformed stream is the lift's io::Error (protocol.rs:96-144) on the reference's recv_event
         if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
         if (rc) return rc;
@@ -903,10 +890,11 @@ private:
     // (ono_sparse_lift_dev_async: the pattern path, one or two launches) reads the frame in place through
     // its device mapping — no copy of the frame into HBM in the hop; a stream it refuses (not drop-shaped,
     // malformed) goes up to HBM and to the blocking device lift, which parses anything and returns the
-    // reference's errors.  *got = the stream's total.  pipe (the SparseCapable hop): a one-launch lift is not
-    // waited for — its refusal is looked at once later stream work has been waited for (resolve), and the
-    // work enqueued behind it in between is replayed after a refusal; ONO_TCP_PIPE=0 waits here (measurement).
-    int lift(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev, bool pipe = false) {
+    // reference's errors.  *got = the stream's total.  The one-launch lift stores the ring's word itself when
+    // it is done (no signal launch behind it; ONO_LIFT_SIGNAL=0 keeps the signal kernel, measurement).
+    // (Round 6 also measured the hop pipelined — the add / copy and the next push's threshold enqueued behind
+    // a lift not waited for, replayed after a refusal: no gain, profiles/r06_s20, r06_s22, r06_s23)
+    int lift(float *out, size_t cap, size_t *got, size_t nbytes, bool in_dev) {
         if (nbytes < 8) return ono_sparse_lift(out, cap, got, r_->sp_rx, nbytes, s_);
         const uint8_t *src = in_dev ? r_->sp_rx_dev : nullptr;
         if (!in_dev) {
@@ -919,31 +907,17 @@ private:
         }
         uint64_t total = 0;
         memcpy(&total, r_->sp_rx, 8);  // (little endian, protocol.rs:102-106)
-        static const bool pipe_on = env_on("ONO_TCP_PIPE");
-        pipe = pipe && pipe_on;
         uint64_t ticket = 0;
         LiftDone d;
         static const bool in_kernel = env_on("ONO_LIFT_SIGNAL");
-        if (in_kernel || pipe) {
+        if (in_kernel) {
             if (++r_->tcp_epoch == 0) r_->tcp_epoch = 1;
             d.word_host = lift_word();
             d.word_dev = r_->tcp_word_dev + 2;
             d.sig = r_->tcp_epoch;
-            d.zero_refused = pipe;
         }
-        int rc = lift_dev_async(out, cap, src, nbytes, r_->sp_status, &ticket, s_, d.word_host ? &d : nullptr);
+        int rc = lift_dev_async(out, cap, src, nbytes, r_->sp_status, &ticket, s_, in_kernel ? &d : nullptr);
         if (rc) return rc;
-        if (d.in_kernel && pipe) {
-            pend_.on = true;
-            pend_.ticket = ticket;
-            pend_.sig = d.sig;
-            pend_.out = out;
-            pend_.cap = cap;
-            pend_.nbytes = nbytes;
-            pend_.in_dev = in_dev;
-            *got = (size_t)total;
-            return ONO_OK;
-        }
         if (d.in_kernel) ONO_HIP(stream_spin(s_, lift_word(), d.sig));
         else if ((rc = wait())) return rc;
         if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
@@ -1068,28 +1042,14 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, false, &v, &k))) return rc;
                 clk.step(4);
-                float *dst = res + off(cr);
-                if ((rc = enq([=]() -> int {
-                         ONO_K(r_, s_, launch_acc(dst, v, k, s_, true));  // :141-143
-                         return ONO_OK;
-                     })))
-                    return rc;
+                ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
             }
             clk.step(5);
             clk.done();
             clk_ = nullptr;
         }
         const int own = mod(pos_ + 1);  // gather (:155-204)
-        {
-            float *dst = grad + off(own);
-            const float *src = res + off(own);
-            const size_t bytes = len(own) * sizeof(float);
-            if ((rc = enq([=]() -> int {
-                     ONO_HIP(dev_copy(dst, src, bytes, s_));  // :166
-                     return ONO_OK;
-                 })))
-                return rc;
-        }
+        ONO_HIP(dev_copy(grad + off(own), res + off(own), len(own) * sizeof(float), s_));  // :166
         for (int j = 0; j < n_ - 1; j++) {
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
@@ -1114,19 +1074,12 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
                 clk.step(4);
-                float *dst = grad + off(cr);
-                const size_t bytes = len(cr) * sizeof(float);
-                if ((rc = enq([=]() -> int {
-                         ONO_HIP(dev_copy(dst, v, bytes, s_));
-                         return ONO_OK;
-                     })))
-                    return rc;
+                ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
             }
             clk.step(5);
             clk.done();
             clk_ = nullptr;
         }
-        if ((rc = resolve(true))) return rc;  // (the last hop's lift, before the division reads its copy)
         ONO_K(r_, s_, launch_scale_zero(grad, grad, r_->size, (float)n_, nullptr, s_));  // :101-105
         return ONO_OK;
     }
@@ -1144,43 +1097,7 @@ private:
         });
     }
 
-    // A received SparseGrad's one-launch lift whose refusal the host has not looked at yet (the pipelined hop):
-    // the stream work enqueued behind it is kept, to run again after the host's own lift if it was refused.
-    struct PendingLift {
-        bool on = false;
-        uint64_t ticket = 0;
-        uint32_t sig = 0;
-        float *out = nullptr;
-        size_t cap = 0, nbytes = 0;
-        bool in_dev = false;
-        std::vector<std::function<int()>> ops;
-    };
-    // stream work behind a pending lift: run now, and kept for a replay
-    int enq(std::function<int()> f) {
-        if (pend_.on) pend_.ops.push_back(f);
-        return f();
-    }
-    // the pending lift looked at (spin: wait for its completion word first; otherwise the caller waited for
-    // later stream work): nothing to do if it was accepted; refused — its output is zero (lift_complete) and
-    // every add of it changed nothing — the host's lift of the stream, then the work behind it again, in order
-    // (*replayed).  A malformed stream is the lift's io::Error here, as in incoming().
-    int resolve(bool spin, bool *replayed = nullptr) {
-        if (replayed) *replayed = false;
-        if (!pend_.on) return ONO_OK;
-        PendingLift p = std::move(pend_);
-        pend_ = PendingLift{};
-        if (spin) ONO_HIP(stream_spin(s_, lift_word(), p.sig));
-        if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != p.ticket) return ONO_OK;
-        size_t got = 0;
-        int rc = codec([&] { return lift_fallback(p.out, p.cap, &got, p.nbytes, p.in_dev); });
-        if (rc == ONO_E_PROTO) return set_error(ONO_E_IO, "%s", ono_last_error());
-        if (rc) return rc;
-        for (auto &f : p.ops)
-            if ((rc = f())) return rc;
-        if (replayed) *replayed = true;
-        return ONO_OK;
-    }
-    uint64_t *lift_word() const { return r_->tcp_word + 2; }
+    uint64_t *lift_word() const { return r_->tcp_word + 2; }  // (the in-kernel completion of a waited lift)
 
     ono_ring *r_;
     hipStream_t s_;
@@ -1189,7 +1106,6 @@ private:
     std::vector<size_t> push_len_;
     size_t push_k_ = 0;
     HopClock *clk_ = nullptr;  // (ONO_TCP_TRACE: the hop in progress)
-    PendingLift pend_;
 };
 
 }  // namespace

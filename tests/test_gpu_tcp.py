@@ -480,12 +480,11 @@ def test_tcp_ring_sparse_socketpairs_vs_oracle(n, length, ratios, zero_copy, mon
 
 @pytest.mark.parametrize("n,length,ratios", [(2, 109386, [0.1, 0.1]), (3, 60000, [0.1, 0.15, 0.05])])
 @pytest.mark.parametrize("refuse", [1, 3, 10 ** 6])
-def test_tcp_ring_sparse_refused_lifts_replayed(n, length, ratios, refuse):
-    """The pipelined SparseCapable hop enqueues the add (or the gather's copy) and the next push's
-    threshold behind a one-launch lift it has not waited for; a refused lift leaves its output zero
-    and the hop lifts the stream on the host's path and replays that work before the push's frame
-    leaves.  Lifts refused by the test hook (the first one, three, or every one of the rings'): the
-    rings stay bit-exact with the restatement, and the refusals were taken."""
+def test_tcp_ring_sparse_refused_lifts(n, length, ratios, refuse):
+    """A received SparseGrad is lifted by the one-launch stream-ordered lift; a stream it refuses goes to the
+    blocking device lift before the hop adds or copies it.  Lifts refused by the test hook (the first one,
+    three, or every one of the rings'): the rings stay bit-exact with the restatement, and the refusals
+    were taken."""
     seeds = [91 + r for r in range(n)]
     ins = inputs_for(n, length, 2, SEED + 45)
     links, pairs = socketpair_links(n)
