@@ -219,18 +219,21 @@ def build_line(*, value, n_gpus, steps, warmup, elapsed, bucket_bytes, wire, ext
 def pmc_traffic(kernel_substr: str, elems: int) -> dict | None:
     """HBM bytes per launch of the dominant kernel from the committed PMC
     summary (profiles/*pmc*.json written by tools/pmc_summary.py), matched on
-    the kernel name and bucket size; None when no such summary exists."""
-    best = None
+    the kernel name and bucket size — the most recently recorded one
+    (recorded_utc; summaries without it rank first, by file name); None when
+    no such summary exists."""
+    best, best_key = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             with open(f) as fh:
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
+        key = (d.get("recorded_utc", ""), os.path.basename(f))
         for k in d.get("kernels", []):
-            if kernel_substr in k.get("name", "") and k.get("elems") == elems:
-                best = dict(k, source=os.path.relpath(f, ROOT), commit=d.get("commit", "unknown"),
-                            session=d.get("session") or "a builder session")
+            if kernel_substr in k.get("name", "") and k.get("elems") == elems and (best_key is None or key >= best_key):
+                best, best_key = dict(k, source=os.path.relpath(f, ROOT), commit=d.get("commit", "unknown"),
+                                      session=d.get("session") or "a builder session"), key
     return best
 
 

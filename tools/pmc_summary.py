@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import csv
 import glob
+import datetime
 import json
 import os
 import re
@@ -105,7 +106,9 @@ def main() -> int:
             "traffic_over_algorithmic": (rd + wr) / algo,
         })
     doc = {"note": "median over launches; read = 2 x FETCH_SIZE x 1 KiB (gfx950 half-count), write = WRITE_SIZE x 1 KiB",
-           "commit": a.commit, "session": a.session, "kernels": kernels}
+           "commit": a.commit, "session": a.session,
+           "recorded_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
+           "kernels": kernels}
     with open(a.out, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc, indent=1))
