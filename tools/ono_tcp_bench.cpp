@@ -64,9 +64,15 @@ int connect_to(int port) {
     return -1;
 }
 
+int g_sockbuf_kib = 0;  // --sockbuf: SO_SNDBUF / SO_RCVBUF of every ring socket (0: the system's autotuning)
 void nodelay(int fd) {
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (g_sockbuf_kib > 0) {
+        int b = g_sockbuf_kib << 10;
+        setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &b, sizeof b);
+        setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &b, sizeof b);
+    }
 }
 
 }  // namespace
@@ -84,6 +90,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[a], "--sparse") && a + 1 < argc) sparse = (float)atof(argv[++a]);
         else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
         else if (!strcmp(argv[a], "--phases") && a + 1 < argc) phases = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--sockbuf") && a + 1 < argc) g_sockbuf_kib = atoi(argv[++a]);
         else { fprintf(stderr, "bad arg %s\n", argv[a]); return 1; }
     }
     if (n < 2 || rounds < 1 || len < (size_t)n) { fprintf(stderr, "need ranks >= 2, len >= ranks\n"); return 1; }
