@@ -3917,6 +3917,11 @@ __device__ __forceinline__ void transpose32(uint32_t (&A)[32]) {
 // keys: the gathered keys, or NULL: the sample is g[0, m) itself.  (Round 6 measured gathering g[idx[i]] here
 // instead of in sp_gather_keys, one launch less: +10 us per SparseCapable push of the config-1 TCP ring — one
 // workgroup's 16384 scattered loads cost more than the gather's launch; profiles/r06_s4_tcp_variants.jsonl.)
+// The select stops early once the chosen digit leaves a single candidate (typically after 10-12 of the 16
+// steps: 16384 samples near the 90th percentile differ within ~12 mantissa bits); that key is the answer, and
+// the lane holding it reads it back from its bit planes (round 6: 9.5 vs 11.0 us per select, config-1 push,
+// tools/thr_bench, profiles/r06_s26_thr_bench.json — where four bits a step, four waves of 64 keys a lane,
+// and the gather and the select in one launch (the last workgroup to arrive selecting) all measured slower).
 __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, const float *g, uint32_t m, uint32_t k,
                                                       float *t_out) {
     __shared__ uint32_t wc[2][kThrT / 64][2];
@@ -3929,7 +3934,8 @@ __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, cons
         C |= i < m ? 1u << (31 - q) : 0u;
     }
     transpose32(A);
-    uint32_t prefix = 0, kk = k;
+    uint32_t prefix = 0, kk = k, cand = m;
+    bool one = false;
     // bits 30..1 two at a time (bit 31 is clear in every key), then bit 0
 #pragma unroll
     for (int s = 0; s < 16; s++) {
@@ -3952,26 +3958,40 @@ __global__ __launch_bounds__(kThrT) void sp_threshold(const uint32_t *keys, cons
             sy += wc[par][w][1];
         }
         const uint32_t n00 = sx & 0xFFFFu, n01 = sx >> 16, n10 = sy;
-        uint32_t d;
+        uint32_t d, nd;
         if (lo < 0) {  // one bit: n00 = candidates with a 0 there
             d = kk < n00 ? 0u : 1u;
+            nd = d ? cand - n00 : n00;
             if (d) kk -= n00;
             C &= d ? P1 : ~P1;
             prefix |= d;
         } else {
-            if (kk < n00) d = 0;
-            else if (kk < n00 + n01) { d = 1; kk -= n00; }
-            else if (kk < n00 + n01 + n10) { d = 2; kk -= n00 + n01; }
-            else { d = 3; kk -= n00 + n01 + n10; }
+            if (kk < n00) { d = 0; nd = n00; }
+            else if (kk < n00 + n01) { d = 1; kk -= n00; nd = n01; }
+            else if (kk < n00 + n01 + n10) { d = 2; kk -= n00 + n01; nd = n10; }
+            else { d = 3; kk -= n00 + n01 + n10; nd = cand - n00 - n01 - n10; }
             C &= (d & 2 ? P1 : ~P1) & (d & 1 ? P0 : ~P0);
             prefix |= d << lo;
         }
+        cand = nd;
+        if (cand == 1 && lo > 0) {  // (uniform) one key left
+            one = true;
+            break;
+        }
     }
-    if (threadIdx.x == 0) {
-        const float mp = 6.103515625e-05f;  // f16::MIN_POSITIVE
-        const float t = __builtin_bit_cast(float, prefix);
-        t_out[0] = prefix > 0x7F800000u ? mp : (t > mp ? t : mp);
+    const float mp = 6.103515625e-05f;  // f16::MIN_POSITIVE
+    uint32_t key = prefix;
+    if (one) {
+        if (!C) return;  // (the lane that holds the candidate writes)
+        const int q = __builtin_clz(C);  // its bit is 31 - q: bit p of that key is bit 31 - q of plane p
+        key = 0;
+#pragma unroll
+        for (int p = 0; p < 31; p++) key |= ((A[31 - p] >> (31 - q)) & 1u) << p;
+    } else if (threadIdx.x != 0) {
+        return;
     }
+    const float t = __builtin_bit_cast(float, key);
+    t_out[0] = key > 0x7F800000u ? mp : (t > mp ? t : mp);
 }
 // the select over g[0, m) (idx NULL) or over g[idx[i]] (keys: m device words for the gathered keys; idx
 // may be the same buffer; in HBM or pinned host memory)
