@@ -4458,7 +4458,8 @@ size_t fused_slots(int tpw) {
 // one-launch grid is remembered; while one stream alone uses the form nothing is recorded (an event after
 // every launch measured 26.5 vs 22.7 us per lift back to back).  A stream's launch takes the one launch
 // when the grids of the other streams that may still run (no event yet, or one not reached) and its own
-// fit in half the device's slots together — round 5 allowed one such lift per device, so two workers
+// fit in half the device's slots together (or nothing of theirs may still run) — round 5 allowed one such
+// lift per device at a time, so two workers
 // sharing a GPU (the TCP bench, the ring tests) lifted every other frame in two launches, 17-19 vs 8-9 us
 // for a config-1 frame (profiles/r06_s17); ONO_LIFT_FUSED_SHARE=0 restores that rule (measurement).
 bool lift_fused_share() {
@@ -4472,6 +4473,7 @@ struct FusedLast {
     hipEvent_t ev = nullptr;
     bool recorded = false;
     size_t grid = 0;
+    std::chrono::steady_clock::time_point at;  // (the launch: an unrecorded one counts for 50 ms)
 };
 struct FusedDev {
     std::map<hipStream_t, FusedLast> last;
@@ -4485,7 +4487,11 @@ bool fused_device_free(int dev, hipStream_t s, size_t grid, size_t slots) {
         FusedLast &f = it->second;
         if (it->first == s || !f.grid) { ++it; continue; }
         others++;
-        const bool done = f.recorded && hipEventQuery(f.ev) != hipErrorNotReady;
+        // an unrecorded launch (made while its stream was the only one) cannot be asked; after 50 ms it is taken
+        // as finished — were it not, the grids would wait for each other until a poll gives up and the call is
+        // refused (the blocking lift then does it): slower, never wrong
+        const bool done = f.recorded ? hipEventQuery(f.ev) != hipErrorNotReady
+                                     : std::chrono::steady_clock::now() - f.at > std::chrono::milliseconds(50);
         if (done) {
             f.grid = 0;
             if (D.last.size() > 64) {  // streams come and go: forget the finished ones
@@ -4503,7 +4509,9 @@ bool fused_device_free(int dev, hipStream_t s, size_t grid, size_t slots) {
         D.multi = true;
         if (!lift_fused_share()) return false;
     }
-    if (!lift_fused_share()) return busy == 0;
+    // nothing of the others may still run: the whole device (the caller checked that the grid fits it);
+    // else both grids in half of it
+    if (busy == 0 || !lift_fused_share()) return busy == 0;
     return busy + grid <= slots / 2;
 }
 void fused_device_mark(int dev, hipStream_t s, size_t grid) {
@@ -4511,6 +4519,7 @@ void fused_device_mark(int dev, hipStream_t s, size_t grid) {
     FusedLast &f = D.last[s];
     f.grid = grid;
     f.recorded = false;
+    f.at = std::chrono::steady_clock::now();
     if (!D.multi) return;
     if (!f.ev && hipEventCreateWithFlags(&f.ev, hipEventDisableTiming) != hipSuccess) {
         f.ev = nullptr;
