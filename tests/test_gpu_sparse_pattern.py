@@ -548,3 +548,34 @@ def test_async_lift_one_launch_with_cu_slots_held_by_another_process():
     assert_bitexact(out[:total].cpu().numpy(), O.grad_lift(b, cap=total))
     print(f"lift with 3/4 of the CUs held elsewhere: {took * 1e3:.2f} ms, refused={refused}")
     assert took < 0.005, f"the one-launch lift took {took * 1e3:.1f} ms while CU slots were held elsewhere"
+
+
+def test_stream_lift_one_launch_after_another_streams_lift():
+    """A stream-ordered lift made while its stream was the device's only lifting one is not recorded; once
+    another stream lifts, that launch must not keep counting as running (round 6's late session: every
+    64 MiB lift of the bench's codec leg then took the two launches, 1.07 instead of 0.023 ms).  After a lift
+    on stream A and 60 ms, twelve back-to-back lifts on stream B run at the one-launch rate, and are exact."""
+    n = 1 << 24
+    g = O.synth(n, SEED + 57, 2)
+    t = max(float(np.quantile(np.abs(g), 0.9)), 6.103515625e-05)
+    wire = SP.grad_drop_dev(dev(g), t)
+    want = O.grad_lift(bytes(wire.cpu().numpy()), cap=n)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(3)]
+    st = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    SP.grad_lift_dev_async(wire, outs[0], st, sa)
+    torch.cuda.synchronize()
+    import time
+    time.sleep(0.06)
+    for i in range(4):  # (warm: the stream's scratch)
+        SP.grad_lift_dev_async(wire, outs[i % 3], st, sb)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(sb)
+    tickets = [SP.grad_lift_dev_async(wire, outs[i % 3], st, sb) for i in range(12)]
+    e1.record(sb)
+    e1.synchronize()
+    per_ms = e0.elapsed_time(e1) / 12
+    assert int(st.item()) != tickets[-1]  # not refused
+    assert_bitexact(outs[11 % 3].cpu().numpy(), want)
+    assert per_ms < 0.3, per_ms  # one launch: ~0.023 ms; the two launches measured 1.07
