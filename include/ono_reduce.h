@@ -367,7 +367,12 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
  * process (a later ring reuses them) until released.  A fresh region whose
  * IPC handle repeats one this process obtained before is parked and another
  * allocated (re-importing a repeated handle handed out partly stale mappings on
- * this ROCm); an import of a handle this process opened before is ONO_E_IO.   */
+ * this ROCm); an import of a handle this process opened before is ONO_E_IO.
+ * RESIDUAL RISK: one wrong result seen in round 4 (a rank read stale lines of a
+ * peer's result slot right after a pool release) was narrowed to the free and
+ * re-import path, not proven; that path is now closed by the
+ * rules above and has not failed since, but a caller that must never see it
+ * can keep its rings (and the pool) for the process's life.                  */
 #define ONO_XGMI_HANDLE_BYTES 128
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
