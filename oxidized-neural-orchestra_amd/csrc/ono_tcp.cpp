@@ -97,7 +97,7 @@ bool thr_hbm() {  // (default off: no gain measured, and the upload lengthened e
 struct HopTrace {
     static constexpr int kSteps = 7;
     std::atomic<uint64_t> ns[kSteps] = {}, hops{0}, draw_ns{0}, draws{0}, wait_ns{0}, waits{0}, misses{0},
-        take_ns{0}, takes{0};
+        take_ns{0}, takes{0}, lifts{0}, lift_call_ns{0}, lift_wait_ns{0};
     ~HopTrace() {
         const uint64_t h = hops.load();
         if (!h) return;
@@ -110,6 +110,10 @@ struct HopTrace {
         if (takes.load())
             fprintf(stderr, "ONO_TCP_TRACE take() calls: %llu, %.2f us each\n", (unsigned long long)takes.load(),
                     take_ns.load() / 1e3 / (double)takes.load());
+        if (lifts.load())
+            fprintf(stderr, "ONO_TCP_TRACE lifts: %llu, us each: the call %.2f, until complete %.2f\n",
+                    (unsigned long long)lifts.load(), lift_call_ns.load() / 1e3 / (double)lifts.load(),
+                    lift_wait_ns.load() / 1e3 / (double)lifts.load());
         static const char *names[kSteps] = {"threshold", "drop", "mask", "exchange", "incoming", "add", "sample"};
         fprintf(stderr, "ONO_TCP_TRACE %llu hops, us per hop:", (unsigned long long)h);
         for (int k = 0; k < kSteps; k++) fprintf(stderr, " %s %.2f", names[k], ns[k].load() / 1e3 / (double)h);
@@ -916,10 +920,18 @@ private:
             d.word_dev = r_->tcp_word_dev + 2;
             d.sig = r_->tcp_epoch;
         }
+        const auto t0 = std::chrono::steady_clock::now();
         int rc = lift_dev_async(out, cap, src, nbytes, r_->sp_status, &ticket, s_, in_kernel ? &d : nullptr);
         if (rc) return rc;
+        const auto t1 = std::chrono::steady_clock::now();
         if (d.in_kernel) ONO_HIP(stream_spin(s_, lift_word(), d.sig));
         else if ((rc = wait())) return rc;
+        if (trace_on()) {
+            g_hop_trace.lifts++;
+            g_hop_trace.lift_call_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+            g_hop_trace.lift_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                            std::chrono::steady_clock::now() - t1).count();
+        }
         if (__atomic_load_n(r_->sp_status, __ATOMIC_ACQUIRE) != ticket) {
             *got = (size_t)total;
             return ONO_OK;
