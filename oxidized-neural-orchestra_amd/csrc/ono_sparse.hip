@@ -4100,12 +4100,38 @@ int take_drop_error(Scratch *sc, const char *when) {
                                            : "a tile's range would pass the end of the buffer; it was not written");
 }
 
+// ONO_TCP_TRACE=1 (measurement): host time of the one-launch drop's calls — entry to the launch call, the
+// launch call, the launch's return to the completion seen — printed at exit
+struct DropHostTrace {
+    std::atomic<uint64_t> calls{0}, pre_ns{0}, launch_ns{0}, wait_ns{0};
+    ~DropHostTrace() {
+        const uint64_t c = calls.load();
+        if (!c || !getenv("ONO_TCP_TRACE")) return;
+        fprintf(stderr, "ONO_TCP_TRACE one-launch drop, %llu calls, us each: before the launch %.2f, the launch %.2f, "
+                "until complete %.2f\n", (unsigned long long)c, pre_ns.load() / 1e3 / c, launch_ns.load() / 1e3 / c,
+                wait_ns.load() / 1e3 / c);
+    }
+};
+DropHostTrace g_drop_trace;
+bool drop_trace_on() {
+    static const bool v = getenv("ONO_TCP_TRACE") != nullptr;
+    return v;
+}
+inline uint64_t ns_since(std::chrono::steady_clock::time_point a) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a).count();
+}
+
 int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, const float *g, size_t n,
                 float threshold, hipStream_t s, const float *t_dev = nullptr) {
+    const auto t_entry = std::chrono::steady_clock::now();
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
     const bool vec = ((uintptr_t)g & 15u) == 0;
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
-    std::lock_guard<std::mutex> lk(g_scratch_mu);  // the host side of one call at a time
+    // The maps and allocations of one call at a time; released before any wait: a stream's scratch is its
+    // own (calls on one stream are ordered by the caller) and never freed, so a wait needs no lock — held
+    // through its spin it made every other ring's drop or lift in the process wait for this one's GPU work
+    // (two TCP workers of one process, config 1: ~11 us of each drop call before its launch, r06_s31)
+    std::unique_lock<std::mutex> lk(g_scratch_mu);
     Scratch *sc = nullptr;
     hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(s, &cap_st) == hipSuccess && cap_st != hipStreamCaptureStatusNone;
@@ -4169,19 +4195,32 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
             target = sc->arrive_base + grid - 1;
             *(volatile uint64_t *)(sc->host_tot + 2) = 0;
         }
+        const bool tr = drop_trace_on();
+        const auto t_pre = std::chrono::steady_clock::now();
         hipLaunchKernelGGL(sp_drop1, dim3(grid), dim3(kIT), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->desc,
                            sc->depoch, drop_fallback_polls(), buf, cap, sc->host_tot_dev, nbytes_dev, sc->arrive,
                            target, sig);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
         if (nbytes_dev) return ONO_OK;
+        const auto t_launched = std::chrono::steady_clock::now();
         volatile uint64_t *tot = sc->host_tot;
         if (in_kernel) {
             sc->arrive_base += grid;
+            lk.unlock();
             e = host_spin(s, sc->host_tot + 2, sig);
         } else {
             if (++sc->calls == 0) sc->calls = 1;
-            e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
+            const uint32_t c = sc->calls;
+            lk.unlock();
+            e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, c);
+        }
+        if (tr) {
+            g_drop_trace.calls++;
+            g_drop_trace.pre_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_pre - t_entry).count();
+            g_drop_trace.launch_ns +=
+                (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_launched - t_pre).count();
+            g_drop_trace.wait_ns += ns_since(t_launched);
         }
         if (e != hipSuccess) return hip_error(e, "sparse drop", __FILE__, __LINE__);
         if ((rc = take_drop_error(sc, ""))) return rc;
@@ -4212,6 +4251,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip; never captured)
         hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, emit ? sc->agg : agg, half,
                            emit ? (const uint32_t *)sc->state : nullptr, (uint32_t)nchunks, sc->host_tot_dev);
+        lk.unlock();  // (the rest of the call uses this stream's scratch only)
         e = hipStreamSynchronize(s);
         // (count + emit: no sp_emit follows, so the call stays `dirty` and the next one re-zeroes)
         if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
@@ -4242,7 +4282,9 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (nbytes_dev) return ONO_OK;
     if (++sc->calls == 0) sc->calls = 1;
-    e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
+    const uint32_t c = sc->calls;
+    if (lk.owns_lock()) lk.unlock();
+    e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, c);
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     int rc = take_drop_error(sc, "");
     if (rc) return rc;
@@ -4469,6 +4511,14 @@ bool lift_fused_share() {
     }();
     return v;
 }
+// ONO_LIFT_SMALL_TRACKED=1 (measurement): small one-launch grids are tracked as the large ones
+bool small_lifts_untracked() {
+    static const bool v = [] {
+        const char *e = getenv("ONO_LIFT_SMALL_TRACKED");
+        return !(e && !strcmp(e, "1"));
+    }();
+    return v;
+}
 struct FusedLast {
     hipEvent_t ev = nullptr;
     bool recorded = false;
@@ -4592,8 +4642,16 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
                            cap_st != hipStreamCaptureStatusNone;
     const bool one = T <= std::min(fused_slots(1), (size_t)ONO_FUSED_ONE_MAX);
     const size_t grid = one ? T : (T + 2) / 3;
+    // A small grid (at most 1/64 of the slots: a config-1 frame's 13 workgroups) is neither asked about nor
+    // recorded: one stream runs its lifts one at a time, so it takes dozens of streams lifting at once to fill
+    // half the device with them, and a small grid that does find the device full of a waiting one's
+    // workgroups ends, like any stalled one, refused after ~100 us of standstill (the caller's blocking lift
+    // then does it) — never wrong.  The event query and record cost ~3 us of host time per lift between two
+    // workers of one process (r06_s32).
+    const bool small = one && grid <= fused_slots(1) / 64 && small_lifts_untracked();
     if (T <= kPatDirect && ((uintptr_t)buf_dev & 7) == 0 && lift_fused() && !capturing &&
-        (T + 2) / 3 <= fused_slots(3) && fused_device_free(dev, s, grid, one ? fused_slots(1) : fused_slots(3))) {
+        (T + 2) / 3 <= fused_slots(3) &&
+        (small || fused_device_free(dev, s, grid, one ? fused_slots(1) : fused_slots(3)))) {
         if (T > P.fcap) {
             const size_t gc = (T + kPatChunk - 1) / kPatChunk;
             (void)hipFree(P.frec);
@@ -4645,7 +4703,7 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
             done->in_kernel = true;
         }
         P.fpar ^= 1;
-        fused_device_mark(dev, s, grid);
+        if (!small) fused_device_mark(dev, s, grid);
         return ONO_OK;
     }
     ONO_HIP(launch_pl_index(buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw, status, epoch, s));
