@@ -4127,10 +4127,10 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     const size_t ntiles = n ? (n + kTile - 1) / kTile : 0;
     const bool vec = ((uintptr_t)g & 15u) == 0;
     const bool worst_case_fits = cap >= ono_sparse_max_bytes(n);
-    // The maps and allocations of one call at a time; released before any wait: a stream's scratch is its
-    // own (calls on one stream are ordered by the caller) and never freed, so a wait needs no lock — held
-    // through its spin it made every other ring's drop or lift in the process wait for this one's GPU work
-    // (two TCP workers of one process, config 1: ~11 us of each drop call before its launch, r06_s31)
+    // The maps and allocations of one call at a time; released before the launches: a stream's scratch is
+    // its own (calls on one stream are ordered by the caller) and never freed, so launches and waits need no
+    // lock — held through its spin it made every other ring's drop or lift in the process wait for this one's
+    // GPU work (two TCP workers of one process, config 1: ~11 us of each drop call before its launch, r06_s31)
     std::unique_lock<std::mutex> lk(g_scratch_mu);
     Scratch *sc = nullptr;
     hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
@@ -4195,6 +4195,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
             target = sc->arrive_base + grid - 1;
             *(volatile uint64_t *)(sc->host_tot + 2) = 0;
         }
+        lk.unlock();  // (the launch and the wait use this stream's scratch only)
         const bool tr = drop_trace_on();
         const auto t_pre = std::chrono::steady_clock::now();
         hipLaunchKernelGGL(sp_drop1, dim3(grid), dim3(kIT), 0, s, g, n, ntiles, threshold, t_dev, vec, sc->desc,
@@ -4207,13 +4208,10 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
         volatile uint64_t *tot = sc->host_tot;
         if (in_kernel) {
             sc->arrive_base += grid;
-            lk.unlock();
             e = host_spin(s, sc->host_tot + 2, sig);
         } else {
             if (++sc->calls == 0) sc->calls = 1;
-            const uint32_t c = sc->calls;
-            lk.unlock();
-            e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, c);
+            e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
         }
         if (tr) {
             g_drop_trace.calls++;
@@ -4227,6 +4225,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
         *nbytes = 8 + 8 * (size_t)tot[1] + 2 * (size_t)tot[0];
         return ONO_OK;
     }
+    lk.unlock();  // (from here on the call uses this stream's scratch only)
     uint2 *recA = sc->rec, *recB = sc->rec + sc->tiles_cap;
     const size_t nchunks = (ntiles + kRecChunk - 1) / kRecChunk;
     const size_t half = kAggHalf;  // (the second array, within each chunk's line)
@@ -4251,7 +4250,6 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     if (e == hipSuccess && !worst_case_fits) {  // the exact size first (one extra host round trip; never captured)
         hipLaunchKernelGGL(sp_totals_out, dim3(1), dim3(64), 0, s, emit ? sc->agg : agg, half,
                            emit ? (const uint32_t *)sc->state : nullptr, (uint32_t)nchunks, sc->host_tot_dev);
-        lk.unlock();  // (the rest of the call uses this stream's scratch only)
         e = hipStreamSynchronize(s);
         // (count + emit: no sp_emit follows, so the call stays `dirty` and the next one re-zeroes)
         if (e == hipSuccess && 8 + 8 * tot[1] + 2 * tot[0] > cap)
@@ -4282,9 +4280,7 @@ int drop_launch(uint8_t *buf, size_t cap, size_t *nbytes, uint64_t *nbytes_dev, 
     }
     if (nbytes_dev) return ONO_OK;
     if (++sc->calls == 0) sc->calls = 1;
-    const uint32_t c = sc->calls;
-    if (lk.owns_lock()) lk.unlock();
-    e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, c);
+    e = host_wait(s, sc->host_tot + 2, sc->host_tot_dev + 2, sc->calls);
     if (e != hipSuccess) return hip_error(e, "sparse write", __FILE__, __LINE__);
     int rc = take_drop_error(sc, "");
     if (rc) return rc;
@@ -4597,7 +4593,7 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
     if (done) done->in_kernel = false;
     if (!status || !ticket || (!buf_dev && nbytes)) return set_error(ONO_E_ARG, "NULL argument");
     if (nbytes < 8) return set_error(ONO_E_PROTO, "The given sparse buffer is smaller than TOTAL_LEN_SIZE");
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    std::unique_lock<std::mutex> lk(g_scratch_mu);  // (the maps and the device's one-launch record)
     int dev = 0;
     ONO_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return set_error(ONO_E_ARG, "device %d", dev);
@@ -4688,6 +4684,7 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
             dtarget = P.done_base + grid - 1;
             *(volatile uint64_t *)done->word_host = 0;
         }
+        if (small) lk.unlock();  // (nothing of the device's record to update after the launch)
         if (one)
             hipLaunchKernelGGL(pl_fused<1>, dim3((unsigned)grid), dim3(kPatT), 0, s, g, buf_dev, M, T, cap, vec, P.frec,
                                cur, next, (uint32_t)P.fgcap, P.aw, status, epoch, P.arrive, target, dw, P.done_arrive,
@@ -4706,6 +4703,7 @@ int lift_dev_async(float *g, size_t cap, const uint8_t *buf_dev, size_t nbytes, 
         if (!small) fused_device_mark(dev, s, grid);
         return ONO_OK;
     }
+    lk.unlock();  // (the two launches use this stream's scratch only)
     ONO_HIP(launch_pl_index(buf_dev, M, T, P.prec, tsum, qcount, P.pwide, P.aw, status, epoch, s));
     if (T > kPatDirect)
         hipLaunchKernelGGL(pl_scan, dim3(1), dim3(kPatScanT), 0, s, buf_dev, P.prec, T, P.pE, status, epoch);
