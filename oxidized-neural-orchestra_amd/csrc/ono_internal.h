@@ -74,6 +74,10 @@ int sparse_threshold_dev(float *t_dev, const float *g, size_t n, const uint32_t 
 int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, size_t n, const float *t_dev,
                      hipStream_t s);
 hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s);
+// one launch: dst[0, k) += src (add) or = src (copy), and the mask of mg[0, mn) (sp_mask's zero_kept form)
+// with the threshold at t_dev — the SparseCapable hop's work after its exchange
+hipError_t launch_hop_post(float *dst, const float *src, size_t k, int add, float *mg, size_t mn, const float *t_dev,
+                           int zero_kept, hipStream_t s);
 // Wait for everything enqueued on s so far by spinning on a host-mapped word
 // that a one-lane kernel sets to `epoch` (a stream synchronisation's wake-up
 // costs several microseconds more; used on the TCP ring's hops).

@@ -1703,6 +1703,28 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, cons
     }
 }
 
+// The TCP ring's SparseCapable hop after its exchange, in one launch (ono_tcp.cpp): the received values into
+// their chunk (dst += src, AccOp's add, for the scatter; dst = src, a copy, for the gather) and the sparse
+// push's mask of the chunk it sent (sp_mask's two forms, the threshold where the push left it) — two
+// different chunks, so the two parts are independent workgroups: one launch instead of two on the hop's path.
+__global__ __launch_bounds__(kSB) void sp_hop_post(float *dst, const float *src, size_t k, int add, float *mg,
+                                                   size_t mn, const float *t_dev, int zero_kept, uint32_t b1) {
+    if (blockIdx.x < b1) {
+        const size_t i = (size_t)blockIdx.x * kSB + threadIdx.x;
+        if (i < k) dst[i] = add ? dst[i] + src[i] : src[i];
+        return;
+    }
+    const size_t i = (size_t)(blockIdx.x - b1) * kSB + threadIdx.x;
+    if (i >= mn) return;
+    const float t = *t_dev;
+    const float x = mg[i];
+    if (zero_kept) {
+        if (kept(x, t)) mg[i] = 0.0f;
+    } else {
+        if (fabsf(x) < t) mg[i] = 0.0f;
+    }
+}
+
 // ---------------------------------------------------------------- lift ----
 // The record stream is a linked list (each header's run length gives the next
 // header's position), cut into segments of kSeg bytes.  Three launches:
@@ -4410,6 +4432,14 @@ int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, s
     int rc = drop_args(g, n, buf, cap);
     if (rc) return rc;
     return drop_launch(buf, cap, nbytes, nullptr, g, n, 0.0f, s, t_dev);
+}
+hipError_t launch_hop_post(float *dst, const float *src, size_t k, int add, float *mg, size_t mn, const float *t_dev,
+                           int zero_kept, hipStream_t s) {
+    const size_t b1 = (k + kSB - 1) / kSB, b2 = (mn + kSB - 1) / kSB;
+    if (b1 + b2 == 0) return hipSuccess;
+    hipLaunchKernelGGL(sp_hop_post, dim3((unsigned)(b1 + b2)), dim3(kSB), 0, s, dst, src, k, add, mg, mn, t_dev,
+                       zero_kept, (uint32_t)b1);
+    return hipGetLastError();
 }
 hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s) {
     if (!n) return hipSuccess;

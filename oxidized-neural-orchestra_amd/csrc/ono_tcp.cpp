@@ -151,9 +151,17 @@ int tcp_spin_us() {
     }();
     return v;
 }
-// ONO_TCP_MASK_EARLY=0: a sparse push's mask after the exchange (round 5) instead of before it
-bool mask_early() {
-    static const bool v = env_on("ONO_TCP_MASK_EARLY");
+// Where a sparse push's mask runs (ONO_TCP_MASK): "fused" (default) in one launch with the hop's add or copy
+// after the exchange (launch_hop_post: neither the send nor the lift waits for a launch of its own), "early"
+// before the exchange, "late" right after it (round 5's form)
+enum MaskAt { MASK_FUSED = 0, MASK_EARLY = 1, MASK_LATE = 2 };
+int mask_at() {
+    static const int v = [] {
+        const char *e = getenv("ONO_TCP_MASK");
+        if (e && !strcmp(e, "early")) return (int)MASK_EARLY;
+        if (e && !strcmp(e, "late")) return (int)MASK_LATE;
+        return (int)MASK_FUSED;
+    }();
     return v;
 }
 
@@ -1036,25 +1044,29 @@ private:
             const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            // :126-132 sent values leave; a dense push (:133) zeroed the chunk in its encoder.  The frame is
-            // complete when out_sparse returns, so the mask runs on the device while the frame is on the socket
-            const bool early = mask_early();
+            // :126-132 sent values leave; a dense push (:133) zeroed the chunk in its encoder (mask_at: where)
+            const int mat = mask_at();
             HopClock clk;
             clk_ = &clk;
             if ((rc = out_sparse(res + off(cs), cs, true, t, sparse, o))) return rc;
-            if (early && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
+            if (mat == MASK_EARLY && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
             clk.step(2);
             if ((rc = xchg(o, in))) return rc;
             clk.step(3);
-            if (!early && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
+            if (mat == MASK_LATE && sparse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
+            const bool fuse = mat == MASK_FUSED && sparse;
             if (in.kind == KIND_DENSE) {
+                if (fuse && (rc = mask(res + off(cs), len(cs), 1))) return rc;
                 ONO_K(r_, s_, launch_decode_add<uint16_t>(res + off(cr), slot(1, cr), len(cr), s_));
             } else {
                 const float *v = nullptr;
                 size_t k = 0;
                 if ((rc = incoming(in, cr, false, &v, &k))) return rc;
                 clk.step(4);
-                ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
+                if (fuse)  // :141-143 with the push's mask
+                    ONO_K(r_, s_, launch_hop_post(res + off(cr), v, k, 1, res + off(cs), len(cs), r_->sp_t_dev, 1, s_));
+                else
+                    ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
             }
             clk.step(5);
             clk.done();
@@ -1066,27 +1078,31 @@ private:
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            const bool early = mask_early();
+            const int mat = mask_at();
             HopClock clk;
             clk_ = &clk;
             if ((rc = out_sparse(grad + off(cs), cs, false, t, sparse, o))) return rc;
-            if (early && sparse && (rc = mask(grad + off(cs), len(cs), 0))) return rc;  // (during the exchange)
+            if (mat == MASK_EARLY && sparse && (rc = mask(grad + off(cs), len(cs), 0))) return rc;
             clk.step(2);
             if ((rc = xchg(o, in))) return rc;
             clk.step(3);
-            if (sparse) {  // :177-190: keep the sent values; the owned residual stays (:178-184 commented out)
-                if (!early && (rc = mask(grad + off(cs), len(cs), 0))) return rc;
-            } else if (j == 0) {  // :191-193
-                ONO_HIP(dev_zero(res + off(own), len(own) * sizeof(float), s_));
-            }
+            // :177-190: a sparse push keeps only the sent values; the owned residual stays (:178-184 commented out)
+            if (mat == MASK_LATE && sparse && (rc = mask(grad + off(cs), len(cs), 0))) return rc;
+            if (!sparse && j == 0) ONO_HIP(dev_zero(res + off(own), len(own) * sizeof(float), s_));  // :191-193
+            const bool fuse = mat == MASK_FUSED && sparse;
             if (in.kind == KIND_DENSE) {
+                if (fuse && (rc = mask(grad + off(cs), len(cs), 0))) return rc;
                 ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(1, cr), len(cr), 1.0f, s_));
             } else {
                 const float *v = nullptr;
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
                 clk.step(4);
-                ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
+                if (fuse)  // :200 with the push's mask
+                    ONO_K(r_, s_, launch_hop_post(grad + off(cr), v, len(cr), 0, grad + off(cs), len(cs), r_->sp_t_dev,
+                                                  0, s_));
+                else
+                    ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
             }
             clk.step(5);
             clk.done();
