@@ -75,9 +75,13 @@ int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, s
                      hipStream_t s);
 hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s);
 // one launch: dst[0, k) += src (add) or = src (copy), and the mask of mg[0, mn) (sp_mask's zero_kept form)
-// with the threshold at t_dev — the SparseCapable hop's work after its exchange
+// with the threshold at t_dev — the SparseCapable hop's work after its exchange; keys != NULL: also the keys
+// |dst[idx[j]]| of the next push's sample (dst, L values), idx bucketed by 256-value blocks (offs: L / 256 + 1)
 hipError_t launch_hop_post(float *dst, const float *src, size_t k, int add, float *mg, size_t mn, const float *t_dev,
-                           int zero_kept, hipStream_t s);
+                           int zero_kept, hipStream_t s, size_t L = 0, const uint32_t *idx = nullptr,
+                           const uint32_t *offs = nullptr, uint32_t *keys = nullptr);
+// the threshold's select alone over m keys already in device memory (launch_hop_post gathered them)
+int sparse_select_keys_dev(float *t_dev, const uint32_t *keys, size_t m, float r, hipStream_t s);
 // Wait for everything enqueued on s so far by spinning on a host-mapped word
 // that a one-lane kernel sets to `epoch` (a stream synchronisation's wake-up
 // costs several microseconds more; used on the TCP ring's hops).

@@ -1707,11 +1707,23 @@ __global__ __launch_bounds__(kSB) void sp_mask(float *g, size_t n, float t, cons
 // their chunk (dst += src, AccOp's add, for the scatter; dst = src, a copy, for the gather) and the sparse
 // push's mask of the chunk it sent (sp_mask's two forms, the threshold where the push left it) — two
 // different chunks, so the two parts are independent workgroups: one launch instead of two on the hop's path.
+// keys != NULL: the next push's sample keys too, whose chunk is dst — its indices bucketed by workgroup (the
+// sampler's helper thread sorted them by idx / kSB: offs[b] .. offs[b + 1] fall in workgroup b's values), so
+// each workgroup reads back the values it has just written (no order between workgroups needed) and the
+// push's own gather launch goes (the select needs the sample's values, not their order).  The first part
+// then covers the whole chunk [0, L) (an add over the shorter length leaves [k, L) as they are).
 __global__ __launch_bounds__(kSB) void sp_hop_post(float *dst, const float *src, size_t k, int add, float *mg,
-                                                   size_t mn, const float *t_dev, int zero_kept, uint32_t b1) {
+                                                   size_t mn, const float *t_dev, int zero_kept, uint32_t b1,
+                                                   const uint32_t *idx, const uint32_t *offs, uint32_t *keys) {
     if (blockIdx.x < b1) {
         const size_t i = (size_t)blockIdx.x * kSB + threadIdx.x;
         if (i < k) dst[i] = add ? dst[i] + src[i] : src[i];
+        if (keys) {  // (uniform)
+            __syncthreads();
+            const uint32_t a = offs[blockIdx.x], e = offs[blockIdx.x + 1];
+            for (uint32_t j = a + threadIdx.x; j < e; j += kSB)  // (|x| as its bits: abs_key)
+                keys[j] = __builtin_bit_cast(uint32_t, dst[idx[j]]) & 0x7FFFFFFFu;
+        }
         return;
     }
     const size_t i = (size_t)(blockIdx.x - b1) * kSB + threadIdx.x;
@@ -4434,12 +4446,22 @@ int sparse_drop_tdev(uint8_t *buf, size_t cap, size_t *nbytes, const float *g, s
     return drop_launch(buf, cap, nbytes, nullptr, g, n, 0.0f, s, t_dev);
 }
 hipError_t launch_hop_post(float *dst, const float *src, size_t k, int add, float *mg, size_t mn, const float *t_dev,
-                           int zero_kept, hipStream_t s) {
-    const size_t b1 = (k + kSB - 1) / kSB, b2 = (mn + kSB - 1) / kSB;
+                           int zero_kept, hipStream_t s, size_t L, const uint32_t *idx, const uint32_t *offs,
+                           uint32_t *keys) {
+    const size_t b1 = ((keys ? L : k) + kSB - 1) / kSB, b2 = (mn + kSB - 1) / kSB;
     if (b1 + b2 == 0) return hipSuccess;
     hipLaunchKernelGGL(sp_hop_post, dim3((unsigned)(b1 + b2)), dim3(kSB), 0, s, dst, src, k, add, mg, mn, t_dev,
-                       zero_kept, (uint32_t)b1);
+                       zero_kept, (uint32_t)b1, idx, offs, keys);
     return hipGetLastError();
+}
+// the select alone over m keys already gathered (sp_hop_post gathered them)
+int sparse_select_keys_dev(float *t_dev, const uint32_t *keys, size_t m, float r, hipStream_t s) {
+    if (!(r > 0.0f && r <= 1.0f)) return set_error(ONO_E_ARG, "ratio %g outside (0, 1]", (double)r);
+    if (m == 0 || m > kSampleMax) return set_error(ONO_E_ARG, "sample of %zu values", m);
+    hipLaunchKernelGGL(sp_threshold, dim3(1), dim3(kThrT), 0, s, keys, (const float *)nullptr, (uint32_t)m,
+                       (uint32_t)threshold_rank(m, r), t_dev);
+    ONO_HIP(hipGetLastError());
+    return ONO_OK;
 }
 hipError_t launch_sparse_mask_tdev(float *g, size_t n, const float *t_dev, int zero_kept, hipStream_t s) {
     if (!n) return hipSuccess;

@@ -69,6 +69,11 @@ namespace {
 constexpr int kTcpPollMs = 100;                   // abort / peer-failure latency
 constexpr size_t kTcpInline = size_t(256) << 10;  // frames up to this go through one poll loop
 constexpr size_t kSampleMax = 16384;              // SAMPLE_SIZE (protocol.rs:13-19)
+// the next push's sample keys gathered by the hop's add / copy (launch_hop_post) for chunks up to this many
+// values: the sampler's helper thread buckets each draw by 256-value block (offsets: L / 256 + 1 words)
+constexpr size_t kFuseKeysMax = size_t(1) << 20;
+constexpr size_t kFuseBlock = 256;
+constexpr size_t kFuseOffs = kFuseKeysMax / kFuseBlock + 1;
 // a SparseGrad push whose worst-case stream fits this is encoded straight into a pinned frame (the drop's
 // own wait covers it: no D2H and no second wait); larger ones come down in pieces beside the send
 constexpr size_t kSparseZeroCopy = size_t(4) << 20;
@@ -465,6 +470,8 @@ struct SampleAhead {
         size_t len = 0, m = 0;
         uint32_t *buf = nullptr;   // pinned, kSampleMax indices
         uint32_t *dbuf = nullptr;  // the same draw in HBM
+        uint32_t *offs = nullptr;  // pinned, kFuseOffs: the draw bucketed by 256-value block (len <= kFuseKeysMax)
+        bool bucketed = false;
         bool ready = false, up = false;
         int rc = ONO_OK;
     };
@@ -485,9 +492,23 @@ struct SampleAhead {
     bool upload = false;        // ONO_THR_HBM=1: each draw also goes up to HBM for the gather
     std::thread th;
 
+    // The draw's indices reordered by 256-value block of the chunk (a counting sort: the threshold takes the
+    // k-th of the sampled values, whatever their order) and offs[b] = the first in block b, offs[nb] = m
+    static bool bucket_by_block(uint32_t *idx, size_t m, size_t L, uint32_t *offs, std::vector<uint32_t> &tmp) {
+        const size_t nb = (L + kFuseBlock - 1) / kFuseBlock;
+        if (nb + 1 > kFuseOffs) return false;
+        std::fill(offs, offs + nb + 1, 0u);
+        for (size_t j = 0; j < m; j++) offs[idx[j] / kFuseBlock + 1]++;
+        for (size_t b = 0; b < nb; b++) offs[b + 1] += offs[b];
+        tmp.assign(idx, idx + m);
+        std::vector<uint32_t> pos(offs, offs + nb);
+        for (size_t j = 0; j < m; j++) idx[pos[tmp[j] / kFuseBlock]++] = tmp[j];
+        return true;
+    }
     void loop() {
         std::unique_lock<std::mutex> lk(mu);
         (void)hipSetDevice(device);
+        std::vector<uint32_t> tmp;
         for (;;) {
             cv.wait(lk, [&] { return stop || (planned && count + (held >= 0) < kDepth); });
             if (stop) return;
@@ -516,6 +537,7 @@ struct SampleAhead {
             lk.unlock();
             const auto t0 = std::chrono::steady_clock::now();
             const int e = ono_sparse_sample_default(&st, L, b, kSampleMax);
+            const bool bk = e == ONO_OK && sl.offs && L <= kFuseKeysMax && bucket_by_block(b, kSampleMax, L, sl.offs, tmp);
             bool u = false;
             if (upload && e == ONO_OK && db && ust &&
                 hipMemcpyAsync(db, b, kSampleMax * sizeof(uint32_t), hipMemcpyHostToDevice, ust) == hipSuccess)
@@ -530,6 +552,7 @@ struct SampleAhead {
             sl.st_out = st;
             sl.rc = e;
             sl.up = u;
+            sl.bucketed = bk;
             sl.ready = true;
             plan_st = st;
             plan_pos++;
@@ -552,9 +575,11 @@ struct SampleAhead {
     // the next push's draw for (st, L, mm) if the queue made it: *idx / *didx point at the slot (valid until
     // the next take), *st advanced, *in_hbm when the HBM copy is there.  The slot the previous push read is
     // freed first (its drop, which read the sample, has returned).
-    bool take(uint64_t *st, size_t L, size_t mm, uint32_t **idx, uint32_t **didx, bool *in_hbm) {
+    bool take(uint64_t *st, size_t L, size_t mm, uint32_t **idx, uint32_t **didx, bool *in_hbm,
+              uint32_t **offs = nullptr) {
         std::unique_lock<std::mutex> lk(mu);
         *in_hbm = false;
+        if (offs) *offs = nullptr;
         if (held >= 0) {
             held = -1;
             cv.notify_all();
@@ -579,6 +604,7 @@ struct SampleAhead {
         *idx = sl.buf;
         *didx = sl.dbuf;
         *in_hbm = sl.up;
+        if (offs && sl.bucketed) *offs = sl.offs;
         *st = sl.st_out;
         cv.notify_all();
         return true;
@@ -595,6 +621,7 @@ void sample_ahead_free(SampleAhead *a) {
     if (a->th.joinable()) a->th.join();
     for (auto &sl : a->slot) {
         if (sl.buf) (void)hipHostFree(sl.buf);
+        if (sl.offs) (void)hipHostFree(sl.offs);
         if (sl.dbuf) (void)hipFree(sl.dbuf);
     }
     if (a->ust) (void)hipStreamDestroy(a->ust);
@@ -753,13 +780,17 @@ private:
         return settle(o);
     }
 
-    // calculate_threshold over the sample the sampler draws (all values up to SAMPLE_SIZE; above, the
-    // caller's sampler or the default one), into r->sp_t_dev in stream order: the drop and the masks read
-    // it there (no host round trip; the host never needs the value)
-    int threshold(const float *chunk, size_t L, size_t k_push) {
+    // The push's sample: the caller's sampler, or the default one's queue (or an inline draw when the queue
+    // does not hold this push's), or none when the chunk is its own sample (at most SAMPLE_SIZE values).
+    // *idx_dev: device-visible indices (NULL: none); *offs_dev: the draw's 256-value block offsets when the
+    // queue bucketed it (launch_hop_post can then gather the keys); *m: the sample's size.
+    int take_sample(size_t L, size_t k_push, uint32_t **idx_dev_out, const uint32_t **offs_dev_out, size_t *m_out) {
         const size_t m = std::min(L, kSampleMax);
+        *m_out = m;
+        *idx_dev_out = nullptr;
+        *offs_dev_out = nullptr;
         bool sampled = false, in_hbm = false;
-        uint32_t *idx_host = r_->sample_idx, *idx_hbm = nullptr;
+        uint32_t *idx_host = r_->sample_idx, *idx_hbm = nullptr, *offs_host = nullptr;
         if (r_->sampler) {
             if (r_->sampler(r_->sampler_ctx, L, r_->sample_idx, m) != 0)
                 return set_error(ONO_E_OTHER, "the sampler failed for a chunk of %zu values", L);
@@ -774,6 +805,8 @@ private:
                     ok = ok &&
                          hipHostMalloc((void **)&sl.buf, kSampleMax * sizeof(uint32_t), hipHostMallocDefault) ==
                              hipSuccess &&
+                         hipHostMalloc((void **)&sl.offs, kFuseOffs * sizeof(uint32_t), hipHostMallocDefault) ==
+                             hipSuccess &&
                          hipMalloc((void **)&sl.dbuf, kSampleMax * sizeof(uint32_t)) == hipSuccess;
                 if (!ok) {
                     sample_ahead_free(a);
@@ -784,7 +817,7 @@ private:
             }
             uint32_t *qi = nullptr, *qd = nullptr;
             const auto tk0 = std::chrono::steady_clock::now();
-            const bool took = r_->ahead->take(&r_->sample_state, L, m, &qi, &qd, &in_hbm);
+            const bool took = r_->ahead->take(&r_->sample_state, L, m, &qi, &qd, &in_hbm, &offs_host);
             if (trace_on()) {
                 g_hop_trace.take_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                                            std::chrono::steady_clock::now() - tk0).count();
@@ -797,6 +830,7 @@ private:
                 int rc = ono_sparse_sample_default(&r_->sample_state, L, r_->sample_idx, m);
                 if (rc) return rc;
                 in_hbm = false;
+                offs_host = nullptr;
                 r_->ahead->plan(r_->sample_state, push_len_, k_push + 1);
             }
             sampled = true;
@@ -805,14 +839,67 @@ private:
         if (sampled && r_->sampler)  // a caller's indices are checked; the default sampler's are in range
             for (size_t i = 0; i < m; i++)
                 if (r_->sample_idx[i] >= L) return set_error(ONO_E_ARG, "sample index %u out of %zu", r_->sample_idx[i], L);
-        // the gather kernel reads the pinned indices in place (an upload by the copy engine cost ~30 us
-        // of cross-engine hand-off per push); the buffer is not rewritten before this push's drop returns
-        // — unless the helper thread already put the draw in HBM, where the gather reads it
+        if (!sampled) return ONO_OK;
+        // the kernels read the pinned indices in place (an upload by the copy engine cost ~30 us of
+        // cross-engine hand-off per push); the buffer is not rewritten before this push's drop returns — unless
+        // the helper thread already put the draw in HBM, where the gather reads it
+        if (in_hbm && thr_hbm()) *idx_dev_out = idx_hbm;
+        else ONO_HIP(hipHostGetDevicePointer((void **)idx_dev_out, idx_host, 0));
+        if (offs_host) ONO_HIP(hipHostGetDevicePointer((void **)offs_dev_out, offs_host, 0));
+        return ONO_OK;
+    }
+    // calculate_threshold over the sample (take_sample), into r->sp_t_dev in stream order: the drop and the
+    // masks read it there (no host round trip; the host never needs the value).  A push whose sample the
+    // previous hop took early (pre_) uses it — and when that hop's add / copy gathered the keys, only the
+    // select is launched.
+    int threshold(const float *chunk, size_t L, size_t k_push) {
+        if (pre_.on && pre_.k_push == k_push && pre_.L == L) {
+            pre_.on = false;
+            if (clk_) clk_->step(6);
+            if (pre_.keys_ready) return sparse_select_keys_dev(r_->sp_t_dev, r_->sp_idx_dev, pre_.m, r_->sparse_r, s_);
+            return sparse_threshold_dev(r_->sp_t_dev, chunk, L, pre_.idx_dev, r_->sp_idx_dev, pre_.m, r_->sparse_r, s_);
+        }
+        pre_.on = false;
         uint32_t *idx_dev = nullptr;
-        if (sampled && in_hbm && thr_hbm()) idx_dev = idx_hbm;
-        else if (sampled) ONO_HIP(hipHostGetDevicePointer((void **)&idx_dev, idx_host, 0));
+        const uint32_t *offs_dev = nullptr;
+        size_t m = 0;
+        int rc = take_sample(L, k_push, &idx_dev, &offs_dev, &m);
+        if (rc) return rc;
         return sparse_threshold_dev(r_->sp_t_dev, chunk, L, idx_dev, r_->sp_idx_dev, m, r_->sparse_r, s_);
     }
+    // The hop after its exchange, when the received values went into the chunk the next push sends
+    // (cr): that push's sample taken now, and — when it comes bucketed — its keys gathered by the same launch
+    // as the add / copy and the push's mask (launch_hop_post; ONO_TCP_FUSE_KEYS=0 keeps the gather launch).
+    int hop_post(float *dst, const float *src, size_t k, int add, float *mg, size_t mn, int zero_kept, size_t L,
+                 bool next_push) {
+        static const bool fuse_keys = env_on("ONO_TCP_FUSE_KEYS");
+        uint32_t *keys = nullptr;
+        if (next_push && fuse_keys && !r_->sampler && L > kSampleMax && L <= kFuseKeysMax) {
+            PreSample p;
+            int rc = take_sample(L, push_k_, &p.idx_dev, &p.offs_dev, &p.m);
+            if (rc) return rc;
+            p.on = true;
+            p.k_push = push_k_;
+            p.L = L;
+            p.keys_ready = p.idx_dev && p.offs_dev;
+            if (p.keys_ready) keys = r_->sp_idx_dev;
+            pre_ = p;
+        }
+        if (!keys && !mn) {  // nothing fused: the add or the copy alone
+            if (add) ONO_K(r_, s_, launch_acc(dst, src, k, s_, true));
+            else ONO_HIP(dev_copy(dst, src, k * sizeof(float), s_));
+            return ONO_OK;
+        }
+        ONO_K(r_, s_, launch_hop_post(dst, src, k, add, mg, mn, r_->sp_t_dev, zero_kept, s_, L, pre_.idx_dev,
+                                      pre_.offs_dev, keys));
+        return ONO_OK;
+    }
+    struct PreSample {
+        bool on = false, keys_ready = false;
+        size_t k_push = 0, L = 0, m = 0;
+        uint32_t *idx_dev = nullptr;
+        const uint32_t *offs_dev = nullptr;
+    };
 
     Incoming in_for(int c, int b) const {
         Incoming in;
@@ -1063,10 +1150,15 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, false, &v, &k))) return rc;
                 clk.step(4);
-                if (fuse)  // :141-143 with the push's mask
-                    ONO_K(r_, s_, launch_hop_post(res + off(cr), v, k, 1, res + off(cs), len(cs), r_->sp_t_dev, 1, s_));
-                else
-                    ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));  // :141-143
+                // :141-143, with the push's mask; the next push sends chunk cr (the next scatter hop's, or the
+                // gather's first: the owned chunk, which the last scatter hop received)
+                if (mat == MASK_FUSED) {
+                    if ((rc = hop_post(res + off(cr), v, k, 1, res + off(cs), fuse ? len(cs) : 0, 1, len(cr),
+                                       st < n_ - 2 || mod(pos_ + 1) == cr)))
+                        return rc;
+                } else {
+                    ONO_K(r_, s_, launch_acc(res + off(cr), v, k, s_, true));
+                }
             }
             clk.step(5);
             clk.done();
@@ -1098,11 +1190,14 @@ private:
                 size_t k = 0;
                 if ((rc = incoming(in, cr, true, &v, &k))) return rc;
                 clk.step(4);
-                if (fuse)  // :200 with the push's mask
-                    ONO_K(r_, s_, launch_hop_post(grad + off(cr), v, len(cr), 0, grad + off(cs), len(cs), r_->sp_t_dev,
-                                                  0, s_));
-                else
+                // :200, with the push's mask; the next gather push (if any this round) sends chunk cr
+                if (mat == MASK_FUSED) {
+                    if ((rc = hop_post(grad + off(cr), v, len(cr), 0, grad + off(cs), fuse ? len(cs) : 0, 0, len(cr),
+                                       j + 1 <= n_ - 2)))
+                        return rc;
+                } else {
                     ONO_HIP(dev_copy(grad + off(cr), v, len(cr) * sizeof(float), s_));
+                }
             }
             clk.step(5);
             clk.done();
@@ -1134,6 +1229,7 @@ private:
     std::vector<size_t> push_len_;
     size_t push_k_ = 0;
     HopClock *clk_ = nullptr;  // (ONO_TCP_TRACE: the hop in progress)
+    PreSample pre_;            // the next push's sample, taken by the hop before it
 };
 
 }  // namespace
