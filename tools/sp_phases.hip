@@ -88,9 +88,13 @@ static void report(const char *name, const std::vector<uint4> &st, uint64_t base
 }
 
 int main(int argc, char **argv) {
-    const size_t mib = argc > 1 ? (size_t)atoi(argv[1]) : 64;
+    // argv[1]: MiB, or eN for N elements (e54693: a config-1 chunk); argv[3] = "pinned": the TCP ring's form —
+    // the blocking drop (its in-kernel completion) into a pinned coherent buffer, timed on the host per call
+    const bool by_elems = argc > 1 && argv[1][0] == 'e';
+    const size_t mib = argc > 1 && !by_elems ? (size_t)atoi(argv[1]) : 64;
     const int K = argc > 2 ? atoi(argv[2]) : 24, NG = 6;
-    const size_t n = mib << 18;
+    const size_t n = by_elems ? (size_t)strtoull(argv[1] + 1, nullptr, 10) : mib << 18;
+    const bool pinned = argc > 3 && !strcmp(argv[3], "pinned");
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<float *> gs(NG);
@@ -101,29 +105,45 @@ int main(int argc, char **argv) {
     const size_t cap = ono_sparse_max_bytes(n);
     uint8_t *buf;
     uint64_t *nbd;
-    CK(hipMalloc((void **)&buf, cap));
+    if (pinned) CK(hipHostMalloc((void **)&buf, cap + 64, hipHostMallocCoherent));
+    else CK(hipMalloc((void **)&buf, cap));
     CK(hipMalloc((void **)&nbd, 8));
     const float thr = 0.9f;
-    for (int i = 0; i < 2 * K; i++)
-        if (drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s)) return 1;
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    float ms = 0;
+    uint64_t wire = 0;
+    if (pinned) {  // blocking calls, as the TCP ring's push makes them
+        size_t nb = 0;
+        for (int i = 0; i < 2 * K; i++)
+            if (drop_launch(buf, cap, &nb, nullptr, gs[i % NG], n, thr, s)) return 1;
+        std::vector<double> us;
+        for (int i = 0; i < K; i++) {
+            const auto t0 = std::chrono::steady_clock::now();
+            if (drop_launch(buf, cap, &nb, nullptr, gs[i % NG], n, thr, s)) return 1;
+            us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        }
+        printf("# sp_phases: %zu values, %d blocking drops into pinned coherent memory: %.2f us per call (host, median), "
+               "wire %zu B\n", n, K, pct(us, .5), nb);
+        wire = nb;
+    } else {
+    for (int i = 0; i < 2 * K; i++)
+        if (drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s)) return 1;
     CK(hipStreamSynchronize(s));
     for (int i = 0; i < 8; i++) drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s);
     CK(hipEventRecord(a, s));
     for (int i = 0; i < K; i++) drop_launch(buf, cap, nullptr, nbd, gs[i % NG], n, thr, s);
     CK(hipEventRecord(b, s));
     CK(hipEventSynchronize(b));
-    float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
-    uint64_t wire = 0;
     CK(hipMemcpy(&wire, nbd, 8, hipMemcpyDeviceToHost));
     const double per = ms * 1e3 / K, bytes = 4.0 * n + (double)wire;
-    printf("# sp_phases: %zu MiB, %d stream-ordered drops over %d gradients, tiles/workgroup %zu: %.2f us per drop "
+    printf("# sp_phases: %zu values, %d stream-ordered drops over %d gradients, tiles/workgroup %zu: %.2f us per drop "
            "(events), wire %llu B, %.1f GB/s = %.3f of 8 TB/s\n",
-           mib, K, NG, kImageTpw, per, (unsigned long long)wire, bytes / per * 1e-3,
+           n, K, NG, kImageTpw, per, (unsigned long long)wire, bytes / per * 1e-3,
            bytes / per * 1e-3 / 8000.0);
+    }
     const size_t ntiles = (n + kTile - 1) / kTile, nwg = (ntiles + kImageTpw - 1) / kImageTpw;
     if (drop_fused() && ntiles <= drop_one_launch_tiles()) {  // the one-launch encoder: per tile {start, look-back done, end} + ticket and image times
         std::vector<uint4> d1(ntiles), d1b(ntiles);
