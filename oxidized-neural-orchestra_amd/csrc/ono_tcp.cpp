@@ -490,7 +490,7 @@ struct SampleAhead {
     int device = 0;
     hipStream_t ust = nullptr;  // (non-blocking: no implicit order with the ring's stream)
     bool upload = false;        // ONO_THR_HBM=1: each draw also goes up to HBM for the gather
-    std::thread th;
+    std::vector<std::thread> th;  // drawing threads (ONO_SAMPLER_THREADS, default 2)
 
     // The draw's indices reordered by 256-value block of the chunk (a counting sort: the threshold takes the
     // k-th of the sampled values, whatever their order) and offs[b] = the first in block b, offs[nb] = m
@@ -533,6 +533,12 @@ struct SampleAhead {
             count++;
             const uint64_t g = gen;
             uint64_t st = plan_st;
+            // a draw of m indices advances splitmix64 by exactly m steps of its constant (one per index,
+            // ono_sparse_sample_default), so the next draw's state is known before this one is made: the
+            // drawing threads make the queue's draws side by side
+            const uint64_t st_next = plan_st + (uint64_t)kSampleMax * 0x9E3779B97F4A7C15ULL;
+            plan_st = st_next;
+            plan_pos++;
             uint32_t *b = sl.buf, *db = sl.dbuf;
             lk.unlock();
             const auto t0 = std::chrono::steady_clock::now();
@@ -550,13 +556,11 @@ struct SampleAhead {
             lk.lock();
             if (g != gen) continue;  // re-planned meanwhile: the slot was dropped
             sl.st_out = st;
-            sl.rc = e;
+            sl.rc = e == ONO_OK && st != st_next ? ONO_E_OTHER : e;  // (never: the state's step is fixed)
             sl.up = u;
             sl.bucketed = bk;
             sl.ready = true;
-            plan_st = st;
-            plan_pos++;
-            if (e != ONO_OK) planned = false;
+            if (sl.rc != ONO_OK) planned = false;
             cv.notify_all();
         }
     }
@@ -618,7 +622,8 @@ void sample_ahead_free(SampleAhead *a) {
         a->stop = true;
         a->cv.notify_all();
     }
-    if (a->th.joinable()) a->th.join();
+    for (auto &t : a->th)
+        if (t.joinable()) t.join();
     for (auto &sl : a->slot) {
         if (sl.buf) (void)hipHostFree(sl.buf);
         if (sl.offs) (void)hipHostFree(sl.offs);
@@ -812,7 +817,12 @@ private:
                     sample_ahead_free(a);
                     return set_error(ONO_E_HIP, "sample buffers");
                 }
-                a->th = std::thread([a] { a->loop(); });
+                static const int nthreads = [] {
+                    const char *e = getenv("ONO_SAMPLER_THREADS");
+                    const int v = e ? atoi(e) : 2;
+                    return v < 1 ? 1 : v > SampleAhead::kDepth ? SampleAhead::kDepth : v;
+                }();
+                for (int t = 0; t < nthreads; t++) a->th.emplace_back([a] { a->loop(); });
                 r_->ahead = a;
             }
             uint32_t *qi = nullptr, *qd = nullptr;
