@@ -107,17 +107,26 @@ template <class T> hipError_t launch_fill(T *dst, T value, size_t n, hipStream_t
 hipError_t dev_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
 hipError_t dev_zero(void *dst, size_t bytes, hipStream_t s);
 
+// a launch that tells the host it is done: its last wave stores `sig` into the host-mapped word (word_dev is
+// its device address); arrive is a device counter that only grows, base the waves launched on it so far
+// (the launch adds its own)
+struct KernelDone {
+    uint64_t *word_dev = nullptr, *arrive = nullptr;
+    uint64_t base = 0;
+    uint32_t sig = 0;
+};
 // wire-templated hop kernels: W = uint16_t (f16 wire) or float (f32 wire)
 template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, hipStream_t s);
 template <class W> hipError_t launch_decode_scale(float *out, const W *in, size_t n, float divisor,
-                                                  hipStream_t s);
-template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s);
+                                                  hipStream_t s, KernelDone *done = nullptr);
+template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s,
+                                                 KernelDone *done = nullptr);
 template <class W> hipError_t launch_decode_add(float *acc, const W *in, size_t n, hipStream_t s);
 template <class W> hipError_t launch_add_encode_zero(W *out, float *acc, const W *in, size_t n,
-                                                     hipStream_t s);
+                                                     hipStream_t s, KernelDone *done = nullptr);
 // last scatter hop of the chunk owner: x = acc + in; grad = x / d; out = x; acc = 0
 template <class W> hipError_t launch_add_finish(float *grad, W *out, float *acc, const W *in,
-                                                size_t n, float divisor, hipStream_t s);
+                                                size_t n, float divisor, hipStream_t s, KernelDone *done = nullptr);
 
 // Chunk owner's reduction of the direct schedule (ono_kernels.hip DirectOp):
 // ins[k] = rank (c+k)'s slice of chunk c (owner's own residual last);

@@ -244,6 +244,25 @@ inline unsigned phase_of(const void *p, size_t esz) {
     return (unsigned)(((uintptr_t)p / esz) & 3u);
 }
 
+// An op whose kernel tells the host it is done (the TCP ring's dense hop, whose frame the op writes into
+// pinned memory): each wave waits for its stores, lane 0 releases at system scope (the frame can sit dirty in
+// its XCD's L2, as sp_drop1's) and counts the wave in; the last wave of the launch stores `sig` into the
+// host-mapped word the host spins on — instead of a stream synchronisation's wake-up after the kernel.
+template <class Op> struct Signaled : Op {
+    uint64_t *word, *arrive;
+    uint64_t target;
+    uint32_t sig;
+    __device__ __forceinline__ void finish() const {
+        if constexpr (HasFinish<Op>::value) Op::finish();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0) {
+            __atomic_thread_fence(__ATOMIC_RELEASE);
+            const uint64_t old = __hip_atomic_fetch_add(arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == target) __hip_atomic_store(word, (uint64_t)sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+};
+
 // Launch `op` over n elements.  phases: the 4-element phase of every operand.
 template <class Op, int B = block_of<Op>()>
 hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph, hipStream_t s) {
@@ -280,6 +299,38 @@ hipError_t launch_ew_arr(const Op &op, size_t n, const unsigned *phases, int nph
 template <class Op>
 hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> phases, hipStream_t s) {
     return launch_ew_arr(op, n, phases.begin(), (int)phases.size(), s);
+}
+// launch_ew whose launch signals its end (Signaled over the same grid as launch_ew_arr's; done->base counts
+// the waves launched so far on its counter); done NULL: launch_ew
+template <class Op>
+hipError_t launch_ew(const Op &op, size_t n, std::initializer_list<unsigned> phases, hipStream_t s, KernelDone *done) {
+    if (!done || n == 0) return launch_ew(op, n, phases, s);
+    constexpr int B0 = block_of<Op>();
+    const int B = (B0 != kBlock && !wide_blocks()) ? kBlock : B0;
+    const unsigned *ph = phases.begin();
+    const int nph = (int)phases.size();
+    bool same = true;
+    for (int i = 0; i < nph; i++) same &= (ph[i] == ph[0]);
+    const int bpc = blocks_per_cu();
+    const size_t cap = bpc > 0 ? (size_t)device_cus() * (size_t)bpc * kBlock / B : (size_t)0x7FFFFFFF;
+    size_t blocks;
+    if (!same) {
+        blocks = std::min((n + B - 1) / B, cap);
+    } else {
+        size_t head = (4 - ph[0]) & 3u;
+        if (head > n) head = n;
+        const size_t nvec = (n - head) / 4, work = nvec > 4 ? nvec : 4;
+        blocks = std::min(std::max<size_t>((work + B - 1) / B, 1), cap);
+    }
+    const uint64_t waves = (uint64_t)blocks * (uint64_t)(B / 64);
+    Signaled<Op> so;
+    static_cast<Op &>(so) = op;
+    so.word = done->word_dev;
+    so.arrive = done->arrive;
+    so.sig = done->sig;
+    so.target = done->base + waves - 1;
+    done->base += waves;
+    return launch_ew_arr(so, n, ph, nph, s);
 }
 
 // ============================================================== ops =======
@@ -948,44 +999,44 @@ template <class W> hipError_t launch_encode(W *out, const float *in, size_t n, h
     return launch_ew(EncodeOp<W>{out, in}, n, {wph(out), phase_of(in, 4)}, s);
 }
 template <class W>
-hipError_t launch_decode_scale(float *out, const W *in, size_t n, float divisor, hipStream_t s) {
+hipError_t launch_decode_scale(float *out, const W *in, size_t n, float divisor, hipStream_t s, KernelDone *done) {
     Scale sc = make_scale(divisor);
     auto ph = {phase_of(out, 4), wph(in)};
     switch (sc.mode) {
-    case SCALE_NONE: return launch_ew(DecodeScaleOp<W, SCALE_NONE>{out, in, sc.v}, n, ph, s);
-    case SCALE_RECIP: return launch_ew(DecodeScaleOp<W, SCALE_RECIP>{out, in, sc.v}, n, ph, s);
-    default: return launch_ew(DecodeScaleOp<W, SCALE_DIV>{out, in, sc.v}, n, ph, s);
+    case SCALE_NONE: return launch_ew(DecodeScaleOp<W, SCALE_NONE>{out, in, sc.v}, n, ph, s, done);
+    case SCALE_RECIP: return launch_ew(DecodeScaleOp<W, SCALE_RECIP>{out, in, sc.v}, n, ph, s, done);
+    default: return launch_ew(DecodeScaleOp<W, SCALE_DIV>{out, in, sc.v}, n, ph, s, done);
     }
 }
-template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s) {
-    return launch_ew(EncodeZeroOp<W>{out, chunk}, n, {wph(out), phase_of(chunk, 4)}, s);
+template <class W> hipError_t launch_encode_zero(W *out, float *chunk, size_t n, hipStream_t s, KernelDone *done) {
+    return launch_ew(EncodeZeroOp<W>{out, chunk}, n, {wph(out), phase_of(chunk, 4)}, s, done);
 }
 template <class W> hipError_t launch_decode_add(float *acc, const W *in, size_t n, hipStream_t s) {
     return launch_ew(DecodeAddOp<W>{acc, in}, n, {phase_of(acc, 4), wph(in)}, s);
 }
 template <class W>
-hipError_t launch_add_encode_zero(W *out, float *acc, const W *in, size_t n, hipStream_t s) {
-    return launch_ew(AddEncodeZeroOp<W>{out, acc, in}, n, {wph(out), phase_of(acc, 4), wph(in)}, s);
+hipError_t launch_add_encode_zero(W *out, float *acc, const W *in, size_t n, hipStream_t s, KernelDone *done) {
+    return launch_ew(AddEncodeZeroOp<W>{out, acc, in}, n, {wph(out), phase_of(acc, 4), wph(in)}, s, done);
 }
 template <class W>
 hipError_t launch_add_finish(float *grad, W *out, float *acc, const W *in, size_t n, float divisor,
-                             hipStream_t s) {
+                             hipStream_t s, KernelDone *done) {
     Scale sc = make_scale(divisor);
     auto ph = {phase_of(grad, 4), wph(out), phase_of(acc, 4), wph(in)};
     switch (sc.mode) {
-    case SCALE_NONE: return launch_ew(AddFinishOp<W, SCALE_NONE>{grad, out, acc, in, sc.v}, n, ph, s);
-    case SCALE_RECIP: return launch_ew(AddFinishOp<W, SCALE_RECIP>{grad, out, acc, in, sc.v}, n, ph, s);
-    default: return launch_ew(AddFinishOp<W, SCALE_DIV>{grad, out, acc, in, sc.v}, n, ph, s);
+    case SCALE_NONE: return launch_ew(AddFinishOp<W, SCALE_NONE>{grad, out, acc, in, sc.v}, n, ph, s, done);
+    case SCALE_RECIP: return launch_ew(AddFinishOp<W, SCALE_RECIP>{grad, out, acc, in, sc.v}, n, ph, s, done);
+    default: return launch_ew(AddFinishOp<W, SCALE_DIV>{grad, out, acc, in, sc.v}, n, ph, s, done);
     }
 }
 
 #define ONO_INST(W)                                                                            \
     template hipError_t launch_encode<W>(W *, const float *, size_t, hipStream_t);            \
-    template hipError_t launch_decode_scale<W>(float *, const W *, size_t, float, hipStream_t); \
-    template hipError_t launch_encode_zero<W>(W *, float *, size_t, hipStream_t);             \
+    template hipError_t launch_decode_scale<W>(float *, const W *, size_t, float, hipStream_t, KernelDone *); \
+    template hipError_t launch_encode_zero<W>(W *, float *, size_t, hipStream_t, KernelDone *);             \
     template hipError_t launch_decode_add<W>(float *, const W *, size_t, hipStream_t);        \
-    template hipError_t launch_add_encode_zero<W>(W *, float *, const W *, size_t, hipStream_t); \
-    template hipError_t launch_add_finish<W>(float *, W *, float *, const W *, size_t, float, hipStream_t);
+    template hipError_t launch_add_encode_zero<W>(W *, float *, const W *, size_t, hipStream_t, KernelDone *); \
+    template hipError_t launch_add_finish<W>(float *, W *, float *, const W *, size_t, float, hipStream_t, KernelDone *);
 ONO_INST(uint16_t)
 ONO_INST(float)
 #undef ONO_INST

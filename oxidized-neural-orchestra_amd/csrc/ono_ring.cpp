@@ -586,6 +586,7 @@ int ono_ring_destroy(ono_ring *r) {
         (void)hipFree(r->sp_rx_dev);
         if (r->sp_status) (void)hipHostFree(r->sp_status);
         if (r->tcp_word) (void)hipHostFree(r->tcp_word);
+        if (r->dn_arrive) (void)hipFree(r->dn_arrive);
         for (auto &reg : r->registered) (void)hipHostUnregister(reg.first);
         for (auto *v : {&r->ev_h, &r->ev_c, &r->ev_d})
             for (hipEvent_t ev : *v) (void)hipEventDestroy(ev);

@@ -147,6 +147,8 @@ struct ono_ring {
     uint64_t *sp_status = nullptr;    // host-mapped: the stream-ordered lift's status word
     uint64_t *tcp_word = nullptr, *tcp_word_dev = nullptr;  // host-mapped: the hops' stream_wait word
     uint32_t tcp_epoch = 0;
+    uint64_t *dn_arrive = nullptr;  // device: the dense hop kernels' wave count (KernelDone), never reset
+    uint64_t dn_base = 0;
     uint8_t *sp_dev = nullptr;
     size_t sp_dev_cap = 0;
     uint8_t *sp_tx = nullptr;  // pinned coherent: a small push's SparseGrad frame, encoded in place

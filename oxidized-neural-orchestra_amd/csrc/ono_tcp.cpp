@@ -722,7 +722,12 @@ private:
             uint8_t *f = reinterpret_cast<uint8_t *>(slot(b, c)) - 12;
             put_header(f, bytes, KIND_DENSE);
             o.frame = f;
-            ONO_HIP(hipStreamSynchronize(s_));
+            if (dn_sig_) {  // the stream's last kernel signals its end (dense_done)
+                ONO_HIP(stream_spin(s_, r_->tcp_word + 1, dn_sig_));
+                dn_sig_ = 0;
+            } else {
+                ONO_HIP(hipStreamSynchronize(s_));
+            }
             return ONO_OK;
         }
         int rc = grow_pinned(&r_->tx, &r_->tx_cap, 12 + bytes);
@@ -1069,6 +1074,34 @@ private:
         return ono_sparse_lift_dev(out, cap, got, r_->sp_rx_dev, nbytes, s_);
     }
 
+    // The dense hop's last kernel before a zero-copy frame leaves, launched to signal its own end
+    // (KernelDone): out_dense then spins on the ring's word 1 instead of synchronizing the stream, whose
+    // wake-up after the kernel was most of the ~15 us a config-1 frame took to be ready (r06_s42);
+    // ONO_TCP_DENSE_SIGNAL=0 keeps the synchronisation (measurement).  NULL when not zero-copy.
+    KernelDone *dense_done() {
+        static const bool on = env_on("ONO_TCP_DENSE_SIGNAL");
+        dn_sig_ = 0;
+        if (!on || !zc_) return nullptr;
+        if (!r_->dn_arrive) {
+            if (hipMalloc((void **)&r_->dn_arrive, 128) != hipSuccess) return nullptr;
+            if (hipMemsetAsync(r_->dn_arrive, 0, 128, s_) != hipSuccess) return nullptr;
+            r_->dn_base = 0;
+        }
+        if (++r_->tcp_epoch == 0) r_->tcp_epoch = 1;
+        *(volatile uint64_t *)(r_->tcp_word + 1) = 0;
+        kd_.word_dev = r_->tcp_word_dev + 1;
+        kd_.arrive = r_->dn_arrive;
+        kd_.base = r_->dn_base;
+        kd_.sig = r_->tcp_epoch;
+        return &kd_;
+    }
+    // after a launch given dense_done(): the counter's new base, and the tag out_dense waits for
+    void dense_launched(const KernelDone *d) {
+        if (!d) return;
+        r_->dn_base = d->base;
+        dn_sig_ = d->sig;
+    }
+
     // ---- Base serializer: the fused codec kernels (ono_ring.cpp's hop ring);
     // an incoming frame that is not a whole-chunk DenseGrad is taken apart first.
     int pull_dense(float *res, float *grad) {
@@ -1076,19 +1109,32 @@ private:
         if (rc) return rc;
         const float fn = (float)n_;
         // scatter: out slot 0, in slot 1
-        ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, pos_), res + off(pos_), len(pos_), s_));
+        {
+            KernelDone *d = dense_done();
+            ONO_K(r_, s_, launch_encode_zero<uint16_t>(slot(0, pos_), res + off(pos_), len(pos_), s_, d));
+            dense_launched(d);
+        }
         for (int st = 0; st < n_ - 1; st++) {
             const int cs = mod(pos_ - st), cr = mod(pos_ - st - 1);
             Outgoing o;
             Incoming in = in_for(cr, 1);
-            if ((rc = out_dense(0, cs, o)) || (rc = xchg(o, in))) return rc;
+            HopClock clk;  // (ONO_TCP_TRACE: "drop" = the frame ready, "add" = the hop's kernel launched)
+            if ((rc = out_dense(0, cs, o))) return rc;
+            clk.step(1);
+            if ((rc = xchg(o, in))) return rc;
+            clk.step(3);
             const bool last = st == n_ - 2;
             if (in.kind == KIND_DENSE) {
+                KernelDone *d = dense_done();
                 if (!last)
-                    ONO_K(r_, s_, launch_add_encode_zero<uint16_t>(slot(0, cr), res + off(cr), slot(1, cr), len(cr), s_));
+                    ONO_K(r_, s_, launch_add_encode_zero<uint16_t>(slot(0, cr), res + off(cr), slot(1, cr), len(cr), s_,
+                                                                   d));
                 else
                     ONO_K(r_, s_, launch_add_finish<uint16_t>(grad + off(cr), slot(0, cr), res + off(cr), slot(1, cr),
-                                                              len(cr), fn, s_));
+                                                              len(cr), fn, s_, d));
+                dense_launched(d);
+                clk.step(5);
+                clk.done();
                 continue;
             }
             const float *v = nullptr;
@@ -1108,9 +1154,17 @@ private:
             const int cs = mod(pos_ + 1 - j), cr = mod(pos_ - j);
             Outgoing o;
             Incoming in = in_for(cr, bi);
-            if ((rc = out_dense(bo, cs, o)) || (rc = xchg(o, in))) return rc;
+            HopClock clk;
+            if ((rc = out_dense(bo, cs, o))) return rc;
+            clk.step(1);
+            if ((rc = xchg(o, in))) return rc;
+            clk.step(3);
             if (in.kind == KIND_DENSE) {
-                ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(bi, cr), len(cr), fn, s_));
+                KernelDone *d = j + 1 < n_ - 1 ? dense_done() : nullptr;  // (a next gather frame waits for it)
+                ONO_K(r_, s_, launch_decode_scale<uint16_t>(grad + off(cr), slot(bi, cr), len(cr), fn, s_, d));
+                dense_launched(d);
+                clk.step(5);
+                clk.done();
             } else {  // :200 copies the received chunk; the next hop forwards its f16 image
                 const float *v = nullptr;
                 size_t k = 0;
@@ -1240,6 +1294,8 @@ private:
     size_t push_k_ = 0;
     HopClock *clk_ = nullptr;  // (ONO_TCP_TRACE: the hop in progress)
     PreSample pre_;            // the next push's sample, taken by the hop before it
+    KernelDone kd_;            // the dense hop's signalling launch (dense_done)
+    uint32_t dn_sig_ = 0;      // its tag, until out_dense has waited for it
 };
 
 }  // namespace
