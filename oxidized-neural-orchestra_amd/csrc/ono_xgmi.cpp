@@ -615,6 +615,13 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
             if (ln[q]) memset(res_host + st[q], 0, ln[q] * sizeof(float));
         return ONO_OK;
     };
+    // Round 6's recurrence of the host-fed wrong result put the wrong values before
+    // the owners' chains, at 128-B lines: a copy engine and the kernels meet at r->residual and r->grad,
+    // so a system-scope fence on every XCD sits at each meeting (ONO_XGMI_HOST_FENCE=0 drops them).
+    static const bool fence = [] {
+        const char *e = getenv("ONO_XGMI_HOST_FENCE");
+        return !(e && strcmp(e, "0") == 0);
+    }();
     auto rounds = [&]() -> int {
         for (size_t j = 0; j < S; j++) {
             piece(j);
@@ -624,10 +631,12 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
                                            hipMemcpyHostToDevice, r->hstream));
             ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
             ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
+            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream));
             int rc2 = r->wire == ONO_WIRE_F16
                           ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
                           : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
             if (rc2) return rc2;
+            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream));
             ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
             ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
             for (int q = 0; q < n; q++)

@@ -184,6 +184,21 @@ __global__ __launch_bounds__(64) void xbump_kernel(uint64_t *counter) {
     peer_stores_done();
 }
 
+// Host-fed rounds: a system-scope fence (L2 write-back + invalidate) on every
+// XCD between the copy engine's writes and the round's first read of them,
+// and between the round's last writes and the copy engine's read.  The
+// workgroups are dealt round-robin over the XCDs, so 256 of them reach each
+// XCD's L2 several times over.
+constexpr unsigned kXFenceBlocks = 256;
+__global__ __launch_bounds__(64) void xfence_kernel() {
+    if (threadIdx.x == 0) {  // the compiler leaves the write-back's wait out of a bare fence; the waits are explicit
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope) L2 write-back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // L2 invalidate
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 template <class Op>
 hipError_t launch_segs(const Op &op, XSegs g, hipStream_t s) {
     uint32_t tiles = 0;
@@ -251,6 +266,11 @@ hipError_t launch_xgmi_signal(const XSignal &sig, hipStream_t s) {
 
 hipError_t launch_xgmi_bump(uint64_t *counter, hipStream_t s) {
     hipLaunchKernelGGL(xbump_kernel, dim3(1), dim3(64), 0, s, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_xgmi_fence_all(hipStream_t s) {
+    hipLaunchKernelGGL(xfence_kernel, dim3(kXFenceBlocks), dim3(64), 0, s);
     return hipGetLastError();
 }
 

@@ -229,10 +229,12 @@ def run_timeout(rank: int, n: int, how: str = "env") -> str | None:
         ring.close()
 
 
-def describe_bad(bad, got, want, ins, prev, length, n) -> str:
+def describe_bad(bad, got, want, ins, prev, length, n, wire="f16", prev_ins=None) -> str:
     """What a wrong host-fed result looks like, for the next diagnosis: the runs of
     differing elements, the 1 MiB sub-rounds and the n owner chunks they fall in, and whether the wrong
-    values are the previous cycle's result, one rank's unreduced input, or zeros."""
+    values are the previous cycle's result, one rank's unreduced input, zeros, the round without one
+    rank's input (a push or chain read that saw zeroed lines) or with one rank's previous-cycle input
+    (one that saw stale lines)."""
     runs = np.split(bad, np.flatnonzero(np.diff(bad) != 1) + 1)
     spans = ", ".join(f"[{r[0]}, {r[-1] + 1})" for r in runs[:6]) + (" ..." if len(runs) > 6 else "")
     sub = sorted(set((bad // (1 << 18)).tolist()))[:8]
@@ -247,7 +249,19 @@ def describe_bad(bad, got, want, ins, prev, length, n) -> str:
             kinds.append(f"= rank {r}'s input")
     if not np.any(g):
         kinds.append("all zero")
-    return f"{len(runs)} runs {spans}; sub-rounds {sub}; owner chunks {owners}; wrong values {kinds or ['other']}"
+    for r in range(n):  # every rank of a ring ends with the same result: e[0] stands for all
+        variants = [("without", np.zeros(length, np.float32))]
+        if prev_ins is not None:
+            variants.append(("with the previous cycle's", np.asarray(prev_ins[r], np.float32)))
+        for label, x in variants:
+            alt = [np.asarray(v, np.float32) if q != r else x for q, v in enumerate(ins)]
+            e, _ = O.ring_pull_grads(alt, wire)
+            hit = int(np.count_nonzero(O.same_or_both_nan(g, e[0][bad])))
+            if hit:
+                kinds.append(f"{hit}/{bad.size} = the round {label} rank {r}'s input")
+    lines = sorted(set((bad * 4 // 128 % 64).tolist()))[:8]  # 128-B line of the f32 bucket within 8 KiB
+    return f"{len(runs)} runs {spans}; sub-rounds {sub}; owner chunks {owners}; lines in 8 KiB {lines}; " \
+           f"wrong values {kinds or ['other']}"
 
 
 # IPC handles this process has exported, across every case (a repeat of one from an earlier case is just
@@ -268,6 +282,7 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
     release = case.get("release", False)  # the pool released between cycles: fresh exports and imports
     freed = 0
     prev = None  # the previous cycle's expected result (stale data from an earlier ring would equal it)
+    prev_ins = None  # and its inputs
     for cyc in range(cycles):
         blobs = {}
 
@@ -290,8 +305,9 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
             bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
             if bad.size:
                 return f"cycle {cyc}: {bad.size}/{length} differ, first at {bad[0]} (handle repeats {HANDLE_REPEATS}); " \
-                       + describe_bad(bad, grad_h, expect[rank], ins, prev, length, n)
-            prev = expect[rank]
+                       + describe_bad(bad, grad_h, expect[rank], ins, prev, length, n, case.get("wire", "f16"),
+                                      prev_ins)
+            prev, prev_ins = expect[rank], ins
             if bits(res_h).any():
                 return f"cycle {cyc}: host residual not zeroed"
             if release:  # refused while this process's ring is alive
