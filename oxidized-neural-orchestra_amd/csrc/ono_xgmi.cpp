@@ -618,11 +618,12 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     // Round 6's recurrence of the host-fed wrong result put the wrong values before
     // the owners' chains, at 128-B lines: a copy engine and the kernels meet at r->residual and r->grad,
     // so a system-scope fence on every XCD sits at each meeting (ONO_XGMI_HOST_FENCE=0 drops them).
-    static const bool fence = [] {
-        const char *e = getenv("ONO_XGMI_HOST_FENCE");
-        return !(e && strcmp(e, "0") == 0);
-    }();
+    const char *fe = getenv("ONO_XGMI_HOST_FENCE");  // read per call (an A/B within one process)
+    const bool fence = !(fe && strcmp(fe, "0") == 0);
     auto rounds = [&]() -> int {
+        // first: dirty lines an earlier kernel left on these addresses (this ring's or a freed buffer's)
+        // reach HBM before the copy engine writes, so no later eviction lands on top of the new data
+        if (fence) ONO_HIP(launch_xgmi_fence_all(r->hstream));
         for (size_t j = 0; j < S; j++) {
             piece(j);
             for (int q = 0; q < n; q++)

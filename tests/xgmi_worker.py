@@ -338,6 +338,39 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
     return None
 
 
+def run_host_fence(rank: int, n: int, case: dict) -> str | None:
+    """Host-fed rounds with and without the copy-engine fences (ONO_XGMI_HOST_FENCE, read per call),
+    alternating, each bit-exact; rank 0 writes the wall times of both to gpurun_out/ when it exists
+    (the fences' cost)."""
+    length, wire, rounds = case.get("length", 1 << 22), case.get("wire", "f32"), case.get("rounds", 6)
+    ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
+    times = {"1": [], "0": []}
+    try:
+        for i in range(2 * rounds):
+            mode = "1" if i % 2 == 0 else "0"
+            os.environ["ONO_XGMI_HOST_FENCE"] = mode
+            ins = [O.synth(length, SEED + 17 * i, r) for r in range(n)]
+            expect, _ = O.ring_pull_grads(ins, wire)
+            res_h = np.ascontiguousarray(ins[rank]).copy()
+            grad_h = np.full(length, 7.0, np.float32)
+            dist.barrier()
+            t0 = time.perf_counter()
+            ring.pull_grads_host(res_h, grad_h)
+            times[mode].append((time.perf_counter() - t0) * 1e3)
+            bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
+            if bad.size:
+                return f"round {i} (fence {mode}): {bad.size}/{length} differ, first at {bad[0]}"
+    finally:
+        os.environ.pop("ONO_XGMI_HOST_FENCE", None)
+        ring.close()
+    out = os.path.join(ROOT, "gpurun_out")
+    if rank == 0 and os.path.isdir(out):
+        med = {k: float(np.median(v[1:])) for k, v in times.items()}  # the first of each: warm-up
+        with open(os.path.join(out, f"xgmi_host_fence_n{n}.json"), "w") as f:
+            json.dump({"n": n, "length": length, "wire": wire, "ms": times, "median_ms_after_first": med}, f)
+    return None
+
+
 def main() -> int:
     rank, n, rdv = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     cases = json.loads(sys.argv[4])
@@ -351,7 +384,7 @@ def main() -> int:
             kind = case.get("kind", "ring")
             msg = run_timeout(rank, n, case.get("how", "env")) if kind == "timeout" else run_ps(rank, n, case) if kind == "ps" else \
                 run_timing(rank, n) if kind == "timing" else run_recreate(rank, n, case) if kind == "recreate" else \
-                run_case(rank, n, case)
+                run_host_fence(rank, n, case) if kind == "host_fence" else run_case(rank, n, case)
         except Exception as e:  # reported, the parent asserts
             msg = f"{type(e).__name__}: {e}"
         results.append({"case": case, "ok": msg is None, "msg": msg or ""})
