@@ -169,8 +169,9 @@ struct XBarrier {
 hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s);
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s);
 hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s);
-// A system-scope fence on every XCD (host-fed rounds, around the copies).
-hipError_t launch_xgmi_fence_all(hipStream_t s);
+// A system-scope fence on every XCD (host-fed rounds, around the copies): L2
+// write-back, then (acquire) L2 invalidate.
+hipError_t launch_xgmi_fence_all(hipStream_t s, bool acquire);
 // Connect verification (ono_xgmi.cpp): stamp the ring id at the start of every
 // page of a region (page 0: at id_off), and read them back through an import
 // (bad[p] = 1 where page p shows anything else).

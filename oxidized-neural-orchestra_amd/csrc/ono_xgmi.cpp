@@ -617,13 +617,16 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     };
     // Round 6's recurrence of the host-fed wrong result put the wrong values before
     // the owners' chains, at 128-B lines: a copy engine and the kernels meet at r->residual and r->grad,
-    // so a system-scope fence on every XCD sits at each meeting (ONO_XGMI_HOST_FENCE=0 drops them).
-    const char *fe = getenv("ONO_XGMI_HOST_FENCE");  // read per call (an A/B within one process)
-    const bool fence = !(fe && strcmp(fe, "0") == 0);
+    // so a system-scope fence on every XCD sits at each meeting: an L2 write-back where the copy engine
+    // reads or is about to write, write-back + invalidate where the kernels read what it wrote.
+    // ONO_XGMI_HOST_FENCE (read per call, an A/B within one process): 0 none, 1 write-back + invalidate
+    // at all three, otherwise (default) that lean form.
+    const char *fe = getenv("ONO_XGMI_HOST_FENCE");
+    const bool fence = !(fe && strcmp(fe, "0") == 0), full = fe && strcmp(fe, "1") == 0;
     auto rounds = [&]() -> int {
         // first: dirty lines an earlier kernel left on these addresses (this ring's or a freed buffer's)
         // reach HBM before the copy engine writes, so no later eviction lands on top of the new data
-        if (fence) ONO_HIP(launch_xgmi_fence_all(r->hstream));
+        if (fence) ONO_HIP(launch_xgmi_fence_all(r->hstream, full));
         for (size_t j = 0; j < S; j++) {
             piece(j);
             for (int q = 0; q < n; q++)
@@ -632,12 +635,12 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
                                            hipMemcpyHostToDevice, r->hstream));
             ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
             ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
-            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream));
+            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream, true));
             int rc2 = r->wire == ONO_WIRE_F16
                           ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
                           : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
             if (rc2) return rc2;
-            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream));
+            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream, full));
             ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
             ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
             for (int q = 0; q < n; q++)

@@ -190,12 +190,14 @@ __global__ __launch_bounds__(64) void xbump_kernel(uint64_t *counter) {
 // workgroups are dealt round-robin over the XCDs, so 256 of them reach each
 // XCD's L2 several times over.
 constexpr unsigned kXFenceBlocks = 256;
-__global__ __launch_bounds__(64) void xfence_kernel() {
+template <bool ACQUIRE> __global__ __launch_bounds__(64) void xfence_kernel() {
     if (threadIdx.x == 0) {  // the compiler leaves the write-back's wait out of a bare fence; the waits are explicit
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope) L2 write-back
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // L2 invalidate
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (ACQUIRE) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // L2 invalidate
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
 }
 
@@ -269,8 +271,9 @@ hipError_t launch_xgmi_bump(uint64_t *counter, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_xgmi_fence_all(hipStream_t s) {
-    hipLaunchKernelGGL(xfence_kernel, dim3(kXFenceBlocks), dim3(64), 0, s);
+hipError_t launch_xgmi_fence_all(hipStream_t s, bool acquire) {
+    if (acquire) hipLaunchKernelGGL(xfence_kernel<true>, dim3(kXFenceBlocks), dim3(64), 0, s);
+    else hipLaunchKernelGGL(xfence_kernel<false>, dim3(kXFenceBlocks), dim3(64), 0, s);
     return hipGetLastError();
 }
 

@@ -142,9 +142,9 @@ def test_xgmi_pool_release_then_fresh_rings(n):
 
 @pytest.mark.parametrize("n", [2, 3])
 def test_xgmi_host_fed_with_and_without_copy_fences(n):
-    """The host-fed round's copy-engine fences change no value: rounds alternate
-    ONO_XGMI_HOST_FENCE=1 / 0 in the same processes, every one bit-exact; rank 0 records the wall time
-    of both under gpurun_out/ (the fences' cost)."""
+    """The host-fed round's copy-engine fences change no value: rounds take
+    ONO_XGMI_HOST_FENCE=2 (lean, the default) / 1 (full) / 0 (none) in turn in the same processes, every
+    one bit-exact; rank 0 records the wall time of each under gpurun_out/ (the fences' cost)."""
     check(run_ranks(n, [{"kind": "host_fence", "length": (1 << 22) + 3, "wire": "f32", "rounds": 5}],
                     ONO_HOST_CHUNK_MIB="4"))
 

@@ -339,15 +339,16 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
 
 
 def run_host_fence(rank: int, n: int, case: dict) -> str | None:
-    """Host-fed rounds with and without the copy-engine fences (ONO_XGMI_HOST_FENCE, read per call),
-    alternating, each bit-exact; rank 0 writes the wall times of both to gpurun_out/ when it exists
-    (the fences' cost)."""
+    """Host-fed rounds under each copy-engine fence mode (ONO_XGMI_HOST_FENCE, read per call: "2" the
+    default lean form, "1" the full form, "0" none), in turn, each bit-exact; rank 0 writes the wall
+    times of every mode to gpurun_out/ when it exists (the fences' cost)."""
     length, wire, rounds = case.get("length", 1 << 22), case.get("wire", "f32"), case.get("rounds", 6)
     ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
-    times = {"1": [], "0": []}
+    modes = case.get("modes", ["2", "1", "0"])
+    times = {m: [] for m in modes}
     try:
-        for i in range(2 * rounds):
-            mode = "1" if i % 2 == 0 else "0"
+        for i in range(len(modes) * rounds):
+            mode = modes[i % len(modes)]
             os.environ["ONO_XGMI_HOST_FENCE"] = mode
             ins = [O.synth(length, SEED + 17 * i, r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, wire)
