@@ -1169,6 +1169,8 @@ def start_backstop(budget: Budget, rank: int) -> threading.Timer:
                 d["cut"] = BOX.running
         if rank == 0:
             print(BOX.dump(), flush=True)
+        # exit 0 on purpose: the backstop only fires after the headline is in the line, and
+        # the driver reads the line by the exit status; the cut leg is named in the line's deadline.cut
         os._exit(0)
 
     t = threading.Timer(max(0.0, budget.left() + GRACE_S), fire)
