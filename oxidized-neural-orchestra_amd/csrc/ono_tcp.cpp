@@ -481,6 +481,7 @@ struct SampleAhead {
     Slot slot[kDepth];
     int head = 0, tail = 0, count = 0;  // slots [head, head + count) drawn or being drawn, in push order
     int held = -1;                      // the slot the ring's current push reads (freed at its next take)
+    int drawing = 0;                    // draws in flight (their threads write their slots' buffers unlocked)
     uint64_t gen = 0;                   // a re-plan discards a draw in flight
     // the plan: the next draw's state, and the cyclic push lengths from plan_pos on
     bool planned = false;
@@ -539,6 +540,7 @@ struct SampleAhead {
             const uint64_t st_next = plan_st + (uint64_t)kSampleMax * 0x9E3779B97F4A7C15ULL;
             plan_st = st_next;
             plan_pos++;
+            drawing++;
             uint32_t *b = sl.buf, *db = sl.dbuf;
             lk.unlock();
             const auto t0 = std::chrono::steady_clock::now();
@@ -554,7 +556,11 @@ struct SampleAhead {
                 g_hop_trace.draws++;
             }
             lk.lock();
-            if (g != gen) continue;  // re-planned meanwhile: the slot was dropped
+            drawing--;
+            if (g != gen) {  // re-planned meanwhile: the slot was dropped (plan() waits for this draw to end)
+                cv.notify_all();
+                continue;
+            }
             sl.st_out = st;
             sl.rc = e == ONO_OK && st != st_next ? ONO_E_OTHER : e;  // (never: the state's step is fixed)
             sl.up = u;
@@ -566,8 +572,12 @@ struct SampleAhead {
     }
     // the queue restarts at state st with the ring's cyclic push lengths from position pos
     void plan(uint64_t st, const std::vector<size_t> &lens, size_t pos) {
-        std::lock_guard<std::mutex> lk(mu);
-        gen++;
+        std::unique_lock<std::mutex> lk(mu);
+        // a draw still in flight writes its slot's buffers: with two drawing threads the re-planned queue could
+        // hand that slot to the other one (or to a take) before it ends, so the re-plan waits for it
+        gen++;  // (a draw ending meanwhile drops its result)
+        planned = false;  // (and no new draw starts)
+        cv.wait(lk, [&] { return drawing == 0; });
         head = tail = (held >= 0 ? (held + 1) % kDepth : 0);
         count = 0;
         plan_st = st;

@@ -70,9 +70,10 @@ class GpuWorker(threading.Thread):
     pull_grads (device or host-fed form); keeps the last round's results."""
 
     def __init__(self, rank, n, length, inputs, prev=None, nxt=None, connect=None, listener=None,
-                 host_fed=False, sparse=None, sampler=None):
+                 host_fed=False, sparse=None, sampler=None, reseed=None):
         super().__init__(daemon=True)
         self.sparse, self.sampler = sparse, sampler  # (ratio, seed) of SparseCapable; a sampler callback
+        self.reseed = reseed or {}  # round -> (ratio, seed): ono_ring_set_sparse again before that round
         self.rank, self.n, self.length, self.inputs = rank, n, length, inputs
         self.prev, self.nxt, self.connect, self.listener = prev, nxt, connect, listener
         self.host_fed = host_fed
@@ -97,7 +98,9 @@ class GpuWorker(threading.Thread):
                 if self.sampler is not None:
                     self.ring.set_sampler(self.sampler)
                 self.ready.set()
-                for x in self.inputs:
+                for k, x in enumerate(self.inputs):
+                    if k in self.reseed:
+                        self.ring.set_sparse(*self.reseed[k])
                     if self.host_fed:
                         res = np.array(x, dtype=np.float32, copy=True)
                         grad = np.full_like(res, 7.0)
@@ -504,6 +507,38 @@ def test_tcp_ring_sparse_refused_lifts(n, length, ratios, refuse):
         assert_bitexact(ws[r].grad, eg[r], f"grad rank {r}")
         assert_bitexact(ws[r].residual, er[r], f"residual rank {r}")
     assert left < refuse and (refuse > 3 or left == 0), left  # (each ring round lifts at least 2 frames)
+
+
+@pytest.mark.parametrize("n,length", [(2, 109386), (3, 60000)])
+def test_tcp_ring_sparse_reseeded_between_rounds(n, length):
+    """ono_ring_set_sparse between rounds restarts the default sampler's stream (and may change the ratio)
+    while the sampler's helper threads are drawing the coming pushes ahead: the queue is re-planned, a draw
+    still in flight is dropped, and no slot a stale draw is still writing is handed out again.  Five rounds,
+    re-seeded before rounds 1, 2 (back to back) and 4 (new ratios): bit-exact with the restatement."""
+    rounds = 5
+    ratios0 = [0.1, 0.1, 0.05][:n]
+    plan = {1: ([0.1, 0.1, 0.05][:n], [500 + r for r in range(n)]),
+            2: ([0.1, 0.1, 0.05][:n], [600 + r for r in range(n)]),
+            4: ([0.2, 0.05, 0.3][:n], [700 + r for r in range(n)])}
+    seeds = [131 + r for r in range(n)]
+    ins = inputs_for(n, length, rounds, SEED + 47)
+    links, pairs = socketpair_links(n)
+    ws = [GpuWorker(r, n, length, [ins[k][r] for k in range(rounds)], *links[r], sparse=(ratios0[r], seeds[r]),
+                    reseed={k: (rs[r], sd[r]) for k, (rs, sd) in plan.items()}) for r in range(n)]
+    try:
+        for w in ws:
+            w.start()
+        join_all(ws)
+    finally:
+        teardown(pairs, ws)
+    st, ratios = list(seeds), list(ratios0)
+    for k, x in enumerate(ins):
+        if k in plan:
+            ratios, st = list(plan[k][0]), list(plan[k][1])
+        g, res, st = O.ring_pull_grads_sparse(x, ratios, st)
+    for r in range(n):
+        assert_bitexact(ws[r].grad, g[r], f"grad rank {r}")
+        assert_bitexact(ws[r].residual, res[r], f"residual rank {r}")
 
 
 def test_tcp_ring_sparse_host_fed_and_sampler_callback():
