@@ -222,6 +222,12 @@ static long usable_cpus() {
     return std::max(1L, n);
 }
 
+int host_threads();
+void host_copy(ono_ring *r, void *dst, const void *src, size_t bytes) {
+    if (!r->pool) r->pool.reset(new HostPool(host_threads(), r->device));
+    r->pool->copy(dst, src, bytes);
+}
+
 int host_threads() {
     const char *e = getenv("ONO_HOST_THREADS");
     if (e && atol(e) > 0) return (int)std::min(atol(e), usable_cpus());
@@ -783,7 +789,7 @@ int ono_ring_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, siz
     const size_t CH = host_chunk_elems();
 
     if (r->n > 1 && resolved_algo(r) == ONO_ALGO_XGMI)  // sub-round pipeline (ono_xgmi.cpp)
-        return xgmi_pull_grads_host(r, res_host, grad_host, CH);
+        return xgmi_pull_grads_host(r, res_host, grad_host, CH, reg);
     const int algo = resolved_algo(r);
     if (r->n > 1 && (algo == ONO_ALGO_HOPS || algo == ONO_ALGO_DIRECT) && r->fd_next < 0 && r->sparse_r <= 0.0f)
         return exact_pull_grads_host(r, algo, res_host, grad_host);  // sub-round pipeline

@@ -203,7 +203,10 @@ int tcp_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s);
 
 // xGMI peer-access schedule (ono_xgmi.cpp)
 int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s);
-int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems);
+// reg: res_host and grad_host are registered with the ring (ono_ring_register_host)
+int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems, bool reg);
+// the ring's host copy pool (ono_ring.cpp; made on first use): dst = src, bytes split over its threads
+void host_copy(ono_ring *r, void *dst, const void *src, size_t bytes);
 int xgmi_ps_step(ono_ring *r, const float *grad, float *params, size_t N, size_t C, float *gshard, float *wshard,
                  const OptLaunch &opt, float *v, float *s_, hipStream_t s);
 void xgmi_abort(ono_ring *r);

@@ -110,6 +110,9 @@ struct XgmiState {
     uint64_t timeout_ticks = 0;
     double timeout_s = 0;
     std::vector<hipEvent_t> ev;       // host-fed sub-round pipeline: H2D / round / D2H per sub-round
+    float *hin = nullptr;             // host-fed input staging (pinned, mapped): two slots of n pieces
+    float *hin_dev = nullptr;         // the same as the kernels address it
+    size_t hin_elems = 0;
     uint64_t id = 0;                  // this ring's id (stamped into the region, sent in the handle blob)
     size_t bytes = 0;                 // the layout's size (every rank of the ring computes the same)
     size_t alloc = 0;                 // the pooled region's size (>= bytes)
@@ -588,7 +591,7 @@ int xgmi_pull_grads(ono_ring *r, float *res, float *grad, hipStream_t s) {
 // does.  Every element still goes through the same chain on the same owner,
 // so the result is the whole-bucket round's bit for bit.  The host residual
 // is zeroed once its sub-round has reached HBM.
-int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems) {
+int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t sub_elems, bool reg) {
     int rc = ensure_connected(r, r->cstream);
     if (rc) return rc;
     XgmiState *x = r->xgmi;
@@ -615,32 +618,70 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
             if (ln[q]) memset(res_host + st[q], 0, ln[q] * sizeof(float));
         return ONO_OK;
     };
-    // Round 6's recurrence of the host-fed wrong result put the wrong values before
-    // the owners' chains, at 128-B lines: a copy engine and the kernels meet at r->residual and r->grad,
-    // so a system-scope fence on every XCD sits at each meeting: an L2 write-back where the copy engine
-    // reads or is about to write, write-back + invalidate where the kernels read what it wrote.
-    // ONO_XGMI_HOST_FENCE (read per call, an A/B within one process): 0 none, 1 write-back + invalidate
-    // at all three, otherwise (default) that lean form.
-    const char *fe = getenv("ONO_XGMI_HOST_FENCE");
-    const bool fence = !(fe && strcmp(fe, "0") == 0), full = fe && strcmp(fe, "1") == 0;
-    auto rounds = [&]() -> int {
-        // first: dirty lines an earlier kernel left on these addresses (this ring's or a freed buffer's)
-        // reach HBM before the copy engine writes, so no later eviction lands on top of the new data
-        if (fence) ONO_HIP(launch_xgmi_fence_all(r->hstream, full));
-        for (size_t j = 0; j < S; j++) {
-            piece(j);
+    // How the bucket reaches HBM.  Round 6's records of the host-fed wrong result put
+    // it before the owners' chains: one rank's residual read back as zeros at scattered 128-B lines, the data
+    // the copy engine had written there not seen by the kernels.  The residual is therefore written by a
+    // kernel, as every other buffer the round reads is: the caller's bucket read in place when it is
+    // registered, else copied by the host pool into a pinned, mapped staging slot (two slots of n pieces,
+    // each piece at the residual's 4-element phase) that a copy kernel on the round's stream reads.
+    // ONO_XGMI_HOST_IN=dma keeps the copy engine's H2D (with the fences below, round 6's first attempt).
+    // Before each D2H a system-scope L2 write-back on every XCD (ONO_XGMI_HOST_FENCE=0 drops it; =1 adds the
+    // write-back + invalidate fences around the copy-engine input as well).
+    const char *ie = getenv("ONO_XGMI_HOST_IN"), *fe = getenv("ONO_XGMI_HOST_FENCE");
+    const bool dma_in = ie && strcmp(ie, "dma") == 0;
+    const bool fence = !(fe && strcmp(fe, "0") == 0), in_fences = dma_in && fence;
+    const float *res_dev = nullptr;  // the caller's registered bucket, as the device addresses it
+    if (!dma_in && reg) {
+        void *p = nullptr;
+        if (hipHostGetDevicePointer(&p, res_host, 0) == hipSuccess) res_dev = static_cast<const float *>(p);
+    }
+    const size_t pad = sub + 4;  // a staging piece: sub elements at any 4-element phase
+    if (!dma_in && !res_dev && x->hin_elems < 2 * (size_t)n * pad) {
+        if (x->hin) ONO_HIP(hipHostFree(x->hin));
+        x->hin = x->hin_dev = nullptr;
+        x->hin_elems = 0;
+        ONO_HIP(hipHostMalloc((void **)&x->hin, 2 * (size_t)n * pad * sizeof(float), hipHostMallocMapped));
+        ONO_HIP(hipHostGetDevicePointer((void **)&x->hin_dev, x->hin, 0));
+        x->hin_elems = 2 * (size_t)n * pad;
+    }
+    auto input = [&](size_t j) -> int {  // sub-round j's pieces into the residual; ev[3 j] after them
+        if (dma_in) {
             for (int q = 0; q < n; q++)
                 if (ln[q])
                     ONO_HIP(hipMemcpyAsync(r->residual + st[q], res_host + st[q], ln[q] * sizeof(float),
                                            hipMemcpyHostToDevice, r->hstream));
             ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
             ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
-            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream, true));
-            int rc2 = r->wire == ONO_WIRE_F16
-                          ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
-                          : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
+            if (in_fences) ONO_HIP(launch_xgmi_fence_all(r->cstream, true));
+            return ONO_OK;
+        }
+        const size_t b = j & 1;
+        if (!res_dev && j >= 2) ONO_HIP(hipEventSynchronize(x->ev[3 * (j - 2)]));  // the slot was read
+        for (int q = 0; q < n; q++) {
+            if (!ln[q]) continue;
+            const float *src = res_dev ? res_dev + st[q] : nullptr;
+            if (!res_dev) {
+                const size_t at = (b * (size_t)n + (size_t)q) * pad + (st[q] & 3);
+                host_copy(r, x->hin + at, res_host + st[q], ln[q] * sizeof(float));
+                src = x->hin_dev + at;
+            }
+            ONO_HIP(launch_copy<float>(r->residual + st[q], src, ln[q], r->cstream));
+        }
+        ONO_HIP(hipEventRecord(x->ev[3 * j], r->cstream));
+        return ONO_OK;
+    };
+    auto rounds = [&]() -> int {
+        // (the copy-engine form: dirty lines an earlier kernel left on these addresses reach HBM first)
+        if (in_fences) ONO_HIP(launch_xgmi_fence_all(r->hstream, true));
+        for (size_t j = 0; j < S; j++) {
+            piece(j);
+            int rc2 = input(j);
             if (rc2) return rc2;
-            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream, full));
+            rc2 = r->wire == ONO_WIRE_F16
+                      ? xgmi_round<uint16_t>(r, r->residual, r->grad, r->cstream, st.data(), ln.data())
+                      : xgmi_round<float>(r, r->residual, r->grad, r->cstream, st.data(), ln.data());
+            if (rc2) return rc2;
+            if (fence) ONO_HIP(launch_xgmi_fence_all(r->cstream, in_fences));
             ONO_HIP(hipEventRecord(x->ev[3 * j + 1], r->cstream));
             ONO_HIP(hipStreamWaitEvent(r->dstream, x->ev[3 * j + 1], 0));
             for (int q = 0; q < n; q++)
@@ -721,6 +762,7 @@ void xgmi_free(ono_ring *r) {
         }
     }
     for (hipEvent_t ev : x->ev) (void)hipEventDestroy(ev);
+    if (x->hin) (void)hipHostFree(x->hin);
     // the region goes back to the pool (or into quarantine); peer mappings stay in the process's table
     if (x->counted) pool().release_ring(x->xbuf, released);
     if (x->err) (void)hipHostFree(x->err);

@@ -141,12 +141,14 @@ def test_xgmi_pool_release_then_fresh_rings(n):
 
 
 @pytest.mark.parametrize("n", [2, 3])
-def test_xgmi_host_fed_with_and_without_copy_fences(n):
-    """The host-fed round's copy-engine fences change no value: rounds take
-    ONO_XGMI_HOST_FENCE=2 (lean, the default) / 1 (full) / 0 (none) in turn in the same processes, every
-    one bit-exact; rank 0 records the wall time of each under gpurun_out/ (the fences' cost)."""
-    check(run_ranks(n, [{"kind": "host_fence", "length": (1 << 22) + 3, "wire": "f32", "rounds": 5}],
-                    ONO_HOST_CHUNK_MIB="4"))
+@pytest.mark.parametrize("registered", [False, True])
+def test_xgmi_host_fed_input_forms(n, registered):
+    """The host-fed round's input forms (a copy kernel writes the residual, the
+    default; the copy engine with fences; the copy engine alone) give the same bits: rounds take them in
+    turn in the same processes, pageable or registered buckets, every one bit-exact with the host residual
+    zeroed; rank 0 records the wall time of each under gpurun_out/ (their cost)."""
+    check(run_ranks(n, [{"kind": "host_fence", "length": (1 << 22) + 3, "wire": "f32", "rounds": 4,
+                         "registered": registered}], ONO_HOST_CHUNK_MIB="4"))
 
 
 def test_xgmi_timing_phases():

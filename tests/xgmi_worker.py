@@ -339,35 +339,52 @@ def run_recreate(rank: int, n: int, case: dict) -> str | None:
 
 
 def run_host_fence(rank: int, n: int, case: dict) -> str | None:
-    """Host-fed rounds under each copy-engine fence mode (ONO_XGMI_HOST_FENCE, read per call: "2" the
-    default lean form, "1" the full form, "0" none), in turn, each bit-exact; rank 0 writes the wall
-    times of every mode to gpurun_out/ when it exists (the fences' cost)."""
+    """Host-fed rounds under each input form in turn, each bit-exact: "kernel" (the
+    default: a copy kernel writes the residual from the caller's registered bucket or a pinned staging slot,
+    an L2 write-back on every XCD before each D2H), "dma+fence" (the copy engine's H2D with write-back +
+    invalidate fences around it), "dma" (the copy engine alone, round 5's form); ONO_XGMI_HOST_IN /
+    ONO_XGMI_HOST_FENCE are read per call.  Rank 0 writes the wall times of every form to gpurun_out/ when
+    it exists (their cost)."""
     length, wire, rounds = case.get("length", 1 << 22), case.get("wire", "f32"), case.get("rounds", 6)
+    forms = {"kernel": {}, "dma+fence": {"ONO_XGMI_HOST_IN": "dma", "ONO_XGMI_HOST_FENCE": "1"},
+             "dma": {"ONO_XGMI_HOST_IN": "dma", "ONO_XGMI_HOST_FENCE": "0"}}
+    modes = case.get("modes", list(forms))
     ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
-    modes = case.get("modes", ["2", "1", "0"])
     times = {m: [] for m in modes}
     try:
         for i in range(len(modes) * rounds):
             mode = modes[i % len(modes)]
-            os.environ["ONO_XGMI_HOST_FENCE"] = mode
+            for k in ("ONO_XGMI_HOST_IN", "ONO_XGMI_HOST_FENCE"):
+                os.environ.pop(k, None)
+            os.environ.update(forms[mode])
             ins = [O.synth(length, SEED + 17 * i, r) for r in range(n)]
             expect, _ = O.ring_pull_grads(ins, wire)
             res_h = np.ascontiguousarray(ins[rank]).copy()
             grad_h = np.full(length, 7.0, np.float32)
+            if case.get("registered"):
+                ring.register_host(res_h)
+                ring.register_host(grad_h)
             dist.barrier()
             t0 = time.perf_counter()
             ring.pull_grads_host(res_h, grad_h)
             times[mode].append((time.perf_counter() - t0) * 1e3)
+            if case.get("registered"):
+                ring.unregister_host(res_h)
+                ring.unregister_host(grad_h)
             bad = np.flatnonzero(~O.same_or_both_nan(grad_h, expect[rank]))
             if bad.size:
-                return f"round {i} (fence {mode}): {bad.size}/{length} differ, first at {bad[0]}"
+                return f"round {i} ({mode}): {bad.size}/{length} differ, first at {bad[0]}"
+            if bits(res_h).any():
+                return f"round {i} ({mode}): host residual not zeroed"
     finally:
-        os.environ.pop("ONO_XGMI_HOST_FENCE", None)
+        for k in ("ONO_XGMI_HOST_IN", "ONO_XGMI_HOST_FENCE"):
+            os.environ.pop(k, None)
         ring.close()
     out = os.path.join(ROOT, "gpurun_out")
     if rank == 0 and os.path.isdir(out):
         med = {k: float(np.median(v[1:])) for k, v in times.items()}  # the first of each: warm-up
-        with open(os.path.join(out, f"xgmi_host_fence_n{n}.json"), "w") as f:
+        tag = "_registered" if case.get("registered") else ""
+        with open(os.path.join(out, f"xgmi_host_fence_n{n}{tag}.json"), "w") as f:
             json.dump({"n": n, "length": length, "wire": wire, "ms": times, "median_ms_after_first": med}, f)
     return None
 
