@@ -534,13 +534,17 @@ int ono_ring_create(ono_ring **out, int pos, int nranks, size_t size, int device
     auto fail = [&](int rc) { ono_ring_destroy(r); return rc; };
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return fail(hip_error(e, "hipSetDevice", __FILE__, __LINE__));
+    // the buckets are zeroed by the library's fill kernel on the ring's own stream, waited for before the
+    // ring is handed out (a null-stream hipMemset is not ordered with the non-blocking streams the host-fed
+    // forms run on)
     if ((e = hipMalloc((void **)&r->grad, size * sizeof(float))) != hipSuccess ||
         (e = hipMalloc((void **)&r->residual, size * sizeof(float))) != hipSuccess ||
-        (e = hipMemset(r->grad, 0, size * sizeof(float))) != hipSuccess ||
-        (e = hipMemset(r->residual, 0, size * sizeof(float))) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&r->hstream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&r->cstream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&r->dstream, hipStreamNonBlocking)) != hipSuccess)
+        (e = hipStreamCreateWithFlags(&r->dstream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = dev_zero(r->grad, size * sizeof(float), r->cstream)) != hipSuccess ||
+        (e = dev_zero(r->residual, size * sizeof(float), r->cstream)) != hipSuccess ||
+        (e = hipStreamSynchronize(r->cstream)) != hipSuccess)
         return fail(hip_error(e, "bucket allocation", __FILE__, __LINE__));
     if (nranks > 1) {  // hop-ring wire buffers, sized for either wire
         for (int b = 0; b < 2; b++)
