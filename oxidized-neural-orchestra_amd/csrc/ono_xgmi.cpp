@@ -622,8 +622,9 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     // it before the owners' chains: one rank's residual read back as zeros at scattered 128-B lines, the data
     // the copy engine had written there not seen by the kernels.  The residual is therefore written by a
     // kernel, as every other buffer the round reads is: the caller's bucket read in place when it is
-    // registered, else copied by the host pool into a pinned, mapped staging slot (two slots of n pieces,
-    // each piece at the residual's 4-element phase) that a copy kernel on the round's stream reads.
+    // registered, else copied by the host pool into a pinned, mapped, coherent staging slot (two slots of n
+    // pieces, each at the residual's 4-element phase) — read system-coherent by one launch on the round's
+    // stream (launch_xgmi_host_in).
     // ONO_XGMI_HOST_IN=dma keeps the copy engine's H2D (with the fences below, round 6's first attempt).
     // Before each D2H a system-scope L2 write-back on every XCD (ONO_XGMI_HOST_FENCE=0 drops it; =1 adds the
     // write-back + invalidate fences around the copy-engine input as well).
@@ -640,7 +641,8 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
         if (x->hin) ONO_HIP(hipHostFree(x->hin));
         x->hin = x->hin_dev = nullptr;
         x->hin_elems = 0;
-        ONO_HIP(hipHostMalloc((void **)&x->hin, 2 * (size_t)n * pad * sizeof(float), hipHostMallocMapped));
+        ONO_HIP(hipHostMalloc((void **)&x->hin, 2 * (size_t)n * pad * sizeof(float),
+                              hipHostMallocMapped | hipHostMallocCoherent));
         ONO_HIP(hipHostGetDevicePointer((void **)&x->hin_dev, x->hin, 0));
         x->hin_elems = 2 * (size_t)n * pad;
     }
@@ -657,6 +659,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
         }
         const size_t b = j & 1;
         if (!res_dev && j >= 2) ONO_HIP(hipEventSynchronize(x->ev[3 * (j - 2)]));  // the slot was read
+        XSegs in{};
         for (int q = 0; q < n; q++) {
             if (!ln[q]) continue;
             const float *src = res_dev ? res_dev + st[q] : nullptr;
@@ -665,8 +668,13 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
                 host_copy(r, x->hin + at, res_host + st[q], ln[q] * sizeof(float));
                 src = x->hin_dev + at;
             }
-            ONO_HIP(launch_copy<float>(r->residual + st[q], src, ln[q], r->cstream));
+            XSeg &sg = in.s[in.nseg++];
+            sg.src = src;
+            sg.dst = r->residual + st[q];
+            sg.n = ln[q];
+            sg.head = head_of(sg.src, 4, sg.dst, 4);
         }
+        ONO_HIP(launch_xgmi_host_in(in, r->cstream));
         ONO_HIP(hipEventRecord(x->ev[3 * j], r->cstream));
         return ONO_OK;
     };
