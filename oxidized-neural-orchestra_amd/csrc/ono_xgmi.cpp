@@ -635,6 +635,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     if (!dma_in && reg) {
         void *p = nullptr;
         if (hipHostGetDevicePointer(&p, res_host, 0) == hipSuccess) res_dev = static_cast<const float *>(p);
+        else (void)hipGetLastError();  // (not mapped: staged; the error must not reach a later launch check)
     }
     const size_t pad = sub + 4;  // a staging piece: sub elements at any 4-element phase
     if (!dma_in && !res_dev && x->hin_elems < 2 * (size_t)n * pad) {
