@@ -623,8 +623,8 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     // the copy engine had written there not seen by the kernels.  The residual is therefore written by a
     // kernel, as every other buffer the round reads is: the caller's bucket read in place when it is
     // registered, else copied by the host pool into a pinned, mapped, coherent staging slot (two slots of n
-    // pieces, each at the residual's 4-element phase) — read system-coherent by one launch on the round's
-    // stream (launch_xgmi_host_in).
+    // pieces, each at the residual's 4-element phase) — read system-coherent by one launch on the copy
+    // stream (launch_xgmi_host_in) that the round's stream waits for.
     // ONO_XGMI_HOST_IN=dma keeps the copy engine's H2D (with the fences below, round 6's first attempt).
     // Before each D2H a system-scope L2 write-back on every XCD (ONO_XGMI_HOST_FENCE=0 drops it; =1 adds the
     // write-back + invalidate fences around the copy-engine input as well).
@@ -675,8 +675,10 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
             sg.n = ln[q];
             sg.head = head_of(sg.src, 4, sg.dst, 4);
         }
-        ONO_HIP(launch_xgmi_host_in(in, r->cstream));
-        ONO_HIP(hipEventRecord(x->ev[3 * j], r->cstream));
+        // (on the copy stream, so it overlaps the previous sub-round's round; the round waits for it)
+        ONO_HIP(launch_xgmi_host_in(in, r->hstream));
+        ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
+        ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
         return ONO_OK;
     };
     auto rounds = [&]() -> int {
