@@ -169,7 +169,7 @@ struct XBarrier {
 hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s);
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s);
 // host-fed input: segment j copies n f32 from host memory (read sc0 sc1) into HBM
-hipError_t launch_xgmi_host_in(const XSegs &g, hipStream_t s);
+hipError_t launch_xgmi_host_in(const XSegs &g, hipStream_t s, bool sys = true);
 hipError_t launch_xgmi_barrier(const XBarrier &b, hipStream_t s);
 // A system-scope fence on every XCD (host-fed rounds, around the copies): L2
 // write-back, then (acquire) L2 invalidate.

@@ -629,7 +629,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
     // Before each D2H a system-scope L2 write-back on every XCD (ONO_XGMI_HOST_FENCE=0 drops it; =1 adds the
     // write-back + invalidate fences around the copy-engine input as well).
     const char *ie = getenv("ONO_XGMI_HOST_IN"), *fe = getenv("ONO_XGMI_HOST_FENCE");
-    const bool dma_in = ie && strcmp(ie, "dma") == 0;
+    const bool dma_in = ie && strcmp(ie, "dma") == 0, plain_in = ie && strcmp(ie, "plain") == 0;
     const bool fence = !(fe && strcmp(fe, "0") == 0), in_fences = dma_in && fence;
     const float *res_dev = nullptr;  // the caller's registered bucket, as the device addresses it
     if (!dma_in && reg) {
@@ -676,7 +676,7 @@ int xgmi_pull_grads_host(ono_ring *r, float *res_host, float *grad_host, size_t 
             sg.head = head_of(sg.src, 4, sg.dst, 4);
         }
         // (on the copy stream, so it overlaps the previous sub-round's round; the round waits for it)
-        ONO_HIP(launch_xgmi_host_in(in, r->hstream));
+        ONO_HIP(launch_xgmi_host_in(in, r->hstream, !plain_in));
         ONO_HIP(hipEventRecord(x->ev[3 * j], r->hstream));
         ONO_HIP(hipStreamWaitEvent(r->cstream, x->ev[3 * j], 0));
         return ONO_OK;

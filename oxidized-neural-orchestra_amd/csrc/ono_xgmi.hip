@@ -72,13 +72,15 @@ template <bool ZERO> struct PushOp {
 
 // host-fed input: the caller's bucket (registered) or a pinned staging slot -> the residual; the host
 // memory is read system-coherent (sc0 sc1: no cache keeps an earlier call's lines of it)
-struct HostInOp {
+template <bool SYS> struct HostInOp {  // SYS = false: nontemporal loads (measurement, ONO_XGMI_HOST_IN=plain)
     static constexpr bool kPeerStores = false;
     __device__ __forceinline__ static void scalar(const XSeg &s, size_t i) {
-        ((float *)s.dst)[i] = ld_sys((const float *)s.src + i);
+        const float *p = (const float *)s.src + i;
+        ((float *)s.dst)[i] = SYS ? ld_sys(p) : __builtin_nontemporal_load(p);
     }
     __device__ __forceinline__ static void vec(const XSeg &s, size_t i) {
-        *(f4 *)((float *)s.dst + i) = ld_sys((const f4 *)((const float *)s.src + i));
+        const f4 *p = (const f4 *)((const float *)s.src + i);
+        *(f4 *)((float *)s.dst + i) = SYS ? ld_sys(p) : __builtin_nontemporal_load(p);
     }
 };
 
@@ -241,7 +243,9 @@ hipError_t launch_xgmi_push(const XSegs &g, bool zero_src, hipStream_t s) {
     return zero_src ? launch_segs(PushOp<true>{}, g, s) : launch_segs(PushOp<false>{}, g, s);
 }
 
-hipError_t launch_xgmi_host_in(const XSegs &g, hipStream_t s) { return launch_segs(HostInOp{}, g, s); }
+hipError_t launch_xgmi_host_in(const XSegs &g, hipStream_t s, bool sys) {
+    return sys ? launch_segs(HostInOp<true>{}, g, s) : launch_segs(HostInOp<false>{}, g, s);
+}
 
 hipError_t launch_xgmi_pull(const XSegs &g, bool f16, float divisor, hipStream_t s) {
     Scale sc = make_scale(divisor);

@@ -346,7 +346,8 @@ def run_host_fence(rank: int, n: int, case: dict) -> str | None:
     ONO_XGMI_HOST_FENCE are read per call.  Rank 0 writes the wall times of every form to gpurun_out/ when
     it exists (their cost)."""
     length, wire, rounds = case.get("length", 1 << 22), case.get("wire", "f32"), case.get("rounds", 6)
-    forms = {"kernel": {}, "dma+fence": {"ONO_XGMI_HOST_IN": "dma", "ONO_XGMI_HOST_FENCE": "1"},
+    forms = {"kernel": {}, "kernel-nt": {"ONO_XGMI_HOST_IN": "plain"},
+             "dma+fence": {"ONO_XGMI_HOST_IN": "dma", "ONO_XGMI_HOST_FENCE": "1"},
              "dma": {"ONO_XGMI_HOST_IN": "dma", "ONO_XGMI_HOST_FENCE": "0"}}
     modes = case.get("modes", list(forms))
     ring = ono_amd.WorkerRingManager.over_xgmi(rank, n, length, allgather, wire=wire)
