@@ -371,8 +371,11 @@ int ono_ring_set_algo(ono_ring *ring, int algo);
  * RESIDUAL RISK: one wrong result seen in round 4 (a rank read stale lines of a
  * peer's result slot right after a pool release) was narrowed to the free and
  * re-import path, not proven; that path is now closed by the
- * rules above and has not failed since, but a caller that must never see it
- * can keep its rings (and the pool) for the process's life.                  */
+ * rules above.  Round 6 saw it twice more in the host-fed form right after a
+ * release, classified as one rank's copy-engine-written residual read back as
+ * zeros at scattered lines; the host-fed round's residual is since written by
+ * a kernel (ono_ring_pull_grads_host).  Not proven either: a caller that must
+ * never see it can keep its rings (and the pool) for the process's life.    */
 #define ONO_XGMI_HANDLE_BYTES 128
 int ono_ring_create_xgmi(ono_ring **out, int pos, int nranks, size_t size, int device, int wire);
 int ono_ring_xgmi_handle(ono_ring *ring, uint8_t handle[ONO_XGMI_HANDLE_BYTES]);
