@@ -847,7 +847,7 @@ def host_fed_n(ono_amd, ring, elems: int, ctl, world: int, rounds: int = 5) -> d
         if ring.wire == "f32" and ring.algo in ("auto", "allreduce"):
             how = "H2D || all-reduce || D2H in 16 MiB chunks"
         elif ring.algo == "xgmi":
-            how = "H2D || xGMI round || D2H in sub-rounds (a slice of every chunk each)"
+            how = "upload kernel (reads the host bucket over PCIe) || xGMI round || D2H in sub-rounds (a slice of every chunk each)"
         else:
             how = f"whole bucket: H2D, {ring.algo} round, D2H"
         return {"workload": f"pull_grads_host on {world} GPUs: registered host buckets of {elems * 4 >> 20} MiB per "
