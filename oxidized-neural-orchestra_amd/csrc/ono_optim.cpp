@@ -49,6 +49,8 @@ int ono_optimizer_create(ono_optimizer **out, const ono_opt_spec *opt, size_t n,
     if (e == hipSuccess && opt->kind == ONO_OPT_ADAM) {
         if ((e = hipMalloc((void **)&p->s, b)) == hipSuccess) e = hipMemset(p->s, 0, b);
     }
+    // the zero fills ran on the null stream; the caller's stream may be a non-blocking one: complete them here
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (prev >= 0) (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         (void)hipFree(p->v);

@@ -84,6 +84,9 @@ int ono_store_create(ono_store **out, int kind, const float *init, size_t nparam
     }
     if (nparams && (e = hipMemcpy(st->params, init, nparams * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e);
+    // the zero fills ran on the null stream, which the store's non-blocking stream is not ordered with:
+    // complete before the store is handed out (as the ring's buckets)
+    if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return fail(e);
     *out = st;
     return ONO_OK;
 }
