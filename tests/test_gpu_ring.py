@@ -85,6 +85,30 @@ def test_ring_n1_owned_buckets(wire):
     ring.close()
 
 
+def test_ring_buckets_zero_at_creation_on_any_stream():
+    """A ring's owned buckets are zero when ono_ring_create returns, as seen from a non-blocking stream the
+    creation never touched (the fill runs on the ring's stream and is waited for).
+    Rings come and go over memory the previous ones used (and dirtied: each round leaves its grad), and
+    the first acc_residual on the new stream starts from +0."""
+    size = (1 << 20) + 3
+    s = torch.cuda.Stream()
+    for k in range(6):
+        ring = ono_amd.WorkerRingManager(0, 1, size)
+        with torch.cuda.stream(s):
+            res0, grad0 = ring.residual.clone(), ring.grad.clone()
+        s.synchronize()
+        assert not host(res0).view(np.uint32).any(), f"ring {k}: residual not zero at creation"
+        assert not host(grad0).view(np.uint32).any(), f"ring {k}: grad not zero at creation"
+        g = O.synth(size, SEED + k, 2)
+        gd = to_dev(g)
+        torch.cuda.synchronize()
+        ring.acc_residual(gd, stream=s)
+        pm = ring.pull_grads(stream=s)
+        s.synchronize()
+        assert_bitexact(host(pm.grad), (np.zeros(size, np.float32) + g).astype(np.float32))
+        ring.close()
+
+
 def test_ring_n1_dev_and_host_forms():
     size = 4099
     ring = ono_amd.WorkerRingManager(0, 1, size)
